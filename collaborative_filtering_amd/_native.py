@@ -1,0 +1,79 @@
+"""ctypes binding of libcf_mi355x.so (the C ABI declared in include/cf_abi.h).
+
+The product path is the HIP library.  There is no CPU fallback: if the shared
+object is missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_uint32, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcf_mi355x.so")
+HOST_LIB_PATH = os.path.join(_HERE, "libcf_host.so")
+
+CF_OK = 0
+CF_SIGS_OWN = 0
+CF_SIGS_COMPAT = 1
+CF_MAX_K = 192
+
+# name -> (restype, argtypes); the list is the ABI contract checked by tests.
+SIGNATURES = {
+    "cf_version": (c_int, []),
+    "cf_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "cf_destroy": (None, [c_void_p]),
+    "cf_last_error": (c_char_p, [c_void_p]),
+    "cf_set_jacobi": (c_int, [c_void_p, c_float, c_int]),
+    "cf_item_graph_upload": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p]),
+    "cf_item_graph_upload_dense": (c_int, [c_void_p, c_uint32, c_void_p, c_int]),
+    "cf_item_graph_device": (c_void_p, [c_void_p, POINTER(c_uint32)]),
+    "cf_plan_create": (c_int, [c_void_p, c_uint32, c_void_p, POINTER(c_void_p)]),
+    "cf_plan_destroy": (None, [c_void_p]),
+    "cf_evec_slots": (c_uint64, [c_uint32]),
+    "cf_evec_offsets": (c_uint64, [c_uint32, c_void_p, c_void_p]),
+    "cf_eigen_batch": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p]),
+    "cf_eigen_run": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_void_p, c_void_p]),
+    "cf_predict_precomp": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_void_p,
+                                   c_void_p]),
+    "cf_predict_run_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                   c_void_p]),
+    "cf_predict_run_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                   c_void_p]),
+}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load libcf_mi355x.so (raises NativeError if it is missing: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(f"{LIB_PATH} not built; run `make` or __graft_entry__.build()")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def ptr(a) -> c_void_p:
+    """Raw pointer of a numpy array or a torch tensor (device pointers pass through)."""
+    if a is None:
+        return c_void_p(0)
+    if hasattr(a, "data_ptr"):
+        return c_void_p(a.data_ptr())
+    return c_void_p(a.ctypes.data)

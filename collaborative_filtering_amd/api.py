@@ -1,0 +1,193 @@
+"""Host-side mirror of the reference's hot-path operators over the HIP C ABI.
+
+Names follow the reference (compute_eigens, neigh_program::apply, weights_calc,
+knn_program): each function below states the reference interface it stands in for.
+Inputs are numpy arrays (host) or torch CUDA tensors for the *_run device paths.
+"""
+from __future__ import annotations
+
+from ctypes import byref, c_uint32, c_void_p
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native
+from ._native import CF_SIGS_COMPAT, CF_SIGS_OWN, NativeError, ptr
+
+
+def _check(lib, ctx, rc, what):
+    if rc != _native.CF_OK:
+        msg = lib.cf_last_error(ctx)
+        raise NativeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def evec_offsets(item_off: np.ndarray) -> tuple[np.ndarray, int]:
+    """Per-user eigenvector slot offsets: slot size k*max(k,2) floats."""
+    k = np.diff(item_off.astype(np.int64))
+    slots = k * np.maximum(k, 2)
+    off = np.zeros(len(k), dtype=np.uint64)
+    if len(k):
+        off[1:] = np.cumsum(slots)[:-1]
+    return off, int(slots.sum())
+
+
+@dataclass
+class EigenResult:
+    """Per-user eigen blocks in the flat layout of cf_eigen_batch (cf_abi.h)."""
+
+    item_off: np.ndarray  # uint64[n_users+1]
+    evec_off: np.ndarray  # uint64[n_users]
+    m: np.ndarray         # int32[n_users]
+    sigs: np.ndarray      # float32[item_off[-1]]
+    evals: np.ndarray     # float32[item_off[-1]] (first min(m,k) valid)
+    evecs: np.ndarray     # float32 flat (k x m row-major at evec_off[u])
+
+    def block(self, u: int):
+        b, e = int(self.item_off[u]), int(self.item_off[u + 1])
+        k, m = e - b, int(self.m[u])
+        ev = np.zeros(m, dtype=np.float32)
+        ev[: min(m, k)] = self.evals[b : b + min(m, k)]
+        o = int(self.evec_off[u])
+        U = self.evecs[o : o + k * m].reshape(k, m)
+        return self.sigs[b:e], ev, U
+
+
+class Context:
+    """One device context (cf_ctx) holding the HBM-resident item graph."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _native.load()
+        h = c_void_p()
+        rc = self.lib.cf_create(device, byref(h))
+        if rc != _native.CF_OK:
+            raise NativeError(f"cf_create(device={device}) failed ({rc}); is a GPU visible?")
+        self.h = h
+        self.n_items = 0
+
+    def close(self):
+        if self.h:
+            self.lib.cf_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        _check(self.lib, self.h, rc, what)
+
+    def set_jacobi(self, tol_scale: float = 1.0, max_sweeps: int = 30):
+        self._chk(self.lib.cf_set_jacobi(self.h, tol_scale, max_sweeps), "cf_set_jacobi")
+
+    # -- item graph (out_fin_) ---------------------------------------------------
+    def upload_graph_dense(self, W):
+        """W: n_items x n_items float32 (numpy, or torch CUDA tensor)."""
+        n = int(W.shape[0])
+        on_dev = int(hasattr(W, "is_cuda") and W.is_cuda)
+        if not on_dev:
+            W = np.ascontiguousarray(W, dtype=np.float32)
+        self._chk(self.lib.cf_item_graph_upload_dense(self.h, n, ptr(W), on_dev), "cf_item_graph_upload_dense")
+        self.n_items = n
+
+    def upload_graph_csr(self, n_items: int, row_ptr, col, w):
+        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.uint64)
+        col = np.ascontiguousarray(col, dtype=np.uint32)
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        self._chk(self.lib.cf_item_graph_upload(self.h, n_items, ptr(row_ptr), ptr(col), ptr(w)),
+                  "cf_item_graph_upload")
+        self.n_items = n_items
+
+    def graph_device_ptr(self) -> int:
+        n = c_uint32()
+        p = self.lib.cf_item_graph_device(self.h, byref(n))
+        return int(p or 0)
+
+    # -- compute_eigens (precompute_local_threads.cpp:100-213) --------------------
+    def eigen_batch(self, item_off, items) -> EigenResult:
+        item_off = np.ascontiguousarray(item_off, dtype=np.uint64)
+        items = np.ascontiguousarray(items, dtype=np.uint32)
+        n_users = len(item_off) - 1
+        evec_off, total = evec_offsets(item_off)
+        n_entries = int(item_off[-1])
+        m = np.zeros(n_users, dtype=np.int32)
+        sigs = np.zeros(n_entries, dtype=np.float32)
+        evals = np.zeros(n_entries, dtype=np.float32)
+        evecs = np.zeros(max(total, 1), dtype=np.float32)
+        self._chk(self.lib.cf_eigen_batch(self.h, n_users, ptr(item_off), ptr(items), ptr(evec_off), ptr(m),
+                                          ptr(sigs), ptr(evals), ptr(evecs)), "cf_eigen_batch")
+        return EigenResult(item_off, evec_off, m, sigs, evals, evecs)
+
+    # -- neigh_program::apply (local_calc_precomp.cpp:217-380) --------------------
+    def predict_precomp(self, item_off, items, ratings, m, evals, evec_off, evecs, sigtab,
+                        sig_mode=CF_SIGS_COMPAT, want_pred=False):
+        """All arrays host numpy; evals/evecs/sigtab float64 (parsed out_eigen_)."""
+        item_off = np.ascontiguousarray(item_off, dtype=np.uint64)
+        items = np.ascontiguousarray(items, dtype=np.uint32)
+        ratings = np.ascontiguousarray(ratings, dtype=np.float32)
+        m = np.ascontiguousarray(m, dtype=np.int32)
+        evals = np.ascontiguousarray(evals, dtype=np.float64)
+        evec_off = np.ascontiguousarray(evec_off, dtype=np.uint64)
+        evecs = np.ascontiguousarray(evecs, dtype=np.float64)
+        sigtab = np.ascontiguousarray(sigtab, dtype=np.float64)
+        n_users = len(item_off) - 1
+        n = int(item_off[-1])
+        mse = np.zeros(n, dtype=np.float32)
+        kk = np.zeros(n, dtype=np.int32)
+        pred = np.zeros(n, dtype=np.float64) if want_pred else None
+        self._chk(self.lib.cf_predict_precomp(self.h, n_users, ptr(item_off), ptr(items), ptr(ratings), ptr(m),
+                                              ptr(evals), ptr(evec_off), ptr(evecs), ptr(sigtab), len(sigtab),
+                                              int(sig_mode), ptr(mse), ptr(kk), ptr(pred)),
+                  "cf_predict_precomp")
+        return (mse, kk, pred) if want_pred else (mse, kk)
+
+    # -- device-resident paths (torch CUDA tensors) -------------------------------
+    def plan(self, item_off_host) -> "Plan":
+        return Plan(self, item_off_host)
+
+
+class Plan:
+    """cf_plan: users bucketed by item count, reusable across eigen/predict runs."""
+
+    def __init__(self, ctx: Context, item_off_host):
+        self.ctx = ctx
+        item_off_host = np.ascontiguousarray(item_off_host, dtype=np.uint64)
+        h = c_void_p()
+        ctx._chk(ctx.lib.cf_plan_create(ctx.h, len(item_off_host) - 1, ptr(item_off_host), byref(h)),
+                 "cf_plan_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.cf_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def eigen_run(self, d_item_off, d_items, d_evec_off, d_m, d_sigs, d_evals, d_evecs, stream=None):
+        c = self.ctx
+        c._chk(c.lib.cf_eigen_run(c.h, self.h, ptr(d_item_off), ptr(d_items), ptr(d_evec_off), ptr(d_m),
+                                  ptr(d_sigs), ptr(d_evals), ptr(d_evecs), c_void_p(stream or 0)),
+               "cf_eigen_run")
+
+    def predict_run(self, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off, d_evecs, d_sigtab,
+                    sig_mode, d_mse, d_kk, d_pred=None, stream=None, fp64=False):
+        c = self.ctx
+        fn = c.lib.cf_predict_run_f64 if fp64 else c.lib.cf_predict_run_f32
+        c._chk(fn(c.h, self.h, ptr(d_item_off), ptr(d_items), ptr(d_ratings), ptr(d_m), ptr(d_evals),
+                  ptr(d_evec_off), ptr(d_evecs), ptr(d_sigtab), int(sig_mode), ptr(d_mse), ptr(d_kk),
+                  ptr(d_pred), c_void_p(stream or 0)), "cf_predict_run")
+
+
+__all__ = ["Context", "Plan", "EigenResult", "evec_offsets", "CF_SIGS_OWN", "CF_SIGS_COMPAT"]

@@ -1,0 +1,401 @@
+// cf_api.hip -- the extern "C" boundary of libcf_mi355x.so (declared in include/cf_abi.h).
+//
+// Host-pointer entry points copy in, run the device path on the context's stream and
+// copy out; *_run entry points take device pointers and an explicit stream.
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+
+#include "cf_internal.h"
+
+int cf_set_error(cf_ctx* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->last_error = msg;
+    return code;
+}
+
+namespace {
+
+// Scatter a CSR graph into the dense matrix.  Duplicate (a,b) keep the LAST
+// occurrence in CSR order, like repeated `weights(m1,m2) = w` assignments
+// (precompute_local_threads.cpp:284): one thread per row walks its edges in order.
+__global__ void dense_scatter_kernel(uint32_t n_items, const uint64_t* row_ptr, const uint32_t* col,
+                                     const float* w, float* dense) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_items) return;
+    float* row = dense + (size_t)r * n_items;
+    for (uint64_t e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
+        const uint32_t c = col[e];
+        if (c < n_items) row[c] = w[e];
+    }
+}
+
+// RAII device buffer used by the host-pointer wrappers.
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+int dev_alloc(cf_ctx* ctx, DevBuf& b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess)
+        return cf_set_error(ctx, CF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return CF_OK;
+}
+
+int set_device(cf_ctx* ctx) {
+    CF_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    return CF_OK;
+}
+
+#define CF_TRY(expr)              \
+    do {                          \
+        int _rc = (expr);         \
+        if (_rc != CF_OK) return _rc; \
+    } while (0)
+
+}  // namespace
+
+int cf_launch_dense_scatter(cf_ctx* ctx, uint32_t n_items, const uint64_t* d_row_ptr,
+                            const uint32_t* d_col, const float* d_w, float* d_dense,
+                            hipStream_t stream) {
+    const int threads = 256;
+    const int blocks = (int)((n_items + threads - 1) / threads);
+    if (blocks > 0) {
+        hipLaunchKernelGGL(dense_scatter_kernel, dim3(blocks), dim3(threads), 0, stream, n_items,
+                           d_row_ptr, d_col, d_w, d_dense);
+        CF_HIP_CHECK(ctx, hipGetLastError());
+    }
+    return CF_OK;
+}
+
+extern "C" {
+
+int cf_version(void) { return 1; }
+
+int cf_create(int device, cf_ctx** out) {
+    if (!out) return CF_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CF_EHIP;
+    if (device < 0 || device >= n) return CF_EINVAL;
+    cf_ctx* ctx = new (std::nothrow) cf_ctx();
+    if (!ctx) return CF_ENOMEM;
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess) {
+        delete ctx;
+        return CF_EHIP;
+    }
+    *out = ctx;
+    return CF_OK;
+}
+
+void cf_destroy(cf_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->d_graph) (void)hipFree(ctx->d_graph);
+    delete ctx;
+}
+
+const char* cf_last_error(const cf_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps) {
+    if (!ctx || !(tol_scale > 0.0f) || max_sweeps <= 0) return cf_set_error(ctx, CF_EINVAL, "bad jacobi options");
+    ctx->tol_scale = tol_scale;
+    ctx->max_sweeps = max_sweeps;
+    return CF_OK;
+}
+
+int cf_item_graph_upload(cf_ctx* ctx, uint32_t n_items, const uint64_t* row_ptr, const uint32_t* col,
+                         const float* w) {
+    if (!ctx || !row_ptr || (row_ptr[n_items] > 0 && (!col || !w)))
+        return cf_set_error(ctx, CF_EINVAL, "cf_item_graph_upload: null argument");
+    CF_TRY(set_device(ctx));
+    const uint64_t nnz = row_ptr[n_items];
+    const size_t dense_bytes = (size_t)n_items * n_items * sizeof(float);
+    if (ctx->d_graph) {
+        (void)hipFree(ctx->d_graph);
+        ctx->d_graph = nullptr;
+        ctx->n_items = 0;
+    }
+    float* dense = nullptr;
+    if (hipMalloc(&dense, std::max<size_t>(dense_bytes, 16)) != hipSuccess)
+        return cf_set_error(ctx, CF_ENOMEM, "cf_item_graph_upload: dense graph allocation failed");
+    DevBuf drp, dcol, dw;
+    int rc = dev_alloc(ctx, drp, sizeof(uint64_t) * (n_items + 1));
+    if (rc == CF_OK) rc = dev_alloc(ctx, dcol, sizeof(uint32_t) * nnz);
+    if (rc == CF_OK) rc = dev_alloc(ctx, dw, sizeof(float) * nnz);
+    if (rc != CF_OK) {
+        (void)hipFree(dense);
+        return rc;
+    }
+    hipError_t e = hipMemset(dense, 0, dense_bytes);
+    if (e == hipSuccess) e = hipMemcpy(drp.p, row_ptr, sizeof(uint64_t) * (n_items + 1), hipMemcpyHostToDevice);
+    if (e == hipSuccess && nnz) e = hipMemcpy(dcol.p, col, sizeof(uint32_t) * nnz, hipMemcpyHostToDevice);
+    if (e == hipSuccess && nnz) e = hipMemcpy(dw.p, w, sizeof(float) * nnz, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(dense);
+        return cf_set_error(ctx, CF_EHIP, std::string("graph upload: ") + hipGetErrorString(e));
+    }
+    rc = cf_launch_dense_scatter(ctx, n_items, (const uint64_t*)drp.p, (const uint32_t*)dcol.p,
+                                 (const float*)dw.p, dense, nullptr);
+    if (rc == CF_OK && hipDeviceSynchronize() != hipSuccess)
+        rc = cf_set_error(ctx, CF_EHIP, "graph scatter failed");
+    if (rc != CF_OK) {
+        (void)hipFree(dense);
+        return rc;
+    }
+    ctx->d_graph = dense;
+    ctx->n_items = n_items;
+    return CF_OK;
+}
+
+int cf_item_graph_upload_dense(cf_ctx* ctx, uint32_t n_items, const float* w_dense, int on_device) {
+    if (!ctx || (!w_dense && n_items)) return cf_set_error(ctx, CF_EINVAL, "cf_item_graph_upload_dense: null");
+    CF_TRY(set_device(ctx));
+    const size_t bytes = (size_t)n_items * n_items * sizeof(float);
+    if (ctx->d_graph) {
+        (void)hipFree(ctx->d_graph);
+        ctx->d_graph = nullptr;
+        ctx->n_items = 0;
+    }
+    float* dense = nullptr;
+    if (hipMalloc(&dense, std::max<size_t>(bytes, 16)) != hipSuccess)
+        return cf_set_error(ctx, CF_ENOMEM, "dense graph allocation failed");
+    hipError_t e = hipMemcpy(dense, w_dense, bytes, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(dense);
+        return cf_set_error(ctx, CF_EHIP, std::string("dense graph copy: ") + hipGetErrorString(e));
+    }
+    ctx->d_graph = dense;
+    ctx->n_items = n_items;
+    return CF_OK;
+}
+
+const float* cf_item_graph_device(const cf_ctx* ctx, uint32_t* n_items) {
+    if (!ctx) return nullptr;
+    if (n_items) *n_items = ctx->n_items;
+    return ctx->d_graph;
+}
+
+uint64_t cf_evec_slots(uint32_t k) { return (uint64_t)k * std::max<uint32_t>(k, 2u); }
+
+uint64_t cf_evec_offsets(uint32_t n_users, const uint64_t* item_off, uint64_t* evec_off) {
+    uint64_t acc = 0;
+    for (uint32_t u = 0; u < n_users; ++u) {
+        if (evec_off) evec_off[u] = acc;
+        acc += cf_evec_slots((uint32_t)(item_off[u + 1] - item_off[u]));
+    }
+    return acc;
+}
+
+int cf_plan_create(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, cf_plan** out) {
+    if (!ctx || !out || (!item_off && n_users)) return cf_set_error(ctx, CF_EINVAL, "cf_plan_create: null");
+    *out = nullptr;
+    CF_TRY(set_device(ctx));
+    cf_plan* plan = new (std::nothrow) cf_plan();
+    if (!plan) return cf_set_error(ctx, CF_ENOMEM, "plan allocation");
+    plan->n_users = n_users;
+    // Bucket by emax = ceil(k/16); within a bucket, largest k first (cost ~ k^3).
+    std::vector<std::vector<uint32_t>> by(13);
+    for (uint32_t u = 0; u < n_users; ++u) {
+        const uint64_t k = item_off[u + 1] - item_off[u];
+        if (k > CF_MAX_K) {
+            delete plan;
+            return cf_set_error(ctx, CF_ERANGE,
+                                "user " + std::to_string(u) + " has k=" + std::to_string(k) +
+                                    " items; the LDS path supports k <= 192");
+        }
+        by[k == 0 ? 1 : (int)((k + 15) / 16)].push_back(u);
+        plan->kmax = std::max<uint32_t>(plan->kmax, (uint32_t)k);
+    }
+    for (int e = 12; e >= 1; --e) {
+        auto& v = by[e];
+        if (v.empty()) continue;
+        std::stable_sort(v.begin(), v.end(), [&](uint32_t x, uint32_t y) {
+            return (item_off[x + 1] - item_off[x]) > (item_off[y + 1] - item_off[y]);
+        });
+        cf_bucket b;
+        b.emax = e;
+        b.first = (uint32_t)plan->h_order.size();
+        b.count = (uint32_t)v.size();
+        b.kmax = (uint32_t)(item_off[v.front() + 1] - item_off[v.front()]);
+        plan->buckets.push_back(b);
+        plan->h_order.insert(plan->h_order.end(), v.begin(), v.end());
+    }
+    if (n_users) {
+        if (hipMalloc(&plan->d_order, sizeof(uint32_t) * n_users) != hipSuccess) {
+            delete plan;
+            return cf_set_error(ctx, CF_ENOMEM, "plan order allocation");
+        }
+        if (hipMemcpy(plan->d_order, plan->h_order.data(), sizeof(uint32_t) * n_users,
+                      hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(plan->d_order);
+            delete plan;
+            return cf_set_error(ctx, CF_EHIP, "plan order copy");
+        }
+    }
+    *out = plan;
+    return CF_OK;
+}
+
+void cf_plan_destroy(cf_plan* plan) {
+    if (!plan) return;
+    if (plan->d_order) (void)hipFree(plan->d_order);
+    delete plan;
+}
+
+int cf_eigen_run(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,
+                 const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals, float* d_evecs,
+                 void* stream) {
+    if (!ctx || !plan) return cf_set_error(ctx, CF_EINVAL, "cf_eigen_run: null");
+    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_eigen_run: no item graph uploaded");
+    CF_TRY(set_device(ctx));
+    return cf_launch_eigen(ctx, plan, d_item_off, d_items, d_evec_off, d_m, d_sigs, d_evals, d_evecs,
+                           (hipStream_t)stream);
+}
+
+int cf_eigen_batch(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, const uint32_t* items,
+                   const uint64_t* evec_off, int32_t* m_out, float* sigs, float* evals, float* evecs) {
+    if (!ctx || !item_off || !evec_off || !m_out || !sigs || !evals || !evecs)
+        return cf_set_error(ctx, CF_EINVAL, "cf_eigen_batch: null argument");
+    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_eigen_batch: no item graph uploaded");
+    CF_TRY(set_device(ctx));
+    const uint64_t n_entries = item_off[n_users];
+    for (uint64_t e = 0; e < n_entries; ++e)
+        if (items[e] >= ctx->n_items) return cf_set_error(ctx, CF_EINVAL, "item index outside the graph");
+    const uint64_t n_evec = n_users ? evec_off[n_users - 1] +
+                                          cf_evec_slots((uint32_t)(item_off[n_users] - item_off[n_users - 1]))
+                                    : 0;
+    cf_plan* plan = nullptr;
+    CF_TRY(cf_plan_create(ctx, n_users, item_off, &plan));
+    DevBuf doff, ditems, deoff, dm, dsig, deval, devec;
+    int rc = dev_alloc(ctx, doff, sizeof(uint64_t) * (n_users + 1));
+    if (rc == CF_OK) rc = dev_alloc(ctx, ditems, sizeof(uint32_t) * n_entries);
+    if (rc == CF_OK) rc = dev_alloc(ctx, deoff, sizeof(uint64_t) * std::max<uint32_t>(n_users, 1));
+    if (rc == CF_OK) rc = dev_alloc(ctx, dm, sizeof(int32_t) * std::max<uint32_t>(n_users, 1));
+    if (rc == CF_OK) rc = dev_alloc(ctx, dsig, sizeof(float) * n_entries);
+    if (rc == CF_OK) rc = dev_alloc(ctx, deval, sizeof(float) * n_entries);
+    if (rc == CF_OK) rc = dev_alloc(ctx, devec, sizeof(float) * n_evec);
+    hipError_t e = hipSuccess;
+    if (rc == CF_OK) {
+        e = hipMemcpy(doff.p, item_off, sizeof(uint64_t) * (n_users + 1), hipMemcpyHostToDevice);
+        if (e == hipSuccess && n_entries)
+            e = hipMemcpy(ditems.p, items, sizeof(uint32_t) * n_entries, hipMemcpyHostToDevice);
+        if (e == hipSuccess && n_users)
+            e = hipMemcpy(deoff.p, evec_off, sizeof(uint64_t) * n_users, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemset(deval.p, 0, sizeof(float) * std::max<uint64_t>(n_entries, 1));
+        if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("eigen H2D: ") + hipGetErrorString(e));
+    }
+    if (rc == CF_OK)
+        rc = cf_launch_eigen(ctx, plan, (const uint64_t*)doff.p, (const uint32_t*)ditems.p,
+                             (const uint64_t*)deoff.p, (int32_t*)dm.p, (float*)dsig.p, (float*)deval.p,
+                             (float*)devec.p, nullptr);
+    if (rc == CF_OK) {
+        e = hipDeviceSynchronize();
+        if (e == hipSuccess && n_users) e = hipMemcpy(m_out, dm.p, sizeof(int32_t) * n_users, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && n_entries) e = hipMemcpy(sigs, dsig.p, sizeof(float) * n_entries, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && n_entries) e = hipMemcpy(evals, deval.p, sizeof(float) * n_entries, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && n_evec) e = hipMemcpy(evecs, devec.p, sizeof(float) * n_evec, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("eigen run: ") + hipGetErrorString(e));
+    }
+    cf_plan_destroy(plan);
+    return rc;
+}
+
+int cf_predict_run_f64(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,
+                       const float* d_ratings, const int32_t* d_m, const double* d_evals,
+                       const uint64_t* d_evec_off, const double* d_evecs, const double* d_sigtab, int sig_mode,
+                       float* d_mse, int32_t* d_kk, double* d_pred, void* stream) {
+    if (!ctx || !plan) return cf_set_error(ctx, CF_EINVAL, "cf_predict_run_f64: null");
+    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_predict_run_f64: no item graph uploaded");
+    CF_TRY(set_device(ctx));
+    return cf_launch_predict<double>(ctx, plan, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off,
+                                     d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, (hipStream_t)stream);
+}
+
+int cf_predict_run_f32(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,
+                       const float* d_ratings, const int32_t* d_m, const float* d_evals,
+                       const uint64_t* d_evec_off, const float* d_evecs, const float* d_sigtab, int sig_mode,
+                       float* d_mse, int32_t* d_kk, double* d_pred, void* stream) {
+    if (!ctx || !plan) return cf_set_error(ctx, CF_EINVAL, "cf_predict_run_f32: null");
+    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_predict_run_f32: no item graph uploaded");
+    CF_TRY(set_device(ctx));
+    return cf_launch_predict<float>(ctx, plan, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off,
+                                    d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, (hipStream_t)stream);
+}
+
+int cf_predict_precomp(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, const uint32_t* items,
+                       const float* ratings, const int32_t* m, const double* evals, const uint64_t* evec_off,
+                       const double* evecs, const double* sigtab, uint64_t sigtab_len, int sig_mode,
+                       float* mse, int32_t* kk, double* pred) {
+    if (!ctx || !item_off || !items || !ratings || !m || !evals || !evec_off || !evecs || !sigtab || !mse || !kk)
+        return cf_set_error(ctx, CF_EINVAL, "cf_predict_precomp: null argument");
+    if (sig_mode != CF_SIGS_OWN && sig_mode != CF_SIGS_COMPAT)
+        return cf_set_error(ctx, CF_EINVAL, "cf_predict_precomp: bad sig_mode");
+    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_predict_precomp: no item graph uploaded");
+    CF_TRY(set_device(ctx));
+    const uint64_t n_entries = item_off[n_users];
+    uint64_t n_evec = 0;
+    for (uint32_t u = 0; u < n_users; ++u) {
+        const uint64_t k = item_off[u + 1] - item_off[u];
+        if (m[u] < 0 || (uint64_t)m[u] > std::max<uint64_t>(k, 2))
+            return cf_set_error(ctx, CF_EINVAL, "cf_predict_precomp: m out of range");
+        n_evec = std::max<uint64_t>(n_evec, evec_off[u] + k * (uint64_t)m[u]);
+        if (sig_mode == CF_SIGS_COMPAT && k > sigtab_len)
+            return cf_set_error(ctx, CF_EINVAL, "cf_predict_precomp: compat sig table shorter than k");
+    }
+    if (sig_mode == CF_SIGS_OWN && sigtab_len < n_entries)
+        return cf_set_error(ctx, CF_EINVAL, "cf_predict_precomp: sig table shorter than item_off[n_users]");
+    for (uint64_t e = 0; e < n_entries; ++e)
+        if (items[e] >= ctx->n_items) return cf_set_error(ctx, CF_EINVAL, "item index outside the graph");
+    cf_plan* plan = nullptr;
+    CF_TRY(cf_plan_create(ctx, n_users, item_off, &plan));
+    DevBuf doff, ditems, drat, dm, deval, deoff, devec, dsig, dmse, dkk, dpred;
+    int rc = dev_alloc(ctx, doff, sizeof(uint64_t) * (n_users + 1));
+    if (rc == CF_OK) rc = dev_alloc(ctx, ditems, sizeof(uint32_t) * n_entries);
+    if (rc == CF_OK) rc = dev_alloc(ctx, drat, sizeof(float) * n_entries);
+    if (rc == CF_OK) rc = dev_alloc(ctx, dm, sizeof(int32_t) * std::max<uint32_t>(n_users, 1));
+    if (rc == CF_OK) rc = dev_alloc(ctx, deval, sizeof(double) * n_entries);
+    if (rc == CF_OK) rc = dev_alloc(ctx, deoff, sizeof(uint64_t) * std::max<uint32_t>(n_users, 1));
+    if (rc == CF_OK) rc = dev_alloc(ctx, devec, sizeof(double) * n_evec);
+    if (rc == CF_OK) rc = dev_alloc(ctx, dsig, sizeof(double) * sigtab_len);
+    if (rc == CF_OK) rc = dev_alloc(ctx, dmse, sizeof(float) * n_entries);
+    if (rc == CF_OK) rc = dev_alloc(ctx, dkk, sizeof(int32_t) * n_entries);
+    if (rc == CF_OK && pred) rc = dev_alloc(ctx, dpred, sizeof(double) * n_entries);
+    hipError_t e = hipSuccess;
+    if (rc == CF_OK) {
+        auto h2d = [&](void* d, const void* h, size_t bytes) {
+            if (e == hipSuccess && bytes) e = hipMemcpy(d, h, bytes, hipMemcpyHostToDevice);
+        };
+        h2d(doff.p, item_off, sizeof(uint64_t) * (n_users + 1));
+        h2d(ditems.p, items, sizeof(uint32_t) * n_entries);
+        h2d(drat.p, ratings, sizeof(float) * n_entries);
+        h2d(dm.p, m, sizeof(int32_t) * n_users);
+        h2d(deval.p, evals, sizeof(double) * n_entries);
+        h2d(deoff.p, evec_off, sizeof(uint64_t) * n_users);
+        h2d(devec.p, evecs, sizeof(double) * n_evec);
+        h2d(dsig.p, sigtab, sizeof(double) * sigtab_len);
+        if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("predict H2D: ") + hipGetErrorString(e));
+    }
+    if (rc == CF_OK)
+        rc = cf_launch_predict<double>(ctx, plan, (const uint64_t*)doff.p, (const uint32_t*)ditems.p,
+                                       (const float*)drat.p, (const int32_t*)dm.p, (const double*)deval.p,
+                                       (const uint64_t*)deoff.p, (const double*)devec.p, (const double*)dsig.p,
+                                       sig_mode, (float*)dmse.p, (int32_t*)dkk.p, (double*)dpred.p, nullptr);
+    if (rc == CF_OK) {
+        e = hipDeviceSynchronize();
+        if (e == hipSuccess && n_entries) e = hipMemcpy(mse, dmse.p, sizeof(float) * n_entries, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && n_entries) e = hipMemcpy(kk, dkk.p, sizeof(int32_t) * n_entries, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && n_entries && pred)
+            e = hipMemcpy(pred, dpred.p, sizeof(double) * n_entries, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("predict run: ") + hipGetErrorString(e));
+    }
+    cf_plan_destroy(plan);
+    return rc;
+}
+
+}  // extern "C"

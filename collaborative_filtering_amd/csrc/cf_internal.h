@@ -1,0 +1,63 @@
+// cf_internal.h -- shared definitions of libcf_mi355x (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "cf_abi.h"
+
+struct cf_ctx {
+    int device = 0;
+    std::string last_error;
+    // Item graph, dense fp32 n_items x n_items row-major, HBM-resident.
+    float* d_graph = nullptr;
+    uint32_t n_items = 0;
+    // Jacobi controls
+    float tol_scale = 1.0f;
+    int max_sweeps = 30;
+};
+
+// One launch of the eigen / predict kernels covers the users of one k-bucket.
+struct cf_bucket {
+    int emax = 0;              // elements per lane of a column (k <= 16*emax)
+    uint32_t count = 0;        // users in the bucket
+    uint32_t first = 0;        // offset into the plan's user order
+    uint32_t kmax = 0;         // largest k in the bucket
+};
+
+struct cf_plan {
+    uint32_t n_users = 0;
+    std::vector<uint32_t> h_order;   // user ids, grouped by bucket, largest k first
+    uint32_t* d_order = nullptr;     // device copy
+    std::vector<cf_bucket> buckets;
+    uint32_t kmax = 0;
+};
+
+int cf_set_error(cf_ctx* ctx, int code, const std::string& msg);
+
+#define CF_HIP_CHECK(ctx, expr)                                                          \
+    do {                                                                                 \
+        hipError_t _e = (expr);                                                          \
+        if (_e != hipSuccess)                                                            \
+            return cf_set_error((ctx), CF_EHIP,                                          \
+                                std::string(#expr) + ": " + hipGetErrorString(_e));      \
+    } while (0)
+
+// Launchers implemented in the .hip translation units.
+int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
+                    const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m,
+                    float* d_sigs, float* d_evals, float* d_evecs, hipStream_t stream);
+
+template <typename T>
+int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
+                      const uint32_t* d_items, const float* d_ratings, const int32_t* d_m,
+                      const T* d_evals, const uint64_t* d_evec_off, const T* d_evecs,
+                      const T* d_sigtab, int sig_mode, float* d_mse, int32_t* d_kk,
+                      double* d_pred, hipStream_t stream);
+
+int cf_launch_dense_scatter(cf_ctx* ctx, uint32_t n_items, const uint64_t* d_row_ptr,
+                            const uint32_t* d_col, const float* d_w, float* d_dense,
+                            hipStream_t stream);

@@ -1,0 +1,131 @@
+/*
+ * cf_abi.h -- C ABI of libcf_mi355x.so, the MI355X-native hot path of
+ * Dhole/collaborative_filtering (per-user local-graph Laplacian eigendecomposition,
+ * graph-signal rating prediction, kNN item similarity).
+ *
+ * Conventions
+ *   - Every entry point returns CF_OK (0) or a negative CF_E* code; a message is
+ *     available from cf_last_error(ctx).  No C++ exception crosses this boundary.
+ *   - Plain pointers and sizes only.  Functions without a suffix take HOST pointers
+ *     (caller-owned, copied in/out, synchronous).  *_run functions take DEVICE
+ *     pointers and a hipStream_t passed as void* (NULL = default stream) and are
+ *     asynchronous on that stream.
+ *   - One cf_ctx per GPU; a context is not thread-safe (callers serialise).
+ *   - Item ids at this boundary are COMPACT indices 0..n_items-1 into the uploaded
+ *     item graph; the host layer maps the reference's movie ids onto them.
+ *
+ * Reference interfaces replaced (file:line in /root/reference):
+ *   cf_item_graph_upload[_dense] : the dense `weights` matrix load of
+ *                                  precompute_local_threads.cpp:253-293 and the
+ *                                  out_fin_ graph_loader of local_calc_precomp.cpp:122-136
+ *   cf_eigen_batch / cf_eigen_run : compute_eigens(), precompute_local_threads.cpp:100-213
+ *                                  (scheduled per user at :306-314)
+ *   cf_predict_precomp / cf_predict_run : neigh_program::apply,
+ *                                  local_calc_precomp.cpp:217-380 (per (movie,user) rating)
+ *   cf_item_cosine               : weights_calc() via graph.transform_edges, knn2.cpp:127-146,206
+ *                                  plus the w > 0.01 writer filter knn2.cpp:155-163
+ *   cf_knn_predict               : knn_program gather/apply + error_vertex_data,
+ *                                  knn3.cpp:185-256
+ */
+#ifndef CF_ABI_H
+#define CF_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CF_OK 0
+#define CF_EINVAL (-1)  /* bad argument / size */
+#define CF_ENOMEM (-2)  /* device or host allocation failed */
+#define CF_EHIP (-3)    /* HIP runtime or kernel launch error */
+#define CF_ERANGE (-4)  /* problem size outside the supported buckets */
+#define CF_ESTATE (-5)  /* missing prerequisite (e.g. no item graph uploaded) */
+
+#define CF_MAX_K 192    /* largest per-user item count handled by the LDS eigen path */
+
+typedef struct cf_ctx cf_ctx;
+typedef struct cf_plan cf_plan;
+
+/* ---- context --------------------------------------------------------------- */
+int cf_version(void);
+int cf_create(int device, cf_ctx** out);
+void cf_destroy(cf_ctx* ctx);
+const char* cf_last_error(const cf_ctx* ctx);
+/* Jacobi off-diagonal tolerance scale (default 1.0) and sweep cap (default 30). */
+int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
+
+/* ---- item graph (out_fin_) ---------------------------------------------------
+ * Directed weighted graph exactly as parsed: w(a,b) and w(b,a) are independent.
+ * Stored on the device as a dense n_items x n_items fp32 matrix (HBM-resident). */
+int cf_item_graph_upload(cf_ctx* ctx, uint32_t n_items, const uint64_t* row_ptr,
+                         const uint32_t* col, const float* w);
+/* w_dense: n_items*n_items row-major; on_device != 0 means w_dense is a device
+ * pointer that the context adopts by copy. */
+int cf_item_graph_upload_dense(cf_ctx* ctx, uint32_t n_items, const float* w_dense,
+                               int on_device);
+/* Device pointer of the resident dense graph (for *_run callers), or NULL. */
+const float* cf_item_graph_device(const cf_ctx* ctx, uint32_t* n_items);
+
+/* ---- user batch plan -----------------------------------------------------------
+ * Buckets users by item count k (host item_off[n_users+1]); reused by eigen and
+ * predict runs over the same user batch. */
+int cf_plan_create(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, cf_plan** out);
+void cf_plan_destroy(cf_plan* plan);
+/* Eigenvector slot size of a user with k items: k*max(k,2) floats. */
+uint64_t cf_evec_slots(uint32_t k);
+/* Fills evec_off[n_users] (prefix sum of cf_evec_slots) and returns the total. */
+uint64_t cf_evec_offsets(uint32_t n_users, const uint64_t* item_off, uint64_t* evec_off);
+
+/* ---- eigen stage: compute_eigens (precompute_local_threads.cpp:100-213) --------
+ * Per user u with k = item_off[u+1]-item_off[u] items (sorted ascending compact ids;
+ * that order is the row order of the user's block):
+ *   sigs [item_off[u] + i]   i < k  : (float)(sig_min_i + 0.01)             (:169-177)
+ *   evals[item_off[u] + j]   j < m  : eigenvalues of L2, ascending          (:164-166,193)
+ *   evecs[evec_off[u] + i*m + j]    : eigenvector j, row i (k x m row-major) (:194,205-209)
+ *   m_out[u]                        : lim, the stored eigenpair count       (:185-191)
+ * k == 1 gives m == 2 with zero padding (reference: uninitialised, :193-194). */
+int cf_eigen_batch(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off,
+                   const uint32_t* items, const uint64_t* evec_off, int32_t* m_out,
+                   float* sigs, float* evals, float* evecs);
+int cf_eigen_run(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
+                 const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m,
+                 float* d_sigs, float* d_evals, float* d_evecs, void* stream);
+
+/* ---- prediction stage: neigh_program::apply (local_calc_precomp.cpp:217-380) ----
+ * For every user u and every row r < k of the user's block (test movie items[r] with
+ * test rating ratings[item_off[u]+r]):
+ *   mse[item_off[u]+r]  = (float)(rating - clamp(pred,1,5))^2     (:307-327,358)
+ *   kk [item_off[u]+r]  = number of the user's items that are out-neighbours of the
+ *                         movie with w > 0.1 (:132,254-265,359)
+ *   pred[item_off[u]+r] = clamp(pred,1,5) (optional, may be NULL)
+ * w_lim for row r:
+ *   sig_mode CF_SIGS_COMPAT: sigtab[r]  -- the reference's accumulating sigs_min
+ *                            vector (:414,437,440,271) reduces to the global
+ *                            concatenation of all records' sigs in file order;
+ *   sig_mode CF_SIGS_OWN:    sigtab[item_off[u]+r] -- the user's own sigs.
+ * evecs are fp64 (parsed out_eigen_) or fp32 (device-resident eigen output). */
+#define CF_SIGS_OWN 0
+#define CF_SIGS_COMPAT 1
+int cf_predict_precomp(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off,
+                       const uint32_t* items, const float* ratings, const int32_t* m,
+                       const double* evals, const uint64_t* evec_off, const double* evecs,
+                       const double* sigtab, uint64_t sigtab_len, int sig_mode,
+                       float* mse, int32_t* kk, double* pred);
+int cf_predict_run_f64(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
+                       const uint32_t* d_items, const float* d_ratings, const int32_t* d_m,
+                       const double* d_evals, const uint64_t* d_evec_off,
+                       const double* d_evecs, const double* d_sigtab, int sig_mode,
+                       float* d_mse, int32_t* d_kk, double* d_pred, void* stream);
+int cf_predict_run_f32(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
+                       const uint32_t* d_items, const float* d_ratings, const int32_t* d_m,
+                       const float* d_evals, const uint64_t* d_evec_off,
+                       const float* d_evecs, const float* d_sigtab, int sig_mode,
+                       float* d_mse, int32_t* d_kk, double* d_pred, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CF_ABI_H */

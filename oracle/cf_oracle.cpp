@@ -1,0 +1,476 @@
+// cf_oracle.cpp -- CPU restatement of the reference hot path (TEST INFRASTRUCTURE ONLY).
+//
+// This file is the parity oracle for the MI355X rebuild.  Only tests/, the
+// __graft_entry__.smoke() check and bench.py's cpu_baseline leg may load it.
+// The product library (collaborative_filtering_amd/libcf_mi355x.so) never
+// links or calls it.
+//
+// PARITY STATUS: "parity unpinned" with respect to the reference binaries.
+// The reference cannot be built here (graphlab.hpp, Eigen/Dense, boost and
+// boost/threadpool.hpp are absent) and it ships no tests,
+// fixtures or golden vectors.  The arithmetic the reference delegates to the
+// third-party Eigen library (Eigen 3.x, GraphLab-2.1 era, version not pinned by
+// the reference: SelfAdjointEigenSolver = Householder tridiagonalisation +
+// implicit symmetric QR; MatrixXd::inverse = PartialPivLU) is restated below
+// from the published algorithms and pinned against numpy/LAPACK (eigh, inv) via
+// the fixtures in tests/golden/ and against closed-form spectra.
+//
+// Every function cites the reference file:line it follows.  Double precision
+// throughout, with the reference's float roundings reproduced where they occur.
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Symmetric eigensolver: Householder reduction to tridiagonal form followed by
+// the implicit-shift QL iteration (EISPACK tred2/tql2 algorithm class, the same
+// class as Eigen's SelfAdjointEigenSolver).  Reads ONLY the lower triangle of
+// a (row-major n x n), like Eigen (precompute_local_threads.cpp:164).
+// On return: d = eigenvalues ascending, V (row-major n x n) columns = vectors.
+// ---------------------------------------------------------------------------
+void tridiag_householder(int n, std::vector<double>& V, std::vector<double>& d,
+                         std::vector<double>& e) {
+    auto at = [&](int r, int c) -> double& { return V[(size_t)r * n + c]; };
+    for (int j = 0; j < n; ++j) d[j] = at(n - 1, j);
+    for (int i = n - 1; i > 0; --i) {
+        double scale = 0.0, h = 0.0;
+        for (int k = 0; k < i; ++k) scale += std::fabs(d[k]);
+        if (scale == 0.0) {
+            e[i] = d[i - 1];
+            for (int j = 0; j < i; ++j) {
+                d[j] = at(i - 1, j);
+                at(i, j) = 0.0;
+                at(j, i) = 0.0;
+            }
+        } else {
+            for (int k = 0; k < i; ++k) {
+                d[k] /= scale;
+                h += d[k] * d[k];
+            }
+            double f = d[i - 1];
+            double g = std::sqrt(h);
+            if (f > 0) g = -g;
+            e[i] = scale * g;
+            h -= f * g;
+            d[i - 1] = f - g;
+            for (int j = 0; j < i; ++j) e[j] = 0.0;
+            for (int j = 0; j < i; ++j) {
+                f = d[j];
+                at(j, i) = f;
+                g = e[j] + at(j, j) * f;
+                for (int k = j + 1; k <= i - 1; ++k) {
+                    g += at(k, j) * d[k];
+                    e[k] += at(k, j) * f;
+                }
+                e[j] = g;
+            }
+            f = 0.0;
+            for (int j = 0; j < i; ++j) {
+                e[j] /= h;
+                f += e[j] * d[j];
+            }
+            double hh = f / (h + h);
+            for (int j = 0; j < i; ++j) e[j] -= hh * d[j];
+            for (int j = 0; j < i; ++j) {
+                f = d[j];
+                g = e[j];
+                for (int k = j; k <= i - 1; ++k) at(k, j) -= (f * e[k] + g * d[k]);
+                d[j] = at(i - 1, j);
+                at(i, j) = 0.0;
+            }
+        }
+        d[i] = h;
+    }
+    // Accumulate the orthogonal transformation.
+    for (int i = 0; i < n - 1; ++i) {
+        at(n - 1, i) = at(i, i);
+        at(i, i) = 1.0;
+        double h = d[i + 1];
+        if (h != 0.0) {
+            for (int k = 0; k <= i; ++k) d[k] = at(k, i + 1) / h;
+            for (int j = 0; j <= i; ++j) {
+                double g = 0.0;
+                for (int k = 0; k <= i; ++k) g += at(k, i + 1) * at(k, j);
+                for (int k = 0; k <= i; ++k) at(k, j) -= g * d[k];
+            }
+        }
+        for (int k = 0; k <= i; ++k) at(k, i + 1) = 0.0;
+    }
+    for (int j = 0; j < n; ++j) {
+        d[j] = at(n - 1, j);
+        at(n - 1, j) = 0.0;
+    }
+    at(n - 1, n - 1) = 1.0;
+    e[0] = 0.0;
+}
+
+// V is passed TRANSPOSED here (VT[col*n + row]) so the rotation sweeps are contiguous.
+void tridiag_ql(int n, std::vector<double>& VT, std::vector<double>& d, std::vector<double>& e) {
+    auto at = [&](int r, int c) -> double& { return VT[(size_t)c * n + r]; };
+    for (int i = 1; i < n; ++i) e[i - 1] = e[i];
+    e[n - 1] = 0.0;
+    double f = 0.0, tst1 = 0.0;
+    const double eps = std::ldexp(1.0, -52);
+    for (int l = 0; l < n; ++l) {
+        tst1 = std::max(tst1, std::fabs(d[l]) + std::fabs(e[l]));
+        int m = l;
+        while (m < n) {
+            if (std::fabs(e[m]) <= eps * tst1) break;
+            ++m;
+        }
+        if (m > l) {
+            int iter = 0;
+            do {
+                ++iter;
+                double g = d[l];
+                double p = (d[l + 1] - g) / (2.0 * e[l]);
+                double r = std::hypot(p, 1.0);
+                if (p < 0) r = -r;
+                d[l] = e[l] / (p + r);
+                d[l + 1] = e[l] * (p + r);
+                double dl1 = d[l + 1];
+                double h = g - d[l];
+                for (int i = l + 2; i < n; ++i) d[i] -= h;
+                f += h;
+                p = d[m];
+                double c = 1.0, c2 = c, c3 = c;
+                double el1 = e[l + 1];
+                double s = 0.0, s2 = 0.0;
+                for (int i = m - 1; i >= l; --i) {
+                    c3 = c2;
+                    c2 = c;
+                    s2 = s;
+                    g = c * e[i];
+                    h = c * p;
+                    r = std::hypot(p, e[i]);
+                    e[i + 1] = s * r;
+                    s = e[i] / r;
+                    c = p / r;
+                    p = c * d[i] - s * g;
+                    d[i + 1] = h + s * (c * g + s * d[i]);
+                    double* vi = &at(0, i);
+                    double* vi1 = &at(0, i + 1);
+                    for (int k = 0; k < n; ++k) {
+                        h = vi1[k];
+                        vi1[k] = s * vi[k] + c * h;
+                        vi[k] = c * vi[k] - s * h;
+                    }
+                }
+                p = -s * s2 * c3 * el1 * e[l] / dl1;
+                e[l] = s * p;
+                d[l] = c * p;
+            } while (std::fabs(e[l]) > eps * tst1 && iter < 60);
+        }
+        d[l] += f;
+        e[l] = 0.0;
+    }
+    // Ascending selection sort of values with their vectors (Eigen sorts the same way).
+    for (int i = 0; i < n - 1; ++i) {
+        int k = i;
+        double p = d[i];
+        for (int j = i + 1; j < n; ++j)
+            if (d[j] < p) {
+                k = j;
+                p = d[j];
+            }
+        if (k != i) {
+            d[k] = d[i];
+            d[i] = p;
+            for (int j = 0; j < n; ++j) std::swap(at(j, i), at(j, k));  // contiguous columns
+        }
+    }
+}
+
+// Eigen-class PartialPivLU, in place on row-major a (n x n); perm[i] = source row.
+// Zero pivots are skipped like Eigen's unblocked_lu (no division, no error).
+void lu_partial_pivot(int n, double* a, std::vector<int>& perm) {
+    perm.resize(n);
+    for (int i = 0; i < n; ++i) perm[i] = i;
+    for (int k = 0; k < n; ++k) {
+        int piv = k;
+        double best = std::fabs(a[(size_t)k * n + k]);
+        for (int i = k + 1; i < n; ++i) {
+            double v = std::fabs(a[(size_t)i * n + k]);
+            if (v > best) {
+                best = v;
+                piv = i;
+            }
+        }
+        if (best != 0.0) {
+            if (piv != k) {
+                for (int j = 0; j < n; ++j) std::swap(a[(size_t)k * n + j], a[(size_t)piv * n + j]);
+                std::swap(perm[k], perm[piv]);
+            }
+            const double pv = a[(size_t)k * n + k];
+            for (int i = k + 1; i < n; ++i) a[(size_t)i * n + k] /= pv;
+        }
+        for (int i = k + 1; i < n; ++i) {
+            const double lik = a[(size_t)i * n + k];
+            for (int j = k + 1; j < n; ++j) a[(size_t)i * n + j] -= lik * a[(size_t)k * n + j];
+        }
+    }
+}
+
+// MatrixXd::inverse() for dynamic sizes = PartialPivLU(a).solve(Identity).
+void lu_inverse(int n, const double* a_in, double* inv) {
+    std::vector<double> lu(a_in, a_in + (size_t)n * n);
+    std::vector<int> perm;
+    lu_partial_pivot(n, lu.data(), perm);
+    std::vector<double> col(n);
+    for (int c = 0; c < n; ++c) {
+        for (int i = 0; i < n; ++i) col[i] = (perm[i] == c) ? 1.0 : 0.0;
+        for (int i = 0; i < n; ++i) {  // unit lower
+            double s = col[i];
+            for (int j = 0; j < i; ++j) s -= lu[(size_t)i * n + j] * col[j];
+            col[i] = s;
+        }
+        for (int i = n - 1; i >= 0; --i) {  // upper
+            double s = col[i];
+            for (int j = i + 1; j < n; ++j) s -= lu[(size_t)i * n + j] * col[j];
+            col[i] = s / lu[(size_t)i * n + i];
+        }
+        for (int i = 0; i < n; ++i) inv[(size_t)i * n + c] = col[i];
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Symmetric eigendecomposition (lower triangle of a, row-major n x n).
+// evals ascending; evecs row-major n x n with eigenvector j in column j.
+int cfo_eigh(int n, const double* a, double* evals, double* evecs) {
+    if (n <= 0) return 0;
+    std::vector<double> V((size_t)n * n), d(n), e(n);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            const int r = std::max(i, j), c = std::min(i, j);
+            V[(size_t)i * n + j] = a[(size_t)r * n + c];
+        }
+    tridiag_householder(n, V, d, e);
+    std::vector<double> VT((size_t)n * n);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) VT[(size_t)j * n + i] = V[(size_t)i * n + j];
+    tridiag_ql(n, VT, d, e);
+    std::memcpy(evals, d.data(), sizeof(double) * n);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) evecs[(size_t)i * n + j] = VT[(size_t)j * n + i];
+    return 0;
+}
+
+int cfo_inverse(int n, const double* a, double* inv) {
+    lu_inverse(n, a, inv);
+    return 0;
+}
+
+// a2-a4: compute_eigens (precompute_local_threads.cpp:100-194).
+//   Wu     : k x k row-major directed weights, Wu[i*k+j] = weights(item_i, item_j) (:118-125)
+//   faithful: 1 = perform the reference's dense LU inverse of D and the two dense
+//             GEMMs (:149-155); 0 = the algebraically identical O(k^2) form.
+//             Both give bit-identical L2 (checked by tests).
+//   L2_out : optional k x k row-major normalized Laplacian (full, unsymmetrised)
+//   sigs   : k values, sigs[i] = (double)sig_min_i + 0.01 (:172-177)
+//   evals  : k slots; first m written (ascending), rest zero
+//   evecs  : k*k slots; first k*m written row-major (k rows, m columns) (:205-209)
+// Returns m (= lim, >= 2).  For k == 1 the reference pads with uninitialised
+// memory (:193-194); the oracle pads with 0.
+int cfo_compute_eigens(int k, const double* Wu, int faithful, double* L2_out, double* sigs,
+                       double* evals, double* evecs) {
+    if (k <= 0) return 0;
+    const size_t kk = (size_t)k * k;
+    std::vector<double> L(kk), L2(kk), dvec(k);
+    // D with the 0 -> 1 rule (:129-141)
+    for (int i = 0; i < k; ++i) {
+        double count = 0;
+        for (int j = 0; j < k; ++j) count += Wu[(size_t)i * k + j];
+        dvec[i] = (count == 0) ? 1.0 : count;
+    }
+    // L = D - W (:144-145)
+    for (int i = 0; i < k; ++i)
+        for (int j = 0; j < k; ++j)
+            L[(size_t)i * k + j] = (i == j ? dvec[i] : 0.0) - Wu[(size_t)i * k + j];
+    if (faithful) {
+        // dd2 = sqrt(inverse(D)) elementwise, L2 = dd2 * L * dd2 (:148-155)
+        std::vector<double> D(kk, 0.0), Di(kk), T(kk);
+        for (int i = 0; i < k; ++i) D[(size_t)i * k + i] = dvec[i];
+        lu_inverse(k, D.data(), Di.data());
+        for (size_t t = 0; t < kk; ++t) Di[t] = std::sqrt(Di[t]);
+        for (int i = 0; i < k; ++i)
+            for (int j = 0; j < k; ++j) {
+                double s = 0;
+                for (int q = 0; q < k; ++q) s += Di[(size_t)i * k + q] * L[(size_t)q * k + j];
+                T[(size_t)i * k + j] = s;
+            }
+        for (int i = 0; i < k; ++i)
+            for (int j = 0; j < k; ++j) {
+                double s = 0;
+                for (int q = 0; q < k; ++q) s += T[(size_t)i * k + q] * Di[(size_t)q * k + j];
+                L2[(size_t)i * k + j] = s;
+            }
+    } else {
+        std::vector<double> sv(k);
+        for (int i = 0; i < k; ++i) sv[i] = std::sqrt(1.0 / dvec[i]);
+        for (int i = 0; i < k; ++i)
+            for (int j = 0; j < k; ++j)
+                L2[(size_t)i * k + j] = (sv[i] * L[(size_t)i * k + j]) * sv[j];
+    }
+    if (L2_out) std::memcpy(L2_out, L2.data(), sizeof(double) * kk);
+
+    std::vector<double> ev(k), V(kk);
+    cfo_eigh(k, L2.data(), ev.data(), V.data());  // (:164-166), lower triangle
+
+    // sig_min per row, accumulated in float (:169-182)
+    float sig_min_max = 0;
+    for (int i = 0; i < k; ++i) {
+        float sig_min = 0;
+        for (int j = 0; j < k; ++j) sig_min += std::pow(L2[(size_t)i * k + j], 2);
+        sig_min = std::sqrt(sig_min);  // float overload
+        sigs[i] = sig_min + 0.01;
+        if (sig_min_max < sig_min) sig_min_max = sig_min;
+    }
+    sig_min_max += 0.01;
+
+    // lim (:185-191)
+    int lim;
+    for (lim = 0; lim < k; ++lim)
+        if (ev[lim] > sig_min_max) break;
+    if (lim < 2) lim = 2;
+
+    for (int j = 0; j < k; ++j) evals[j] = 0.0;
+    for (size_t t = 0; t < kk; ++t) evecs[t] = 0.0;
+    for (int j = 0; j < lim && j < k; ++j) evals[j] = ev[j];
+    for (int i = 0; i < k; ++i)
+        for (int j = 0; j < lim; ++j)
+            evecs[(size_t)i * lim + j] = (j < k) ? V[(size_t)i * k + j] : 0.0;
+    return lim;
+}
+
+// Batched precompute_local_threads (precompute_local_threads.cpp:215-317) over a
+// dense float item-weight matrix W (n_items x n_items, row-major, directed).
+//   item_off[n_users+1], items[] : per-user item indices into W (any order; the
+//                                  rows of the user's block follow this order)
+//   evec_off[n_users]            : offset of each user's k*k evec slot
+//   outputs: m_out[u], sigs/evals at item_off[u], evecs at evec_off[u] (k x m row-major)
+// n_threads = std::thread pool size (the reference's boost::threadpool, :300-314).
+int cfo_precompute_batch(int n_users, const int64_t* item_off, const int32_t* items,
+                         int64_t n_items, const float* W, const int64_t* evec_off,
+                         int n_threads, int faithful, int32_t* m_out, double* sigs,
+                         double* evals, double* evecs) {
+    std::atomic<int> next(0);
+    auto worker = [&]() {
+        std::vector<double> Wu;
+        for (;;) {
+            const int u = next.fetch_add(1);
+            if (u >= n_users) break;
+            const int64_t b = item_off[u];
+            const int k = (int)(item_off[u + 1] - b);
+            if (k <= 0) {
+                m_out[u] = 0;
+                continue;
+            }
+            Wu.assign((size_t)k * k, 0.0);
+            for (int i = 0; i < k; ++i) {
+                const float* row = W + (size_t)items[b + i] * n_items;
+                for (int j = 0; j < k; ++j) Wu[(size_t)i * k + j] = (double)row[items[b + j]];
+            }
+            m_out[u] = cfo_compute_eigens(k, Wu.data(), faithful, nullptr, sigs + b, evals + b,
+                                          evecs + evec_off[u]);
+        }
+    };
+    if (n_threads <= 1) {
+        worker();
+    } else {
+        std::vector<std::thread> pool;
+        for (int t = 0; t < n_threads; ++t) pool.emplace_back(worker);
+        for (auto& t : pool) t.join();
+    }
+    return 0;
+}
+
+// a7: neigh_program::apply inner loop for ONE user (local_calc_precomp.cpp:230-360),
+// evaluated for every one of the user's k test movies (rows).
+//   k, m          : user's item count and stored eigenpair count
+//   items[k]      : the user's items as indices into W (row order of the eigen block)
+//   ratings[k]    : the user's test ratings of those items (out_test_rat_)
+//   evals[m], U   : eigenvalues and k x m row-major eigenvectors (out_eigen_)
+//   sigtab[k]     : w_lim per row: the concatenated-sigs table in compat mode
+//                   (:414,437,440,271), or the user's own sigs in fixed mode
+//   W, n_items    : dense float out_fin_ weights; neighbour iff (double)w > 0.1 (:129-133)
+//   rows[n_rows]  : which rows (test movies) to evaluate
+// Outputs per evaluated row: mse (float, :358), kk (= c, :359), pred (clamped, double),
+// cond-flag bit 0 = Gram matrix had a zero pivot.
+int cfo_predict_user(int k, int m, const int32_t* items, const double* ratings,
+                     const double* evals, const double* U, const double* sigtab,
+                     const float* W, int64_t n_items, int n_rows, const int32_t* rows,
+                     float* mse_out, int32_t* kk_out, double* pred_out) {
+    std::vector<int> C;
+    std::vector<int> keep;
+    for (int t = 0; t < n_rows; ++t) {
+        const int r = rows[t];
+        const double rat_real = ratings[r];
+        const float* nrow = W + (size_t)items[r] * n_items;
+        // connected movies in the user's row order (:254-265)
+        C.clear();
+        for (int j = 0; j < k; ++j)
+            if ((double)nrow[items[j]] > 0.1) C.push_back(j);
+        const int c = (int)C.size();
+        // lim from w_lim (:271-279)
+        const double w_lim = sigtab[r];
+        int lim;
+        for (lim = 0; lim < m; ++lim)
+            if (evals[lim] > w_lim) break;
+        if (lim < 2) lim = 2;
+        if (lim > m) lim = m;  // unreachable for m >= 2 (reference would read past the block)
+        // zero-column filter (:284-304)
+        keep.clear();
+        for (int col = 0; col < lim; ++col) {
+            int i;
+            for (i = 0; i < c; ++i)
+                if (U[(size_t)C[i] * m + col] >= 0.0001) break;
+            if (i < c) keep.push_back(col);
+        }
+        const int Lc = (int)keep.size();
+        // rating mean and centred ratings (:311-312)
+        double sum = 0;
+        for (int i = 0; i < c; ++i) sum += ratings[C[i]];
+        const double rat_mean = sum / c;
+        // t = Uh^T (r - mean); mm = Uh^T Uh; x = inverse(mm) t; pred = vv . x + mean (:308-315)
+        std::vector<double> tv(Lc, 0.0), mm((size_t)Lc * Lc, 0.0), inv((size_t)Lc * Lc), x(Lc, 0.0);
+        for (int a = 0; a < Lc; ++a) {
+            double s = 0;
+            for (int i = 0; i < c; ++i) s += U[(size_t)C[i] * m + keep[a]] * (ratings[C[i]] - rat_mean);
+            tv[a] = s;
+            for (int b2 = 0; b2 < Lc; ++b2) {
+                double g = 0;
+                for (int i = 0; i < c; ++i)
+                    g += U[(size_t)C[i] * m + keep[a]] * U[(size_t)C[i] * m + keep[b2]];
+                mm[(size_t)a * Lc + b2] = g;
+            }
+        }
+        if (Lc > 0) lu_inverse(Lc, mm.data(), inv.data());
+        for (int a = 0; a < Lc; ++a) {
+            double s = 0;
+            for (int b2 = 0; b2 < Lc; ++b2) s += inv[(size_t)a * Lc + b2] * tv[b2];
+            x[a] = s;
+        }
+        double pred = 0;
+        for (int a = 0; a < Lc; ++a) pred += U[(size_t)r * m + keep[a]] * x[a];
+        pred += rat_mean;
+        if (pred > 5) pred = 5;  // (:322-325)
+        if (pred < 1) pred = 1;
+        const double err = std::pow(rat_real - pred, 2);
+        mse_out[t] = (float)err;
+        kk_out[t] = c;
+        if (pred_out) pred_out[t] = pred;
+    }
+    return 0;
+}
+
+}  // extern "C"

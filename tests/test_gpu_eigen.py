@@ -1,0 +1,85 @@
+"""GPU parity: cf_eigen_batch (HIP one-sided Jacobi) vs the CPU oracle's compute_eigens.
+
+Tolerances: eigenvalues abs <= 1e-5, sigs rel <= 1e-5, m exact
+unless an eigenvalue sits within tolerance of the cut, clustered projectors
+||P_gpu - P_ref||_F <= 1e-3, residual and orthonormality <= 1e-4.
+"""
+import numpy as np
+import pytest
+
+import cases
+import oracle_ref as orc
+
+pytestmark = pytest.mark.gpu
+
+KS = [1, 2, 3, 5, 8, 15, 16, 17, 31, 32, 33, 47, 64, 65, 100, 127, 128, 129, 150, 180, 191, 192]
+
+
+def _check_batch(ctx, W, item_off, items, label):
+    ctx.upload_graph_dense(W)
+    res = ctx.eigen_batch(item_off, items)
+    bad = []
+    for u in range(len(item_off) - 1):
+        b, e = int(item_off[u]), int(item_off[u + 1])
+        it = items[b:e].astype(np.int64)
+        Wu = W[np.ix_(it, it)].astype(np.float64)
+        m_ref, sig_ref, _, U_ref, L2 = orc.compute_eigens(Wu)
+        ev_full, V_full = orc.eigh(orc.sym_lower(L2))
+        sig_g, ev_g, U_g = res.block(u)
+        k = e - b
+        if np.max(np.abs(sig_g - sig_ref) / np.abs(sig_ref)) > 1e-5:
+            bad.append((label, u, k, "sigs"))
+        smm = np.float32(np.float32(np.max(sig_ref - 0.01)) + 0.01)
+        near_cut = np.any(np.abs(ev_full - smm) <= 1e-5)
+        if int(res.m[u]) != m_ref and not near_cut:
+            bad.append((label, u, k, f"m {res.m[u]} != {m_ref}"))
+            continue
+        if int(res.m[u]) != m_ref:
+            continue
+        if k == 1:
+            assert np.allclose(U_g, [[1.0, 0.0]]) and abs(ev_g[0] - 1.0) < 1e-6 and ev_g[1] == 0
+            continue
+        f = orc.compare_eigen_block(L2, m_ref, ev_full, V_full[:, :m_ref], int(res.m[u]), ev_g, U_g)
+        if f:
+            bad.append((label, u, k, f))
+    assert not bad, bad
+
+
+def test_eigen_bucket_edges_dense(gpu_ctx):
+    W = cases.item_graph(260, 0.9, seed=11)
+    off, items = cases.user_items(260, KS, seed=12)
+    _check_batch(gpu_ctx, W, off, items, "dense")
+
+
+def test_eigen_sparse_disconnected(gpu_ctx):
+    # sparse graph: many components (lambda = 0 multiplicities) and isolated items (lambda = 1)
+    W = cases.item_graph(260, 0.02, seed=21, isolated_frac=0.2)
+    off, items = cases.user_items(260, KS, seed=22)
+    _check_batch(gpu_ctx, W, off, items, "sparse")
+
+
+def test_eigen_many_users_random_order(gpu_ctx):
+    rng = np.random.default_rng(31)
+    ks = rng.integers(1, 193, size=300)
+    W = cases.item_graph(300, 0.3, seed=32)
+    off, items = cases.user_items(300, ks, seed=33)
+    _check_batch(gpu_ctx, W, off, items, "mixed")
+
+
+def test_eigen_closed_form_spectra(gpu_ctx):
+    """Complete graph K_n: {0, n/(n-1) x (n-1)}; star S_n: {0, 1 x (n-2), 2}."""
+    n_items = 200
+    W = np.zeros((n_items, n_items), dtype=np.float32)
+    W[:100, :100] = 1.0          # K_100 on items 0..99
+    W[100:150, 100] = 1.0        # star centred on item 100 with 49 leaves
+    W[100, 100:150] = 1.0
+    np.fill_diagonal(W, 0.0)
+    gpu_ctx.upload_graph_dense(W)
+    off = np.array([0, 100, 150], dtype=np.uint64)
+    items = np.concatenate([np.arange(100), np.arange(100, 150)]).astype(np.uint32)
+    res = gpu_ctx.eigen_batch(off, items)
+    _, ev, _ = res.block(0)
+    assert abs(ev[0]) < 1e-5 and np.all(np.abs(ev[1:] - 100 / 99) < 1e-5) and res.m[0] == 100
+    _, ev, _ = res.block(1)
+    exp = np.array([0.0] + [1.0] * 48 + [2.0])
+    assert np.all(np.abs(ev - exp[: len(ev)]) < 1e-5)
