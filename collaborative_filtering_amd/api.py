@@ -87,6 +87,16 @@ class Context:
     def set_jacobi(self, tol_scale: float = 1.0, max_sweeps: int = 30):
         self._chk(self.lib.cf_set_jacobi(self.h, tol_scale, max_sweeps), "cf_set_jacobi")
 
+    def debug_stats(self, enable: bool = True, read: bool = False):
+        """Jacobi diagnostics: returns {sweeps_mean, users, sweeps_max, capped} when read."""
+        out = np.zeros(4, dtype=np.uint64) if read else None
+        self._chk(self.lib.cf_debug_stats(self.h, int(enable), ptr(out)), "cf_debug_stats")
+        if read:
+            n = max(int(out[1]), 1)
+            return {"sweeps_mean": int(out[0]) / n, "users": int(out[1]), "sweeps_max": int(out[2]),
+                    "capped": int(out[3])}
+        return None
+
     # -- item graph (out_fin_) ---------------------------------------------------
     def upload_graph_dense(self, W):
         """W: n_items x n_items float32 (numpy, or torch CUDA tensor)."""

@@ -97,7 +97,28 @@ void cf_destroy(cf_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->d_graph) (void)hipFree(ctx->d_graph);
+    if (ctx->d_stats) (void)hipFree(ctx->d_stats);
     delete ctx;
+}
+
+int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out4) {
+    if (!ctx) return CF_EINVAL;
+    CF_TRY(set_device(ctx));
+    if (enable && !ctx->d_stats) {
+        if (hipMalloc(&ctx->d_stats, 4 * sizeof(unsigned long long)) != hipSuccess)
+            return cf_set_error(ctx, CF_ENOMEM, "stats allocation");
+        CF_HIP_CHECK(ctx, hipMemset(ctx->d_stats, 0, 4 * sizeof(unsigned long long)));
+    }
+    if (out4 && ctx->d_stats) {
+        CF_HIP_CHECK(ctx, hipDeviceSynchronize());
+        CF_HIP_CHECK(ctx, hipMemcpy(out4, ctx->d_stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        CF_HIP_CHECK(ctx, hipMemset(ctx->d_stats, 0, 4 * sizeof(unsigned long long)));
+    }
+    if (!enable && ctx->d_stats) {
+        (void)hipFree(ctx->d_stats);
+        ctx->d_stats = nullptr;
+    }
+    return CF_OK;
 }
 
 const char* cf_last_error(const cf_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }

@@ -13,8 +13,9 @@
 //      its singular values are its eigenvalues and the rotated columns of B are the
 //      eigenvectors scaled by (lambda + 1);
 //   4. one-sided (Hestenes) Jacobi sweeps in LDS: each step of a round-robin
-//      tournament rotates k/2 disjoint column pairs; a pair is owned by one DPP row
-//      (16 lanes), whose three dot products are reduced with DPP row ops;
+//      tournament rotates k/2 disjoint column pairs; a pair is owned by one DPP quad
+//      (4 lanes, float2 = ds_read_b64 per row pair, packed v_pk_fma_f32), whose three
+//      dot products are reduced with two DPP quad_perm steps;
 //   5. lambda_j = ||b_j|| / ||v_j|| - 1 (||v_j|| tracks the fp32 rotation drift),
 //      rank sort ascending, lim (:184-191), write the k x m row-major block, sigs,
 //      evals and m.
@@ -25,21 +26,19 @@
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kGroup = 16;                   // lanes per column pair = one DPP row
-constexpr int kGroups = kThreads / kGroup;   // column pairs in flight per workgroup
+constexpr int kGroup = 4;   // lanes per column pair = one DPP quad
+
+using f2 = __attribute__((ext_vector_type(2))) float;
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float x) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
 }
 
-// All-reduce (sum) over the 16 lanes of a DPP row; every lane receives the total.
-__device__ __forceinline__ float row16_sum(float x) {
+// All-reduce (sum) over the 4 lanes of a DPP quad; every lane receives the total.
+__device__ __forceinline__ float quad_sum(float x) {
     x += dpp_mov<0xB1>(x);   // quad_perm [1,0,3,2]
     x += dpp_mov<0x4E>(x);   // quad_perm [2,3,0,1]
-    x += dpp_mov<0x141>(x);  // row_half_mirror
-    x += dpp_mov<0x140>(x);  // row_mirror
     return x;
 }
 
@@ -57,12 +56,20 @@ struct EigenArgs {
     float* evecs;
     float tol_scale;
     int max_sweeps;
+    unsigned long long* stats;
 };
 
+// Bucket geometry: k <= NR = 16 * EMAX rows.  A column is read/written as float2
+// (ds_read_b64 / ds_write_b64): lane l of a quad owns rows 8t + 2l, 8t + 2l + 1.
+// LD == 8 (mod 64) floats: the 8 consecutive columns that the 8 quads of a half-wave
+// touch in one tournament step start in distinct 8-bank octants, so the b64 accesses
+// are conflict-free (MI355X_MICROARCH.md, LDS table: b64 bank = (a/4) mod 64).
 template <int EMAX>
-struct EigenLds {
-    static constexpr int NR = kGroup * EMAX;  // padded row count (>= k)
-    static constexpr int LD = NR + 1;         // odd: column-parallel LDS access is conflict-free
+struct EigenGeom {
+    static constexpr int NR = 16 * EMAX;
+    static constexpr int E2 = NR / 8;                          // float2 chunks per lane
+    static constexpr int LD = NR + ((8 - NR) % 64 + 64) % 64;  // >= NR, == 8 mod 64
+    static constexpr int NT = (NR > 128) ? 512 : 256;          // 1 pass per step up to NT/4 pairs
     static constexpr size_t bytes() {
         return sizeof(float) * (size_t)NR * LD     // B
                + sizeof(uint32_t) * NR             // items
@@ -73,10 +80,13 @@ struct EigenLds {
 };
 
 template <int EMAX>
-__global__ __launch_bounds__(kThreads) void eigen_kernel(EigenArgs a) {
-    using Lds = EigenLds<EMAX>;
-    constexpr int NR = Lds::NR;
-    constexpr int LD = Lds::LD;
+__global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a) {
+    using G = EigenGeom<EMAX>;
+    constexpr int NR = G::NR;
+    constexpr int LD = G::LD;
+    constexpr int E2 = G::E2;
+    constexpr int NT = G::NT;
+    constexpr int NG = NT / kGroup;
     extern __shared__ float smem[];
     float* B = smem;
     uint32_t* s_item = reinterpret_cast<uint32_t*>(B + (size_t)NR * LD);
@@ -91,6 +101,7 @@ __global__ __launch_bounds__(kThreads) void eigen_kernel(EigenArgs a) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
+    constexpr int NW = NT / 64;
     const uint32_t u = a.order[a.first + blockIdx.x];
     const uint64_t base = a.item_off[u];
     const int k = (int)(a.item_off[u + 1] - base);
@@ -100,17 +111,17 @@ __global__ __launch_bounds__(kThreads) void eigen_kernel(EigenArgs a) {
     }
 
     // ---- 1. gather W_u (column-major, B[j*LD + i] = W(i,j)) ----------------------
-    for (int i = tid; i < k; i += kThreads) s_item[i] = a.items[base + i];
-    for (int idx = tid; idx < NR * LD; idx += kThreads) B[idx] = 0.0f;
+    for (int i = tid; i < k; i += NT) s_item[i] = a.items[base + i];
+    for (int idx = tid; idx < NR * LD; idx += NT) B[idx] = 0.0f;
     __syncthreads();
-    for (int i = wave; i < k; i += kThreads / 64) {
+    for (int i = wave; i < k; i += NW) {
         const float* row = a.graph + (size_t)s_item[i] * a.n_items;
         for (int j = lane; j < k; j += 64) B[j * LD + i] = row[s_item[j]];
     }
     __syncthreads();
 
     // ---- 2. degrees, D^-1/2, diagonal of L2, sig_min -------------------------------
-    for (int i = tid; i < k; i += kThreads) {
+    for (int i = tid; i < k; i += NT) {
         double d = 0.0;
         for (int j = 0; j < k; ++j) d += (double)B[j * LD + i];
         if (d == 0.0) d = 1.0;                      // (:137-140)
@@ -119,7 +130,7 @@ __global__ __launch_bounds__(kThreads) void eigen_kernel(EigenArgs a) {
         s_l2d[i] = (float)((s * (d - (double)B[i * LD + i])) * s);
     }
     __syncthreads();
-    for (int i = tid; i < k; i += kThreads) {
+    for (int i = tid; i < k; i += NT) {
         const float si = s_s[i];
         float acc = 0.0f;
         for (int j = 0; j < k; ++j) {
@@ -131,7 +142,7 @@ __global__ __launch_bounds__(kThreads) void eigen_kernel(EigenArgs a) {
     __syncthreads();
 
     // ---- 3. B = sym_lower(L2) + I, in place ------------------------------------------
-    for (int i = wave; i < k; i += kThreads / 64) {
+    for (int i = wave; i < k; i += NW) {
         const float si = s_s[i];
         for (int j = lane; j < i; j += 64) {
             const float v = -(si * B[j * LD + i]) * s_s[j];
@@ -140,7 +151,7 @@ __global__ __launch_bounds__(kThreads) void eigen_kernel(EigenArgs a) {
         }
         if (lane == 0) B[i * LD + i] = s_l2d[i] + 1.0f;
     }
-    for (int i = tid; i < k; i += kThreads) s_dev[i] = 0.0f;
+    for (int i = tid; i < k; i += NT) s_dev[i] = 0.0f;
     if (tid == 0) s_flag[0] = 0;
     __syncthreads();
 
@@ -150,46 +161,54 @@ __global__ __launch_bounds__(kThreads) void eigen_kernel(EigenArgs a) {
     const int g = tid / kGroup;
     const int lig = tid % kGroup;
     const float tol = a.tol_scale * sqrtf((float)k) * 2.384185791015625e-07f;  // sqrt(k) * 2^-22
-    for (int sweep = 0; sweep < a.max_sweeps && k > 1; ++sweep) {
+    const float tol2 = tol * tol;
+    int sweep = 0;
+    for (; sweep < a.max_sweeps && k > 1; ++sweep) {
         for (int step = 0; step < n - 1; ++step) {
-            for (int pi = g; pi < npairs; pi += kGroups) {
+            for (int pi = g; pi < npairs; pi += NG) {
                 int p, q;
                 if (pi == 0) {
                     p = n - 1;
                     q = step;
                 } else {
-                    p = (step + pi) % (n - 1);
-                    q = (step - pi + n - 1) % (n - 1);
+                    p = step + pi;
+                    if (p >= n - 1) p -= n - 1;
+                    q = step - pi;
+                    if (q < 0) q += n - 1;
                 }
                 if (p >= k || q >= k) continue;
-                float* bp = B + p * LD + lig;
-                float* bq = B + q * LD + lig;
-                float xp[EMAX], xq[EMAX];
-                float al = 0.f, be = 0.f, ga = 0.f;
+                f2* bp = reinterpret_cast<f2*>(B + p * LD) + lig;
+                f2* bq = reinterpret_cast<f2*>(B + q * LD) + lig;
+                f2 xp[E2], xq[E2];
+                f2 al2 = {0.f, 0.f}, be2 = {0.f, 0.f}, ga2 = {0.f, 0.f};
 #pragma unroll
-                for (int t = 0; t < EMAX; ++t) {
+                for (int t = 0; t < E2; ++t) {
                     xp[t] = bp[kGroup * t];
                     xq[t] = bq[kGroup * t];
-                    al = fmaf(xp[t], xp[t], al);
-                    be = fmaf(xq[t], xq[t], be);
-                    ga = fmaf(xp[t], xq[t], ga);
+                    al2 = __builtin_elementwise_fma(xp[t], xp[t], al2);
+                    be2 = __builtin_elementwise_fma(xq[t], xq[t], be2);
+                    ga2 = __builtin_elementwise_fma(xp[t], xq[t], ga2);
                 }
-                al = row16_sum(al);
-                be = row16_sum(be);
-                ga = row16_sum(ga);
-                if (fabsf(ga) > tol * sqrtf(al * be)) {
-                    const float zeta = (be - al) / (2.0f * ga);
-                    const float t = copysignf(1.0f, zeta) / (fabsf(zeta) + sqrtf(1.0f + zeta * zeta));
-                    const float c = 1.0f / sqrtf(1.0f + t * t);
+                const float al = quad_sum(al2.x + al2.y);
+                const float be = quad_sum(be2.x + be2.y);
+                const float ga = quad_sum(ga2.x + ga2.y);
+                if (ga * ga > tol2 * (al * be)) {
+                    // Hardware rcp/rsq/sqrt: the rotation only has to annihilate ga well
+                    // enough; its scale error (c^2 + s^2 != 1) is tracked exactly below.
+                    const float zeta = (be - al) * __builtin_amdgcn_rcpf(2.0f * ga);
+                    const float az = fabsf(zeta);
+                    const float t = copysignf(__builtin_amdgcn_rcpf(az + __builtin_amdgcn_sqrtf(fmaf(az, az, 1.0f))),
+                                              zeta);
+                    const float c = __builtin_amdgcn_rsqf(fmaf(t, t, 1.0f));
                     const float s = c * t;
+                    const f2 c2 = {c, c}, s2 = {s, s}, ns2 = {-s, -s};
 #pragma unroll
-                    for (int e = 0; e < EMAX; ++e) {
-                        bp[kGroup * e] = c * xp[e] - s * xq[e];
-                        bq[kGroup * e] = s * xp[e] + c * xq[e];
+                    for (int e = 0; e < E2; ++e) {
+                        bp[kGroup * e] = __builtin_elementwise_fma(ns2, xq[e], c2 * xp[e]);
+                        bq[kGroup * e] = __builtin_elementwise_fma(s2, xp[e], c2 * xq[e]);
                     }
-                    // fp32 (c, s) are not exactly orthonormal: c^2 + s^2 = 1 + delta.
-                    // Track each column's accumulated scale so lambda is not biased by
-                    // ~k * sweeps * delta (2.4e-5 at k = 128 without this).
+                    // c^2 + s^2 = 1 + delta: track each column's accumulated scale so
+                    // lambda = ||b_j|| / ||v_j|| - 1 carries no rotation drift.
                     const float delta = fmaf(s, s, fmaf(c, c, -1.0f));
                     const float dp = s_dev[p], dq = s_dev[q];
                     const float cc = c * c, ss = s * s;
@@ -208,10 +227,16 @@ __global__ __launch_bounds__(kThreads) void eigen_kernel(EigenArgs a) {
         if (tid == 0) s_flag[0] = 0;
         __syncthreads();
     }
+    if (a.stats && tid == 0) {
+        atomicAdd(&a.stats[0], (unsigned long long)(sweep + 1));
+        atomicAdd(&a.stats[1], 1ull);
+        atomicMax(&a.stats[2], (unsigned long long)(sweep + 1));
+        if (sweep >= a.max_sweeps) atomicAdd(&a.stats[3], 1ull);
+    }
 
     // ---- 5. eigenvalues, ordering, lim, output ----------------------------------------
     // ||b_j|| accumulated in fp64: a k-term fp32 sum would cost ~k ulps (3e-5 at k=192).
-    for (int j = tid; j < k; j += kThreads) {
+    for (int j = tid; j < k; j += NT) {
         double acc = 0.0;
         for (int i = 0; i < k; ++i) {
             const double v = (double)B[j * LD + i];
@@ -222,7 +247,7 @@ __global__ __launch_bounds__(kThreads) void eigen_kernel(EigenArgs a) {
         s_s[j] = (float)(1.0 / nrm);                             // unit-normalises v_j
     }
     __syncthreads();
-    for (int j = tid; j < k; j += kThreads) {
+    for (int j = tid; j < k; j += NT) {
         const float mj = s_mu[j];
         int rank = 0;
         for (int i = 0; i < k; ++i) {
@@ -246,10 +271,10 @@ __global__ __launch_bounds__(kThreads) void eigen_kernel(EigenArgs a) {
     }
     __syncthreads();
     const int m = s_flag[1];
-    for (int i = tid; i < k; i += kThreads) a.sigs[base + i] = (float)((double)s_sig[i] + 0.01);
-    for (int r = tid; r < m && r < k; r += kThreads) a.evals[base + r] = s_mu[s_perm[r]] - 1.0f;
+    for (int i = tid; i < k; i += NT) a.sigs[base + i] = (float)((double)s_sig[i] + 0.01);
+    for (int r = tid; r < m && r < k; r += NT) a.evals[base + r] = s_mu[s_perm[r]] - 1.0f;
     float* out = a.evecs + a.evec_off[u];
-    for (int idx = tid; idx < k * m; idx += kThreads) {
+    for (int idx = tid; idx < k * m; idx += NT) {
         const int i = idx / m;
         const int r = idx - i * m;
         float v = 0.0f;
@@ -263,14 +288,15 @@ __global__ __launch_bounds__(kThreads) void eigen_kernel(EigenArgs a) {
 
 template <int EMAX>
 int launch_bucket(cf_ctx* ctx, const EigenArgs& args, uint32_t count, hipStream_t stream) {
-    const size_t lds = EigenLds<EMAX>::bytes();
+    const size_t lds = EigenGeom<EMAX>::bytes();
+    static_assert(EigenGeom<EMAX>::bytes() <= 163840, "eigen bucket exceeds 160 KiB LDS");
     static bool configured = false;
     if (!configured) {
         CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_kernel<EMAX>,
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         configured = true;
     }
-    hipLaunchKernelGGL(eigen_kernel<EMAX>, dim3(count), dim3(kThreads), lds, stream, args);
+    hipLaunchKernelGGL(eigen_kernel<EMAX>, dim3(count), dim3(EigenGeom<EMAX>::NT), lds, stream, args);
     CF_HIP_CHECK(ctx, hipGetLastError());
     return CF_OK;
 }
@@ -293,6 +319,7 @@ int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off
     args.evecs = d_evecs;
     args.tol_scale = ctx->tol_scale;
     args.max_sweeps = ctx->max_sweeps;
+    args.stats = ctx->d_stats;
     for (const cf_bucket& b : plan->buckets) {
         if (b.count == 0) continue;
         args.first = b.first;

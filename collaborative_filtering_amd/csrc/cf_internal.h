@@ -18,6 +18,8 @@ struct cf_ctx {
     // Jacobi controls
     float tol_scale = 1.0f;
     int max_sweeps = 30;
+    // Optional device counters: [0] sum of sweeps, [1] users, [2] max sweeps, [3] capped users.
+    unsigned long long* d_stats = nullptr;
 };
 
 // One launch of the eigen / predict kernels covers the users of one k-bucket.

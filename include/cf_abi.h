@@ -56,6 +56,10 @@ void cf_destroy(cf_ctx* ctx);
 const char* cf_last_error(const cf_ctx* ctx);
 /* Jacobi off-diagonal tolerance scale (default 1.0) and sweep cap (default 30). */
 int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
+/* Diagnostics: enable != 0 allocates device counters that the eigen kernel fills;
+ * out4 (optional) receives and resets {sum of sweeps, users, max sweeps, users that
+ * hit the sweep cap}.  enable == 0 frees them. */
+int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out4);
 
 /* ---- item graph (out_fin_) ---------------------------------------------------
  * Directed weighted graph exactly as parsed: w(a,b) and w(b,a) are independent.
