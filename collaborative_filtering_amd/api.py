@@ -97,6 +97,14 @@ class Context:
                     "capped": int(out[3])}
         return None
 
+    def debug_phases(self, enable: bool = True, read: bool = False):
+        """Predictor phase cycles {conn, lim+filter, mean, gram, lu, solve} when read."""
+        out = np.zeros(6, dtype=np.uint64) if read else None
+        self._chk(self.lib.cf_debug_phases(self.h, int(enable), ptr(out)), "cf_debug_phases")
+        if read:
+            return dict(zip(["conn", "lim_filter", "mean", "gram", "lu", "solve"], map(int, out)))
+        return None
+
     # -- item graph (out_fin_) ---------------------------------------------------
     def upload_graph_dense(self, W):
         """W: n_items x n_items float32 (numpy, or torch CUDA tensor)."""

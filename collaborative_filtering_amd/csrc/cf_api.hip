@@ -98,7 +98,29 @@ void cf_destroy(cf_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->d_graph) (void)hipFree(ctx->d_graph);
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
+    if (ctx->d_phase) (void)hipFree(ctx->d_phase);
+    if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     delete ctx;
+}
+
+int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out6) {
+    if (!ctx) return CF_EINVAL;
+    CF_TRY(set_device(ctx));
+    if (enable && !ctx->d_phase) {
+        if (hipMalloc(&ctx->d_phase, 6 * sizeof(unsigned long long)) != hipSuccess)
+            return cf_set_error(ctx, CF_ENOMEM, "phase counters");
+        CF_HIP_CHECK(ctx, hipMemset(ctx->d_phase, 0, 6 * sizeof(unsigned long long)));
+    }
+    if (out6 && ctx->d_phase) {
+        CF_HIP_CHECK(ctx, hipDeviceSynchronize());
+        CF_HIP_CHECK(ctx, hipMemcpy(out6, ctx->d_phase, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        CF_HIP_CHECK(ctx, hipMemset(ctx->d_phase, 0, 6 * sizeof(unsigned long long)));
+    }
+    if (!enable && ctx->d_phase) {
+        (void)hipFree(ctx->d_phase);
+        ctx->d_phase = nullptr;
+    }
+    return CF_OK;
 }
 
 int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out4) {

@@ -12,16 +12,20 @@
 //   pred = v_S . (U_CS^T U_CS)^-1 U_CS^T (r_C - mean) + mean          (:308-315)
 //   mse  = (float)(r - clamp(pred, 1, 5))^2, kk = |C|                 (:318-359)
 //
-// All arithmetic after the gather is fp64 (the reference's double path), the Gram
-// matrix lives in LDS and is solved by LU with partial pivoting (Eigen's
-// PartialPivLU class) followed by one wave's back substitution.
+// All arithmetic after the gather is fp64 (the reference's double path).  The
+// reference forms mm = U_CS^T U_CS and multiplies by its PartialPivLU inverse.  Here
+// the Gram matrix (SPD whenever the prediction is well-posed) is factored by a
+// blocked Cholesky in packed LDS storage, bordered by t^T and v^T so the
+// factorisation itself yields y = L^-1 t and z = L^-1 v and pred = y.z + mean
+// (v^T M^-1 t = (L^-1 v)^T (L^-1 t)).  For SPD M this agrees with the inverse-based
+// formula to cond(M) * eps; a rank-deficient M (c < L) is ill-posed in the reference
+// too, where the output is decided by rounding (NaN or a clamped 1 / 5).
 
 #include "cf_internal.h"
 
 namespace {
 
 constexpr int kThreads = 256;
-constexpr size_t kMaxLdsGram = 128u * 128u * sizeof(double);
 
 template <typename T>
 struct PredArgs {
@@ -41,9 +45,9 @@ struct PredArgs {
     float* mse;
     int32_t* kk;
     double* pred;
-    double* scratch;       // per-block Gram storage when it does not fit in LDS
+    unsigned long long* phase_cycles;  // diagnostics: per-phase s_memtime totals (or null)
     int lmax;              // Gram dimension bound of the launch
-    int gram_in_lds;
+    double* gbar;          // per-block scratch: Gbar = U^T U (lmax x lmax, full), fp64
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -69,24 +73,45 @@ __device__ int block_compact(bool flag, int idx, int* out, int* s_cnt) {
     return total;
 }
 
+// Packed lower-triangular index (row-major rows of increasing length).
+__device__ __forceinline__ int tri(int i, int j) { return (i * (i + 1)) / 2 + j; }
+
+#define WAVE_SYNC()                                              \
+    do {                                                         \
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   \
+        __builtin_amdgcn_wave_barrier();                         \
+    } while (0)
+
+constexpr int kNB = 16;   // Cholesky panel width
+
 template <typename T>
 __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32_t count) {
     extern __shared__ double dsm[];
     const int lmax = a.lmax;
-    double* M_lds = dsm;                                   // lmax*lmax (if gram_in_lds)
-    double* tv = dsm + (a.gram_in_lds ? (size_t)lmax * lmax : 0);
-    double* s_misc = tv + lmax;                            // [0] mean
+    // A: packed lower triangle of the bordered matrix [[M, .], [t^T, .], [v^T, .]],
+    //    (lmax + 2) rows; rows L and L+1 hold t and v and become y = L^-1 t, z = L^-1 v.
+    double* A = dsm;
+    double* s_misc = A + (size_t)(lmax + 2) * (lmax + 3) / 2;   // [0] mean, [1] pred sum
     uint32_t* s_item = reinterpret_cast<uint32_t*>(s_misc + 4);
     float* s_rat = reinterpret_cast<float*>(s_item + CF_MAX_K);
     int* s_conn = reinterpret_cast<int*>(s_rat + CF_MAX_K);
     int* s_keep = s_conn + CF_MAX_K;
-    int* s_rowp = s_keep + CF_MAX_K;
-    int* s_cnt = s_rowp + CF_MAX_K;                        // [0..3] compaction, [4] lim, [5] piv
-    double* M = a.gram_in_lds ? M_lds : a.scratch + (size_t)blockIdx.x * lmax * lmax;
+    int* s_nconn = s_keep + CF_MAX_K;                      // rows NOT in C (complement)
+    int* s_cnt = s_nconn + CF_MAX_K;                       // [0..3] compaction, [4] lim
+    double* Gb = a.gbar + (size_t)blockIdx.x * lmax * lmax;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
+    // Diagnostic phase stamps (thread 0 only; no effect on outputs).
+    unsigned long long ph_acc[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long ph_t = 0;
+#define PHASE_STAMP(ph)                                                   \
+    if (a.phase_cycles && tid == 0) {                                     \
+        const unsigned long long now = __builtin_amdgcn_s_memtime();      \
+        if ((ph) >= 0) ph_acc[(ph) < 0 ? 0 : (ph)] += now - ph_t;         \
+        ph_t = now;                                                       \
+    }
 
     for (uint32_t ub = blockIdx.x; ub < count; ub += gridDim.x) {
         const uint32_t u = a.order[a.first + ub];
@@ -100,30 +125,82 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
             s_item[i] = a.items[base + i];
             s_rat[i] = a.ratings[base + i];
         }
+        // Gbar = U^T U over all k rows (fp64, full m x m), once per user: a prediction
+        // whose connected set C covers most rows forms its Gram matrix as
+        // Gbar_SS - sum_{i not in C} u_i u_i^T, which is the same sum with O(eps)
+        // cancellation error instead of c * L^2 work.
+        {
+            const int nt4 = (m + 3) >> 2;
+            const int ntile = nt4 * (nt4 + 1) / 2;
+            for (int tix = tid; tix < ntile; tix += kThreads) {
+                int ta = 0, rem = tix;
+                while (rem > ta) {
+                    rem -= ta + 1;
+                    ++ta;
+                }
+                const int tb = rem;
+                double acc[4][4];
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                    for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+                const int a0 = min(4 * ta, m - 4 > 0 ? m - 4 : 0), b0 = 4 * tb;
+                for (int i = 0; i < k; ++i) {
+                    const T* row = U + (size_t)i * m;
+                    double va[4], vb[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        va[q] = (double)row[min(4 * ta + q, m - 1)];
+                        vb[q] = (double)row[min(b0 + q, m - 1)];
+                    }
+#pragma unroll
+                    for (int x = 0; x < 4; ++x)
+#pragma unroll
+                        for (int y = 0; y < 4; ++y) acc[x][y] = fma(va[x], vb[y], acc[x][y]);
+                }
+                (void)a0;
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                    for (int y = 0; y < 4; ++y) {
+                        const int ia = 4 * ta + x, ib = b0 + y;
+                        if (ia < m && ib < m && ib <= ia) {
+                            Gb[(size_t)ia * lmax + ib] = acc[x][y];
+                            Gb[(size_t)ib * lmax + ia] = acc[x][y];
+                        }
+                    }
+            }
+        }
         __syncthreads();
 
         for (int r = 0; r < k; ++r) {
-            // --- connected set C (ascending row order) ---
+            PHASE_STAMP(-1);
+            // --- connected set C: the user's items that are out-neighbours of movie r (:254-265)
             const float* nrow = a.graph + (size_t)s_item[r] * a.n_items;
             const bool conn = tid < k && (double)nrow[s_item[tid < k ? tid : 0]] > 0.1;
             const int c = block_compact(conn, tid, s_conn, s_cnt);
+            const int nc = block_compact(tid < k && !conn, tid, s_nconn, s_cnt);
+            const bool use_complement = nc < c;
+            PHASE_STAMP(0);
 
-            // --- lim from w_lim ---
-            if (tid == 0) {
-                const double w_lim = (double)a.sigtab[a.sig_mode == CF_SIGS_COMPAT ? (uint64_t)r : base + r];
-                int lim = 0;
-                for (; lim < m; ++lim) {
-                    const double e = lim < k ? (double)ev[lim] : 0.0;
-                    if (e > w_lim) break;
-                }
+            // --- lim = first eigenvalue index above w_lim, >= 2 (:271-282) ---
+            {
+                const double w_lim =
+                    (double)a.sigtab[a.sig_mode == CF_SIGS_COMPAT ? (uint64_t)r : base + r];
+                const bool above = tid < m && (double)(tid < k ? ev[tid] : (T)0) > w_lim;
+                const unsigned long long bal = __ballot(above);
+                if (lane == 0) s_cnt[wave] = bal ? (__ffsll((long long)bal) - 1 + 64 * wave) : 0x7fffffff;
+                __syncthreads();
+                int lim = min(min(s_cnt[0], s_cnt[1]), min(s_cnt[2], s_cnt[3]));
+                lim = min(lim, m);
                 if (lim < 2) lim = 2;
                 if (lim > m) lim = m;
-                s_cnt[4] = lim;
+                __syncthreads();
+                s_cnt[4] = lim;   // every thread writes the same value
             }
-            __syncthreads();
             const int lim = s_cnt[4];
 
-            // --- zero-column filter (signed, >= 1e-4) ---
+            // --- zero-column filter: keep column j < lim iff some U(C, j) >= 1e-4 (:284-304)
             bool keep = false;
             if (tid < lim) {
                 for (int i = 0; i < c; ++i)
@@ -133,8 +210,9 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                     }
             }
             const int L = block_compact(keep, tid, s_keep, s_cnt);
+            PHASE_STAMP(1);
 
-            // --- centred ratings mean ---
+            // --- mean of the connected ratings (:311) ---
             if (wave == 0) {
                 double sum = 0.0;
                 for (int i = lane; i < c; i += 64) sum += (double)s_rat[s_conn[i]];
@@ -143,105 +221,217 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
             }
             __syncthreads();
             const double mean = s_misc[0];
+            PHASE_STAMP(2);
 
-            // --- Gram M = G^T G and rhs t = G^T (r - mean), G = U(C, S) ---
-            for (int e = tid; e < L * L; e += kThreads) {
-                const int ia = e / L, ib = e - ia * L;
-                if (ib < ia) continue;
-                const int ca = s_keep[ia], cb = s_keep[ib];
-                double acc = 0.0;
-                for (int i = 0; i < c; ++i) {
-                    const T* row = U + (size_t)s_conn[i] * m;
-                    acc = fma((double)row[ca], (double)row[cb], acc);
+            // --- bordered Gram: A[i][j] = (G^T G)_ij (j <= i < L), A[L][j] = t_j, A[L+1][j] = v_j
+            // 4x4 register tiles of the lower triangle, 8 independent loads per row of G.
+            {
+                const int nt4 = (L + 3) >> 2;
+                const int ntile = nt4 * (nt4 + 1) / 2;
+                for (int tix = tid; tix < ntile; tix += kThreads) {
+                    int ta = 0, rem = tix;   // tix -> (ta >= tb), row-major over the lower triangle
+                    while (rem > ta) {
+                        rem -= ta + 1;
+                        ++ta;
+                    }
+                    const int tb = rem;
+                    int ca[4], cb[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int ia = 4 * ta + q, ib = 4 * tb + q;
+                        ca[q] = s_keep[ia < L ? ia : L - 1];
+                        cb[q] = s_keep[ib < L ? ib : L - 1];
+                    }
+                    double acc[4][4];
+#pragma unroll
+                    for (int x = 0; x < 4; ++x)
+#pragma unroll
+                        for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+                    const int nrows = use_complement ? nc : c;
+                    const int* rows = use_complement ? s_nconn : s_conn;
+                    int i = 0;
+                    for (; i + 1 < nrows; i += 2) {   // two rows in flight: 16 independent loads
+                        const T* row0 = U + (size_t)rows[i] * m;
+                        const T* row1 = U + (size_t)rows[i + 1] * m;
+                        double va0[4], vb0[4], va1[4], vb1[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            va0[q] = (double)row0[ca[q]];
+                            vb0[q] = (double)row0[cb[q]];
+                            va1[q] = (double)row1[ca[q]];
+                            vb1[q] = (double)row1[cb[q]];
+                        }
+#pragma unroll
+                        for (int x = 0; x < 4; ++x)
+#pragma unroll
+                            for (int y = 0; y < 4; ++y)
+                                acc[x][y] = fma(va1[x], vb1[y], fma(va0[x], vb0[y], acc[x][y]));
+                    }
+                    for (; i < nrows; ++i) {
+                        const T* row = U + (size_t)rows[i] * m;
+                        double va[4], vb[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            va[q] = (double)row[ca[q]];
+                            vb[q] = (double)row[cb[q]];
+                        }
+#pragma unroll
+                        for (int x = 0; x < 4; ++x)
+#pragma unroll
+                            for (int y = 0; y < 4; ++y) acc[x][y] = fma(va[x], vb[y], acc[x][y]);
+                    }
+#pragma unroll
+                    for (int x = 0; x < 4; ++x)
+#pragma unroll
+                        for (int y = 0; y < 4; ++y) {
+                            const int ia = 4 * ta + x, ib = 4 * tb + y;
+                            if (ia < L && ib <= ia)
+                                A[tri(ia, ib)] = use_complement
+                                                     ? Gb[(size_t)ca[x] * lmax + cb[y]] - acc[x][y]
+                                                     : acc[x][y];
+                        }
                 }
-                M[ia * L + ib] = acc;
-                M[ib * L + ia] = acc;
-            }
-            for (int ia = tid; ia < L; ia += kThreads) {
-                const int ca = s_keep[ia];
-                double acc = 0.0;
-                for (int i = 0; i < c; ++i)
-                    acc = fma((double)U[(size_t)s_conn[i] * m + ca], (double)s_rat[s_conn[i]] - mean, acc);
-                tv[ia] = acc;
-                s_rowp[ia] = ia;
+                // t = G^T (r - mean): 4 lanes per column, each a strided quarter of C,
+                // combined with two DPP-free shuffles; v = U(r, S).
+                for (int e = tid; e < 4 * L; e += kThreads) {
+                    const int j = e >> 2, part = e & 3;
+                    const int cj = s_keep[j];
+                    double acc0 = 0.0, acc1 = 0.0;
+                    int i = part;
+                    for (; i + 4 < c; i += 8) {
+                        const int r0 = s_conn[i], r1 = s_conn[i + 4];
+                        acc0 = fma((double)U[(size_t)r0 * m + cj], (double)s_rat[r0] - mean, acc0);
+                        acc1 = fma((double)U[(size_t)r1 * m + cj], (double)s_rat[r1] - mean, acc1);
+                    }
+                    for (; i < c; i += 4) {
+                        const int r0 = s_conn[i];
+                        acc0 = fma((double)U[(size_t)r0 * m + cj], (double)s_rat[r0] - mean, acc0);
+                    }
+                    double acc = acc0 + acc1;
+                    acc += __shfl_xor(acc, 1);
+                    acc += __shfl_xor(acc, 2);
+                    if (part == 0) {
+                        A[tri(L, j)] = acc;
+                        A[tri(L + 1, j)] = (double)U[(size_t)r * m + cj];
+                    }
+                }
             }
             __syncthreads();
+            PHASE_STAMP(3);
 
-            // --- LU with partial pivoting (row permutation kept in s_rowp) ---
-            for (int kc = 0; kc < L; ++kc) {
+            // --- blocked right-looking Cholesky of M, carrying the two border rows ---
+            for (int kb = 0; kb < L; kb += kNB) {
+                const int b = min(kNB, L - kb);
+                // (1) diagonal block, unblocked, in wave 0's registers: lane i < b holds
+                //     row kb + i of the block; column j is broadcast by shuffles.
                 if (wave == 0) {
-                    double best = -1.0;
-                    int bi = 0x7fffffff;
-                    for (int i = kc + lane; i < L; i += 64) {
-                        const double v = fabs(M[s_rowp[i] * L + kc]);
-                        if (v > best) {
-                            best = v;
-                            bi = i;
+                    double rowv[kNB];
+                    const int i = lane;
+                    const bool live = i < b;
+#pragma unroll
+                    for (int q = 0; q < kNB; ++q)
+                        rowv[q] = (live && q <= i) ? A[tri(kb + i, kb + q)] : 0.0;
+#pragma unroll
+                    for (int j = 0; j < kNB; ++j) {
+                        if (j < b) {
+                            // L_jj = sqrt(a_jj), held by lane j
+                            const double ljj = sqrt(__shfl(rowv[j], j));
+                            if (i == j) rowv[j] = ljj;
+                            double lij = 0.0;
+                            if (i > j) {
+                                lij = rowv[j] / ljj;
+                                rowv[j] = lij;
+                            }
+                            // a_iq -= L_ij L_qj, j < q <= i
+#pragma unroll
+                            for (int q = j + 1; q < kNB; ++q) {
+                                const double lqj = __shfl(lij, q);
+                                if (q <= i) rowv[q] = fma(-lij, lqj, rowv[q]);
+                            }
                         }
                     }
 #pragma unroll
-                    for (int off = 32; off >= 1; off >>= 1) {
-                        const double ob = __shfl_xor(best, off);
-                        const int oi = __shfl_xor(bi, off);
-                        if (ob > best || (ob == best && oi < bi)) {
-                            best = ob;
-                            bi = oi;
-                        }
-                    }
-                    if (lane == 0) {
-                        if (best > 0.0 && bi != kc) {
-                            const int t = s_rowp[kc];
-                            s_rowp[kc] = s_rowp[bi];
-                            s_rowp[bi] = t;
-                        }
-                        s_cnt[5] = best > 0.0;
-                    }
+                    for (int q = 0; q < kNB; ++q)
+                        if (live && q <= i) A[tri(kb + i, kb + q)] = rowv[q];
                 }
                 __syncthreads();
-                if (s_cnt[5]) {
-                    const int pr = s_rowp[kc];
-                    const double pinv = 1.0 / M[pr * L + kc];
-                    const int rows = L - kc - 1;
-                    const int cols = L - kc;  // column kc carries the multiplier
-                    for (int e = tid; e < rows * cols; e += kThreads) {
-                        const int ri = e / cols;
-                        const int cj = e - ri * cols;
-                        const int row = s_rowp[kc + 1 + ri];
-                        const double l = M[row * L + kc] * pinv;
-                        if (cj == 0) {
-                            tv[row] -= l * tv[pr];
-                        } else {
-                            M[row * L + kc + cj] -= l * M[pr * L + kc + cj];
+                // (2) panel: rows below the block (incl. the border rows) solve against L11^T
+                for (int i = kb + b + tid; i < L + 2; i += kThreads) {
+                    double* Ai = A + tri(i, kb);
+                    double x[kNB];
+#pragma unroll
+                    for (int jj = 0; jj < kNB; ++jj) x[jj] = jj < b ? Ai[jj] : 0.0;
+#pragma unroll
+                    for (int jj = 0; jj < kNB; ++jj) {
+                        if (jj < b) {
+                            const double* Aj = A + tri(kb + jj, kb);   // broadcast reads of L11
+                            double sacc = x[jj];
+#pragma unroll
+                            for (int q = 0; q < jj; ++q) sacc = fma(-x[q], Aj[q], sacc);
+                            x[jj] = sacc / Aj[jj];
+                        }
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < kNB; ++jj)
+                        if (jj < b) Ai[jj] = x[jj];
+                }
+                __syncthreads();
+                // (3) trailing update A22 -= L21 L21^T over rows [kb+b, L+2), columns [kb+b, min(i, L-1)]
+                {
+                    const int r0 = kb + b;
+                    const int nr = L + 2 - r0;   // rows
+                    const int nc = L - r0;       // columns
+                    if (nc > 0) {
+                        const int tr = (nr + 3) >> 2, tcn = (nc + 3) >> 2;
+                        for (int tix = tid; tix < tr * tcn; tix += kThreads) {
+                            const int ti = tix / tcn, tq = tix - ti * tcn;
+                            if (tq > ti) continue;   // strictly above the diagonal tiles
+                            double acc[4][4];
+#pragma unroll
+                            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                                for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+                            const double* Ar[4];
+                            const double* Aq[4];
+#pragma unroll
+                            for (int x = 0; x < 4; ++x) {
+                                const int gi = min(r0 + 4 * ti + x, L + 1);
+                                const int gq = min(r0 + 4 * tq + x, L - 1);
+                                Ar[x] = A + tri(gi, 0);
+                                Aq[x] = A + tri(gq, 0);
+                            }
+                            for (int j = kb; j < kb + b; ++j) {
+                                double vr[4], vq[4];
+#pragma unroll
+                                for (int x = 0; x < 4; ++x) {
+                                    vr[x] = Ar[x][j];
+                                    vq[x] = Aq[x][j];
+                                }
+#pragma unroll
+                                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                                    for (int y = 0; y < 4; ++y) acc[x][y] = fma(vr[x], vq[y], acc[x][y]);
+                            }
+#pragma unroll
+                            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                                for (int y = 0; y < 4; ++y) {
+                                    const int gi = r0 + 4 * ti + x, gq = r0 + 4 * tq + y;
+                                    if (gi < L + 2 && gq < L && gq <= gi) A[tri(gi, gq)] -= acc[x][y];
+                                }
                         }
                     }
                 }
                 __syncthreads();
             }
+            PHASE_STAMP(4);
 
-            // --- back substitution (one wave) and prediction ---
+            // --- pred = v^T M^-1 t + mean = (L^-1 v) . (L^-1 t) + mean; clamp; error (:314-327)
             if (wave == 0) {
-                // x_j lives in lane (j & 63), slot (j >> 6): L <= CF_MAX_K = 3 * 64.
-                double x0 = 0.0, x1 = 0.0, x2 = 0.0;
-                for (int i = L - 1; i >= 0; --i) {
-                    const int row = s_rowp[i];
-                    const double* Mr = M + (size_t)row * L;
-                    double s = 0.0;
-                    if (lane > i && lane < L) s = fma(Mr[lane], x0, s);
-                    if (lane + 64 > i && lane + 64 < L) s = fma(Mr[lane + 64], x1, s);
-                    if (lane + 128 > i && lane + 128 < L) s = fma(Mr[lane + 128], x2, s);
-                    s = wave_sum(s);
-                    const double xi = (tv[row] - s) / Mr[i];
-                    if (lane == (i & 63)) {
-                        if (i < 64) x0 = xi;
-                        else if (i < 128) x1 = xi;
-                        else x2 = xi;
-                    }
-                }
                 double dot = 0.0;
-                const T* vrow = U + (size_t)r * m;
-                if (lane < L) dot = fma((double)vrow[s_keep[lane]], x0, dot);
-                if (lane + 64 < L) dot = fma((double)vrow[s_keep[lane + 64]], x1, dot);
-                if (lane + 128 < L) dot = fma((double)vrow[s_keep[lane + 128]], x2, dot);
+                const double* y = A + tri(L, 0);
+                const double* z = A + tri(L + 1, 0);
+                for (int j = lane; j < L; j += 64) dot = fma(y[j], z[j], dot);
                 dot = wave_sum(dot);
                 if (lane == 0) {
                     double pred = dot + mean;
@@ -254,30 +444,29 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                 }
             }
             __syncthreads();
+            PHASE_STAMP(5);
         }
     }
+    if (a.phase_cycles && tid == 0)
+        for (int ph = 0; ph < 6; ++ph) atomicAdd(&a.phase_cycles[ph], ph_acc[ph]);
 }
 
 template <typename T>
-int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lmax,
-                          double** scratch, size_t* scratch_bytes, hipStream_t stream) {
-    const size_t gram = (size_t)lmax * lmax * sizeof(double);
+int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lmax, hipStream_t stream) {
     args.lmax = lmax;
-    args.gram_in_lds = gram <= kMaxLdsGram;
-    const size_t lds = (args.gram_in_lds ? gram : 0) + lmax * sizeof(double) + 4 * sizeof(double) +
+    const size_t lds = sizeof(double) * ((size_t)(lmax + 2) * (lmax + 3) / 2 + 4) +
                        CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 3 * sizeof(int)) + 8 * sizeof(int);
+    if (lds > 163840) return cf_set_error(ctx, CF_ERANGE, "predict bucket exceeds LDS");
     int blocks = (int)std::min<uint32_t>(count, 2048u);
-    if (!args.gram_in_lds) {
-        const size_t need = (size_t)blocks * gram;
-        if (need > *scratch_bytes) {
-            if (*scratch) (void)hipFree(*scratch);
-            *scratch = nullptr;
-            *scratch_bytes = 0;
-            CF_HIP_CHECK(ctx, hipMalloc(scratch, need));
-            *scratch_bytes = need;
-        }
-        args.scratch = *scratch;
+    const size_t need = (size_t)blocks * lmax * lmax * sizeof(double);
+    if (need > ctx->scratch_bytes) {
+        if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+        ctx->d_scratch = nullptr;
+        ctx->scratch_bytes = 0;
+        CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_scratch, need));
+        ctx->scratch_bytes = need;
     }
+    args.gbar = reinterpret_cast<double*>(ctx->d_scratch);
     CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)predict_kernel<T>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(predict_kernel<T>, dim3(blocks), dim3(kThreads), lds, stream, args, count);
@@ -309,19 +498,14 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
     args.mse = d_mse;
     args.kk = d_kk;
     args.pred = d_pred;
-    double* scratch = nullptr;
-    size_t scratch_bytes = 0;
+    args.phase_cycles = ctx->d_phase;
     int rc = CF_OK;
     for (const cf_bucket& b : plan->buckets) {
         if (b.count == 0) continue;
         args.first = b.first;
         const int lmax = std::max<int>(2, 16 * b.emax);
-        rc = launch_predict_bucket<T>(ctx, args, b.count, lmax, &scratch, &scratch_bytes, stream);
+        rc = launch_predict_bucket<T>(ctx, args, b.count, lmax, stream);
         if (rc != CF_OK) break;
-    }
-    if (scratch) {
-        (void)hipStreamSynchronize(stream);
-        (void)hipFree(scratch);
     }
     return rc;
 }

@@ -60,6 +60,9 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
  * out4 (optional) receives and resets {sum of sweeps, users, max sweeps, users that
  * hit the sweep cap}.  enable == 0 frees them. */
 int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out4);
+/* Diagnostics: predictor phase cycle totals (s_memtime, thread 0 of each block):
+ * {connected set, lim + column filter, mean, Gram, LU, solve}. */
+int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out6);
 
 /* ---- item graph (out_fin_) ---------------------------------------------------
  * Directed weighted graph exactly as parsed: w(a,b) and w(b,a) are independent.
