@@ -14,12 +14,13 @@
 //
 // All arithmetic after the gather is fp64 (the reference's double path).  The
 // reference forms mm = U_CS^T U_CS and multiplies by its PartialPivLU inverse.  Here
-// the Gram matrix (SPD whenever the prediction is well-posed) is factored by a
-// blocked Cholesky in packed LDS storage, bordered by t^T and v^T so the
-// factorisation itself yields y = L^-1 t and z = L^-1 v and pred = y.z + mean
-// (v^T M^-1 t = (L^-1 v)^T (L^-1 t)).  For SPD M this agrees with the inverse-based
-// formula to cond(M) * eps; a rank-deficient M (c < L) is ill-posed in the reference
-// too, where the output is decided by rounding (NaN or a clamped 1 / 5).
+// the symmetric Gram matrix is factored M = L D L^T (blocked, right-looking, packed
+// lower triangle in LDS), bordered by t^T and v^T so the factorisation itself yields
+// L^-1 t and L^-1 v and pred = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean.  For a
+// well-conditioned M this agrees with the inverse-based formula to cond(M) * eps.
+// Like Gaussian elimination (and unlike Cholesky) LDL^T carries on through negative
+// pivots, so a numerically indefinite, near-singular M gives the same kind of
+// finite, clamped garbage as the reference instead of a NaN.
 
 #include "cf_internal.h"
 
@@ -319,11 +320,12 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
             __syncthreads();
             PHASE_STAMP(3);
 
-            // --- blocked right-looking Cholesky of M, carrying the two border rows ---
+            // --- blocked right-looking LDL^T of M, carrying the two border rows ---
             for (int kb = 0; kb < L; kb += kNB) {
                 const int b = min(kNB, L - kb);
-                // (1) diagonal block, unblocked, in wave 0's registers: lane i < b holds
-                //     row kb + i of the block; column j is broadcast by shuffles.
+                // (1) diagonal block, unblocked LDL^T, in wave 0's registers: lane i < b
+                //     holds row kb + i; column j is broadcast by shuffles.  D_j stays on
+                //     the diagonal, L_ij (unit lower) below it.
                 if (wave == 0) {
                     double rowv[kNB];
                     const int i = lane;
@@ -334,20 +336,16 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
 #pragma unroll
                     for (int j = 0; j < kNB; ++j) {
                         if (j < b) {
-                            // L_jj = sqrt(a_jj), held by lane j
-                            const double ljj = sqrt(__shfl(rowv[j], j));
-                            if (i == j) rowv[j] = ljj;
-                            double lij = 0.0;
-                            if (i > j) {
-                                lij = rowv[j] / ljj;
-                                rowv[j] = lij;
-                            }
-                            // a_iq -= L_ij L_qj, j < q <= i
+                            const double dj = __shfl(rowv[j], j);
+                            const double w = (i > j) ? rowv[j] : 0.0;   // unscaled a_ij
+                            const double lij = w / dj;
+                            // a_iq -= L_ij * a_qj, j < q <= i
 #pragma unroll
                             for (int q = j + 1; q < kNB; ++q) {
-                                const double lqj = __shfl(lij, q);
-                                if (q <= i) rowv[q] = fma(-lij, lqj, rowv[q]);
+                                const double wq = __shfl(w, q);
+                                if (q <= i) rowv[q] = fma(-lij, wq, rowv[q]);
                             }
+                            if (i > j) rowv[j] = lij;
                         }
                     }
 #pragma unroll
@@ -364,10 +362,12 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
 #pragma unroll
                     for (int jj = 0; jj < kNB; ++jj) {
                         if (jj < b) {
-                            const double* Aj = A + tri(kb + jj, kb);   // broadcast reads of L11
+                            // L_ij = (a_ij - sum_q L_iq D_q L_jq) / D_j   (broadcast reads of L11, D)
+                            const double* Aj = A + tri(kb + jj, kb);
                             double sacc = x[jj];
 #pragma unroll
-                            for (int q = 0; q < jj; ++q) sacc = fma(-x[q], Aj[q], sacc);
+                            for (int q = 0; q < jj; ++q)
+                                sacc = fma(-x[q] * A[tri(kb + q, kb + q)], Aj[q], sacc);
                             x[jj] = sacc / Aj[jj];
                         }
                     }
@@ -402,9 +402,10 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                             }
                             for (int j = kb; j < kb + b; ++j) {
                                 double vr[4], vq[4];
+                                const double dj = A[tri(j, j)];
 #pragma unroll
                                 for (int x = 0; x < 4; ++x) {
-                                    vr[x] = Ar[x][j];
+                                    vr[x] = Ar[x][j] * dj;
                                     vq[x] = Aq[x][j];
                                 }
 #pragma unroll
@@ -426,12 +427,13 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
             }
             PHASE_STAMP(4);
 
-            // --- pred = v^T M^-1 t + mean = (L^-1 v) . (L^-1 t) + mean; clamp; error (:314-327)
+            // --- pred = v^T M^-1 t + mean = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean (:314-327)
+            //     (the border rows hold (L^-1 t)_j / D_j and (L^-1 v)_j / D_j)
             if (wave == 0) {
                 double dot = 0.0;
                 const double* y = A + tri(L, 0);
                 const double* z = A + tri(L + 1, 0);
-                for (int j = lane; j < L; j += 64) dot = fma(y[j], z[j], dot);
+                for (int j = lane; j < L; j += 64) dot = fma(y[j] * z[j], A[tri(j, j)], dot);
                 dot = wave_sum(dot);
                 if (lane == 0) {
                     double pred = dot + mean;
