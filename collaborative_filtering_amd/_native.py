@@ -47,6 +47,11 @@ SIGNATURES = {
     "cf_predict_run_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                    c_void_p]),
+    "cf_item_cosine": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int,
+                               c_void_p]),
+    "cf_item_cosine_run": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_int, c_float,
+                                   c_int, c_void_p, c_void_p]),
+    "cf_knn_predict": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 _lib = None

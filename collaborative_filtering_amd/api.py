@@ -166,6 +166,35 @@ class Context:
                   "cf_predict_precomp")
         return (mse, kk, pred) if want_pred else (mse, kk)
 
+    # -- weights_calc (knn2.cpp:127-164) -------------------------------------------
+    def item_cosine(self, n_items, user_off, items, ratings, w_min=0.01, cnt_min=5, adopt=False,
+                    want_matrix=True):
+        """Dense item-weight matrix of knn2 from per-user train ratings (CSR)."""
+        user_off = np.ascontiguousarray(user_off, dtype=np.uint64)
+        items = np.ascontiguousarray(items, dtype=np.uint32)
+        ratings = np.ascontiguousarray(ratings, dtype=np.float32)
+        W = np.zeros((n_items, n_items), dtype=np.float32) if want_matrix else None
+        self._chk(self.lib.cf_item_cosine(self.h, len(user_off) - 1, n_items, ptr(user_off), ptr(items),
+                                          ptr(ratings), float(w_min), int(cnt_min), int(adopt), ptr(W)),
+                  "cf_item_cosine")
+        if adopt:
+            self.n_items = n_items
+        return W
+
+    # -- knn_program + error_vertex_data (knn3.cpp:185-256) ------------------------
+    def knn_predict(self, user_off, items, ratings):
+        """Returns (pred per test rating, per-movie MSE float32, per-movie test count)."""
+        user_off = np.ascontiguousarray(user_off, dtype=np.uint64)
+        items = np.ascontiguousarray(items, dtype=np.uint32)
+        ratings = np.ascontiguousarray(ratings, dtype=np.float32)
+        n = int(user_off[-1])
+        pred = np.zeros(n, dtype=np.float64)
+        mse = np.zeros(self.n_items, dtype=np.float32)
+        cnt = np.zeros(self.n_items, dtype=np.uint32)
+        self._chk(self.lib.cf_knn_predict(self.h, len(user_off) - 1, ptr(user_off), ptr(items), ptr(ratings),
+                                          ptr(pred), ptr(mse), ptr(cnt)), "cf_knn_predict")
+        return pred, mse, cnt
+
     # -- device-resident paths (torch CUDA tensors) -------------------------------
     def plan(self, item_off_host) -> "Plan":
         return Plan(self, item_off_host)

@@ -4,6 +4,7 @@
 // copy out; *_run entry points take device pointers and an explicit stream.
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <new>
 
@@ -100,6 +101,7 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
     if (ctx->d_phase) (void)hipFree(ctx->d_phase);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    if (ctx->d_knn) (void)hipFree(ctx->d_knn);
     delete ctx;
 }
 
@@ -438,6 +440,124 @@ int cf_predict_precomp(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, 
         if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("predict run: ") + hipGetErrorString(e));
     }
     cf_plan_destroy(plan);
+    return rc;
+}
+
+// ---- knn2: weights_calc over transform_edges (knn2.cpp:127-164) ---------------------
+static bool integer_small(const float* r, uint64_t n) {
+    for (uint64_t i = 0; i < n; ++i)
+        if (!(r[i] == std::nearbyint(r[i])) || r[i] < -11.0f || r[i] > 11.0f) return false;
+    return true;
+}
+
+int cf_item_cosine_run(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64_t* d_user_off,
+                       const uint32_t* d_item, const float* d_rating, int integer_ratings, float w_min,
+                       int cnt_min, float* d_w_out, void* stream) {
+    if (!ctx || !d_w_out) return cf_set_error(ctx, CF_EINVAL, "cf_item_cosine_run: null");
+    CF_TRY(set_device(ctx));
+    return cf_launch_knn2(ctx, n_users, n_items, d_user_off, d_item, d_rating, integer_ratings, w_min, cnt_min,
+                          d_w_out, (hipStream_t)stream);
+}
+
+int cf_item_cosine(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64_t* user_off,
+                   const uint32_t* item, const float* rating, float w_min, int cnt_min, int adopt_as_graph,
+                   float* w_out) {
+    if (!ctx || !user_off || (user_off[n_users] && (!item || !rating)) || (!w_out && !adopt_as_graph))
+        return cf_set_error(ctx, CF_EINVAL, "cf_item_cosine: null argument");
+    CF_TRY(set_device(ctx));
+    const uint64_t n = user_off[n_users];
+    for (uint64_t e = 0; e < n; ++e)
+        if (item[e] >= n_items) return cf_set_error(ctx, CF_EINVAL, "cf_item_cosine: item index out of range");
+    const int integer = integer_small(rating, n);
+    DevBuf doff, ditem, drat;
+    float* dW = nullptr;
+    int rc = dev_alloc(ctx, doff, sizeof(uint64_t) * (n_users + 1));
+    if (rc == CF_OK) rc = dev_alloc(ctx, ditem, sizeof(uint32_t) * n);
+    if (rc == CF_OK) rc = dev_alloc(ctx, drat, sizeof(float) * n);
+    if (rc == CF_OK && hipMalloc(&dW, std::max<size_t>((size_t)n_items * n_items * sizeof(float), 16)) != hipSuccess)
+        rc = cf_set_error(ctx, CF_ENOMEM, "cf_item_cosine: weight matrix allocation");
+    hipError_t e = hipSuccess;
+    if (rc == CF_OK) {
+        e = hipMemcpy(doff.p, user_off, sizeof(uint64_t) * (n_users + 1), hipMemcpyHostToDevice);
+        if (e == hipSuccess && n) e = hipMemcpy(ditem.p, item, sizeof(uint32_t) * n, hipMemcpyHostToDevice);
+        if (e == hipSuccess && n) e = hipMemcpy(drat.p, rating, sizeof(float) * n, hipMemcpyHostToDevice);
+        if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("knn2 H2D: ") + hipGetErrorString(e));
+    }
+    if (rc == CF_OK)
+        rc = cf_launch_knn2(ctx, n_users, n_items, (const uint64_t*)doff.p, (const uint32_t*)ditem.p,
+                            (const float*)drat.p, integer, w_min, cnt_min, dW, nullptr);
+    if (rc == CF_OK) {
+        e = hipDeviceSynchronize();
+        if (e == hipSuccess && w_out)
+            e = hipMemcpy(w_out, dW, (size_t)n_items * n_items * sizeof(float), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("knn2 run: ") + hipGetErrorString(e));
+    }
+    if (rc == CF_OK && adopt_as_graph) {
+        if (ctx->d_graph) (void)hipFree(ctx->d_graph);
+        ctx->d_graph = dW;
+        ctx->n_items = n_items;
+        dW = nullptr;
+    }
+    if (dW) (void)hipFree(dW);
+    return rc;
+}
+
+// ---- knn3: knn_program + error_vertex_data (knn3.cpp:185-256) ----------------------
+int cf_knn_predict(cf_ctx* ctx, uint32_t n_users, const uint64_t* user_off, const uint32_t* items,
+                   const float* ratings, double* pred, float* movie_mse, uint32_t* movie_count) {
+    if (!ctx || !user_off || !movie_mse || (user_off[n_users] && (!items || !ratings)))
+        return cf_set_error(ctx, CF_EINVAL, "cf_knn_predict: null argument");
+    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_knn_predict: no item graph uploaded");
+    CF_TRY(set_device(ctx));
+    const uint64_t n = user_off[n_users];
+    for (uint64_t e = 0; e < n; ++e)
+        if (items[e] >= ctx->n_items) return cf_set_error(ctx, CF_EINVAL, "cf_knn_predict: item out of range");
+    const uint32_t I = ctx->n_items;
+    const bool integer = integer_small(ratings, n);
+    DevBuf doff, ditem, drat, dpred, dsq, dsqr, dcnt;
+    int rc = dev_alloc(ctx, doff, sizeof(uint64_t) * (n_users + 1));
+    if (rc == CF_OK) rc = dev_alloc(ctx, ditem, sizeof(uint32_t) * n);
+    if (rc == CF_OK) rc = dev_alloc(ctx, drat, sizeof(float) * n);
+    if (rc == CF_OK) rc = dev_alloc(ctx, dpred, sizeof(double) * n);
+    if (rc == CF_OK) rc = dev_alloc(ctx, dsq, sizeof(unsigned long long) * I);
+    if (rc == CF_OK) rc = dev_alloc(ctx, dsqr, sizeof(double) * I);
+    if (rc == CF_OK) rc = dev_alloc(ctx, dcnt, sizeof(unsigned int) * I);
+    hipError_t e = hipSuccess;
+    if (rc == CF_OK) {
+        e = hipMemcpy(doff.p, user_off, sizeof(uint64_t) * (n_users + 1), hipMemcpyHostToDevice);
+        if (e == hipSuccess && n) e = hipMemcpy(ditem.p, items, sizeof(uint32_t) * n, hipMemcpyHostToDevice);
+        if (e == hipSuccess && n) e = hipMemcpy(drat.p, ratings, sizeof(float) * n, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemset(dsq.p, 0, sizeof(unsigned long long) * I);
+        if (e == hipSuccess) e = hipMemset(dsqr.p, 0, sizeof(double) * I);
+        if (e == hipSuccess) e = hipMemset(dcnt.p, 0, sizeof(unsigned int) * I);
+        if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("knn3 H2D: ") + hipGetErrorString(e));
+    }
+    if (rc == CF_OK)
+        rc = cf_launch_knn3(ctx, n_users, (const uint64_t*)doff.p, (const uint32_t*)ditem.p, (const float*)drat.p,
+                            (double*)dpred.p, (unsigned long long*)dsq.p, (double*)dsqr.p, (unsigned int*)dcnt.p,
+                            nullptr);
+    std::vector<unsigned long long> sq(I);
+    std::vector<double> sqr(I);
+    std::vector<unsigned int> cnt(I);
+    if (rc == CF_OK) {
+        e = hipDeviceSynchronize();
+        if (e == hipSuccess && pred && n) e = hipMemcpy(pred, dpred.p, sizeof(double) * n, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(sq.data(), dsq.p, sizeof(unsigned long long) * I, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(sqr.data(), dsqr.p, sizeof(double) * I, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(cnt.data(), dcnt.p, sizeof(unsigned int) * I, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("knn3 run: ") + hipGetErrorString(e));
+    }
+    if (rc == CF_OK) {
+        for (uint32_t i = 0; i < I; ++i) {
+            float v = 0.0f;   // vertices without test ratings contribute 0 (:254-255)
+            if (cnt[i]) {
+                const float err = integer ? (float)sq[i] : (float)sqr[i];
+                v = std::isnan(err) ? 0.0f : err / (float)cnt[i];   // (:249-253)
+            }
+            movie_mse[i] = v;
+            if (movie_count) movie_count[i] = cnt[i];
+        }
+    }
     return rc;
 }
 

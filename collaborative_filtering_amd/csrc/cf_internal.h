@@ -25,6 +25,9 @@ struct cf_ctx {
     // Device scratch owned by the context (predictor per-block U^T U), grown on demand.
     void* d_scratch = nullptr;
     size_t scratch_bytes = 0;
+    // knn2 rating planes (R, S, B), grown on demand.
+    void* d_knn = nullptr;
+    size_t knn_bytes = 0;
 };
 
 // One launch of the eigen / predict kernels covers the users of one k-bucket.
@@ -64,6 +67,13 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
                       const T* d_evals, const uint64_t* d_evec_off, const T* d_evecs,
                       const T* d_sigtab, int sig_mode, float* d_mse, int32_t* d_kk,
                       double* d_pred, hipStream_t stream);
+
+int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64_t* d_user_off,
+                   const uint32_t* d_item, const float* d_rating, int integer_ratings, float w_min,
+                   int cnt_min, float* d_w_out, hipStream_t stream);
+int cf_launch_knn3(cf_ctx* ctx, uint32_t n_users, const uint64_t* d_user_off, const uint32_t* d_items,
+                   const float* d_ratings, double* d_pred, unsigned long long* d_sq, double* d_sq_real,
+                   unsigned int* d_cnt, hipStream_t stream);
 
 int cf_launch_dense_scatter(cf_ctx* ctx, uint32_t n_items, const uint64_t* d_row_ptr,
                             const uint32_t* d_col, const float* d_w, float* d_dense,

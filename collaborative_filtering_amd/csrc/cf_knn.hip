@@ -1,0 +1,269 @@
+// cf_knn.hip -- the kNN item-similarity stage on gfx950.
+//
+// knn2 (knn2.cpp:127-164).  For item pair (a, b) over the users present in both
+// train maps (presence, not non-zero: knn.cpp:89-98 loads .predict files with
+// rating 0):  num = sum r_a r_b, den1 = sum r_a^2, den2 = sum r_b^2, cnt = #users;
+// w = num / (sqrtf(den1) * sqrtf(den2)) if cnt > 5, written when w > 0.01.
+// Dense form over the item-major planes R (ratings), S = R*R and B (presence):
+//     num = R^T R,  den1 = S^T B,  den2 = B^T S,  cnt = B^T B
+// -- four products sharing the same K (user) loop.  Integer ratings in [-11, 11]
+// run on v_mfma_i32_32x32x32_i8 (exact; the reference's float accumulators are
+// exact too while the sums stay below 2^24), real ratings on
+// v_mfma_f32_32x32x2_f32.  The fused epilogue applies the thresholds with IEEE
+// sqrtf / division and writes the dense item-weight matrix (the layout the eigen
+// stage reads), both directions from one upper-triangle tile.
+//
+// knn3 (knn3.cpp:185-256), regrouped by user: for each test rating (m, u),
+// pred = sum_j w(m,j) r_uj / sum_j w(m,j) over u's test items j with
+// w(m, j) > 0.1 (the out-neighbours of m that hold a test rating of u); the squared
+// error of round(pred) (0 if pred < 0.1) is accumulated per movie exactly in int64.
+
+#include "cf_internal.h"
+
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+// ---- plane construction ------------------------------------------------------------
+// One thread per (user, rating): item-major planes, [item][user] with leading dim ldu.
+__global__ void planes_i8_kernel(uint32_t n_users, const uint64_t* user_off, const uint32_t* item,
+                                 const float* rating, uint64_t ldu, int8_t* R, int8_t* S, int8_t* Bp) {
+    const uint32_t u = blockIdx.x;
+    if (u >= n_users) return;
+    for (uint64_t e = user_off[u] + threadIdx.x; e < user_off[u + 1]; e += blockDim.x) {
+        const int r = (int)rating[e];
+        const size_t idx = (size_t)item[e] * ldu + u;
+        R[idx] = (int8_t)r;
+        S[idx] = (int8_t)(r * r);
+        Bp[idx] = 1;
+    }
+}
+
+__global__ void planes_f32_kernel(uint32_t n_users, const uint64_t* user_off, const uint32_t* item,
+                                  const float* rating, uint64_t ldu, float* R, float* S, float* Bp) {
+    const uint32_t u = blockIdx.x;
+    if (u >= n_users) return;
+    for (uint64_t e = user_off[u] + threadIdx.x; e < user_off[u + 1]; e += blockDim.x) {
+        const float r = rating[e];
+        const size_t idx = (size_t)item[e] * ldu + u;
+        R[idx] = r;
+        S[idx] = r * r;
+        Bp[idx] = 1.0f;
+    }
+}
+
+// Upper-triangle tile index -> (ta, tb), ta <= tb.
+__device__ __forceinline__ void tile_pair(uint32_t t, uint32_t nt, uint32_t& ta, uint32_t& tb) {
+    // rows of decreasing length nt, nt-1, ...: solve with a float estimate, then fix up
+    float fn = (float)nt + 0.5f;
+    uint32_t a = (uint32_t)(fn - sqrtf(fn * fn - 2.0f * (float)t));
+    if (a > 0) --a;
+    auto start = [&](uint32_t x) { return x * nt - x * (x - 1) / 2; };
+    while (a + 1 < nt && start(a + 1) <= t) ++a;
+    while (a > 0 && start(a) > t) --a;
+    ta = a;
+    tb = a + (t - start(a));
+}
+
+struct Knn2Args {
+    const void* R;
+    const void* S;
+    const void* B;
+    uint64_t ldu;       // users per plane row (multiple of 32)
+    uint32_t n_items;
+    uint32_t n_tiles;   // tiles per side (64 items each)
+    float w_min;
+    int cnt_min;
+    float* w_out;       // n_items x n_items
+};
+
+// Epilogue for one 32x32 accumulator block: lane holds column c = lane&31 and rows
+// (reg&3) + 8*(reg>>2) + 4*(lane>>5).
+template <typename ACC>
+__device__ __forceinline__ void knn2_store(const Knn2Args& a, uint32_t a0, uint32_t b0, bool diag_tile,
+                                           const ACC& num, const ACC& den1, const ACC& den2,
+                                           const ACC& cnt) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t col = b0 + (lane & 31);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const uint32_t row = a0 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+        if (row >= a.n_items || col >= a.n_items) continue;
+        float w = 0.0f;
+        if (row != col && (int)cnt[reg] > a.cnt_min) {
+            const float fn = (float)num[reg], f1 = (float)den1[reg], f2 = (float)den2[reg];
+            const float v = fn / (sqrtf(f1) * sqrtf(f2));                     // (:143)
+            if ((double)v > (double)a.w_min) w = v;                           // (:157)
+        }
+        a.w_out[(size_t)row * a.n_items + col] = w;
+        if (!diag_tile) a.w_out[(size_t)col * a.n_items + row] = w;          // w(b,a) == w(a,b)
+    }
+}
+
+// 256 threads = 4 waves; workgroup tile 64 x 64 items, wave (wy, wx) owns 32 x 32.
+__global__ __launch_bounds__(256) void knn2_i8_kernel(Knn2Args a) {
+    uint32_t ta, tb;
+    tile_pair(blockIdx.x, a.n_tiles, ta, tb);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t a0 = ta * 64 + 32 * (wave >> 1), b0 = tb * 64 + 32 * (wave & 1);
+    const int r = lane & 31, h = lane >> 5;
+    const uint32_t ra = min(a0 + r, a.n_items - 1), rb = min(b0 + r, a.n_items - 1);
+    const int8_t* Ra = (const int8_t*)a.R + (size_t)ra * a.ldu + 16 * h;
+    const int8_t* Sa = (const int8_t*)a.S + (size_t)ra * a.ldu + 16 * h;
+    const int8_t* Ba = (const int8_t*)a.B + (size_t)ra * a.ldu + 16 * h;
+    const int8_t* Rb = (const int8_t*)a.R + (size_t)rb * a.ldu + 16 * h;
+    const int8_t* Sb = (const int8_t*)a.S + (size_t)rb * a.ldu + 16 * h;
+    const int8_t* Bb = (const int8_t*)a.B + (size_t)rb * a.ldu + 16 * h;
+    v16i num = {}, den1 = {}, den2 = {}, cnt = {};
+    for (uint64_t k0 = 0; k0 < a.ldu; k0 += 32) {
+        const v4i ra_ = *(const v4i*)(Ra + k0), sa = *(const v4i*)(Sa + k0), ba = *(const v4i*)(Ba + k0);
+        const v4i rb_ = *(const v4i*)(Rb + k0), sb = *(const v4i*)(Sb + k0), bb = *(const v4i*)(Bb + k0);
+        num = __builtin_amdgcn_mfma_i32_32x32x32_i8(ra_, rb_, num, 0, 0, 0);
+        den1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(sa, bb, den1, 0, 0, 0);
+        den2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ba, sb, den2, 0, 0, 0);
+        cnt = __builtin_amdgcn_mfma_i32_32x32x32_i8(ba, bb, cnt, 0, 0, 0);
+    }
+    knn2_store(a, a0, b0, ta == tb, num, den1, den2, cnt);
+}
+
+// fp32 planes (real-valued ratings): v_mfma_f32_32x32x2_f32 consumes users
+// (s, 16 + s) of each 32-user step as its two k values (h = lane >> 5).
+__global__ __launch_bounds__(256) void knn2_f32_kernel(Knn2Args a) {
+    uint32_t ta, tb;
+    tile_pair(blockIdx.x, a.n_tiles, ta, tb);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t a0 = ta * 64 + 32 * (wave >> 1), b0 = tb * 64 + 32 * (wave & 1);
+    const int r = lane & 31, h = lane >> 5;
+    const uint32_t ra = min(a0 + r, a.n_items - 1), rb = min(b0 + r, a.n_items - 1);
+    const float* Ra = (const float*)a.R + (size_t)ra * a.ldu + 16 * h;
+    const float* Sa = (const float*)a.S + (size_t)ra * a.ldu + 16 * h;
+    const float* Ba = (const float*)a.B + (size_t)ra * a.ldu + 16 * h;
+    const float* Rb = (const float*)a.R + (size_t)rb * a.ldu + 16 * h;
+    const float* Sb = (const float*)a.S + (size_t)rb * a.ldu + 16 * h;
+    const float* Bb = (const float*)a.B + (size_t)rb * a.ldu + 16 * h;
+    v16f num = {}, den1 = {}, den2 = {}, cnt = {};
+    for (uint64_t k0 = 0; k0 < a.ldu; k0 += 32) {
+#pragma unroll 4
+        for (int s = 0; s < 16; ++s) {
+            const float xa = Ra[k0 + s], ya = Sa[k0 + s], za = Ba[k0 + s];
+            const float xb = Rb[k0 + s], yb = Sb[k0 + s], zb = Bb[k0 + s];
+            num = __builtin_amdgcn_mfma_f32_32x32x2f32(xa, xb, num, 0, 0, 0);
+            den1 = __builtin_amdgcn_mfma_f32_32x32x2f32(ya, zb, den1, 0, 0, 0);
+            den2 = __builtin_amdgcn_mfma_f32_32x32x2f32(za, yb, den2, 0, 0, 0);
+            cnt = __builtin_amdgcn_mfma_f32_32x32x2f32(za, zb, cnt, 0, 0, 0);
+        }
+    }
+    knn2_store(a, a0, b0, ta == tb, num, den1, den2, cnt);
+}
+
+// ---- knn3 ---------------------------------------------------------------------------
+struct Knn3Args {
+    uint32_t n_users;
+    const uint64_t* user_off;
+    const uint32_t* items;     // test items of each user (compact ids)
+    const float* ratings;      // test ratings
+    const float* graph;        // dense out_fin_ weights (as parsed floats)
+    uint64_t n_items;
+    double* pred;              // per test rating, 0 when no neighbour (ratings_knn default)
+    unsigned long long* sq_err;  // per movie: sum of tmp^2 (integer-valued for integer ratings)
+    double* sq_err_real;       // per movie: same in fp64 (non-integer ratings)
+    unsigned int* n_test;      // per movie: number of test ratings
+};
+
+__global__ __launch_bounds__(256) void knn3_kernel(Knn3Args a) {
+    const uint32_t u = blockIdx.x;
+    if (u >= a.n_users) return;
+    const uint64_t base = a.user_off[u];
+    const int k = (int)(a.user_off[u + 1] - base);
+    for (int r = threadIdx.x; r < k; r += blockDim.x) {
+        const uint32_t m = a.items[base + r];
+        const float* wrow = a.graph + (size_t)m * a.n_items;
+        double sw = 0.0, swr = 0.0;
+        for (int j = 0; j < k; ++j) {
+            const float w = wrow[a.items[base + j]];
+            if ((double)w > 0.1) {                               // knn3.cpp:91
+                sw += (double)w;
+                swr += (double)w * (double)a.ratings[base + j];  // :202
+            }
+        }
+        const double pred = sw > 0.0 ? swr / sw : 0.0;           // :216, missing key -> 0
+        a.pred[base + r] = pred;
+        const float tmp = (pred < 0.1) ? 0.0f : (float)((double)a.ratings[base + r] - round(pred));  // :243-246
+        const float sq = tmp * tmp;
+        atomicAdd(&a.sq_err[m], (unsigned long long)sq);
+        atomicAdd(&a.sq_err_real[m], (double)sq);
+        atomicAdd(&a.n_test[m], 1u);
+    }
+}
+
+}  // namespace
+
+int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64_t* d_user_off,
+                   const uint32_t* d_item, const float* d_rating, int integer_ratings, float w_min,
+                   int cnt_min, float* d_w_out, hipStream_t stream) {
+    const uint64_t ldu = ((uint64_t)n_users + 31) / 32 * 32;
+    const size_t esz = integer_ratings ? 1 : 4;
+    const size_t plane = (size_t)n_items * ldu * esz;
+    const size_t need = 3 * plane;
+    if (need > ctx->knn_bytes) {
+        if (ctx->d_knn) (void)hipFree(ctx->d_knn);
+        ctx->d_knn = nullptr;
+        ctx->knn_bytes = 0;
+        if (hipMalloc(&ctx->d_knn, need) != hipSuccess)
+            return cf_set_error(ctx, CF_ENOMEM, "knn2 planes (" + std::to_string(need) + " bytes)");
+        ctx->knn_bytes = need;
+    }
+    char* base = (char*)ctx->d_knn;
+    CF_HIP_CHECK(ctx, hipMemsetAsync(base, 0, need, stream));
+    if (n_users) {
+        if (integer_ratings)
+            hipLaunchKernelGGL(planes_i8_kernel, dim3(n_users), dim3(64), 0, stream, n_users, d_user_off, d_item,
+                               d_rating, ldu, (int8_t*)base, (int8_t*)(base + plane), (int8_t*)(base + 2 * plane));
+        else
+            hipLaunchKernelGGL(planes_f32_kernel, dim3(n_users), dim3(64), 0, stream, n_users, d_user_off, d_item,
+                               d_rating, ldu, (float*)base, (float*)(base + plane), (float*)(base + 2 * plane));
+        CF_HIP_CHECK(ctx, hipGetLastError());
+    }
+    Knn2Args a{};
+    a.R = base;
+    a.S = base + plane;
+    a.B = base + 2 * plane;
+    a.ldu = ldu;
+    a.n_items = n_items;
+    a.n_tiles = (n_items + 63) / 64;
+    a.w_min = w_min;
+    a.cnt_min = cnt_min;
+    a.w_out = d_w_out;
+    const uint32_t ntp = a.n_tiles * (a.n_tiles + 1) / 2;
+    if (ntp) {
+        if (integer_ratings)
+            hipLaunchKernelGGL(knn2_i8_kernel, dim3(ntp), dim3(256), 0, stream, a);
+        else
+            hipLaunchKernelGGL(knn2_f32_kernel, dim3(ntp), dim3(256), 0, stream, a);
+        CF_HIP_CHECK(ctx, hipGetLastError());
+    }
+    return CF_OK;
+}
+
+int cf_launch_knn3(cf_ctx* ctx, uint32_t n_users, const uint64_t* d_user_off, const uint32_t* d_items,
+                   const float* d_ratings, double* d_pred, unsigned long long* d_sq, double* d_sq_real,
+                   unsigned int* d_cnt, hipStream_t stream) {
+    Knn3Args a{};
+    a.n_users = n_users;
+    a.user_off = d_user_off;
+    a.items = d_items;
+    a.ratings = d_ratings;
+    a.graph = ctx->d_graph;
+    a.n_items = ctx->n_items;
+    a.pred = d_pred;
+    a.sq_err = d_sq;
+    a.sq_err_real = d_sq_real;
+    a.n_test = d_cnt;
+    if (n_users) {
+        hipLaunchKernelGGL(knn3_kernel, dim3(n_users), dim3(256), 0, stream, a);
+        CF_HIP_CHECK(ctx, hipGetLastError());
+    }
+    return CF_OK;
+}

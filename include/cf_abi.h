@@ -132,6 +132,31 @@ int cf_predict_run_f32(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_
                        const float* d_evecs, const float* d_sigtab, int sig_mode,
                        float* d_mse, int32_t* d_kk, double* d_pred, void* stream);
 
+/* ---- kNN stage ------------------------------------------------------------------
+ * knn2 weights_calc (knn2.cpp:127-164): for every item pair a != b over the users
+ * present in both train lists, cnt > cnt_min ? w = num/(sqrtf(den1)*sqrtf(den2)) : 0,
+ * kept iff w > w_min (the reference writes w > 0.01, cnt > 5).  Output is the dense
+ * n_items x n_items weight matrix (0 = no out_fin_ edge); symmetric for integer
+ * ratings.  user_off/item/rating: per-user train ratings (CSR over users).
+ * Integer ratings in [-11, 11] run on int8 MFMA (exact), others on fp32 MFMA.
+ * adopt_as_graph != 0 also installs the result as the context's item graph. */
+int cf_item_cosine(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64_t* user_off,
+                   const uint32_t* item, const float* rating, float w_min, int cnt_min,
+                   int adopt_as_graph, float* w_out);
+int cf_item_cosine_run(cf_ctx* ctx, uint32_t n_users, uint32_t n_items,
+                       const uint64_t* d_user_off, const uint32_t* d_item, const float* d_rating,
+                       int integer_ratings, float w_min, int cnt_min, float* d_w_out,
+                       void* stream);
+/* knn3 knn_program + error_vertex_data (knn3.cpp:185-256) on the uploaded graph:
+ * per test rating (user u, movie items[e]) pred[e] = sum w*r / sum w over u's test
+ * items j with w(movie, j) > 0.1 (0 when none); per movie (compact id)
+ * movie_mse[i] = (sum over its test ratings of (r - round(pred))^2, 0 if pred < 0.1)
+ * / count, and 0 for movies without test ratings.  The "Knn Average MSE" is
+ * sum(movie_mse) / num_vertices (computed by the caller, knn3.cpp:263). */
+int cf_knn_predict(cf_ctx* ctx, uint32_t n_users, const uint64_t* user_off,
+                   const uint32_t* items, const float* ratings, double* pred,
+                   float* movie_mse, uint32_t* movie_count);
+
 #ifdef __cplusplus
 }
 #endif

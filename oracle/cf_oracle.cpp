@@ -24,6 +24,7 @@
 #include <cstdint>
 #include <cstring>
 #include <thread>
+#include <utility>
 #include <vector>
 
 namespace {
@@ -469,6 +470,94 @@ int cfo_predict_user(int k, int m, const int32_t* items, const double* ratings,
         mse_out[t] = (float)err;
         kk_out[t] = c;
         if (pred_out) pred_out[t] = pred;
+    }
+    return 0;
+}
+
+// a10: weights_calc for every ordered item pair (knn2.cpp:127-146) + the writer's
+// w > 0.01 filter (:157).  Train ratings come per user (CSR); each item's map is
+// built in ascending user order (the reference iterates a boost::unordered_map, so
+// its order -- and with real-valued ratings the float rounding -- is unpinned).
+//   W_out[a*n_items + b] = w if written, else 0.  cnt_out (optional) = common users.
+int cfo_knn2(int n_users, const int64_t* user_off, const int32_t* item, const double* rating,
+             int n_items, float* W_out, int32_t* cnt_out) {
+    std::vector<std::vector<std::pair<int, double>>> maps(n_items);
+    for (int u = 0; u < n_users; ++u)
+        for (int64_t e = user_off[u]; e < user_off[u + 1]; ++e) maps[item[e]].push_back({u, rating[e]});
+    for (int a = 0; a < n_items; ++a) {
+        for (int b = 0; b < n_items; ++b) {
+            float w = 0.0f;
+            int num_rat = 0;
+            if (a != b) {
+                const auto& ma = maps[a];
+                const auto& mb = maps[b];
+                float num = 0, den1 = 0, den2 = 0;
+                size_t j = 0;
+                for (size_t i = 0; i < ma.size(); ++i) {  // (:133-140)
+                    while (j < mb.size() && mb[j].first < ma[i].first) ++j;
+                    if (j < mb.size() && mb[j].first == ma[i].first) {
+                        num_rat++;
+                        num += ma[i].second * mb[j].second;
+                        den1 += ma[i].second * ma[i].second;
+                        den2 += mb[j].second * mb[j].second;
+                    }
+                }
+                double obs = 0;
+                if (num_rat > 5) obs = num / (std::sqrt(den1) * std::sqrt(den2));  // (:142-145)
+                if (obs > 0.01) w = (float)obs;                                     // (:157)
+            }
+            W_out[(size_t)a * n_items + b] = w;
+            if (cnt_out) cnt_out[(size_t)a * n_items + b] = num_rat;
+        }
+    }
+    return 0;
+}
+
+// a11: knn_program gather/apply + error_vertex_data (knn3.cpp:185-256).
+//   W: dense out_fin_ weights as parsed floats; edge m -> nb iff (double)w > 0.1 (:91)
+//   test ratings per movie (CSR over movies): movie_off, user, rating (out_test_rat_)
+//   pred[e]      : ratings_knn[user] of entry e (0 when missing, the operator[] default)
+//   movie_mse[m] : error_vertex_data of vertex m (float)
+int cfo_knn3(int n_items, const float* W, const int64_t* movie_off, const int32_t* user,
+             const double* rating, double* pred, float* movie_mse) {
+    std::vector<std::vector<std::pair<int, double>>> test(n_items);
+    for (int m = 0; m < n_items; ++m)
+        for (int64_t e = movie_off[m]; e < movie_off[m + 1]; ++e) test[m].push_back({user[e], rating[e]});
+    std::vector<double> sum_r, sum_w;
+    for (int m = 0; m < n_items; ++m) {
+        // gather over out-edges (:197-205) and sum (:151-179), keyed by user
+        std::vector<std::pair<int, std::pair<double, double>>> acc;  // user -> (sum w*r, sum w)
+        for (int nb = 0; nb < n_items; ++nb) {
+            const double obs = (double)W[(size_t)m * n_items + nb];
+            if (!(obs > 0.1)) continue;
+            for (const auto& ur : test[nb]) acc.push_back({ur.first, {obs * ur.second, obs}});
+        }
+        std::sort(acc.begin(), acc.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+        float err = 0, tmp;
+        for (int64_t e = movie_off[m]; e < movie_off[m + 1]; ++e) {
+            const int u = user[e];
+            double sr = 0, sw = 0;
+            bool found = false;
+            auto it = std::lower_bound(acc.begin(), acc.end(), u,
+                                       [](const auto& x, int key) { return x.first < key; });
+            for (; it != acc.end() && it->first == u; ++it) {
+                sr += it->second.first;
+                sw += it->second.second;
+                found = true;
+            }
+            const double p = found ? sr / sw : 0.0;  // (:216); missing key -> 0 (:243)
+            pred[e] = p;
+            if (p < 0.1)
+                tmp = 0;
+            else
+                tmp = (float)(rating[e] - std::round(p));  // (:246), boost::math::round
+            err += tmp * tmp;
+        }
+        const int64_t sz = movie_off[m + 1] - movie_off[m];
+        if (sz > 0)
+            movie_mse[m] = std::isnan(err) ? 0.0f : err / (float)sz;  // (:249-253)
+        else
+            movie_mse[m] = 0.0f;
     }
     return 0;
 }

@@ -33,6 +33,8 @@ def lib():
         L.cfo_compute_eigens.restype = ci
         L.cfo_precompute_batch.argtypes = [ci, vp, vp, ctypes.c_int64, vp, vp, ci, ci, vp, vp, vp, vp]
         L.cfo_predict_user.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, ctypes.c_int64, ci, vp, vp, vp, vp]
+        L.cfo_knn2.argtypes = [ci, vp, vp, vp, ci, vp, vp]
+        L.cfo_knn3.argtypes = [ci, vp, vp, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -106,6 +108,29 @@ def predict_user(items, ratings, evals, U, sigtab, W, rows=None):
     lib().cfo_predict_user(k, m, _p(items), _p(ratings), _p(evals), _p(U), _p(sigtab), _p(W), W.shape[0],
                            len(rows), _p(rows), _p(mse), _p(kk), _p(pred))
     return mse, kk, pred
+
+
+def knn2(user_off, item, rating, n_items):
+    """weights_calc + w > 0.01 filter: (dense W float32, common-user counts)."""
+    user_off = np.ascontiguousarray(user_off, dtype=np.int64)
+    item = np.ascontiguousarray(item, dtype=np.int32)
+    rating = np.ascontiguousarray(rating, dtype=np.float64)
+    W = np.zeros((n_items, n_items), dtype=np.float32)
+    C = np.zeros((n_items, n_items), dtype=np.int32)
+    lib().cfo_knn2(len(user_off) - 1, _p(user_off), _p(item), _p(rating), n_items, _p(W), _p(C))
+    return W, C
+
+
+def knn3(W, movie_off, user, rating):
+    """knn_program + error_vertex_data: (pred per test entry, per-movie mse float32)."""
+    W = np.ascontiguousarray(W, dtype=np.float32)
+    movie_off = np.ascontiguousarray(movie_off, dtype=np.int64)
+    user = np.ascontiguousarray(user, dtype=np.int32)
+    rating = np.ascontiguousarray(rating, dtype=np.float64)
+    pred = np.zeros(max(int(movie_off[-1]), 1))
+    mse = np.zeros(W.shape[0], dtype=np.float32)
+    lib().cfo_knn3(W.shape[0], _p(W), _p(movie_off), _p(user), _p(rating), _p(pred), _p(mse))
+    return pred[: int(movie_off[-1])], mse
 
 
 # ---------------------------------------------------------------------------

@@ -91,3 +91,35 @@ def test_oracle_batch_matches_single_user():
     assert m[0] == m1 and np.array_equal(sigs[:32], s1)
     assert np.array_equal(evecs[: 32 * m1].reshape(32, m1), U1)
     assert m[1] == 8  # 8 isolated items: every eigenvalue is 1 <= smm = 1.01
+
+
+def test_knn2_matches_golden():
+    z = load("knn2_cases.npz")
+    R, P = z["R"], z["P"]
+    n_users, n_items = R.shape
+    off = [0]
+    items, rats = [], []
+    for u in range(n_users):
+        its = np.nonzero(P[u])[0]
+        items += list(its)
+        rats += list(R[u, its])
+        off.append(len(items))
+    W, C = orc.knn2(np.array(off), np.array(items), np.array(rats), n_items)
+    assert np.array_equal(C[~np.eye(n_items, dtype=bool)], z["cnt"][~np.eye(n_items, dtype=bool)])
+    Wg = np.where(z["W"] > 0.01, z["W"], 0.0).astype(np.float32)
+    assert np.array_equal(W, Wg)            # bit-exact: integer ratings, exact float sums
+    assert np.array_equal(W, W.T)           # both directions agree
+
+
+def test_knn3_hand_computed():
+    """Three movies, movie 0 -> {1, 2} with w 0.5 / 0.25, movie 1 -> {0} with w 0.05 (dropped)."""
+    W = np.zeros((3, 3), np.float32)
+    W[0, 1], W[0, 2], W[1, 0] = 0.5, 0.25, 0.05
+    # test ratings per movie: movie 0: users 7 (4), 8 (2); movie 1: user 7 (5); movie 2: users 7 (2), 8 (1)
+    movie_off = np.array([0, 2, 3, 5])
+    user = np.array([7, 8, 7, 7, 8])
+    rating = np.array([4.0, 2.0, 5.0, 2.0, 1.0])
+    pred, mse = orc.knn3(W, movie_off, user, rating)
+    # user 7 on movie 0: (0.5*5 + 0.25*2) / 0.75 = 4.0 -> tmp 0; user 8: 0.25*1/0.25 = 1 -> tmp 1
+    assert np.allclose(pred[:2], [4.0, 1.0])
+    assert mse[0] == np.float32(0.5) and mse[1] == 0.0 and mse[2] == 0.0
