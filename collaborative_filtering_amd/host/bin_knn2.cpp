@@ -1,0 +1,63 @@
+// knn2 -- drop-in for knn2.cpp (a10): cosine item weights on the out_edg_ edges from
+// the out_rat_ train maps; writes out_fin_ "a b w" for w > 0.01 (knn2.cpp:151-164).
+// The weights come from cf_item_cosine (int8 / fp32 MFMA over all item pairs); the
+// writer keeps exactly the out_edg_ edges, in out_edg_ order per source.
+#include <cstdio>
+
+#include "cf_cli.hpp"
+
+int main(int argc, char** argv) {
+    const int nshards = std::stoi(cfcli::opt(argc, argv, "nshards", "4"));
+    cfio::VertexRatings rat = cfio::load_vertex_ratings(".", "out_rat_", false);   // :79-102
+    auto edges = cfio::load_adjacency(".", "out_edg_");                            // :104-121
+    std::vector<uint32_t> all;
+    for (auto& kv : rat) all.push_back(kv.first);
+    for (auto& e : edges) {
+        all.push_back(e.first);
+        all.push_back(e.second);
+    }
+    cfio::IdMap items;
+    items.build(all);
+    // per-user train CSR over compact items
+    std::vector<uint32_t> uids;
+    for (auto& kv : rat)
+        for (auto& ur : kv.second) uids.push_back(ur.first);
+    cfio::IdMap users;
+    users.build(uids);
+    std::vector<uint64_t> off(users.size() + 1, 0);
+    for (auto& kv : rat)
+        for (auto& ur : kv.second) off[users.at[ur.first] + 1]++;
+    for (uint32_t u = 0; u < users.size(); ++u) off[u + 1] += off[u];
+    std::vector<uint32_t> it(off.back());
+    std::vector<float> r(off.back());
+    std::vector<uint64_t> fill(off.begin(), off.end() - 1);
+    for (auto& kv : rat)
+        for (auto& ur : kv.second) {
+            const uint64_t p = fill[users.at[ur.first]]++;
+            it[p] = items.at[kv.first];
+            r[p] = (float)ur.second;
+        }
+    const uint32_t n = items.size();
+    std::vector<float> W((size_t)n * n);
+    cf_ctx* ctx = cfcli::open_device();
+    cfcli::check(ctx, cf_item_cosine(ctx, users.size(), n, off.data(), it.data(), r.data(), 0.01f, 5, 0, W.data()),
+                 "cf_item_cosine");
+    cf_destroy(ctx);
+    cfio::ShardWriter fin(".", "out_fin", nshards);
+    size_t written = 0;
+    for (auto& e : edges) {
+        const float w = W[(size_t)items.at[e.first] * n + items.at[e.second]];
+        if (!(w > 0.0f)) continue;
+        std::string& out = fin.shard(e.first);
+        cfio::append_u(out, e.first);
+        out += ' ';
+        cfio::append_u(out, e.second);
+        out += ' ';
+        cfio::append_g(out, (double)w);
+        out += '\n';
+        ++written;
+    }
+    fin.flush();
+    std::printf("Wrote %zu out_fin_ edges of %zu out_edg_ edges\n", written, edges.size());
+    return 0;
+}

@@ -1,0 +1,130 @@
+// local_calc_precomp -- drop-in for local_calc_precomp.cpp (a6, a7).
+//   :406-482 load_precomputed_data("out_eigen_") incl. the accumulating sigs_min
+//            vector (:414,437,440): user n sees the concatenation of every record's
+//            sigs up to its own, so w_lim for row r is the r-th sig of the whole file
+//   :122-136 out_fin_ edges (out-neighbour iff float weight > 0.1)
+//   :138-160 out_test_rat_ vertices
+//   :217-380 neigh_program::apply per test rating -> cf_predict_precomp (HIP, fp64)
+//   :393-404 writer "movie user mse kk" -> out_res_<i>_of_<N>
+// Options: --pct P (percent of movie vertices, sampled like rand()%100 < P; default
+// 100), --seed S (default: time, as the reference), --compat ref|fixed (fixed = each
+// user's own sigs), --verbosity (accepted, ignored), --nshards N.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <limits>
+#include <ctime>
+#include <map>
+#include <random>
+
+#include "cf_cli.hpp"
+
+int main(int argc, char** argv) {
+    int pct = std::stoi(cfcli::opt(argc, argv, "pct", "100"));
+    if (argc > 1 && argv[1][0] != '-') pct = std::atoi(argv[1]);   // positional pct (:495)
+    const std::string compat = cfcli::opt(argc, argv, "compat", "ref");
+    const unsigned seed = (unsigned)std::stoul(cfcli::opt(argc, argv, "seed", std::to_string((unsigned)std::time(nullptr))));
+    const int nshards = std::stoi(cfcli::opt(argc, argv, "nshards", "4"));
+    const std::string eig_path = cfcli::opt(argc, argv, "eigen", "out_eigen_");
+
+    std::vector<cfio::EigenRecord> recs = cfio::load_eigen_file(eig_path);
+    std::printf("Loaded %zu test users\n", recs.size());
+    auto edges = cfio::load_edges(".", "out_fin_");
+    for (auto& e : edges) e.w = (double)(float)e.w;   // parsed as float (:129)
+    cfio::VertexRatings test = cfio::load_vertex_ratings(".", "out_test_rat_", true);
+
+    std::vector<uint32_t> all;
+    for (auto& e : edges) {
+        all.push_back(e.a);
+        all.push_back(e.b);
+    }
+    for (auto& kv : test) all.push_back(kv.first);
+    for (auto& r : recs) all.insert(all.end(), r.movies.begin(), r.movies.end());
+    cfio::IdMap items;
+    items.build(all);
+
+    // user -> (movie -> test rating), for the rating vectors of the blocks
+    std::unordered_map<uint32_t, std::unordered_map<uint32_t, double>> urat;
+    for (auto& kv : test)
+        for (auto& ur : kv.second) urat[ur.first][kv.first] = ur.second;
+
+    const uint32_t n_users = (uint32_t)recs.size();
+    std::vector<uint64_t> off(n_users + 1, 0), eoff(n_users);
+    std::vector<uint32_t> its;
+    std::vector<float> rats;
+    std::vector<int32_t> m(n_users);
+    std::vector<double> evals, evecs, own_sigs, concat;
+    std::unordered_map<uint32_t, uint32_t> rec_of_user;
+    uint64_t eacc = 0;
+    for (uint32_t u = 0; u < n_users; ++u) {
+        const auto& r = recs[u];
+        const uint32_t k = (uint32_t)r.movies.size();
+        if (k > CF_MAX_K) cfcli::die("record with k > 192 is outside the supported buckets");
+        rec_of_user[r.user] = u;   // a later record of the same user replaces it (:472)
+        m[u] = (int32_t)r.evals.size();
+        auto& ur = urat[r.user];
+        for (uint32_t j = 0; j < k; ++j) {
+            its.push_back(items.at[r.movies[j]]);
+            auto it = ur.find(r.movies[j]);
+            rats.push_back(it == ur.end() ? 0.0f : (float)it->second);   // operator[] default 0 (:259)
+            evals.push_back(j < r.evals.size() ? r.evals[j] : 0.0);
+            own_sigs.push_back(r.sigs[j]);
+        }
+        concat.insert(concat.end(), r.sigs.begin(), r.sigs.end());
+        off[u + 1] = its.size();
+        eoff[u] = eacc;
+        evecs.insert(evecs.end(), r.evecs.begin(), r.evecs.end());
+        eacc += r.evecs.size();
+    }
+    if (evecs.empty()) evecs.push_back(0.0);
+    const bool ref = compat != "fixed";
+    std::vector<float> mse(its.size());
+    std::vector<int32_t> kk(its.size());
+    cf_ctx* ctx = cfcli::open_device();
+    cfcli::upload_edges(ctx, items, edges);
+    if (n_users)
+        cfcli::check(ctx, cf_predict_precomp(ctx, n_users, off.data(), its.data(), rats.data(), m.data(), evals.data(),
+                                             eoff.data(), evecs.data(), ref ? concat.data() : own_sigs.data(),
+                                             ref ? concat.size() : own_sigs.size(),
+                                             ref ? CF_SIGS_COMPAT : CF_SIGS_OWN, mse.data(), kk.data(), nullptr),
+                     "cf_predict_precomp");
+    cf_destroy(ctx);
+
+    // rows per test movie vertex (:230-361), sampled per vertex (:221)
+    std::mt19937 rng(seed);
+    std::map<uint32_t, std::vector<std::pair<uint32_t, double>>> movies(test.begin(), test.end());
+    cfio::ShardWriter res(".", "out_res", nshards);
+    size_t rows = 0, missing = 0;
+    for (auto& kv : movies) {
+        if ((unsigned)(rng() % 100) >= (unsigned)pct) continue;
+        const uint32_t movie = kv.first;
+        std::string& out = res.shard(movie);
+        for (auto& ur : kv.second) {
+            float e = std::numeric_limits<float>::quiet_NaN();
+            int32_t c = 0;
+            auto ri = rec_of_user.find(ur.first);
+            if (ri != rec_of_user.end()) {
+                const auto& r = recs[ri->second];
+                for (uint32_t j = 0; j < r.movies.size(); ++j)
+                    if (r.movies[j] == movie) {
+                        e = mse[off[ri->second] + j];
+                        c = kk[off[ri->second] + j];
+                        break;
+                    }
+            }
+            if (c == 0 && std::isnan(e)) ++missing;
+            cfio::append_u(out, movie);   // "movie user mse kk" (:397-399)
+            out += ' ';
+            cfio::append_u(out, ur.first);
+            out += ' ';
+            cfio::append_g(out, (double)e);
+            out += ' ';
+            cfio::append_u(out, (uint32_t)c);
+            out += '\n';
+            ++rows;
+        }
+    }
+    res.flush();
+    std::printf("Wrote %zu predictions (%zu without a connected item) to out_res_*\n", rows, missing);
+    return 0;
+}

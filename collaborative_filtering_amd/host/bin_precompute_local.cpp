@@ -1,0 +1,91 @@
+// precompute_local -- drop-in for precompute_local_threads.cpp (a1-a5; the
+// run_test_precompute.sh stage `./precompute_local 8`).
+//   :230-250 load movielens/*.validate -> users[uimax - uid][movie]
+//   :253-293 load out_fin_* -> item weights (directed, as parsed; last duplicate wins)
+//   :100-213 compute_eigens per user  -> cf_eigen_batch (HIP, one workgroup per user)
+//   :196-211 append "uid k m / evals / evecs" records to out_eigen_ (truncated first)
+// Differences (documented in DESIGN.md): the item graph is dense over the compact id
+// space of all ids seen (the reference's 2000x2000 matrix is only defined for ids
+// < 2000); users are written in ascending uid order with their movies ascending (the
+// reference's order is boost::unordered_map order); k is limited to 192 per user.
+#include <cstdio>
+#include <fstream>
+#include <map>
+
+#include "cf_cli.hpp"
+
+int main(int argc, char** argv) {
+    if (argc < 2) {   // (:217-220)
+        std::printf("Usage:\n%s n_threads\n", argv[0]);
+        return 1;
+    }
+    const std::string out_path = cfcli::opt(argc, argv, "output", "out_eigen_");
+    std::map<uint32_t, std::map<uint32_t, double>> users;
+    for (const auto& path : cfio::files_with_suffix("movielens/", ".validate")) {
+        std::printf("Reading file: %s\n", path.c_str());
+        std::string text = cfio::read_file(path);
+        size_t pos = 0;
+        while (pos < text.size()) {
+            size_t nl = text.find('\n', pos);
+            if (nl == std::string::npos) nl = text.size();
+            unsigned long u, m;
+            double r;
+            if (std::sscanf(text.c_str() + pos, "%lu %lu %lf", &u, &m, &r) >= 2)
+                users[cfio::kUimax - (uint32_t)u][(uint32_t)m] = r;
+            pos = nl + 1;
+        }
+    }
+    auto edges = cfio::load_edges(".", "out_fin_");
+    std::ofstream(out_path, std::ofstream::out).close();   // truncate (:289-290)
+    std::vector<uint32_t> all;
+    for (auto& e : edges) {
+        all.push_back(e.a);
+        all.push_back(e.b);
+    }
+    for (auto& kv : users)
+        for (auto& mr : kv.second) all.push_back(mr.first);
+    cfio::IdMap items;
+    items.build(all);
+    std::printf("Number of movies: %u\nNumber of users: %zu\n", items.size(), users.size());
+
+    const uint32_t n_users = (uint32_t)users.size();
+    std::vector<uint64_t> off(n_users + 1, 0);
+    std::vector<uint32_t> uid(n_users), its, movies;
+    uint32_t u = 0;
+    for (auto& kv : users) {
+        uid[u] = kv.first;
+        for (auto& mr : kv.second) {   // ascending movie id == ascending compact id
+            its.push_back(items.at[mr.first]);
+            movies.push_back(mr.first);
+        }
+        off[++u] = its.size();
+        if (kv.second.size() > CF_MAX_K)
+            cfcli::die("user " + std::to_string(kv.first) + " rated " + std::to_string(kv.second.size()) +
+                       " movies; the LDS eigen path supports k <= 192");
+    }
+    std::vector<uint64_t> eoff(n_users);
+    const uint64_t n_evec = cf_evec_offsets(n_users, off.data(), eoff.data());
+    std::vector<int32_t> m(n_users);
+    std::vector<float> sigs(off.back()), evals(off.back()), evecs(std::max<uint64_t>(n_evec, 1));
+    cf_ctx* ctx = cfcli::open_device();
+    cfcli::upload_edges(ctx, items, edges);
+    cfcli::check(ctx, cf_eigen_batch(ctx, n_users, off.data(), its.data(), eoff.data(), m.data(), sigs.data(),
+                                     evals.data(), evecs.data()),
+                 "cf_eigen_batch");
+    cf_destroy(ctx);
+    std::string out;
+    out.reserve(1 << 20);
+    std::ofstream f(out_path, std::ofstream::out | std::ofstream::app | std::ofstream::binary);
+    for (uint32_t i = 0; i < n_users; ++i) {
+        const uint32_t k = (uint32_t)(off[i + 1] - off[i]);
+        cfio::append_eigen_record(out, uid[i], k, (uint32_t)m[i], movies.data() + off[i], sigs.data() + off[i],
+                                  evals.data() + off[i], evecs.data() + eoff[i]);
+        if (out.size() > (64u << 20)) {
+            f.write(out.data(), (std::streamsize)out.size());
+            out.clear();
+        }
+    }
+    f.write(out.data(), (std::streamsize)out.size());
+    std::printf("Wrote %u eigen records to %s\n", n_users, out_path.c_str());
+    return 0;
+}

@@ -1,0 +1,91 @@
+// cf_io.hpp -- the reference's CWD text-file contract in C++.
+//
+// Files are whitespace-separated ASCII; numbers use the iostream defaults of the
+// reference (%g, 6 significant digits).  GraphLab's graph.save writes
+// "<prefix>_<i>_of_<N>" shards (evidence: extract_user.py:7-10); the shard a vertex
+// lands in is unpinned upstream, here it is (id % N) + 1 and lines are in ascending
+// id order.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace cfio {
+
+constexpr uint32_t kUimax = 2147483647u;  // std::numeric_limits<int>::max() as unsigned (knn.cpp:19)
+
+// Sorted regular files in `dir` whose name ends with / starts with the given string
+// (list_files_with_suffix / _prefix, precompute_local_threads.cpp:42-87).
+std::vector<std::string> files_with_suffix(const std::string& dir, const std::string& suffix);
+std::vector<std::string> files_with_prefix(const std::string& dir, const std::string& prefix);
+std::string read_file(const std::string& path);
+
+// %g with precision 6, exactly as `std::ostream << double` with default flags.
+void append_g(std::string& out, double v);
+void append_u(std::string& out, uint64_t v);
+
+// A movielens rating triplet (user id already remapped to uimax - uid where asked).
+struct Rating {
+    uint32_t user;
+    uint32_t movie;
+    double value;
+    bool validate;
+};
+
+// movielens/*: role VALIDATE if the file name ends with ".validate", else TRAIN
+// (knn.cpp:88-92); source id remapped to uimax - id (knn.cpp:103).
+std::vector<Rating> load_movielens(const std::string& dir, bool remap_users);
+
+// Per-vertex lines "id a b a b ..." (out_rat_, out_test_rat_): id -> [(user, rating)].
+using VertexRatings = std::unordered_map<uint32_t, std::vector<std::pair<uint32_t, double>>>;
+VertexRatings load_vertex_ratings(const std::string& dir, const std::string& prefix,
+                                  bool require_nonempty);
+
+// Edge lines "a b w" (out_fin_).  Keeps the last occurrence of a duplicate pair.
+struct Edge {
+    uint32_t a, b;
+    double w;
+};
+std::vector<Edge> load_edges(const std::string& dir, const std::string& prefix);
+
+// Adjacency lines "a b c d ..." (out_edg_).
+std::vector<std::pair<uint32_t, uint32_t>> load_adjacency(const std::string& dir,
+                                                          const std::string& prefix);
+
+// Sharded writer: line for vertex `id` goes to <prefix>_<(id % n)+1>_of_<n>.
+class ShardWriter {
+   public:
+    ShardWriter(const std::string& dir, const std::string& prefix, int nshards);
+    std::string& shard(uint32_t id) { return buf_[id % buf_.size()]; }
+    void flush();
+
+   private:
+    std::string dir_, prefix_;
+    std::vector<std::string> buf_;
+};
+
+// Compact id space: sorted unique ids -> 0..n-1.
+struct IdMap {
+    std::vector<uint32_t> ids;                 // compact -> id
+    std::unordered_map<uint32_t, uint32_t> at; // id -> compact
+    void build(std::vector<uint32_t> all);
+    uint32_t size() const { return (uint32_t)ids.size(); }
+};
+
+// out_eigen_ record (README.md:14-19; precompute_local_threads.cpp:196-210).
+struct EigenRecord {
+    uint32_t user = 0;
+    std::vector<uint32_t> movies;   // row order of the block
+    std::vector<double> sigs;
+    std::vector<double> evals;      // m values
+    std::vector<double> evecs;      // k*m row-major
+};
+void append_eigen_record(std::string& out, uint32_t user, uint32_t k, uint32_t m,
+                         const uint32_t* movies, const float* sigs, const float* evals,
+                         const float* evecs);
+// load_precomputed_data (local_calc_precomp.cpp:406-482): the 3-line state machine.
+std::vector<EigenRecord> load_eigen_file(const std::string& path);
+
+}  // namespace cfio

@@ -1,0 +1,176 @@
+"""Drop-in pipeline on the GPU: the stage sequence of run_test_precompute.sh:10-19
+(knn -> knn2 -> precompute_local 8 -> local_calc_precomp) plus knn3, through the
+rebuild's binaries in a scratch working directory; every text file a stage writes is
+checked against the oracle run on the text file the stage read."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_ref as orc
+import pipeline_util as pu
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "bin")
+
+
+def run(workdir, *args):
+    p = subprocess.run([os.path.join(BIN, args[0]), *args[1:]], cwd=workdir, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    return p.stdout
+
+
+@pytest.fixture(scope="module")
+def work(tmp_path_factory):
+    if not __import__("torch").cuda.is_available():
+        pytest.skip("no GPU visible")
+    wd = str(tmp_path_factory.mktemp("cwd"))
+    pu.write_movielens(wd, seed=11)
+    return wd
+
+
+def movielens_ratings(wd):
+    train, test = {}, {}
+    for name, dst in [("u0.train", train), ("u0.validate", test)]:
+        for ln in open(os.path.join(wd, "movielens", name)):
+            u, m, r = ln.split()
+            dst.setdefault(int(m), {})[pu.UIMAX - int(u)] = float(r)
+    return train, test
+
+
+def test_stage_knn(work):
+    run(work, "knn")
+    train, test = movielens_ratings(work)
+    rat = pu.parse_vertex_ratings(pu.read_shards(work, "out_rat_"))
+    trat = pu.parse_vertex_ratings(pu.read_shards(work, "out_test_rat_"))
+    movies = set(train) | set(test)
+    assert set(rat) == movies and set(trat) == movies
+    for m in movies:
+        assert rat[m] == train.get(m, {}) and trat[m] == test.get(m, {})
+    # co-rated lists: train and validate roles both count (knn.cpp:224-227)
+    per_user = {}
+    for src in (train, test):
+        for m, ur in src.items():
+            for u in ur:
+                per_user.setdefault(u, set()).add(m)
+    expect = {m: set() for m in movies}
+    for ms in per_user.values():
+        for a in ms:
+            expect[a] |= ms - {a}
+    got = {}
+    for ln in pu.read_shards(work, "out_edg_"):
+        t = [int(x) for x in ln.split()]
+        got[t[0]] = t[1:]
+        assert t[1:] == sorted(set(t[1:]))
+    assert {m: set(v) for m, v in got.items()} == expect
+
+
+def test_stage_knn2(work):
+    run(work, "knn2")
+    rat = pu.parse_vertex_ratings(pu.read_shards(work, "out_rat_"))
+    fin = pu.parse_edges(pu.read_shards(work, "out_fin_"))
+    ids = sorted(rat)
+    at = {m: i for i, m in enumerate(ids)}
+    users = sorted({u for ur in rat.values() for u in ur})
+    uat = {u: i for i, u in enumerate(users)}
+    per_user = [[] for _ in users]
+    for m, ur in rat.items():
+        for u, r in ur.items():
+            per_user[uat[u]].append((at[m], r))
+    off, it, rr = [0], [], []
+    for lst in per_user:
+        lst.sort()
+        it += [x[0] for x in lst]
+        rr += [x[1] for x in lst]
+        off.append(len(it))
+    W, _ = orc.knn2(np.array(off), np.array(it), np.array(rr), len(ids))
+    edg = set()
+    for ln in pu.read_shards(work, "out_edg_"):
+        t = [int(x) for x in ln.split()]
+        edg |= {(t[0], b) for b in t[1:]}
+    expect = {(a, b): float(f"{W[at[a], at[b]]:g}") for (a, b) in edg if W[at[a], at[b]] > 0}
+    assert len(expect) > 100
+    assert fin == expect   # text-identical weights and edge set (integer ratings: bit-exact)
+
+
+def test_stage_precompute_local(work):
+    run(work, "precompute_local", "8")
+    recs = pu.parse_eigen(os.path.join(work, "out_eigen_"))
+    fin = pu.parse_edges(pu.read_shards(work, "out_fin_"))
+    _, test = movielens_ratings(work)
+    assert sorted(r["user"] for r in recs) == sorted({u for ur in test.values() for u in ur})
+    bad = []
+    for r in recs:
+        mv = r["movies"]
+        Wu = np.array([[fin.get((a, b), 0.0) for b in mv] for a in mv])
+        m, sigs, ev, U, L2 = orc.compute_eigens(Wu)
+        k = len(mv)
+        if not np.allclose(r["sigs"], sigs, rtol=1e-5):
+            bad.append((r["user"], "sigs"))
+        full, V = orc.eigh(orc.sym_lower(L2))
+        if len(r["evals"]) != m:
+            smm = np.float32(np.float32(np.max(sigs - 0.01)) + 0.01)
+            if not np.any(np.abs(full - smm) <= 1e-5):
+                bad.append((r["user"], "m", len(r["evals"]), m))
+            continue
+        if k == 1:
+            continue
+        f = orc.compare_eigen_block(L2, m, full, V[:, :m], m, r["evals"], r["U"], ev_tol=2e-5, res_tol=2e-4)
+        if f:
+            bad.append((r["user"], f))
+    assert not bad, bad[:5]
+
+
+def test_stage_local_calc_precomp(work):
+    run(work, "local_calc_precomp", "--pct", "100", "--seed", "1")
+    res = pu.parse_res(pu.read_shards(work, "out_res_"))
+    recs = pu.parse_eigen(os.path.join(work, "out_eigen_"))
+    fin = pu.parse_edges(pu.read_shards(work, "out_fin_"))
+    trat = pu.parse_vertex_ratings(pu.read_shards(work, "out_test_rat_"))
+    ids = sorted({a for e in fin for a in e} | set(trat) | {m for r in recs for m in r["movies"]})
+    at = {m: i for i, m in enumerate(ids)}
+    W = np.zeros((len(ids), len(ids)), np.float32)
+    for (a, b), w in fin.items():
+        W[at[a], at[b]] = np.float32(w)
+    concat = np.concatenate([r["sigs"] for r in recs])   # the accumulating sigs_min table
+    n_rows = sum(len(v) for v in trat.values())
+    assert len(res) == n_rows
+    good = 0
+    for r in recs:
+        items = np.array([at[m] for m in r["movies"]])
+        rat = np.array([trat[m].get(r["user"], 0.0) for m in r["movies"]], np.float32)
+        mse, kk, _ = orc.predict_user(items, rat.astype(np.float64), r["evals"], r["U"], concat[: len(items)], W)
+        for j, m in enumerate(r["movies"]):
+            g_mse, g_kk = res[(m, r["user"])]
+            assert g_kk == kk[j]
+            if kk[j] == 0:
+                assert np.isnan(g_mse) and np.isnan(mse[j])
+            elif np.isfinite(mse[j]) and abs(g_mse - mse[j]) <= 1e-5 * max(1, mse[j]):
+                good += 1
+    assert good >= 0.5 * n_rows, (good, n_rows)
+
+
+def test_stage_knn3(work):
+    out = run(work, "knn3")
+    avg = float(out.strip().split("Knn Average MSE:")[1])
+    fin = pu.parse_edges(pu.read_shards(work, "out_fin_"))
+    trat = pu.parse_vertex_ratings(pu.read_shards(work, "out_test_rat_"))
+    ids = sorted({a for e in fin for a in e} | set(trat))
+    at = {m: i for i, m in enumerate(ids)}
+    W = np.zeros((len(ids), len(ids)), np.float32)
+    for (a, b), w in fin.items():
+        W[at[a], at[b]] = np.float32(w)
+    mo, us, rs = [0], [], []
+    for m in ids:
+        ur = sorted(trat.get(m, {}).items())
+        us += [u for u, _ in ur]
+        rs += [x for _, x in ur]
+        mo.append(len(us))
+    _, mse = orc.knn3(W, np.array(mo), np.array(us), np.array(rs))
+    verts = {a for (a, b), w in fin.items() if np.float32(w) > 0.1} | {b for (a, b), w in fin.items()
+                                                                       if np.float32(w) > 0.1} | set(trat)
+    expect = np.float32(mse.sum(dtype=np.float32) / np.float32(len(verts)))
+    assert abs(avg - expect) <= 1e-5 * max(1.0, abs(expect))
