@@ -54,11 +54,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("CF_DIST_BACKEND", "nccl")   # "gloo" only to rehearse N>1 on one GPU
+    dev_index = local_rank % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", dev_index)
 
     from collaborative_filtering_amd import synth
     from collaborative_filtering_amd.api import CF_SIGS_COMPAT, Context, evec_offsets
@@ -72,7 +77,7 @@ def main():
     evec_off, n_evec = evec_offsets(off)
     n_entries = int(off[-1])
 
-    ctx = Context(local_rank)
+    ctx = Context(dev_index)
     ctx.upload_graph_dense(W)
     plan = ctx.plan(off)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
@@ -124,9 +129,31 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        coll_dev = dev if backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # Final gather of the eigen blocks (out_eigen_ content) to rank 0 over RCCL p2p,
+    # once, outside the timed steps (the only exchange step of the path).
+    gather = None
+    if world > 1:
+        from collaborative_filtering_amd.multi import exchange_counts, gather_to_rank0
+
+        coll_dev = dev if backend == "nccl" else torch.device("cpu")
+        parts = [d_m, d_sigs, d_evals, d_evecs]
+        parts = [p_ if backend == "nccl" else p_.cpu() for p_ in parts]
+        counts = exchange_counts([p_.numel() for p_ in parts], device=coll_dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter()
+        got = gather_to_rank0(parts, counts)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        gsec = time.perf_counter() - tg
+        gbytes = float(sum(counts[r][i] * parts[i].element_size() for r in range(1, world) for i in range(len(parts))))
+        gather = {"gather_eigen_ms": gsec * 1e3, "bytes_to_rank0": gbytes, "GBps": gbytes / gsec / 1e9,
+                  "users_gathered": int(got[0].numel()) if got is not None else None}
 
     # Per-stage durations (separate, event-bracketed passes; outside the timed region).
     for _ in range(max(2, args.steps)):
@@ -193,6 +220,7 @@ def main():
             "algorithmic_bytes_per_stage": bytes_eig,
             "algorithmic_GBps": bytes_eig / eig_s / 1e9,
         },
+        "gather": gather,
         "setup_s": setup_s,
         "m_mean": float(m_h.mean()),
         "kk_mean": float(kk_h.mean()),

@@ -1,0 +1,79 @@
+"""Multi-GPU sharding of the eigen / predict stages.
+
+Users are independent through compute_eigens and neigh_program::apply, so each rank
+(one process per GPU, torch.distributed over RCCL/xGMI) owns a contiguous range of
+users chosen by cumulative cost (sum of k^3: both stages are cubic in the user's item
+count), runs both stages locally, and the only exchange is the final gather of the
+variable-size eigen blocks to rank 0 for the out_eigen_ file: per-peer send/recv
+posted together (batch_isend_irecv), so rank 0 ingests on all xGMI links at once
+instead of through a ring.  The reference instead replicates out_eigen_ on every
+rank and partitions by movie (local_calc_precomp.cpp:509, GraphLab finalize).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def cost_split(k: np.ndarray, world: int) -> np.ndarray:
+    """Split points (world + 1 user indices) balancing sum(k^3) over contiguous ranges."""
+    k = np.asarray(k, dtype=np.float64)
+    if world <= 1 or len(k) == 0:
+        return np.array([0, len(k)], dtype=np.int64) if world <= 1 else \
+            np.zeros(world + 1, dtype=np.int64)
+    cum = np.concatenate([[0.0], np.cumsum(k ** 3)])
+    targets = cum[-1] * np.arange(1, world) / world
+    cuts = np.searchsorted(cum, targets, side="left")
+    out = np.concatenate([[0], cuts, [len(k)]]).astype(np.int64)
+    return np.maximum.accumulate(out)
+
+
+def local_slice(item_off: np.ndarray, lo: int, hi: int):
+    """Re-based item_off of users [lo, hi) and the entry range they cover."""
+    item_off = np.asarray(item_off, dtype=np.uint64)
+    b, e = int(item_off[lo]), int(item_off[hi])
+    return (item_off[lo:hi + 1] - np.uint64(b)).astype(np.uint64), b, e
+
+
+def gather_to_rank0(tensors, counts_per_rank, group=None):
+    """Variable-size gather of 1-D tensors to rank 0 with per-peer p2p (one group).
+
+    tensors: this rank's list of 1-D tensors (same dtypes on every rank).
+    counts_per_rank: [world][len(tensors)] element counts (every rank knows them).
+    Returns, on rank 0, the list of concatenations in rank order; None elsewhere.
+    """
+    import torch
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    if rank != 0:
+        ops = [dist.P2POp(dist.isend, t.contiguous(), 0, group) for t in tensors if t.numel()]
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return None
+    bufs = [[None] * len(tensors) for _ in range(world)]
+    ops = []
+    for r in range(world):
+        for i, t in enumerate(tensors):
+            n = int(counts_per_rank[r][i])
+            if r == 0:
+                bufs[r][i] = t
+                continue
+            bufs[r][i] = torch.empty(n, dtype=t.dtype, device=t.device)
+            if n:
+                ops.append(dist.P2POp(dist.irecv, bufs[r][i], r, group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return [torch.cat([bufs[r][i] for r in range(world)]) for i in range(len(tensors))]
+
+
+def exchange_counts(local_counts, device=None):
+    """all_gather of this rank's element counts -> [world][n] numpy int64."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor(list(local_counts), dtype=torch.int64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return np.stack([o.cpu().numpy() for o in out])
