@@ -88,13 +88,15 @@ class Context:
         self._chk(self.lib.cf_set_jacobi(self.h, tol_scale, max_sweeps), "cf_set_jacobi")
 
     def debug_stats(self, enable: bool = True, read: bool = False):
-        """Jacobi diagnostics: returns {sweeps_mean, users, sweeps_max, capped} when read."""
-        out = np.zeros(4, dtype=np.uint64) if read else None
+        """Jacobi diagnostics (sweeps, per-phase s_memtime cycles) when read."""
+        out = np.zeros(8, dtype=np.uint64) if read else None
         self._chk(self.lib.cf_debug_stats(self.h, int(enable), ptr(out)), "cf_debug_stats")
         if read:
             n = max(int(out[1]), 1)
             return {"sweeps_mean": int(out[0]) / n, "users": int(out[1]), "sweeps_max": int(out[2]),
-                    "capped": int(out[3])}
+                    "capped": int(out[3]), "assembly_cyc_per_user": int(out[4]) / n,
+                    "jacobi_cyc_per_user": int(out[5]) / n, "epilogue_cyc_per_user": int(out[6]) / n,
+                    "jacobi_cyc_per_step": int(out[5]) / max(int(out[7]), 1)}
         return None
 
     def debug_phases(self, enable: bool = True, read: bool = False):

@@ -129,14 +129,14 @@ int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out4) {
     if (!ctx) return CF_EINVAL;
     CF_TRY(set_device(ctx));
     if (enable && !ctx->d_stats) {
-        if (hipMalloc(&ctx->d_stats, 4 * sizeof(unsigned long long)) != hipSuccess)
+        if (hipMalloc(&ctx->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess)
             return cf_set_error(ctx, CF_ENOMEM, "stats allocation");
-        CF_HIP_CHECK(ctx, hipMemset(ctx->d_stats, 0, 4 * sizeof(unsigned long long)));
+        CF_HIP_CHECK(ctx, hipMemset(ctx->d_stats, 0, 8 * sizeof(unsigned long long)));
     }
     if (out4 && ctx->d_stats) {
         CF_HIP_CHECK(ctx, hipDeviceSynchronize());
-        CF_HIP_CHECK(ctx, hipMemcpy(out4, ctx->d_stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-        CF_HIP_CHECK(ctx, hipMemset(ctx->d_stats, 0, 4 * sizeof(unsigned long long)));
+        CF_HIP_CHECK(ctx, hipMemcpy(out4, ctx->d_stats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        CF_HIP_CHECK(ctx, hipMemset(ctx->d_stats, 0, 8 * sizeof(unsigned long long)));
     }
     if (!enable && ctx->d_stats) {
         (void)hipFree(ctx->d_stats);

@@ -1,7 +1,7 @@
 // cf_eigen.hip -- batched per-user normalized-Laplacian eigendecomposition on gfx950.
 //
 // Replaces compute_eigens() of precompute_local_threads.cpp:100-213 (same math as
-// precompute_local.cpp:165-281).  One 256-thread workgroup owns one user:
+// precompute_local.cpp:165-281).  One workgroup (512 or 1024 threads) owns one user:
 //
 //   1. gather W_u(i,j) = graph[item_i][item_j] from the HBM-resident dense graph
 //      straight into LDS (k x k fp32, column-major, odd leading dimension);
@@ -13,9 +13,12 @@
 //      its singular values are its eigenvalues and the rotated columns of B are the
 //      eigenvectors scaled by (lambda + 1);
 //   4. one-sided (Hestenes) Jacobi sweeps in LDS: each step of a round-robin
-//      tournament rotates k/2 disjoint column pairs; a pair is owned by one DPP quad
-//      (4 lanes, float2 = ds_read_b64 per row pair, packed v_pk_fma_f32), whose three
-//      dot products are reduced with two DPP quad_perm steps;
+//      tournament rotates k/2 disjoint column pairs; a pair is owned by 8 lanes
+//      (float2 = ds_read_b64 per row pair, packed v_pk_fma_f32), whose three dot
+//      products are reduced with three DPP steps.  Each step reads and writes the
+//      whole k x k matrix, so the sweep is bound by LDS bandwidth (128 B/clk/CU),
+//      not by VALU issue: 2, 4 and 8 lanes per pair measured 3820, 2828 and 2727
+//      cycles per step (tools/probe_eigen.py, 20k users);
 //   5. lambda_j = ||b_j|| / ||v_j|| - 1 (||v_j|| tracks the fp32 rotation drift),
 //      rank sort ascending, lim (:184-191), write the k x m row-major block, sigs,
 //      evals and m.
@@ -26,7 +29,7 @@
 
 namespace {
 
-constexpr int kGroup = 4;   // lanes per column pair = one DPP quad
+constexpr int kGroup = 8;   // lanes per column pair (half a DPP row)
 
 using f2 = __attribute__((ext_vector_type(2))) float;
 
@@ -35,10 +38,11 @@ __device__ __forceinline__ float dpp_mov(float x) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
 }
 
-// All-reduce (sum) over the 4 lanes of a DPP quad; every lane receives the total.
-__device__ __forceinline__ float quad_sum(float x) {
+// All-reduce (sum) over the 8 lanes of a column pair; every lane receives the total.
+__device__ __forceinline__ float pair_sum(float x) {
     x += dpp_mov<0xB1>(x);   // quad_perm [1,0,3,2]
     x += dpp_mov<0x4E>(x);   // quad_perm [2,3,0,1]
+    x += dpp_mov<0x141>(x);  // row_half_mirror (lanes i <-> 7-i within 8)
     return x;
 }
 
@@ -60,16 +64,18 @@ struct EigenArgs {
 };
 
 // Bucket geometry: k <= NR = 16 * EMAX rows.  A column is read/written as float2
-// (ds_read_b64 / ds_write_b64): lane l of a quad owns rows 8t + 2l, 8t + 2l + 1.
-// LD == 8 (mod 64) floats: the 8 consecutive columns that the 8 quads of a half-wave
-// touch in one tournament step start in distinct 8-bank octants, so the b64 accesses
-// are conflict-free (MI355X_MICROARCH.md, LDS table: b64 bank = (a/4) mod 64).
+// (ds_read_b64 / ds_write_b64): lane l of a pair owns rows 16t + 2l, 16t + 2l + 1.
+// LD == 16 (mod 64) floats: the 4 consecutive columns that the 4 pairs of a
+// half-wave touch in one tournament step start in distinct 16-bank quarters, so the
+// b64 accesses are conflict-free (MI355X_MICROARCH.md, LDS table: b64 bank = (a/4) mod 64).
 template <int EMAX>
 struct EigenGeom {
     static constexpr int NR = 16 * EMAX;
-    static constexpr int E2 = NR / 8;                          // float2 chunks per lane
-    static constexpr int LD = NR + ((8 - NR) % 64 + 64) % 64;  // >= NR, == 8 mod 64
-    static constexpr int NT = (NR > 128) ? 512 : 256;          // 1 pass per step up to NT/4 pairs
+    static constexpr int E2 = NR / (2 * kGroup);               // float2 chunks per lane
+    // == 16 mod 64 where it fits in LDS; the k <= 192 bucket falls back to NR + 8
+    static constexpr int LD = (NR * (NR + ((16 - NR) % 64 + 64) % 64) + 9 * NR <= 40960 - 4)
+                                  ? NR + ((16 - NR) % 64 + 64) % 64 : NR + 8;
+    static constexpr int NT = (NR > 128) ? 1024 : 512;         // 1 pass per step up to NT/8 pairs
     static constexpr size_t bytes() {
         return sizeof(float) * (size_t)NR * LD     // B
                + sizeof(uint32_t) * NR             // items
@@ -102,6 +108,9 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     const int lane = tid & 63;
     const int wave = tid >> 6;
     constexpr int NW = NT / 64;
+    // diagnostics (stats != null): s_memtime per phase, thread 0, summed into stats[4..6]
+    unsigned long long t_phase0 = (a.stats && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
+    unsigned long long t_phase1 = 0, t_phase2 = 0;
     const uint32_t u = a.order[a.first + blockIdx.x];
     const uint64_t base = a.item_off[u];
     const int k = (int)(a.item_off[u + 1] - base);
@@ -155,6 +164,7 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     if (tid == 0) s_flag[0] = 0;
     __syncthreads();
 
+    if (a.stats && tid == 0) t_phase1 = __builtin_amdgcn_s_memtime();
     // ---- 4. one-sided Jacobi --------------------------------------------------------
     const int n = (k + 1) & ~1;          // players in the round-robin tournament
     const int npairs = n >> 1;
@@ -189,9 +199,9 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
                     be2 = __builtin_elementwise_fma(xq[t], xq[t], be2);
                     ga2 = __builtin_elementwise_fma(xp[t], xq[t], ga2);
                 }
-                const float al = quad_sum(al2.x + al2.y);
-                const float be = quad_sum(be2.x + be2.y);
-                const float ga = quad_sum(ga2.x + ga2.y);
+                const float al = pair_sum(al2.x + al2.y);
+                const float be = pair_sum(be2.x + be2.y);
+                const float ga = pair_sum(ga2.x + ga2.y);
                 if (ga * ga > tol2 * (al * be)) {
                     // Hardware rcp/rsq/sqrt: the rotation only has to annihilate ga well
                     // enough; its scale error (c^2 + s^2 != 1) is tracked exactly below.
@@ -227,6 +237,7 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
         if (tid == 0) s_flag[0] = 0;
         __syncthreads();
     }
+    if (a.stats && tid == 0) t_phase2 = __builtin_amdgcn_s_memtime();
     if (a.stats && tid == 0) {
         atomicAdd(&a.stats[0], (unsigned long long)(sweep + 1));
         atomicAdd(&a.stats[1], 1ull);
@@ -283,6 +294,13 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
             v = B[j * LD + i] * s_s[j];
         }
         out[idx] = v;
+    }
+    if (a.stats && tid == 0) {
+        const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+        atomicAdd(&a.stats[4], t_phase1 - t_phase0);
+        atomicAdd(&a.stats[5], t_phase2 - t_phase1);
+        atomicAdd(&a.stats[6], t3 - t_phase2);
+        atomicAdd(&a.stats[7], (unsigned long long)((sweep + 1) * (((k + 1) & ~1) - 1)));
     }
 }
 

@@ -57,9 +57,10 @@ const char* cf_last_error(const cf_ctx* ctx);
 /* Jacobi off-diagonal tolerance scale (default 1.0) and sweep cap (default 30). */
 int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
 /* Diagnostics: enable != 0 allocates device counters that the eigen kernel fills;
- * out4 (optional) receives and resets {sum of sweeps, users, max sweeps, users that
- * hit the sweep cap}.  enable == 0 frees them. */
-int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out4);
+ * out8 (optional) receives and resets {sum of sweeps, users, max sweeps, users that
+ * hit the sweep cap, assembly cycles, Jacobi cycles, epilogue cycles, tournament
+ * steps} (cycles: s_memtime of thread 0).  enable == 0 frees them. */
+int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out8);
 /* Diagnostics: predictor phase cycle totals (s_memtime, thread 0 of each block):
  * {connected set, lim + column filter, mean, Gram, LU, solve}. */
 int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out6);
