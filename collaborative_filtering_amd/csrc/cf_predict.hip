@@ -12,21 +12,45 @@
 //   pred = v_S . (U_CS^T U_CS)^-1 U_CS^T (r_C - mean) + mean          (:308-315)
 //   mse  = (float)(r - clamp(pred, 1, 5))^2, kk = |C|                 (:318-359)
 //
-// All arithmetic after the gather is fp64 (the reference's double path).  The
-// reference forms mm = U_CS^T U_CS and multiplies by its PartialPivLU inverse.  Here
-// the symmetric Gram matrix is factored M = L D L^T (blocked, right-looking, packed
-// lower triangle in LDS), bordered by t^T and v^T so the factorisation itself yields
-// L^-1 t and L^-1 v and pred = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean.  For a
-// well-conditioned M this agrees with the inverse-based formula to cond(M) * eps.
-// Like Gaussian elimination (and unlike Cholesky) LDL^T carries on through negative
-// pivots, so a numerically indefinite, near-singular M gives the same kind of
-// finite, clamped garbage as the reference instead of a NaN.
+// All arithmetic after the gather is fp64 (the reference's double path).
+//
+// Fast path (per user, then one wave per rating).  The prediction is the value at row
+// r of the least-squares fit of r_C - mean on span(U_CS): it depends on U_S only
+// through an orthonormal basis Q_S of its column span.  Once per user:
+//   Gbar = U^T U over the columns [0, Lu), Lu = max_r lim_r;  Gbar = L D L^T;
+//   Q = U L^-T D^-1/2 (Cholesky QR; the leading lim columns of Q span the leading lim
+//   columns of U, so one Q serves every row's prefix S = [0, lim));
+//   g = Q^T r, h = Q^T 1.
+// With P = Q_S Q_S^T (the k x k projector), Cbar = rows not in C (nc of them),
+// y = r - mean, and Q_S^T Q_S = I:
+//   pred - mean = a_r + P_{r,Cbar} K^-1 b,   K = I - P_{Cbar,Cbar}  (nc x nc),
+//   a_r = (P y)_r - P_{r,Cbar} y_Cbar,   b = (P y)_Cbar - P_{Cbar,Cbar} y_Cbar,
+// (Woodbury on U_CS^T U_CS = Q_S^T Q_S - Q_CbarS^T Q_CbarS), where (P y)_i =
+// Q_iS.g_S - mean Q_iS.h_S.  A rating therefore costs (nc + 3)^2 / 2 dot products of
+// length lim and an nc x nc LDL^T instead of a lim x lim factorisation.
+//
+// Dense path (block-wide, the rating's own Gram matrix) for the ratings the fast path
+// does not take: the column filter drops a column, nc > kNcMax, c = 0, a pivot of K
+// below kPivMin while c >= lim (full rank but ill-conditioned: U_CS^T U_CS has an
+// eigenvalue < kPivMin), or Q is not trusted that far (a D_j of Gbar below half of
+// Gbar_jj: U is not near-orthonormal).
+// It factors M = U_CS^T U_CS = L D L^T (blocked, right-looking, packed lower triangle
+// in LDS), bordered by t^T and v^T so the factorisation itself yields L^-1 t and
+// L^-1 v and pred = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean.  When the complement is
+// smaller it forms M as Gbar_SS - sum_{i not in C} u_i u_i^T.  Like Gaussian
+// elimination (and unlike Cholesky) LDL^T carries on through negative pivots, so a
+// numerically indefinite, near-singular M gives the same kind of finite, clamped
+// garbage as the reference's inverse (:314) instead of a NaN.
 
 #include "cf_internal.h"
 
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int kNcMax = 62;            // fast path: nc + 2 border rows <= 64 lanes
+constexpr double kPivMin = 1e-6;      // fast path: smallest pivot of K = I - P_CbarCbar
+constexpr double kBasisMin = 0.5;     // D_j / Gbar_jj below this: Q not trusted from j on
 
 template <typename T>
 struct PredArgs {
@@ -48,7 +72,11 @@ struct PredArgs {
     double* pred;
     unsigned long long* phase_cycles;  // diagnostics: per-phase s_memtime totals (or null)
     int lmax;              // Gram dimension bound of the launch
+    int ncw;               // fast-path bound on nc for this launch
+    int ew;                // doubles of per-wave fast-path scratch
+    int a_elems;           // doubles of the shared factorisation / scratch region
     double* gbar;          // per-block scratch: Gbar = U^T U (lmax x lmax, full), fp64
+    double* qs;            // per-block scratch: Q ((lmax + 2) x lmax rows: Q, g, h), fp64
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -83,28 +111,191 @@ __device__ __forceinline__ int tri(int i, int j) { return (i * (i + 1)) / 2 + j;
         __builtin_amdgcn_wave_barrier();                         \
     } while (0)
 
-constexpr int kNB = 16;   // Cholesky panel width
+constexpr int kNB = 16;   // LDL^T panel width
+
+// Blocked right-looking LDL^T of the leading L x L block of the packed lower triangle
+// A (rows [0, nrows), nrows >= L), carrying rows [L, nrows) as border rows: on return
+// A holds unit-lower L below the diagonal, D on it, and border row i holds
+// (L^-1 a_i)_j / D_j.  Called by the whole block; starts and ends synchronised.
+__device__ void ldlt_bordered(double* A, int L, int nrows) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    for (int kb = 0; kb < L; kb += kNB) {
+        const int b = min(kNB, L - kb);
+        // (1) diagonal block, unblocked LDL^T, in wave 0's registers: lane i < b holds
+        //     row kb + i; column j is broadcast by shuffles.
+        if (wave == 0) {
+            double rowv[kNB];
+            const int i = lane;
+            const bool live = i < b;
+#pragma unroll
+            for (int q = 0; q < kNB; ++q) rowv[q] = (live && q <= i) ? A[tri(kb + i, kb + q)] : 0.0;
+#pragma unroll
+            for (int j = 0; j < kNB; ++j) {
+                if (j < b) {
+                    const double dj = __shfl(rowv[j], j);
+                    const double w = (i > j) ? rowv[j] : 0.0;   // unscaled a_ij
+                    const double lij = w / dj;
+#pragma unroll
+                    for (int q = j + 1; q < kNB; ++q) {
+                        const double wq = __shfl(w, q);
+                        if (q <= i) rowv[q] = fma(-lij, wq, rowv[q]);
+                    }
+                    if (i > j) rowv[j] = lij;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kNB; ++q)
+                if (live && q <= i) A[tri(kb + i, kb + q)] = rowv[q];
+        }
+        __syncthreads();
+        // (2) panel: rows below the block (incl. the border rows) solve against L11^T
+        for (int i = kb + b + tid; i < nrows; i += kThreads) {
+            double* Ai = A + tri(i, kb);
+            double x[kNB];
+#pragma unroll
+            for (int jj = 0; jj < kNB; ++jj) x[jj] = jj < b ? Ai[jj] : 0.0;
+#pragma unroll
+            for (int jj = 0; jj < kNB; ++jj) {
+                if (jj < b) {
+                    const double* Aj = A + tri(kb + jj, kb);
+                    double sacc = x[jj];
+#pragma unroll
+                    for (int q = 0; q < jj; ++q) sacc = fma(-x[q] * A[tri(kb + q, kb + q)], Aj[q], sacc);
+                    x[jj] = sacc / Aj[jj];
+                }
+            }
+#pragma unroll
+            for (int jj = 0; jj < kNB; ++jj)
+                if (jj < b) Ai[jj] = x[jj];
+        }
+        __syncthreads();
+        // (3) trailing update A22 -= L21 D L21^T over rows [kb+b, nrows), columns [kb+b, L)
+        {
+            const int r0 = kb + b;
+            const int nr = nrows - r0;
+            const int nc = L - r0;
+            if (nc > 0) {
+                const int tr = (nr + 3) >> 2, tcn = (nc + 3) >> 2;
+                for (int tix = tid; tix < tr * tcn; tix += kThreads) {
+                    const int ti = tix / tcn, tq = tix - ti * tcn;
+                    if (tq > ti) continue;   // strictly above the diagonal tiles
+                    double acc[4][4];
+#pragma unroll
+                    for (int x = 0; x < 4; ++x)
+#pragma unroll
+                        for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+                    const double* Ar[4];
+                    const double* Aq[4];
+#pragma unroll
+                    for (int x = 0; x < 4; ++x) {
+                        Ar[x] = A + tri(min(r0 + 4 * ti + x, nrows - 1), 0);
+                        Aq[x] = A + tri(min(r0 + 4 * tq + x, L - 1), 0);
+                    }
+                    for (int j = kb; j < kb + b; ++j) {
+                        double vr[4], vq[4];
+                        const double dj = A[tri(j, j)];
+#pragma unroll
+                        for (int x = 0; x < 4; ++x) {
+                            vr[x] = Ar[x][j] * dj;
+                            vq[x] = Aq[x][j];
+                        }
+#pragma unroll
+                        for (int x = 0; x < 4; ++x)
+#pragma unroll
+                            for (int y = 0; y < 4; ++y) acc[x][y] = fma(vr[x], vq[y], acc[x][y]);
+                    }
+#pragma unroll
+                    for (int x = 0; x < 4; ++x)
+#pragma unroll
+                        for (int y = 0; y < 4; ++y) {
+                            const int gi = r0 + 4 * ti + x, gq = r0 + 4 * tq + y;
+                            if (gi < nrows && gq < L && gq <= gi) A[tri(gi, gq)] -= acc[x][y];
+                        }
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Symmetric Gram of the columns [0, n) of U over rows rows[0..nr) (or all k rows when
+// rows == null), 4x4 register tiles of the lower triangle.  Writes G(ia, ib) to
+// out(ia, ib) via the functor.
+template <typename T, typename Out>
+__device__ void gram_tiles(const T* U, int m, int n, int k, Out out) {
+    const int nt4 = (n + 3) >> 2;
+    const int ntile = nt4 * (nt4 + 1) / 2;
+    for (int tix = threadIdx.x; tix < ntile; tix += kThreads) {
+        int ta = 0, rem = tix;
+        while (rem > ta) {
+            rem -= ta + 1;
+            ++ta;
+        }
+        const int tb = rem;
+        int ca[4], cb[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ca[q] = min(4 * ta + q, n - 1);
+            cb[q] = min(4 * tb + q, n - 1);
+        }
+        double acc[4][4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+        for (int i = 0; i < k; ++i) {
+            const T* row = U + (size_t)i * m;
+            double va[4], vb[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                va[q] = (double)row[ca[q]];
+                vb[q] = (double)row[cb[q]];
+            }
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) acc[x][y] = fma(va[x], vb[y], acc[x][y]);
+        }
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) {
+                const int ia = 4 * ta + x, ib = 4 * tb + y;
+                if (ia < n && ib <= ia) out(ia, ib, acc[x][y]);
+            }
+    }
+}
 
 template <typename T>
 __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32_t count) {
     extern __shared__ double dsm[];
     const int lmax = a.lmax;
-    // A: packed lower triangle of the bordered matrix [[M, .], [t^T, .], [v^T, .]],
-    //    (lmax + 2) rows; rows L and L+1 hold t and v and become y = L^-1 t, z = L^-1 v.
+    // A: the factorisation region.  Per user it holds Gbar's LDL^T, then the per-wave
+    //    fast-path scratch, then (dense path) the packed lower triangle of the bordered
+    //    matrix [[M, .], [t^T, .], [v^T, .]] ((lmax + 2) rows).
     double* A = dsm;
-    double* s_misc = A + (size_t)(lmax + 2) * (lmax + 3) / 2;   // [0] mean, [1] pred sum
+    double* s_misc = A + a.a_elems;   // [0] mean (dense path), [1] sum of the user's ratings
     uint32_t* s_item = reinterpret_cast<uint32_t*>(s_misc + 4);
     float* s_rat = reinterpret_cast<float*>(s_item + CF_MAX_K);
     int* s_conn = reinterpret_cast<int*>(s_rat + CF_MAX_K);
     int* s_keep = s_conn + CF_MAX_K;
     int* s_nconn = s_keep + CF_MAX_K;                      // rows NOT in C (complement)
-    int* s_cnt = s_nconn + CF_MAX_K;                       // [0..3] compaction, [4] lim
+    int* s_lim = s_nconn + CF_MAX_K;                       // lim of every row
+    int* s_cpos = s_lim + CF_MAX_K;                        // #rows with U(i, j) >= 1e-4
+    int* s_slow = s_cpos + CF_MAX_K;                       // rows left to the dense path
+    int* s_cnt = s_slow + CF_MAX_K;                        // [0..3] compaction, [4] lim,
+                                                           // [5] Lu, [6] Lq, [7] #dense rows
+    int* s_cbar = s_conn;   // fast path: per-wave complement lists (kWaves x 64), aliases s_conn/s_keep
     double* Gb = a.gbar + (size_t)blockIdx.x * lmax * lmax;
+    double* Qs = a.qs + (size_t)blockIdx.x * (lmax + 2) * lmax;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    // Diagnostic phase stamps (thread 0 only; no effect on outputs).
+    // Diagnostic phase stamps (thread 0 only; no effect on outputs):
+    // {user setup, basis Q, fast ratings, dense ratings} cycles, {#fast, #dense} ratings.
     unsigned long long ph_acc[6] = {0, 0, 0, 0, 0, 0};
     unsigned long long ph_t = 0;
 #define PHASE_STAMP(ph)                                                   \
@@ -122,86 +313,251 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
         const T* U = a.evecs + a.evec_off[u];
         const T* ev = a.evals + base;
         __syncthreads();
+        PHASE_STAMP(-1);
+        if (tid == 0) {
+            s_cnt[5] = 0;
+            s_cnt[7] = 0;
+        }
+        __syncthreads();
         for (int i = tid; i < k; i += kThreads) {
             s_item[i] = a.items[base + i];
             s_rat[i] = a.ratings[base + i];
+            // lim = first eigenvalue index above w_lim, clamped to [2, m] (:271-282)
+            const double w_lim = (double)a.sigtab[a.sig_mode == CF_SIGS_COMPAT ? (uint64_t)i : base + i];
+            int lim = m;
+            for (int j = 0; j < m; ++j)
+                if ((double)ev[j] > w_lim) {
+                    lim = j;
+                    break;
+                }
+            lim = min(max(lim, 2), m);
+            s_lim[i] = lim;
+            atomicMax(&s_cnt[5], lim);
         }
-        // Gbar = U^T U over all k rows (fp64, full m x m), once per user: a prediction
-        // whose connected set C covers most rows forms its Gram matrix as
-        // Gbar_SS - sum_{i not in C} u_i u_i^T, which is the same sum with O(eps)
-        // cancellation error instead of c * L^2 work.
+        if (wave == 0) {
+            double sum = 0.0;
+            for (int i = lane; i < k; i += 64) sum += (double)a.ratings[base + i];
+            sum = wave_sum(sum);
+            if (lane == 0) s_misc[1] = sum;
+        }
+        __syncthreads();
+        const int Lu = s_cnt[5];
+
+        // Gbar = U^T U over the columns [0, Lu), all k rows: full copy in Gb (the dense
+        // path's complement form reads it), lower triangle packed into A for LDL^T.
+        gram_tiles(U, m, Lu, k, [&](int ia, int ib, double v) {
+            Gb[(size_t)ia * lmax + ib] = v;
+            Gb[(size_t)ib * lmax + ia] = v;
+            A[tri(ia, ib)] = v;
+        });
+        for (int j = tid; j < Lu; j += kThreads) {
+            int cnt = 0;
+            for (int i = 0; i < k; ++i) cnt += (double)U[(size_t)i * m + j] >= 0.0001;
+            s_cpos[j] = cnt;
+        }
+        __syncthreads();
+        ldlt_bordered(A, Lu, Lu);
+        if (tid == 0) s_cnt[6] = Lu;
+        __syncthreads();
+        for (int j = tid; j < Lu; j += kThreads)
+            if (!(A[tri(j, j)] >= kBasisMin * Gb[(size_t)j * lmax + j])) atomicMin(&s_cnt[6], j);
+        __syncthreads();
+        const int Lq = s_cnt[6];
+        PHASE_STAMP(0);
+
+        // Q = U L^-T D^-1/2 (row i of Q: forward substitution of row i of U against the
+        // unit-lower L, 16 columns at a time in registers), then g = Q^T r, h = Q^T 1
+        // as rows k and k + 1.  Row stride Lq.
+        for (int i = tid; i < k; i += kThreads) {
+            double* qi = Qs + (size_t)i * Lq;
+            const T* ui = U + (size_t)i * m;
+            for (int j0 = 0; j0 < Lq; j0 += 16) {
+                double x[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) x[q] = (j0 + q < Lq) ? (double)ui[j0 + q] : 0.0;
+                for (int p = 0; p < j0; ++p) {
+                    const double wp = qi[p];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q)
+                        if (j0 + q < Lq) x[q] = fma(-A[tri(j0 + q, p)], wp, x[q]);
+                }
+#pragma unroll
+                for (int q = 1; q < 16; ++q)
+#pragma unroll
+                    for (int p = 0; p < q; ++p)
+                        if (j0 + q < Lq) x[q] = fma(-A[tri(j0 + q, j0 + p)], x[p], x[q]);
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    if (j0 + q < Lq) qi[j0 + q] = x[q];
+            }
+            for (int j = 0; j < Lq; ++j) qi[j] *= 1.0 / sqrt(A[tri(j, j)]);
+        }
+        __syncthreads();
+        for (int j = tid; j < Lq; j += kThreads) {
+            double g = 0.0, h = 0.0;
+            for (int i = 0; i < k; ++i) {
+                const double q = Qs[(size_t)i * Lq + j];
+                g = fma(q, (double)s_rat[i], g);
+                h += q;
+            }
+            Qs[(size_t)k * Lq + j] = g;
+            Qs[(size_t)(k + 1) * Lq + j] = h;
+        }
+        __syncthreads();
+        PHASE_STAMP(1);
+
+        // ---- fast path: one wave per rating ------------------------------------------
         {
-            const int nt4 = (m + 3) >> 2;
-            const int ntile = nt4 * (nt4 + 1) / 2;
-            for (int tix = tid; tix < ntile; tix += kThreads) {
-                int ta = 0, rem = tix;
-                while (rem > ta) {
-                    rem -= ta + 1;
-                    ++ta;
-                }
-                const int tb = rem;
-                double acc[4][4];
-#pragma unroll
-                for (int x = 0; x < 4; ++x)
-#pragma unroll
-                    for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
-                const int a0 = min(4 * ta, m - 4 > 0 ? m - 4 : 0), b0 = 4 * tb;
-                for (int i = 0; i < k; ++i) {
-                    const T* row = U + (size_t)i * m;
-                    double va[4], vb[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        va[q] = (double)row[min(4 * ta + q, m - 1)];
-                        vb[q] = (double)row[min(b0 + q, m - 1)];
+            double* Ew = A + (size_t)wave * a.ew;
+            int* cb = s_cbar + wave * 64;
+            const double sum_all = s_misc[1];
+            for (int r = wave; r < k; r += kWaves) {
+                const float* nrow = a.graph + (size_t)s_item[r] * a.n_items;
+                int nc = 0;
+                double sc = 0.0;
+                for (int i0 = 0; i0 < k; i0 += 64) {
+                    const int i = i0 + lane;
+                    const bool out = i < k && !((double)nrow[s_item[i]] > 0.1);   // (:259)
+                    const unsigned long long bal = __ballot(out);
+                    if (out) {
+                        const int pos = nc + __popcll(bal & ((1ull << lane) - 1ull));
+                        if (pos < 64) cb[pos] = i;
+                        sc += (double)s_rat[i];
                     }
-#pragma unroll
-                    for (int x = 0; x < 4; ++x)
-#pragma unroll
-                        for (int y = 0; y < 4; ++y) acc[x][y] = fma(va[x], vb[y], acc[x][y]);
+                    nc += __popcll(bal);
                 }
-                (void)a0;
-#pragma unroll
-                for (int x = 0; x < 4; ++x)
-#pragma unroll
-                    for (int y = 0; y < 4; ++y) {
-                        const int ia = 4 * ta + x, ib = b0 + y;
-                        if (ia < m && ib < m && ib <= ia) {
-                            Gb[(size_t)ia * lmax + ib] = acc[x][y];
-                            Gb[(size_t)ib * lmax + ia] = acc[x][y];
+                sc = wave_sum(sc);
+                const int c = k - nc;
+                const int lim = s_lim[r];
+                bool slow = c == 0 || nc > a.ncw || lim > Lq || m < 2;
+                WAVE_SYNC();
+                if (!slow) {
+                    // column j < lim is dropped (:284-304) iff every row with
+                    // U(i, j) >= 1e-4 lies in Cbar
+                    bool drop = false;
+                    for (int j = lane; j < lim; j += 64) {
+                        const int cp = s_cpos[j];
+                        if (cp <= nc) {
+                            int hit = 0;
+                            for (int q = 0; q < nc; ++q) hit += (double)U[(size_t)cb[q] * m + j] >= 0.0001;
+                            drop |= hit == cp;
                         }
                     }
+                    slow = __ballot(drop) != 0ull;
+                }
+                if (slow) {
+                    if (lane == 0) s_slow[atomicAdd(&s_cnt[7], 1)] = r;
+                    continue;
+                }
+                const double mu = (sum_all - sc) / (double)c;   // mean over C (:311)
+
+                // E = Gram over j < lim of the Q rows [Cbar..., r, g, h] (packed lower).
+                // `parts` lanes share one entry (strided j, xor-reduced).
+                const int ne = nc + 3;
+                const int nent = ne * (ne + 1) / 2;
+                int parts = 64;
+                while (parts > 1 && nent * parts > 64) parts >>= 1;
+                const int p = lane & (parts - 1);
+                for (int e0 = 0; e0 < nent; e0 += 64 / parts) {
+                    const int e = e0 + lane / parts;
+                    double acc = 0.0;
+                    if (e < nent) {
+                        int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+                        while (ra * (ra + 1) / 2 > e) --ra;
+                        while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
+                        const int rb = e - ra * (ra + 1) / 2;
+                        const int qa = ra < nc ? cb[ra] : (ra == nc ? r : k + ra - nc - 1);
+                        const int qb = rb < nc ? cb[rb] : (rb == nc ? r : k + rb - nc - 1);
+                        const double* xa = Qs + (size_t)qa * Lq;
+                        const double* xb = Qs + (size_t)qb * Lq;
+                        for (int j = p; j < lim; j += parts) acc = fma(xa[j], xb[j], acc);
+                    }
+                    for (int off = parts >> 1; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+                    if (p == 0 && e < nent) Ew[e] = acc;
+                }
+                WAVE_SYNC();
+                // Border rows: row nc = P_{r,Cbar} (already in place), row nc + 1 := b.
+                // a_r on lane 63 (never a border lane's register).
+                double bl = 0.0, ar = 0.0;
+                if (lane < nc) {
+                    bl = Ew[tri(nc + 1, lane)] - mu * Ew[tri(nc + 2, lane)];
+                    for (int q = 0; q < nc; ++q) {
+                        const double eq = q <= lane ? Ew[tri(lane, q)] : Ew[tri(q, lane)];
+                        bl = fma(-eq, (double)s_rat[cb[q]] - mu, bl);
+                    }
+                }
+                if (lane == 63) {
+                    ar = Ew[tri(nc + 1, nc)] - mu * Ew[tri(nc + 2, nc)];
+                    for (int q = 0; q < nc; ++q) ar = fma(-Ew[tri(nc, q)], (double)s_rat[cb[q]] - mu, ar);
+                }
+                WAVE_SYNC();
+                if (lane < nc) {
+                    Ew[tri(nc + 1, lane)] = bl;
+                    for (int q = 0; q <= lane; ++q) Ew[tri(lane, q)] = (q == lane ? 1.0 : 0.0) - Ew[tri(lane, q)];
+                }
+                WAVE_SYNC();
+                // LDL^T of K (nc columns), border rows nc (P_{r,Cbar}) and nc + 1 (b);
+                // lane i owns row i.
+                double minpiv = 1.0;
+                for (int j = 0; j < nc; ++j) {
+                    const double dj = Ew[tri(j, j)];
+                    minpiv = fmin(minpiv, dj);
+                    const bool mine = lane > j && lane < nc + 2;
+                    const double lij = mine ? Ew[tri(lane, j)] / dj : 0.0;
+                    if (mine) {
+                        const int qend = min(lane, nc - 1);
+                        for (int q = j + 1; q <= qend; ++q)
+                            Ew[tri(lane, q)] = fma(-lij, Ew[tri(q, j)], Ew[tri(lane, q)]);
+                    }
+                    WAVE_SYNC();
+                    if (mine) Ew[tri(lane, j)] = lij;
+                    WAVE_SYNC();
+                }
+                double dot = 0.0;
+                if (lane < nc) dot = Ew[tri(nc, lane)] * Ew[tri(nc + 1, lane)] * Ew[tri(lane, lane)];
+                dot = wave_sum(dot);
+                ar = __shfl(ar, 63);
+                WAVE_SYNC();
+                // Full-rank but ill-conditioned (c >= lim): the dense path, whose error
+                // matches the reference's.  Rank-deficient (c < lim: U_CS^T U_CS is
+                // singular in exact arithmetic, the reference's inverse returns rounding
+                // noise) stays here: b is orthogonal to null(K) exactly as t is to null(M),
+                // so this is the same kind of noise-amplified value.
+                if (!(minpiv >= kPivMin) && c >= lim) {
+                    if (lane == 0) s_slow[atomicAdd(&s_cnt[7], 1)] = r;
+                    continue;
+                }
+                if (lane == 0) {
+                    double pred = mu + ar + dot;
+                    if (pred > 5) pred = 5;
+                    if (pred < 1) pred = 1;
+                    const double d = (double)s_rat[r] - pred;
+                    a.mse[base + r] = (float)(d * d);
+                    a.kk[base + r] = c;
+                    if (a.pred) a.pred[base + r] = pred;
+                }
             }
         }
         __syncthreads();
+        const int nslow = s_cnt[7];
+        if (a.phase_cycles && tid == 0) {
+            ph_acc[4] += (unsigned long long)(k - nslow);
+            ph_acc[5] += (unsigned long long)nslow;
+        }
+        PHASE_STAMP(2);
 
-        for (int r = 0; r < k; ++r) {
-            PHASE_STAMP(-1);
-            // --- connected set C: the user's items that are out-neighbours of movie r (:254-265)
+        // ---- dense path: block-wide, the rating's own bordered Gram matrix ----------------
+        for (int si = 0; si < nslow; ++si) {
+            const int r = s_slow[si];
+            // connected set C: the user's items that are out-neighbours of movie r (:254-265)
             const float* nrow = a.graph + (size_t)s_item[r] * a.n_items;
             const bool conn = tid < k && (double)nrow[s_item[tid < k ? tid : 0]] > 0.1;
             const int c = block_compact(conn, tid, s_conn, s_cnt);
             const int nc = block_compact(tid < k && !conn, tid, s_nconn, s_cnt);
             const bool use_complement = nc < c;
-            PHASE_STAMP(0);
+            const int lim = s_lim[r];
 
-            // --- lim = first eigenvalue index above w_lim, >= 2 (:271-282) ---
-            {
-                const double w_lim =
-                    (double)a.sigtab[a.sig_mode == CF_SIGS_COMPAT ? (uint64_t)r : base + r];
-                const bool above = tid < m && (double)(tid < k ? ev[tid] : (T)0) > w_lim;
-                const unsigned long long bal = __ballot(above);
-                if (lane == 0) s_cnt[wave] = bal ? (__ffsll((long long)bal) - 1 + 64 * wave) : 0x7fffffff;
-                __syncthreads();
-                int lim = min(min(s_cnt[0], s_cnt[1]), min(s_cnt[2], s_cnt[3]));
-                lim = min(lim, m);
-                if (lim < 2) lim = 2;
-                if (lim > m) lim = m;
-                __syncthreads();
-                s_cnt[4] = lim;   // every thread writes the same value
-            }
-            const int lim = s_cnt[4];
-
-            // --- zero-column filter: keep column j < lim iff some U(C, j) >= 1e-4 (:284-304)
+            // zero-column filter: keep column j < lim iff some U(C, j) >= 1e-4 (:284-304)
             bool keep = false;
             if (tid < lim) {
                 for (int i = 0; i < c; ++i)
@@ -211,9 +567,8 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                     }
             }
             const int L = block_compact(keep, tid, s_keep, s_cnt);
-            PHASE_STAMP(1);
 
-            // --- mean of the connected ratings (:311) ---
+            // mean of the connected ratings (:311)
             if (wave == 0) {
                 double sum = 0.0;
                 for (int i = lane; i < c; i += 64) sum += (double)s_rat[s_conn[i]];
@@ -222,15 +577,13 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
             }
             __syncthreads();
             const double mean = s_misc[0];
-            PHASE_STAMP(2);
 
-            // --- bordered Gram: A[i][j] = (G^T G)_ij (j <= i < L), A[L][j] = t_j, A[L+1][j] = v_j
-            // 4x4 register tiles of the lower triangle, 8 independent loads per row of G.
+            // bordered Gram: A[i][j] = (G^T G)_ij (j <= i < L), A[L][j] = t_j, A[L+1][j] = v_j
             {
                 const int nt4 = (L + 3) >> 2;
                 const int ntile = nt4 * (nt4 + 1) / 2;
                 for (int tix = tid; tix < ntile; tix += kThreads) {
-                    int ta = 0, rem = tix;   // tix -> (ta >= tb), row-major over the lower triangle
+                    int ta = 0, rem = tix;
                     while (rem > ta) {
                         rem -= ta + 1;
                         ++ta;
@@ -292,8 +645,8 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                                                      : acc[x][y];
                         }
                 }
-                // t = G^T (r - mean): 4 lanes per column, each a strided quarter of C,
-                // combined with two DPP-free shuffles; v = U(r, S).
+                // t = G^T (r - mean): 4 lanes per column, each a strided quarter of C;
+                // v = U(r, S).
                 for (int e = tid; e < 4 * L; e += kThreads) {
                     const int j = e >> 2, part = e & 3;
                     const int cj = s_keep[j];
@@ -318,117 +671,10 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                 }
             }
             __syncthreads();
-            PHASE_STAMP(3);
 
-            // --- blocked right-looking LDL^T of M, carrying the two border rows ---
-            for (int kb = 0; kb < L; kb += kNB) {
-                const int b = min(kNB, L - kb);
-                // (1) diagonal block, unblocked LDL^T, in wave 0's registers: lane i < b
-                //     holds row kb + i; column j is broadcast by shuffles.  D_j stays on
-                //     the diagonal, L_ij (unit lower) below it.
-                if (wave == 0) {
-                    double rowv[kNB];
-                    const int i = lane;
-                    const bool live = i < b;
-#pragma unroll
-                    for (int q = 0; q < kNB; ++q)
-                        rowv[q] = (live && q <= i) ? A[tri(kb + i, kb + q)] : 0.0;
-#pragma unroll
-                    for (int j = 0; j < kNB; ++j) {
-                        if (j < b) {
-                            const double dj = __shfl(rowv[j], j);
-                            const double w = (i > j) ? rowv[j] : 0.0;   // unscaled a_ij
-                            const double lij = w / dj;
-                            // a_iq -= L_ij * a_qj, j < q <= i
-#pragma unroll
-                            for (int q = j + 1; q < kNB; ++q) {
-                                const double wq = __shfl(w, q);
-                                if (q <= i) rowv[q] = fma(-lij, wq, rowv[q]);
-                            }
-                            if (i > j) rowv[j] = lij;
-                        }
-                    }
-#pragma unroll
-                    for (int q = 0; q < kNB; ++q)
-                        if (live && q <= i) A[tri(kb + i, kb + q)] = rowv[q];
-                }
-                __syncthreads();
-                // (2) panel: rows below the block (incl. the border rows) solve against L11^T
-                for (int i = kb + b + tid; i < L + 2; i += kThreads) {
-                    double* Ai = A + tri(i, kb);
-                    double x[kNB];
-#pragma unroll
-                    for (int jj = 0; jj < kNB; ++jj) x[jj] = jj < b ? Ai[jj] : 0.0;
-#pragma unroll
-                    for (int jj = 0; jj < kNB; ++jj) {
-                        if (jj < b) {
-                            // L_ij = (a_ij - sum_q L_iq D_q L_jq) / D_j   (broadcast reads of L11, D)
-                            const double* Aj = A + tri(kb + jj, kb);
-                            double sacc = x[jj];
-#pragma unroll
-                            for (int q = 0; q < jj; ++q)
-                                sacc = fma(-x[q] * A[tri(kb + q, kb + q)], Aj[q], sacc);
-                            x[jj] = sacc / Aj[jj];
-                        }
-                    }
-#pragma unroll
-                    for (int jj = 0; jj < kNB; ++jj)
-                        if (jj < b) Ai[jj] = x[jj];
-                }
-                __syncthreads();
-                // (3) trailing update A22 -= L21 L21^T over rows [kb+b, L+2), columns [kb+b, min(i, L-1)]
-                {
-                    const int r0 = kb + b;
-                    const int nr = L + 2 - r0;   // rows
-                    const int nc = L - r0;       // columns
-                    if (nc > 0) {
-                        const int tr = (nr + 3) >> 2, tcn = (nc + 3) >> 2;
-                        for (int tix = tid; tix < tr * tcn; tix += kThreads) {
-                            const int ti = tix / tcn, tq = tix - ti * tcn;
-                            if (tq > ti) continue;   // strictly above the diagonal tiles
-                            double acc[4][4];
-#pragma unroll
-                            for (int x = 0; x < 4; ++x)
-#pragma unroll
-                                for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
-                            const double* Ar[4];
-                            const double* Aq[4];
-#pragma unroll
-                            for (int x = 0; x < 4; ++x) {
-                                const int gi = min(r0 + 4 * ti + x, L + 1);
-                                const int gq = min(r0 + 4 * tq + x, L - 1);
-                                Ar[x] = A + tri(gi, 0);
-                                Aq[x] = A + tri(gq, 0);
-                            }
-                            for (int j = kb; j < kb + b; ++j) {
-                                double vr[4], vq[4];
-                                const double dj = A[tri(j, j)];
-#pragma unroll
-                                for (int x = 0; x < 4; ++x) {
-                                    vr[x] = Ar[x][j] * dj;
-                                    vq[x] = Aq[x][j];
-                                }
-#pragma unroll
-                                for (int x = 0; x < 4; ++x)
-#pragma unroll
-                                    for (int y = 0; y < 4; ++y) acc[x][y] = fma(vr[x], vq[y], acc[x][y]);
-                            }
-#pragma unroll
-                            for (int x = 0; x < 4; ++x)
-#pragma unroll
-                                for (int y = 0; y < 4; ++y) {
-                                    const int gi = r0 + 4 * ti + x, gq = r0 + 4 * tq + y;
-                                    if (gi < L + 2 && gq < L && gq <= gi) A[tri(gi, gq)] -= acc[x][y];
-                                }
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-            PHASE_STAMP(4);
+            ldlt_bordered(A, L, L + 2);
 
-            // --- pred = v^T M^-1 t + mean = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean (:314-327)
-            //     (the border rows hold (L^-1 t)_j / D_j and (L^-1 v)_j / D_j)
+            // pred = v^T M^-1 t + mean = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean (:314-327)
             if (wave == 0) {
                 double dot = 0.0;
                 const double* y = A + tri(L, 0);
@@ -446,8 +692,8 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                 }
             }
             __syncthreads();
-            PHASE_STAMP(5);
         }
+        PHASE_STAMP(3);
     }
     if (a.phase_cycles && tid == 0)
         for (int ph = 0; ph < 6; ++ph) atomicAdd(&a.phase_cycles[ph], ph_acc[ph]);
@@ -456,11 +702,15 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
 template <typename T>
 int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lmax, hipStream_t stream) {
     args.lmax = lmax;
-    const size_t lds = sizeof(double) * ((size_t)(lmax + 2) * (lmax + 3) / 2 + 4) +
-                       CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 3 * sizeof(int)) + 8 * sizeof(int);
+    args.ncw = std::min(kNcMax, lmax);
+    args.ew = (args.ncw + 3) * (args.ncw + 4) / 2;
+    args.a_elems = std::max((lmax + 2) * (lmax + 3) / 2, kWaves * args.ew);
+    const size_t lds = sizeof(double) * ((size_t)args.a_elems + 4) +
+                       CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 6 * sizeof(int)) + 8 * sizeof(int);
     if (lds > 163840) return cf_set_error(ctx, CF_ERANGE, "predict bucket exceeds LDS");
     int blocks = (int)std::min<uint32_t>(count, 2048u);
-    const size_t need = (size_t)blocks * lmax * lmax * sizeof(double);
+    const size_t per_block = (size_t)lmax * lmax + (size_t)(lmax + 2) * lmax;
+    const size_t need = (size_t)blocks * per_block * sizeof(double);
     if (need > ctx->scratch_bytes) {
         if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
         ctx->d_scratch = nullptr;
@@ -469,6 +719,7 @@ int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lma
         ctx->scratch_bytes = need;
     }
     args.gbar = reinterpret_cast<double*>(ctx->d_scratch);
+    args.qs = args.gbar + (size_t)blocks * lmax * lmax;
     CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)predict_kernel<T>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(predict_kernel<T>, dim3(blocks), dim3(kThreads), lds, stream, args, count);

@@ -61,8 +61,9 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
  * hit the sweep cap, assembly cycles, Jacobi cycles, epilogue cycles, tournament
  * steps} (cycles: s_memtime of thread 0).  enable == 0 frees them. */
 int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out8);
-/* Diagnostics: predictor phase cycle totals (s_memtime, thread 0 of each block):
- * {connected set, lim + column filter, mean, Gram, LU, solve}. */
+/* Diagnostics: predictor phase totals (s_memtime cycles, thread 0 of each block):
+ * {per-user setup, basis Q, fast-path ratings, dense-path ratings} cycles, then the
+ * number of ratings taken by the fast and by the dense path. */
 int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out6);
 
 /* ---- item graph (out_fin_) ---------------------------------------------------

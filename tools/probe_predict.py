@@ -28,7 +28,65 @@ t = time.perf_counter(); pred(); torch.cuda.synchronize(); dt = time.perf_counte
 print(f"predict {n} ratings in {dt*1e3:.1f} ms -> {n/dt:.0f}/s", flush=True)
 ctx.debug_phases(True); pred(); torch.cuda.synchronize()
 ph = ctx.debug_phases(True, read=True)
-tot = sum(ph.values())
-print({k_: f"{v/tot*100:.1f}%" for k_, v in ph.items()}, "cycles/prediction:", tot / n * 1.0)
+cyc = {k_: v for k_, v in ph.items() if not k_.startswith("n_")}
+tot = sum(cyc.values())
+print({k_: f"{v/tot*100:.1f}%" for k_, v in cyc.items()}, "cycles/prediction:", tot / n,
+      "fast", ph["n_fast"], "dense", ph["n_dense"])
 m = d["m"].cpu().numpy(); kk = d["kk"].cpu().numpy()
 print("m mean", m.mean(), "kk mean", kk.mean(), "k mean", k.mean())
+# lim distribution (compat sig table: w_lim of row r is sigs[r] of the global table)
+ev = d["evals"].cpu().numpy(); sg = d["sigs"].cpu().numpy()
+lims = []; cs = []
+for u in range(min(users, 3000)):
+    b, e = int(off[u]), int(off[u + 1]); mu = int(m[u])
+    for r in range(e - b):
+        above = np.nonzero(ev[b:b + mu] > sg[r])[0]
+        lim = int(above[0]) if len(above) else mu
+        lims.append(min(max(lim, 2), mu)); cs.append(kk[b + r])
+lims = np.array(lims); cs = np.array(cs)
+print("lim mean", lims.mean(), "p50", np.median(lims), "p90", np.percentile(lims, 90), "max", lims.max())
+print("c mean", cs.mean(), "lim^3 mean", (lims.astype(float) ** 3).mean())
+# complement size and zero-column filter statistics
+ev_off = eoff
+ncs = []; drops = []; drop0 = 0; nrat = 0; prefix = 0
+for u in range(min(users, 1500)):
+    b, e = int(off[u]), int(off[u + 1]); mu = int(m[u]); ku = e - b
+    if mu <= 0: continue
+    Uu = d["evecs"][int(ev_off[u]):int(ev_off[u]) + ku * mu].cpu().numpy().reshape(ku, mu)
+    it = items[b:e]
+    for r in range(ku):
+        conn = W[it[r], it] > 0.1
+        above = np.nonzero(ev[b:b + mu] > sg[r])[0]
+        lim = min(max(int(above[0]) if len(above) else mu, 2), mu)
+        keep = (Uu[conn][:, :lim] >= 1e-4).any(axis=0) if conn.any() else np.zeros(lim, bool)
+        ncs.append(ku - conn.sum()); nd = lim - keep.sum(); drops.append(nd)
+        drop0 += (not keep[0]); nrat += 1; prefix += keep.all()
+ncs = np.array(ncs); drops = np.array(drops)
+print("nc mean", ncs.mean(), "p50", np.median(ncs), "p90", np.percentile(ncs, 90), "frac nc<=8", (ncs <= 8).mean(), "frac nc<=16", (ncs <= 16).mean())
+print("dropped cols mean", drops.mean(), "frac prefix", prefix / nrat, "frac col0 dropped", drop0 / nrat, "max drop", drops.max())
+# why ratings leave the fast path (sample)
+reasons = dict(c0=0, nc_big=0, drop=0, singular=0, ill=0, fast=0, nc_big_singular=0)
+for u in range(min(users, 600)):
+    b, e = int(off[u]), int(off[u + 1]); mu = int(m[u]); ku = e - b
+    if mu < 2: continue
+    Uu = d["evecs"][int(ev_off[u]):int(ev_off[u]) + ku * mu].cpu().numpy().reshape(ku, mu).astype(np.float64)
+    it = items[b:e]
+    for r in range(ku):
+        conn = W[it[r], it] > 0.1
+        above = np.nonzero(ev[b:b + mu] > sg[r])[0]
+        lim = min(max(int(above[0]) if len(above) else mu, 2), mu)
+        c = int(conn.sum()); nc = ku - c
+        if c == 0: reasons["c0"] += 1; continue
+        keep = (Uu[conn][:, :lim] >= 1e-4).any(axis=0)
+        if not keep.all(): reasons["drop"] += 1; continue
+        if nc > 62:
+            reasons["nc_big"] += 1
+            if c < lim: reasons["nc_big_singular"] += 1
+            continue
+        if c < lim: reasons["singular"] += 1; continue
+        Q, _ = np.linalg.qr(Uu[:, :lim])
+        B = Q[~conn]
+        K = np.eye(nc) - B @ B.T
+        if nc and np.linalg.eigvalsh(K).min() < 1e-6: reasons["ill"] += 1
+        else: reasons["fast"] += 1
+print("reasons", reasons)
