@@ -101,10 +101,10 @@ class Context:
 
     def debug_phases(self, enable: bool = True, read: bool = False):
         """Predictor phase cycles {setup, basis, fast, dense} and rating counts {n_fast, n_dense}."""
-        out = np.zeros(6, dtype=np.uint64) if read else None
+        out = np.zeros(8, dtype=np.uint64) if read else None
         self._chk(self.lib.cf_debug_phases(self.h, int(enable), ptr(out)), "cf_debug_phases")
         if read:
-            return dict(zip(["setup", "basis", "fast", "dense", "n_fast", "n_dense"], map(int, out)))
+            return dict(zip(["setup", "basis", "fast", "dense", "n_fast", "n_dense", "w0_conn", "w0_entries"], map(int, out)))
         return None
 
     # -- item graph (out_fin_) ---------------------------------------------------

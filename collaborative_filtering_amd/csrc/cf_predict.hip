@@ -20,14 +20,15 @@
 //   Gbar = U^T U over the columns [0, Lu), Lu = max_r lim_r;  Gbar = L D L^T;
 //   Q = U L^-T D^-1/2 (Cholesky QR; the leading lim columns of Q span the leading lim
 //   columns of U, so one Q serves every row's prefix S = [0, lim));
-//   g = Q^T r, h = Q^T 1.
+//   g = Q^T r, h = Q^T 1, and the prefix tables PG(i, l) = sum_{j<l} Q_ij g_j,
+//   PH(i, l) = sum_{j<l} Q_ij h_j.
 // With P = Q_S Q_S^T (the k x k projector), Cbar = rows not in C (nc of them),
 // y = r - mean, and Q_S^T Q_S = I:
 //   pred - mean = a_r + P_{r,Cbar} K^-1 b,   K = I - P_{Cbar,Cbar}  (nc x nc),
 //   a_r = (P y)_r - P_{r,Cbar} y_Cbar,   b = (P y)_Cbar - P_{Cbar,Cbar} y_Cbar,
 // (Woodbury on U_CS^T U_CS = Q_S^T Q_S - Q_CbarS^T Q_CbarS), where (P y)_i =
-// Q_iS.g_S - mean Q_iS.h_S.  A rating therefore costs (nc + 3)^2 / 2 dot products of
-// length lim and an nc x nc LDL^T instead of a lim x lim factorisation.
+// PG(i, lim) - mean PH(i, lim).  A rating therefore costs (nc + 1)(nc + 2) / 2 dot
+// products of length lim and an nc x nc LDL^T instead of a lim x lim factorisation.
 //
 // Dense path (block-wide, the rating's own Gram matrix) for the ratings the fast path
 // does not take: the column filter drops a column, nc > kNcMax, c = 0, a pivot of K
@@ -48,8 +49,12 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-constexpr int kNcMax = 62;            // fast path: nc + 2 border rows <= 64 lanes
-constexpr double kPivMin = 1e-6;      // fast path: smallest pivot of K = I - P_CbarCbar
+constexpr int kNcMax = 62;            // fast path: complement rows (nc + 2 border rows <= 64 lanes)
+constexpr int kJC = 32;               // fast path: minimum columns of X staged per chunk
+// fast path: smallest pivot of K = I - P_CbarCbar (its pivots bound the smallest
+// eigenvalue of U_CS^T U_CS in the Q basis, so this admits cond <~ 1e10, where the
+// reference's own explicit inverse is accurate to ~cond * eps; parity is tested to 1e8)
+constexpr double kPivMin = 1e-10;
 constexpr double kBasisMin = 0.5;     // D_j / Gbar_jj below this: Q not trusted from j on
 
 template <typename T>
@@ -73,10 +78,12 @@ struct PredArgs {
     unsigned long long* phase_cycles;  // diagnostics: per-phase s_memtime totals (or null)
     int lmax;              // Gram dimension bound of the launch
     int ncw;               // fast-path bound on nc for this launch
-    int ew;                // doubles of per-wave fast-path scratch
+    int ew;                // doubles of per-wave fast-path matrix E / K
+    int xs;                // doubles of per-wave fast-path staging buffer
     int a_elems;           // doubles of the shared factorisation / scratch region
     double* gbar;          // per-block scratch: Gbar = U^T U (lmax x lmax, full), fp64
     double* qs;            // per-block scratch: Q ((lmax + 2) x lmax rows: Q, g, h), fp64
+    double* pgh;           // per-block scratch: {PG, PH}(i, l), lmax x (lmax + 1) pairs, fp64
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -245,7 +252,24 @@ __device__ void gram_tiles(const T* U, int m, int n, int k, Out out) {
         for (int x = 0; x < 4; ++x)
 #pragma unroll
             for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
-        for (int i = 0; i < k; ++i) {
+        int i = 0;
+        for (; i + 1 < k; i += 2) {   // two rows in flight: 16 independent loads
+            const T* row0 = U + (size_t)i * m;
+            const T* row1 = row0 + m;
+            double va0[4], vb0[4], va1[4], vb1[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                va0[q] = (double)row0[ca[q]];
+                vb0[q] = (double)row0[cb[q]];
+                va1[q] = (double)row1[ca[q]];
+                vb1[q] = (double)row1[cb[q]];
+            }
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) acc[x][y] = fma(va1[x], vb1[y], fma(va0[x], vb0[y], acc[x][y]));
+        }
+        if (i < k) {
             const T* row = U + (size_t)i * m;
             double va[4], vb[4];
 #pragma unroll
@@ -290,13 +314,15 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
     int* s_cbar = s_conn;   // fast path: per-wave complement lists (kWaves x 64), aliases s_conn/s_keep
     double* Gb = a.gbar + (size_t)blockIdx.x * lmax * lmax;
     double* Qs = a.qs + (size_t)blockIdx.x * (lmax + 2) * lmax;
+    double* PGH = a.pgh + (size_t)blockIdx.x * lmax * (lmax + 1) * 2;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     // Diagnostic phase stamps (thread 0 only; no effect on outputs):
-    // {user setup, basis Q, fast ratings, dense ratings} cycles, {#fast, #dense} ratings.
-    unsigned long long ph_acc[6] = {0, 0, 0, 0, 0, 0};
+    // {user setup, basis Q, fast ratings, dense ratings} cycles, {#fast, #dense} ratings,
+    // wave 0's {connected set + filter, projector entries} cycles in the fast path.
+    unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long ph_t = 0;
 #define PHASE_STAMP(ph)                                                   \
     if (a.phase_cycles && tid == 0) {                                     \
@@ -318,6 +344,7 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
             s_cnt[5] = 0;
             s_cnt[7] = 0;
         }
+        for (int j = tid; j < m; j += kThreads) A[j] = (double)ev[j];   // evals staged in A
         __syncthreads();
         for (int i = tid; i < k; i += kThreads) {
             s_item[i] = a.items[base + i];
@@ -326,7 +353,7 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
             const double w_lim = (double)a.sigtab[a.sig_mode == CF_SIGS_COMPAT ? (uint64_t)i : base + i];
             int lim = m;
             for (int j = 0; j < m; ++j)
-                if ((double)ev[j] > w_lim) {
+                if (A[j] > w_lim) {
                     lim = j;
                     break;
                 }
@@ -352,7 +379,13 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
         });
         for (int j = tid; j < Lu; j += kThreads) {
             int cnt = 0;
-            for (int i = 0; i < k; ++i) cnt += (double)U[(size_t)i * m + j] >= 0.0001;
+            for (int i0 = 0; i0 < k; i0 += 8) {
+                double v[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) v[t] = i0 + t < k ? (double)U[(size_t)(i0 + t) * m + j] : 0.0;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) cnt += v[t] >= 0.0001;
+            }
             s_cpos[j] = cnt;
         }
         __syncthreads();
@@ -375,11 +408,15 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                 double x[16];
 #pragma unroll
                 for (int q = 0; q < 16; ++q) x[q] = (j0 + q < Lq) ? (double)ui[j0 + q] : 0.0;
-                for (int p = 0; p < j0; ++p) {
-                    const double wp = qi[p];
+                for (int p = 0; p < j0; p += 4) {   // j0 is a multiple of 16
+                    double wv[4];
 #pragma unroll
-                    for (int q = 0; q < 16; ++q)
-                        if (j0 + q < Lq) x[q] = fma(-A[tri(j0 + q, p)], wp, x[q]);
+                    for (int t = 0; t < 4; ++t) wv[t] = qi[p + t];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+#pragma unroll
+                        for (int q = 0; q < 16; ++q)
+                            if (j0 + q < Lq) x[q] = fma(-A[tri(j0 + q, p + t)], wv[t], x[q]);
                 }
 #pragma unroll
                 for (int q = 1; q < 16; ++q)
@@ -393,31 +430,76 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
             for (int j = 0; j < Lq; ++j) qi[j] *= 1.0 / sqrt(A[tri(j, j)]);
         }
         __syncthreads();
+        // g, h (global rows k, k + 1 of Qs, and staged in A: L is no longer needed)
+        double* s_g = A;
+        double* s_h = A + Lq;
         for (int j = tid; j < Lq; j += kThreads) {
             double g = 0.0, h = 0.0;
-            for (int i = 0; i < k; ++i) {
-                const double q = Qs[(size_t)i * Lq + j];
-                g = fma(q, (double)s_rat[i], g);
-                h += q;
+            for (int i0 = 0; i0 < k; i0 += 8) {
+                double v[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) v[t] = i0 + t < k ? Qs[(size_t)(i0 + t) * Lq + j] : 0.0;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    g = fma(v[t], i0 + t < k ? (double)s_rat[i0 + t] : 0.0, g);
+                    h += v[t];
+                }
             }
             Qs[(size_t)k * Lq + j] = g;
             Qs[(size_t)(k + 1) * Lq + j] = h;
+            s_g[j] = g;
+            s_h[j] = h;
+        }
+        __syncthreads();
+        for (int i = tid; i < k; i += kThreads) {
+            const double* qi = Qs + (size_t)i * Lq;
+            double2* out = reinterpret_cast<double2*>(PGH) + (size_t)i * (Lq + 1);
+            double pg = 0.0, ph = 0.0;
+            out[0] = make_double2(0.0, 0.0);
+            for (int j0 = 0; j0 < Lq; j0 += 8) {
+                double v[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) v[t] = j0 + t < Lq ? qi[j0 + t] : 0.0;
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    if (j0 + t < Lq) {
+                        pg = fma(v[t], s_g[j0 + t], pg);
+                        ph = fma(v[t], s_h[j0 + t], ph);
+                        out[j0 + t + 1] = make_double2(pg, ph);
+                    }
+            }
         }
         __syncthreads();
         PHASE_STAMP(1);
 
         // ---- fast path: one wave per rating ------------------------------------------
         {
-            double* Ew = A + (size_t)wave * a.ew;
+            double* Ew = A + (size_t)wave * (a.ew + a.xs);
+            double* Xs = Ew + a.ew;   // (ncw + 4) x kJC staged chunk of X
             int* cb = s_cbar + wave * 64;
             const double sum_all = s_misc[1];
+            // graph(movie_r, item_i) for this wave's next rating, loaded one rating ahead
+            // (k <= 192: three loads per lane)
+            float gv_next[3];
+            auto load_graph_row = [&](int rr, float* gv) {
+                const float* nrow = a.graph + (size_t)s_item[rr < k ? rr : 0] * a.n_items;
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    const int i = 64 * t + lane;
+                    gv[t] = (rr < k && i < k) ? nrow[s_item[i]] : 0.0f;
+                }
+            };
+            load_graph_row(wave, gv_next);
             for (int r = wave; r < k; r += kWaves) {
-                const float* nrow = a.graph + (size_t)s_item[r] * a.n_items;
+                unsigned long long t_w0 = (a.phase_cycles && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
+                float gv[3] = {gv_next[0], gv_next[1], gv_next[2]};
+                load_graph_row(r + kWaves, gv_next);
                 int nc = 0;
                 double sc = 0.0;
-                for (int i0 = 0; i0 < k; i0 += 64) {
-                    const int i = i0 + lane;
-                    const bool out = i < k && !((double)nrow[s_item[i]] > 0.1);   // (:259)
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    const int i = 64 * t + lane;
+                    const bool out = i < k && !((double)gv[t] > 0.1);   // (:259)
                     const unsigned long long bal = __ballot(out);
                     if (out) {
                         const int pos = nc + __popcll(bal & ((1ull << lane) - 1ull));
@@ -450,44 +532,105 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                     continue;
                 }
                 const double mu = (sum_all - sc) / (double)c;   // mean over C (:311)
+                if (a.phase_cycles && tid == 0) {
+                    const unsigned long long now = __builtin_amdgcn_s_memtime();
+                    ph_acc[6] += now - t_w0;
+                    t_w0 = now;
+                }
 
-                // E = Gram over j < lim of the Q rows [Cbar..., r, g, h] (packed lower).
-                // `parts` lanes share one entry (strided j, xor-reduced).
-                const int ne = nc + 3;
-                const int nent = ne * (ne + 1) / 2;
+                // E = Gram over j < lim of the Q rows X = [Cbar..., r] (np rows, packed
+                // lower): column chunks of X, as wide as the wave's staging buffer allows
+                // (all of [0, lim) at once for small np), are staged in LDS with coalesced
+                // loads (8 in flight per lane); E is formed in 4x4 register tiles,
+                // `parts` lanes share a tile (strided j, xor-reduced) when there are few.
+                const int np = nc + 1;
+                const int jw = min(lim, a.xs / (np + 3));   // chunk width (rows up to 4*nt4 read)
+                const int nt4 = (np + 3) >> 2;
+                const int ntile = nt4 * (nt4 + 1) / 2;
                 int parts = 64;
-                while (parts > 1 && nent * parts > 64) parts >>= 1;
+                while (parts > 1 && ntile * parts > 64) parts >>= 1;
                 const int p = lane & (parts - 1);
-                for (int e0 = 0; e0 < nent; e0 += 64 / parts) {
-                    const int e = e0 + lane / parts;
-                    double acc = 0.0;
-                    if (e < nent) {
-                        int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-                        while (ra * (ra + 1) / 2 > e) --ra;
-                        while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
-                        const int rb = e - ra * (ra + 1) / 2;
-                        const int qa = ra < nc ? cb[ra] : (ra == nc ? r : k + ra - nc - 1);
-                        const int qb = rb < nc ? cb[rb] : (rb == nc ? r : k + rb - nc - 1);
-                        const double* xa = Qs + (size_t)qa * Lq;
-                        const double* xb = Qs + (size_t)qb * Lq;
-                        for (int j = p; j < lim; j += parts) acc = fma(xa[j], xb[j], acc);
+                for (int t0 = 0; t0 < ntile; t0 += 64 / parts) {
+                    const int tix = t0 + lane / parts;
+                    int ta = 0, rem = tix < ntile ? tix : 0;
+                    while (rem > ta) {
+                        rem -= ta + 1;
+                        ++ta;
                     }
-                    for (int off = parts >> 1; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
-                    if (p == 0 && e < nent) Ew[e] = acc;
+                    const int tb = rem;
+                    double acc[4][4];
+#pragma unroll
+                    for (int x = 0; x < 4; ++x)
+#pragma unroll
+                        for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+                    for (int jc = 0; jc < lim; jc += jw) {
+                        const int jn = min(jw, lim - jc);
+                        WAVE_SYNC();   // the previous chunk is consumed
+                        for (int e0 = 0; e0 < np * jn; e0 += 8 * 64) {
+                            double v[8];
+#pragma unroll
+                            for (int t = 0; t < 8; ++t) {
+                                const int e = e0 + 64 * t + lane;
+                                const int ra = e / jn, j = e - ra * jn;
+                                v[t] = ra < np ? Qs[(size_t)(ra < nc ? cb[ra] : r) * Lq + jc + j] : 0.0;
+                            }
+#pragma unroll
+                            for (int t = 0; t < 8; ++t) {
+                                const int e = e0 + 64 * t + lane;
+                                if (e < np * jn) Xs[e] = v[t];
+                            }
+                        }
+                        WAVE_SYNC();
+                        if (tix < ntile) {
+                            const double* xa = Xs + 4 * ta * jn;
+                            const double* xb = Xs + 4 * tb * jn;
+                            for (int j = p; j < jn; j += parts) {
+                                double va[4], vb[4];
+#pragma unroll
+                                for (int x = 0; x < 4; ++x) {
+                                    va[x] = xa[x * jn + j];
+                                    vb[x] = xb[x * jn + j];
+                                }
+#pragma unroll
+                                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                                    for (int y = 0; y < 4; ++y) acc[x][y] = fma(va[x], vb[y], acc[x][y]);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int x = 0; x < 4; ++x)
+#pragma unroll
+                        for (int y = 0; y < 4; ++y)
+                            for (int off = parts >> 1; off >= 1; off >>= 1)
+                                acc[x][y] += __shfl_xor(acc[x][y], off);
+                    if (p == 0 && tix < ntile) {
+#pragma unroll
+                        for (int x = 0; x < 4; ++x)
+#pragma unroll
+                            for (int y = 0; y < 4; ++y) {
+                                const int ia = 4 * ta + x, ib = 4 * tb + y;
+                                if (ia < np && ib <= ia) Ew[tri(ia, ib)] = acc[x][y];
+                            }
+                    }
                 }
                 WAVE_SYNC();
+                if (a.phase_cycles && tid == 0) ph_acc[7] += __builtin_amdgcn_s_memtime() - t_w0;
                 // Border rows: row nc = P_{r,Cbar} (already in place), row nc + 1 := b.
                 // a_r on lane 63 (never a border lane's register).
+                const double2* pgh_lim = reinterpret_cast<const double2*>(PGH) + lim;
                 double bl = 0.0, ar = 0.0;
                 if (lane < nc) {
-                    bl = Ew[tri(nc + 1, lane)] - mu * Ew[tri(nc + 2, lane)];
+                    const double2 py = pgh_lim[(size_t)cb[lane] * (Lq + 1)];
+                    bl = py.x - mu * py.y;
                     for (int q = 0; q < nc; ++q) {
                         const double eq = q <= lane ? Ew[tri(lane, q)] : Ew[tri(q, lane)];
                         bl = fma(-eq, (double)s_rat[cb[q]] - mu, bl);
                     }
                 }
                 if (lane == 63) {
-                    ar = Ew[tri(nc + 1, nc)] - mu * Ew[tri(nc + 2, nc)];
+                    const double2 py = pgh_lim[(size_t)r * (Lq + 1)];
+                    ar = py.x - mu * py.y;
                     for (int q = 0; q < nc; ++q) ar = fma(-Ew[tri(nc, q)], (double)s_rat[cb[q]] - mu, ar);
                 }
                 WAVE_SYNC();
@@ -696,20 +839,21 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
         PHASE_STAMP(3);
     }
     if (a.phase_cycles && tid == 0)
-        for (int ph = 0; ph < 6; ++ph) atomicAdd(&a.phase_cycles[ph], ph_acc[ph]);
+        for (int ph = 0; ph < 8; ++ph) atomicAdd(&a.phase_cycles[ph], ph_acc[ph]);
 }
 
 template <typename T>
 int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lmax, hipStream_t stream) {
     args.lmax = lmax;
     args.ncw = std::min(kNcMax, lmax);
-    args.ew = (args.ncw + 3) * (args.ncw + 4) / 2;
-    args.a_elems = std::max((lmax + 2) * (lmax + 3) / 2, kWaves * args.ew);
+    args.ew = (args.ncw + 2) * (args.ncw + 3) / 2;
+    args.xs = (args.ncw + 4) * kJC;
+    args.a_elems = std::max((lmax + 2) * (lmax + 3) / 2, kWaves * (args.ew + args.xs));
     const size_t lds = sizeof(double) * ((size_t)args.a_elems + 4) +
                        CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 6 * sizeof(int)) + 8 * sizeof(int);
     if (lds > 163840) return cf_set_error(ctx, CF_ERANGE, "predict bucket exceeds LDS");
     int blocks = (int)std::min<uint32_t>(count, 2048u);
-    const size_t per_block = (size_t)lmax * lmax + (size_t)(lmax + 2) * lmax;
+    const size_t per_block = (size_t)lmax * lmax + (size_t)(lmax + 2) * lmax + (size_t)lmax * (lmax + 1) * 2;
     const size_t need = (size_t)blocks * per_block * sizeof(double);
     if (need > ctx->scratch_bytes) {
         if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
@@ -720,6 +864,7 @@ int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lma
     }
     args.gbar = reinterpret_cast<double*>(ctx->d_scratch);
     args.qs = args.gbar + (size_t)blocks * lmax * lmax;
+    args.pgh = args.qs + (size_t)blocks * (lmax + 2) * lmax;
     CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)predict_kernel<T>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(predict_kernel<T>, dim3(blocks), dim3(kThreads), lds, stream, args, count);

@@ -63,8 +63,9 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
 int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out8);
 /* Diagnostics: predictor phase totals (s_memtime cycles, thread 0 of each block):
  * {per-user setup, basis Q, fast-path ratings, dense-path ratings} cycles, then the
- * number of ratings taken by the fast and by the dense path. */
-int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out6);
+ * number of ratings taken by the fast and by the dense path, then wave 0's cycles in
+ * the fast path's connected-set gather and in its projector entries. */
+int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out8);
 
 /* ---- item graph (out_fin_) ---------------------------------------------------
  * Directed weighted graph exactly as parsed: w(a,b) and w(b,a) are independent.
