@@ -17,24 +17,31 @@
 // Fast path (per user, then one wave per rating).  The prediction is the value at row
 // r of the least-squares fit of r_C - mean on span(U_CS): it depends on U_S only
 // through an orthonormal basis Q_S of its column span.  Once per user:
-//   Gbar = U^T U over the columns [0, Lu), Lu = max_r lim_r;  Gbar = L D L^T;
-//   Q = U L^-T D^-1/2 (Cholesky QR; the leading lim columns of Q span the leading lim
-//   columns of U, so one Q serves every row's prefix S = [0, lim));
-//   g = Q^T r, h = Q^T 1, and the prefix tables PG(i, l) = sum_{j<l} Q_ij g_j,
-//   PH(i, l) = sum_{j<l} Q_ij h_j.
+//   Gbar = U^T U over the columns [0, Lu), Lu = max_r lim_r;
+//   Q = U T1 T2 with T = I - su(G - I) - diag(G - I) / 2 (su = strictly upper part),
+//   T1 from Gbar and T2 from (U T1)^T (U T1).  U is near-orthonormal (eigenvectors:
+//   |Gbar - I| ~ 1e-6), each step squares the orthogonality error (1e-6 -> 1e-12 ->
+//   1e-24), and T1, T2 are upper triangular, so the leading lim columns of Q span the
+//   leading lim columns of U and one Q serves every row's prefix S = [0, lim).  All
+//   four products are tiled GEMM-shaped work (no sequential factorisation);
+//   g = Q^T r, h = Q^T 1, the prefix tables PG(i, l) = sum_{j<l} Q_ij g_j,
+//   PH(i, l) = sum_{j<l} Q_ij h_j, and the projector P = Q Q^T (k x k).
 // With P = Q_S Q_S^T (the k x k projector), Cbar = rows not in C (nc of them),
 // y = r - mean, and Q_S^T Q_S = I:
 //   pred - mean = a_r + P_{r,Cbar} K^-1 b,   K = I - P_{Cbar,Cbar}  (nc x nc),
 //   a_r = (P y)_r - P_{r,Cbar} y_Cbar,   b = (P y)_Cbar - P_{Cbar,Cbar} y_Cbar,
 // (Woodbury on U_CS^T U_CS = Q_S^T Q_S - Q_CbarS^T Q_CbarS), where (P y)_i =
-// PG(i, lim) - mean PH(i, lim).  A rating therefore costs (nc + 1)(nc + 2) / 2 dot
-// products of length lim and an nc x nc LDL^T instead of a lim x lim factorisation.
+// PG(i, lim) - mean PH(i, lim).  lim is all but constant within a user (mean Lu - lim
+// = 0.08 on the C2 workload), so the entries of P_S = P - sum_{j in [lim, Lu)} Q_j Q_j^T
+// are gathers from P with a (usually empty) tail correction.  A rating therefore costs
+// (nc + 1)(nc + 2) / 2 gathers and an nc x nc LDL^T instead of a lim x lim
+// factorisation.
 //
 // Dense path (block-wide, the rating's own Gram matrix) for the ratings the fast path
 // does not take: the column filter drops a column, nc > kNcMax, c = 0, a pivot of K
 // below kPivMin while c >= lim (full rank but ill-conditioned: U_CS^T U_CS has an
-// eigenvalue < kPivMin), or Q is not trusted that far (a D_j of Gbar below half of
-// Gbar_jj: U is not near-orthonormal).
+// eigenvalue < kPivMin), or U is not near-orthonormal (max |Gbar - I| > kOrthoMax: no
+// Q for this user).
 // It factors M = U_CS^T U_CS = L D L^T (blocked, right-looking, packed lower triangle
 // in LDS), bordered by t^T and v^T so the factorisation itself yields L^-1 t and
 // L^-1 v and pred = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean.  When the complement is
@@ -50,12 +57,11 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kNcMax = 62;            // fast path: complement rows (nc + 2 border rows <= 64 lanes)
-constexpr int kJC = 32;               // fast path: minimum columns of X staged per chunk
 // fast path: smallest pivot of K = I - P_CbarCbar (its pivots bound the smallest
 // eigenvalue of U_CS^T U_CS in the Q basis, so this admits cond <~ 1e10, where the
 // reference's own explicit inverse is accurate to ~cond * eps; parity is tested to 1e8)
 constexpr double kPivMin = 1e-10;
-constexpr double kBasisMin = 0.5;     // D_j / Gbar_jj below this: Q not trusted from j on
+constexpr double kOrthoMax = 1e-5;    // max |Gbar - I| for the two-step basis (error ~ 1e-20)
 
 template <typename T>
 struct PredArgs {
@@ -79,10 +85,10 @@ struct PredArgs {
     int lmax;              // Gram dimension bound of the launch
     int ncw;               // fast-path bound on nc for this launch
     int ew;                // doubles of per-wave fast-path matrix E / K
-    int xs;                // doubles of per-wave fast-path staging buffer
     int a_elems;           // doubles of the shared factorisation / scratch region
     double* gbar;          // per-block scratch: Gbar = U^T U (lmax x lmax, full), fp64
     double* qs;            // per-block scratch: Q ((lmax + 2) x lmax rows: Q, g, h), fp64
+    double* q1;            // per-block scratch: U T1, then P = Q Q^T (lmax x lmax), fp64
     double* pgh;           // per-block scratch: {PG, PH}(i, l), lmax x (lmax + 1) pairs, fp64
 };
 
@@ -292,6 +298,109 @@ __device__ void gram_tiles(const T* U, int m, int n, int k, Out out) {
     }
 }
 
+// P(i, l) = sum_{j < n} Q(i, j) Q(l, j), i, l < k (Q row-major, stride n), written in
+// full (stride k).  4x4 register tiles of the lower triangle, two j in flight.
+__device__ void row_gram_tiles(const double* Q, int n, int k, double* P) {
+    const int nt4 = (k + 3) >> 2;
+    const int ntile = nt4 * (nt4 + 1) / 2;
+    for (int tix = threadIdx.x; tix < ntile; tix += kThreads) {
+        int ta = 0, rem = tix;
+        while (rem > ta) {
+            rem -= ta + 1;
+            ++ta;
+        }
+        const int tb = rem;
+        const double* qa[4];
+        const double* qb[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            qa[x] = Q + (size_t)min(4 * ta + x, k - 1) * n;
+            qb[x] = Q + (size_t)min(4 * tb + x, k - 1) * n;
+        }
+        double acc[4][4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+        for (int j = 0; j < n; j += 2) {
+            double va[2][4], vb[2][4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int jj = min(j + h, n - 1);
+                const double w = (j + h < n) ? 1.0 : 0.0;
+#pragma unroll
+                for (int x = 0; x < 4; ++x) {
+                    va[h][x] = qa[x][jj] * w;
+                    vb[h][x] = qb[x][jj];
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                    for (int y = 0; y < 4; ++y) acc[x][y] = fma(va[h][x], vb[h][y], acc[x][y]);
+        }
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) {
+                const int ia = 4 * ta + x, ib = 4 * tb + y;
+                if (ia < k && ib <= ia) {
+                    P[(size_t)ia * k + ib] = acc[x][y];
+                    P[(size_t)ib * k + ia] = acc[x][y];
+                }
+            }
+    }
+}
+
+// out(i, j) = sum_{l <= j} X(i, l) T(l, j) for i < k, j < n: X row-major (stride ldx),
+// T upper triangular, stored as the packed lower triangle of T^T (Tt[tri(j, l)] =
+// T(l, j)).  4x4 register tiles, two l in flight.
+template <typename TX>
+__device__ void trmm_tiles(const TX* X, int ldx, int k, int n, const double* Tt, double* out, int ldo) {
+    const int tr = (k + 3) >> 2, tc = (n + 3) >> 2;
+    for (int tix = threadIdx.x; tix < tr * tc; tix += kThreads) {
+        const int ti = tix / tc, tj = tix - ti * tc;
+        const TX* xr[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) xr[x] = X + (size_t)min(4 * ti + x, k - 1) * ldx;
+        int jr[4];
+#pragma unroll
+        for (int y = 0; y < 4; ++y) jr[y] = min(4 * tj + y, n - 1);
+        double acc[4][4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+        const int lend = jr[3] + 1;   // T(l, j) = 0 for l > j
+        for (int l = 0; l < lend; l += 2) {
+            double xv[2][4], tv[2][4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int ll = min(l + h, lend - 1);
+#pragma unroll
+                for (int x = 0; x < 4; ++x) xv[h][x] = (l + h < lend) ? (double)xr[x][ll] : 0.0;
+#pragma unroll
+                for (int y = 0; y < 4; ++y) tv[h][y] = (ll <= jr[y]) ? Tt[tri(jr[y], ll)] : 0.0;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                    for (int y = 0; y < 4; ++y) acc[x][y] = fma(xv[h][x], tv[h][y], acc[x][y]);
+        }
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) {
+                const int i = 4 * ti + x, j = 4 * tj + y;
+                if (i < k && j < n) out[(size_t)i * ldo + j] = acc[x][y];
+            }
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32_t count) {
     extern __shared__ double dsm[];
@@ -371,11 +480,15 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
         const int Lu = s_cnt[5];
 
         // Gbar = U^T U over the columns [0, Lu), all k rows: full copy in Gb (the dense
-        // path's complement form reads it), lower triangle packed into A for LDL^T.
+        // path's complement form reads it); max |Gbar - I| (non-negative floats order
+        // as their bit patterns) decides whether this user gets a basis.
+        if (tid == 0) s_cnt[6] = 0;
+        __syncthreads();
         gram_tiles(U, m, Lu, k, [&](int ia, int ib, double v) {
             Gb[(size_t)ia * lmax + ib] = v;
             Gb[(size_t)ib * lmax + ia] = v;
-            A[tri(ia, ib)] = v;
+            const float dev = (float)fabs(v - (ia == ib ? 1.0 : 0.0));
+            atomicMax(&s_cnt[6], __float_as_int(dev == dev ? dev : 3.0e38f));
         });
         for (int j = tid; j < Lu; j += kThreads) {
             int cnt = 0;
@@ -389,48 +502,37 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
             s_cpos[j] = cnt;
         }
         __syncthreads();
-        ldlt_bordered(A, Lu, Lu);
-        if (tid == 0) s_cnt[6] = Lu;
-        __syncthreads();
-        for (int j = tid; j < Lu; j += kThreads)
-            if (!(A[tri(j, j)] >= kBasisMin * Gb[(size_t)j * lmax + j])) atomicMin(&s_cnt[6], j);
-        __syncthreads();
-        const int Lq = s_cnt[6];
+        const int Lq = (__int_as_float(s_cnt[6]) <= (float)kOrthoMax) ? Lu : 0;
         PHASE_STAMP(0);
 
-        // Q = U L^-T D^-1/2 (row i of Q: forward substitution of row i of U against the
-        // unit-lower L, 16 columns at a time in registers), then g = Q^T r, h = Q^T 1
-        // as rows k and k + 1.  Row stride Lq.
-        for (int i = tid; i < k; i += kThreads) {
-            double* qi = Qs + (size_t)i * Lq;
-            const T* ui = U + (size_t)i * m;
-            for (int j0 = 0; j0 < Lq; j0 += 16) {
-                double x[16];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) x[q] = (j0 + q < Lq) ? (double)ui[j0 + q] : 0.0;
-                for (int p = 0; p < j0; p += 4) {   // j0 is a multiple of 16
-                    double wv[4];
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) wv[t] = qi[p + t];
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-#pragma unroll
-                        for (int q = 0; q < 16; ++q)
-                            if (j0 + q < Lq) x[q] = fma(-A[tri(j0 + q, p + t)], wv[t], x[q]);
-                }
-#pragma unroll
-                for (int q = 1; q < 16; ++q)
-#pragma unroll
-                    for (int p = 0; p < q; ++p)
-                        if (j0 + q < Lq) x[q] = fma(-A[tri(j0 + q, j0 + p)], x[p], x[q]);
-#pragma unroll
-                for (int q = 0; q < 16; ++q)
-                    if (j0 + q < Lq) qi[j0 + q] = x[q];
+        // Q = (U T1) T2; T^T packed lower in A: T(l, j) = -G(l, j) (l < j), 1.5 - G(j, j) / 2.
+        double* Q1 = a.q1 + (size_t)blockIdx.x * lmax * lmax;
+        if (Lq > 0) {
+            for (int e = tid; e < Lq * (Lq + 1) / 2; e += kThreads) {
+                int j = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+                while (j * (j + 1) / 2 > e) --j;
+                while ((j + 1) * (j + 2) / 2 <= e) ++j;
+                const int l = e - j * (j + 1) / 2;
+                const double g = Gb[(size_t)l * lmax + j];
+                A[e] = (l == j) ? 1.5 - 0.5 * g : -g;
             }
-            for (int j = 0; j < Lq; ++j) qi[j] *= 1.0 / sqrt(A[tri(j, j)]);
+            __syncthreads();
+            trmm_tiles(U, m, k, Lq, A, Q1, Lq);
+            __syncthreads();
+            gram_tiles(Q1, Lq, Lq, k, [&](int ia, int ib, double v) { A[tri(ia, ib)] = v; });
+            __syncthreads();
+            for (int e = tid; e < Lq * (Lq + 1) / 2; e += kThreads) {
+                int j = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+                while (j * (j + 1) / 2 > e) --j;
+                while ((j + 1) * (j + 2) / 2 <= e) ++j;
+                const int l = e - j * (j + 1) / 2;
+                A[e] = (l == j) ? 1.5 - 0.5 * A[e] : -A[e];   // G2 symmetric: G2(l, j) = A[tri(j, l)]
+            }
+            __syncthreads();
+            trmm_tiles(Q1, Lq, k, Lq, A, Qs, Lq);
         }
         __syncthreads();
-        // g, h (global rows k, k + 1 of Qs, and staged in A: L is no longer needed)
+        // g, h (global rows k, k + 1 of Qs, and staged in A: T2 is no longer needed)
         double* s_g = A;
         double* s_h = A + Lq;
         for (int j = tid; j < Lq; j += kThreads) {
@@ -469,13 +571,14 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                     }
             }
         }
+        double* Pm = Q1;   // U T1 is consumed: P = Q Q^T takes its place
+        if (Lq > 0) row_gram_tiles(Qs, Lq, k, Pm);
         __syncthreads();
         PHASE_STAMP(1);
 
         // ---- fast path: one wave per rating ------------------------------------------
         {
-            double* Ew = A + (size_t)wave * (a.ew + a.xs);
-            double* Xs = Ew + a.ew;   // (ncw + 4) x kJC staged chunk of X
+            double* Ew = A + (size_t)wave * a.ew;
             int* cb = s_cbar + wave * 64;
             const double sum_all = s_misc[1];
             // graph(movie_r, item_i) for this wave's next rating, loaded one rating ahead
@@ -538,81 +641,22 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                     t_w0 = now;
                 }
 
-                // E = Gram over j < lim of the Q rows X = [Cbar..., r] (np rows, packed
-                // lower): column chunks of X, as wide as the wave's staging buffer allows
-                // (all of [0, lim) at once for small np), are staged in LDS with coalesced
-                // loads (8 in flight per lane); E is formed in 4x4 register tiles,
-                // `parts` lanes share a tile (strided j, xor-reduced) when there are few.
+                // E = P_S over the rows [Cbar..., r] (np rows, packed lower): gathers
+                // from P, minus the tail sum_{j in [lim, Lq)} Q_aj Q_bj when lim < Lq.
                 const int np = nc + 1;
-                const int jw = min(lim, a.xs / (np + 3));   // chunk width (rows up to 4*nt4 read)
-                const int nt4 = (np + 3) >> 2;
-                const int ntile = nt4 * (nt4 + 1) / 2;
-                int parts = 64;
-                while (parts > 1 && ntile * parts > 64) parts >>= 1;
-                const int p = lane & (parts - 1);
-                for (int t0 = 0; t0 < ntile; t0 += 64 / parts) {
-                    const int tix = t0 + lane / parts;
-                    int ta = 0, rem = tix < ntile ? tix : 0;
-                    while (rem > ta) {
-                        rem -= ta + 1;
-                        ++ta;
-                    }
-                    const int tb = rem;
-                    double acc[4][4];
-#pragma unroll
-                    for (int x = 0; x < 4; ++x)
-#pragma unroll
-                        for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
-                    for (int jc = 0; jc < lim; jc += jw) {
-                        const int jn = min(jw, lim - jc);
-                        WAVE_SYNC();   // the previous chunk is consumed
-                        for (int e0 = 0; e0 < np * jn; e0 += 8 * 64) {
-                            double v[8];
-#pragma unroll
-                            for (int t = 0; t < 8; ++t) {
-                                const int e = e0 + 64 * t + lane;
-                                const int ra = e / jn, j = e - ra * jn;
-                                v[t] = ra < np ? Qs[(size_t)(ra < nc ? cb[ra] : r) * Lq + jc + j] : 0.0;
-                            }
-#pragma unroll
-                            for (int t = 0; t < 8; ++t) {
-                                const int e = e0 + 64 * t + lane;
-                                if (e < np * jn) Xs[e] = v[t];
-                            }
-                        }
-                        WAVE_SYNC();
-                        if (tix < ntile) {
-                            const double* xa = Xs + 4 * ta * jn;
-                            const double* xb = Xs + 4 * tb * jn;
-                            for (int j = p; j < jn; j += parts) {
-                                double va[4], vb[4];
-#pragma unroll
-                                for (int x = 0; x < 4; ++x) {
-                                    va[x] = xa[x * jn + j];
-                                    vb[x] = xb[x * jn + j];
-                                }
-#pragma unroll
-                                for (int x = 0; x < 4; ++x)
-#pragma unroll
-                                    for (int y = 0; y < 4; ++y) acc[x][y] = fma(va[x], vb[y], acc[x][y]);
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int x = 0; x < 4; ++x)
-#pragma unroll
-                        for (int y = 0; y < 4; ++y)
-                            for (int off = parts >> 1; off >= 1; off >>= 1)
-                                acc[x][y] += __shfl_xor(acc[x][y], off);
-                    if (p == 0 && tix < ntile) {
-#pragma unroll
-                        for (int x = 0; x < 4; ++x)
-#pragma unroll
-                            for (int y = 0; y < 4; ++y) {
-                                const int ia = 4 * ta + x, ib = 4 * tb + y;
-                                if (ia < np && ib <= ia) Ew[tri(ia, ib)] = acc[x][y];
-                            }
-                    }
+                const int nent = np * (np + 1) / 2;
+                for (int e = lane; e < nent; e += 64) {
+                    int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+                    while (ra * (ra + 1) / 2 > e) --ra;
+                    while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
+                    const int rb = e - ra * (ra + 1) / 2;
+                    const int ia = ra < nc ? cb[ra] : r;
+                    const int ib = rb < nc ? cb[rb] : r;
+                    double v = Pm[(size_t)ia * k + ib];
+                    const double* xa = Qs + (size_t)ia * Lq;
+                    const double* xb = Qs + (size_t)ib * Lq;
+                    for (int j = lim; j < Lq; ++j) v = fma(-xa[j], xb[j], v);
+                    Ew[e] = v;
                 }
                 WAVE_SYNC();
                 if (a.phase_cycles && tid == 0) ph_acc[7] += __builtin_amdgcn_s_memtime() - t_w0;
@@ -847,13 +891,13 @@ int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lma
     args.lmax = lmax;
     args.ncw = std::min(kNcMax, lmax);
     args.ew = (args.ncw + 2) * (args.ncw + 3) / 2;
-    args.xs = (args.ncw + 4) * kJC;
-    args.a_elems = std::max((lmax + 2) * (lmax + 3) / 2, kWaves * (args.ew + args.xs));
+    args.a_elems = std::max((lmax + 2) * (lmax + 3) / 2, kWaves * args.ew);
     const size_t lds = sizeof(double) * ((size_t)args.a_elems + 4) +
                        CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 6 * sizeof(int)) + 8 * sizeof(int);
     if (lds > 163840) return cf_set_error(ctx, CF_ERANGE, "predict bucket exceeds LDS");
     int blocks = (int)std::min<uint32_t>(count, 2048u);
-    const size_t per_block = (size_t)lmax * lmax + (size_t)(lmax + 2) * lmax + (size_t)lmax * (lmax + 1) * 2;
+    const size_t per_block = (size_t)lmax * lmax + (size_t)(lmax + 2) * lmax + (size_t)lmax * (lmax + 1) * 2 +
+                             (size_t)lmax * lmax;
     const size_t need = (size_t)blocks * per_block * sizeof(double);
     if (need > ctx->scratch_bytes) {
         if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
@@ -865,6 +909,7 @@ int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lma
     args.gbar = reinterpret_cast<double*>(ctx->d_scratch);
     args.qs = args.gbar + (size_t)blocks * lmax * lmax;
     args.pgh = args.qs + (size_t)blocks * (lmax + 2) * lmax;
+    args.q1 = args.pgh + (size_t)blocks * lmax * (lmax + 1) * 2;
     CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)predict_kernel<T>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(predict_kernel<T>, dim3(blocks), dim3(kThreads), lds, stream, args, count);

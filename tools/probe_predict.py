@@ -92,3 +92,16 @@ for u in range(min(users, 600)):
         if nc and np.linalg.eigvalsh(K).min() < 1e-6: reasons["ill"] += 1
         else: reasons["fast"] += 1
 print("reasons", reasons)
+# entry-work distribution and tail length (all users)
+tot_e = 0.0; tot_tail = 0.0; tot_lim = 0.0; nr = 0; e_by = np.zeros(8)
+bins = [0, 4, 8, 16, 24, 32, 48, 63, 10**9]
+for u in range(users):
+    b, e = int(off[u]), int(off[u + 1]); mu = int(m[u]); ku = e - b
+    if mu < 2: continue
+    lim = np.minimum(np.maximum(np.searchsorted(ev[b:b + mu], sg[:ku], side="right"), 2), mu)
+    nc_u = ku - kk[b:e]
+    w = (nc_u + 1) * (nc_u + 2) / 2 * lim
+    tot_e += w.sum(); tot_tail += (lim.max() - lim).sum(); tot_lim += lim.sum(); nr += ku
+    e_by += np.histogram(nc_u, bins=bins, weights=w)[0]
+print("entry FMA per rating", tot_e / nr, "mean lim", tot_lim / nr, "mean tail Lu-lim", tot_tail / nr)
+print("entry-work share by nc bins", dict(zip([f"<{b}" for b in bins[1:]], np.round(e_by / e_by.sum(), 3))))
