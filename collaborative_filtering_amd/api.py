@@ -100,11 +100,11 @@ class Context:
         return None
 
     def debug_phases(self, enable: bool = True, read: bool = False):
-        """Predictor phase cycles {setup, basis, fast, dense} and rating counts {n_fast, n_dense}."""
+        """Predictor phase cycles {setup, basis, fast, block} and rating counts; see cf_abi.h."""
         out = np.zeros(8, dtype=np.uint64) if read else None
         self._chk(self.lib.cf_debug_phases(self.h, int(enable), ptr(out)), "cf_debug_phases")
         if read:
-            return dict(zip(["setup", "basis", "fast", "dense", "n_fast", "n_dense", "w0_conn", "w0_entries"], map(int, out)))
+            return dict(zip(["setup", "basis", "fast", "dense", "n_fast", "n_dense", "gram", "wide"], map(int, out)))
         return None
 
     # -- item graph (out_fin_) ---------------------------------------------------

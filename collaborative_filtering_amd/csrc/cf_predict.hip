@@ -233,172 +233,86 @@ __device__ void ldlt_bordered(double* A, int L, int nrows) {
     }
 }
 
-// Symmetric Gram of the columns [0, n) of U over rows rows[0..nr) (or all k rows when
-// rows == null), 4x4 register tiles of the lower triangle.  Writes G(ia, ib) to
-// out(ia, ib) via the functor.
-template <typename T, typename Out>
-__device__ void gram_tiles(const T* U, int m, int n, int k, Out out) {
-    const int nt4 = (n + 3) >> 2;
-    const int ntile = nt4 * (nt4 + 1) / 2;
-    for (int tix = threadIdx.x; tix < ntile; tix += kThreads) {
-        int ta = 0, rem = tix;
-        while (rem > ta) {
-            rem -= ta + 1;
-            ++ta;
-        }
-        const int tb = rem;
-        int ca[4], cb[4];
+// Block-level GEMM on 64 x 64 output blocks: C(i, j) = sum_{l < kend(j0)} A(i, l) B(l, j)
+// for i < M, j < N, over the blocks (i0, j0) with want(i0, j0).  A(i, l) =
+// xA(i, l, loadA(i, l)) and likewise B: load* only reads memory, x* converts / applies
+// a formula, so the loads of the next 16-deep chunk stay in flight (raw, in registers)
+// while the current chunk -- staged in LDS as fp64 (`stage`: kStageElems doubles) with
+// coalesced loads -- is consumed; the conversions run when the chunk is written to LDS.
+// A_LFAST / B_LFAST say whether l is the operand's contiguous index in memory.  Each
+// thread owns a 4 x 4 register tile.  Called by the whole block; the caller
+// synchronises before reading C.
+constexpr int kStageLd = 65;                       // odd stride: conflict-free staging writes
+constexpr int kStageElems = 2 * 16 * kStageLd;
+template <bool A_LFAST, bool B_LFAST, class LA, class XA, class LB, class XB, class FK, class FW, class FO>
+__device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK kend, FW want, FO out,
+                           double* stage) {
+    double* As = stage;
+    double* Bs = stage + 16 * kStageLd;
+    const int tid = threadIdx.x;
+    const int tx = tid & 15, ty = tid >> 4;
+    using RA = decltype(loadA(0, 0));
+    using RB = decltype(loadB(0, 0));
+    for (int i0 = 0; i0 < M; i0 += 64)
+        for (int j0 = 0; j0 < N; j0 += 64) {
+            if (!want(i0, j0)) continue;
+            const int K = kend(j0);
+            double acc[4][4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            ca[q] = min(4 * ta + q, n - 1);
-            cb[q] = min(4 * tb + q, n - 1);
-        }
-        double acc[4][4];
+            for (int x = 0; x < 4; ++x)
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
+                for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+            RA ra[4];
+            RB rb[4];
+            // unconditional loads from clamped indices: a guarded load would become a
+            // branch with its own wait (one full latency per load)
+            auto fetch = [&](int l0) {
 #pragma unroll
-            for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
-        int i = 0;
-        for (; i + 1 < k; i += 2) {   // two rows in flight: 16 independent loads
-            const T* row0 = U + (size_t)i * m;
-            const T* row1 = row0 + m;
-            double va0[4], vb0[4], va1[4], vb1[4];
+                for (int t = 0; t < 4; ++t) {
+                    const int e = tid + kThreads * t;
+                    const int ia = A_LFAST ? (e >> 4) : (e & 63), la = A_LFAST ? (e & 15) : (e >> 6);
+                    const int jb = B_LFAST ? (e >> 4) : (e & 63), lb = B_LFAST ? (e & 15) : (e >> 6);
+                    ra[t] = loadA(min(i0 + ia, M - 1), min(l0 + la, K - 1));
+                    rb[t] = loadB(min(l0 + lb, K - 1), min(j0 + jb, N - 1));
+                }
+            };
+            if (K > 0) fetch(0);
+            for (int l0 = 0; l0 < K; l0 += 16) {
+                __syncthreads();   // the previous chunk is consumed
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                va0[q] = (double)row0[ca[q]];
-                vb0[q] = (double)row0[cb[q]];
-                va1[q] = (double)row1[ca[q]];
-                vb1[q] = (double)row1[cb[q]];
+                for (int t = 0; t < 4; ++t) {
+                    const int e = tid + kThreads * t;
+                    const int ia = A_LFAST ? (e >> 4) : (e & 63), la = A_LFAST ? (e & 15) : (e >> 6);
+                    const int jb = B_LFAST ? (e >> 4) : (e & 63), lb = B_LFAST ? (e & 15) : (e >> 6);
+                    const bool oka = i0 + ia < M && l0 + la < K;
+                    const bool okb = j0 + jb < N && l0 + lb < K;
+                    As[la * kStageLd + ia] = oka ? xA(i0 + ia, l0 + la, ra[t]) : 0.0;
+                    Bs[lb * kStageLd + jb] = okb ? xB(l0 + lb, j0 + jb, rb[t]) : 0.0;
+                }
+                __syncthreads();
+                if (l0 + 16 < K) fetch(l0 + 16);
+#pragma unroll 4
+                for (int l = 0; l < 16; ++l) {
+                    double av[4], bv[4];
+#pragma unroll
+                    for (int x = 0; x < 4; ++x) {
+                        av[x] = As[l * kStageLd + 4 * ty + x];
+                        bv[x] = Bs[l * kStageLd + 4 * tx + x];
+                    }
+#pragma unroll
+                    for (int x = 0; x < 4; ++x)
+#pragma unroll
+                        for (int y = 0; y < 4; ++y) acc[x][y] = fma(av[x], bv[y], acc[x][y]);
+                }
             }
 #pragma unroll
             for (int x = 0; x < 4; ++x)
 #pragma unroll
-                for (int y = 0; y < 4; ++y) acc[x][y] = fma(va1[x], vb1[y], fma(va0[x], vb0[y], acc[x][y]));
-        }
-        if (i < k) {
-            const T* row = U + (size_t)i * m;
-            double va[4], vb[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                va[q] = (double)row[ca[q]];
-                vb[q] = (double)row[cb[q]];
-            }
-#pragma unroll
-            for (int x = 0; x < 4; ++x)
-#pragma unroll
-                for (int y = 0; y < 4; ++y) acc[x][y] = fma(va[x], vb[y], acc[x][y]);
-        }
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y = 0; y < 4; ++y) {
-                const int ia = 4 * ta + x, ib = 4 * tb + y;
-                if (ia < n && ib <= ia) out(ia, ib, acc[x][y]);
-            }
-    }
-}
-
-// P(i, l) = sum_{j < n} Q(i, j) Q(l, j), i, l < k (Q row-major, stride n), written in
-// full (stride k).  4x4 register tiles of the lower triangle, two j in flight.
-__device__ void row_gram_tiles(const double* Q, int n, int k, double* P) {
-    const int nt4 = (k + 3) >> 2;
-    const int ntile = nt4 * (nt4 + 1) / 2;
-    for (int tix = threadIdx.x; tix < ntile; tix += kThreads) {
-        int ta = 0, rem = tix;
-        while (rem > ta) {
-            rem -= ta + 1;
-            ++ta;
-        }
-        const int tb = rem;
-        const double* qa[4];
-        const double* qb[4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-            qa[x] = Q + (size_t)min(4 * ta + x, k - 1) * n;
-            qb[x] = Q + (size_t)min(4 * tb + x, k - 1) * n;
-        }
-        double acc[4][4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
-        for (int j = 0; j < n; j += 2) {
-            double va[2][4], vb[2][4];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int jj = min(j + h, n - 1);
-                const double w = (j + h < n) ? 1.0 : 0.0;
-#pragma unroll
-                for (int x = 0; x < 4; ++x) {
-                    va[h][x] = qa[x][jj] * w;
-                    vb[h][x] = qb[x][jj];
+                for (int y = 0; y < 4; ++y) {
+                    const int i = i0 + 4 * ty + x, j = j0 + 4 * tx + y;
+                    if (i < M && j < N) out(i, j, acc[x][y]);
                 }
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int x = 0; x < 4; ++x)
-#pragma unroll
-                    for (int y = 0; y < 4; ++y) acc[x][y] = fma(va[h][x], vb[h][y], acc[x][y]);
         }
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y = 0; y < 4; ++y) {
-                const int ia = 4 * ta + x, ib = 4 * tb + y;
-                if (ia < k && ib <= ia) {
-                    P[(size_t)ia * k + ib] = acc[x][y];
-                    P[(size_t)ib * k + ia] = acc[x][y];
-                }
-            }
-    }
-}
-
-// out(i, j) = sum_{l <= j} X(i, l) T(l, j) for i < k, j < n: X row-major (stride ldx),
-// T upper triangular, stored as the packed lower triangle of T^T (Tt[tri(j, l)] =
-// T(l, j)).  4x4 register tiles, two l in flight.
-template <typename TX>
-__device__ void trmm_tiles(const TX* X, int ldx, int k, int n, const double* Tt, double* out, int ldo) {
-    const int tr = (k + 3) >> 2, tc = (n + 3) >> 2;
-    for (int tix = threadIdx.x; tix < tr * tc; tix += kThreads) {
-        const int ti = tix / tc, tj = tix - ti * tc;
-        const TX* xr[4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x) xr[x] = X + (size_t)min(4 * ti + x, k - 1) * ldx;
-        int jr[4];
-#pragma unroll
-        for (int y = 0; y < 4; ++y) jr[y] = min(4 * tj + y, n - 1);
-        double acc[4][4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
-        const int lend = jr[3] + 1;   // T(l, j) = 0 for l > j
-        for (int l = 0; l < lend; l += 2) {
-            double xv[2][4], tv[2][4];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int ll = min(l + h, lend - 1);
-#pragma unroll
-                for (int x = 0; x < 4; ++x) xv[h][x] = (l + h < lend) ? (double)xr[x][ll] : 0.0;
-#pragma unroll
-                for (int y = 0; y < 4; ++y) tv[h][y] = (ll <= jr[y]) ? Tt[tri(jr[y], ll)] : 0.0;
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int x = 0; x < 4; ++x)
-#pragma unroll
-                    for (int y = 0; y < 4; ++y) acc[x][y] = fma(xv[h][x], tv[h][y], acc[x][y]);
-        }
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y = 0; y < 4; ++y) {
-                const int i = 4 * ti + x, j = 4 * tj + y;
-                if (i < k && j < n) out[(size_t)i * ldo + j] = acc[x][y];
-            }
-    }
 }
 
 template <typename T>
@@ -429,8 +343,8 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
     const int lane = tid & 63;
     const int wave = tid >> 6;
     // Diagnostic phase stamps (thread 0 only; no effect on outputs):
-    // {user setup, basis Q, fast ratings, dense ratings} cycles, {#fast, #dense} ratings,
-    // wave 0's {connected set + filter, projector entries} cycles in the fast path.
+    // {user setup, basis Q, fast ratings, block-wide ratings} cycles, {#fast, #block-wide}
+    // ratings, {Gbar GEMM, block-wide K path} cycles.
     unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long ph_t = 0;
 #define PHASE_STAMP(ph)                                                   \
@@ -481,23 +395,41 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
 
         // Gbar = U^T U over the columns [0, Lu), all k rows: full copy in Gb (the dense
         // path's complement form reads it); max |Gbar - I| (non-negative floats order
-        // as their bit patterns) decides whether this user gets a basis.
+        // as their bit patterns) decides whether this user gets a basis.  All products
+        // of this phase are block_gemm calls staged through A (free until the fast path).
+        double* stage = A;
         if (tid == 0) s_cnt[6] = 0;
         __syncthreads();
-        gram_tiles(U, m, Lu, k, [&](int ia, int ib, double v) {
-            Gb[(size_t)ia * lmax + ib] = v;
-            Gb[(size_t)ib * lmax + ia] = v;
-            const float dev = (float)fabs(v - (ia == ib ? 1.0 : 0.0));
-            atomicMax(&s_cnt[6], __float_as_int(dev == dev ? dev : 3.0e38f));
-        });
+        unsigned long long tg0 = (a.phase_cycles && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
+        const auto all_blocks = [](int, int) { return true; };
+        const auto lower_blocks = [](int i0, int j0) { return j0 <= i0; };
+        float dev = 0.0f;   // this thread's max |Gbar - I|
+        const auto as_double = [](int, int, auto v) { return (double)v; };
+        // T(l, j) from a symmetric G: -G(l, j) (l < j), 1.5 - G(j, j) / 2 (l = j), 0 (l > j)
+        const auto tri_T = [](int l, int j, double g) { return l < j ? -g : (l == j ? 1.5 - 0.5 * g : 0.0); };
+        block_gemm<false, false>(
+            Lu, Lu, [&](int i, int l) { return U[(size_t)l * m + i]; }, as_double,
+            [&](int l, int j) { return U[(size_t)l * m + j]; }, as_double, [&](int) { return k; }, lower_blocks,
+            [&](int i, int j, double v) {
+                if (j > i) return;
+                Gb[(size_t)i * lmax + j] = v;
+                Gb[(size_t)j * lmax + i] = v;
+                const float d = (float)fabs(v - (i == j ? 1.0 : 0.0));
+                dev = fmaxf(dev, d == d ? d : 3.0e38f);
+            },
+            stage);
+        for (int off = 32; off >= 1; off >>= 1) dev = fmaxf(dev, __shfl_xor(dev, off));
+        if (lane == 0) atomicMax(&s_cnt[6], __float_as_int(dev));
+        __syncthreads();
+        if (a.phase_cycles && tid == 0) ph_acc[6] += __builtin_amdgcn_s_memtime() - tg0;
         for (int j = tid; j < Lu; j += kThreads) {
             int cnt = 0;
             for (int i0 = 0; i0 < k; i0 += 8) {
                 double v[8];
 #pragma unroll
-                for (int t = 0; t < 8; ++t) v[t] = i0 + t < k ? (double)U[(size_t)(i0 + t) * m + j] : 0.0;
+                for (int t = 0; t < 8; ++t) v[t] = (double)U[(size_t)min(i0 + t, k - 1) * m + j];
 #pragma unroll
-                for (int t = 0; t < 8; ++t) cnt += v[t] >= 0.0001;
+                for (int t = 0; t < 8; ++t) cnt += (i0 + t < k) && v[t] >= 0.0001;
             }
             s_cpos[j] = cnt;
         }
@@ -505,31 +437,30 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
         const int Lq = (__int_as_float(s_cnt[6]) <= (float)kOrthoMax) ? Lu : 0;
         PHASE_STAMP(0);
 
-        // Q = (U T1) T2; T^T packed lower in A: T(l, j) = -G(l, j) (l < j), 1.5 - G(j, j) / 2.
+        // Q = (U T1) T2, T(l, j) = -G(l, j) (l < j), 1.5 - G(j, j) / 2 (l = j), 0 (l > j),
+        // T1 from Gbar, T2 from G2 = (U T1)^T (U T1) (held in the PGH buffer until the
+        // prefix tables are built).
         double* Q1 = a.q1 + (size_t)blockIdx.x * lmax * lmax;
+        double* G2 = PGH;
         if (Lq > 0) {
-            for (int e = tid; e < Lq * (Lq + 1) / 2; e += kThreads) {
-                int j = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-                while (j * (j + 1) / 2 > e) --j;
-                while ((j + 1) * (j + 2) / 2 <= e) ++j;
-                const int l = e - j * (j + 1) / 2;
-                const double g = Gb[(size_t)l * lmax + j];
-                A[e] = (l == j) ? 1.5 - 0.5 * g : -g;
-            }
+            const auto tri_end = [&](int j0) { return min(Lq, j0 + 64); };
+            block_gemm<true, false>(
+                k, Lq, [&](int i, int l) { return U[(size_t)i * m + l]; }, as_double,
+                [&](int l, int j) { return Gb[(size_t)l * lmax + j]; }, tri_T, tri_end, all_blocks, [&](int i, int j, double v) { Q1[(size_t)i * Lq + j] = v; }, stage);
             __syncthreads();
-            trmm_tiles(U, m, k, Lq, A, Q1, Lq);
+            block_gemm<false, false>(
+                Lq, Lq, [&](int i, int l) { return Q1[(size_t)l * Lq + i]; }, as_double,
+                [&](int l, int j) { return Q1[(size_t)l * Lq + j]; }, as_double, [&](int) { return k; }, lower_blocks,
+                [&](int i, int j, double v) {
+                    if (j > i) return;
+                    G2[(size_t)i * Lq + j] = v;
+                    G2[(size_t)j * Lq + i] = v;
+                },
+                stage);
             __syncthreads();
-            gram_tiles(Q1, Lq, Lq, k, [&](int ia, int ib, double v) { A[tri(ia, ib)] = v; });
-            __syncthreads();
-            for (int e = tid; e < Lq * (Lq + 1) / 2; e += kThreads) {
-                int j = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-                while (j * (j + 1) / 2 > e) --j;
-                while ((j + 1) * (j + 2) / 2 <= e) ++j;
-                const int l = e - j * (j + 1) / 2;
-                A[e] = (l == j) ? 1.5 - 0.5 * A[e] : -A[e];   // G2 symmetric: G2(l, j) = A[tri(j, l)]
-            }
-            __syncthreads();
-            trmm_tiles(Q1, Lq, k, Lq, A, Qs, Lq);
+            block_gemm<true, false>(
+                k, Lq, [&](int i, int l) { return Q1[(size_t)i * Lq + l]; }, as_double,
+                [&](int l, int j) { return G2[(size_t)l * Lq + j]; }, tri_T, tri_end, all_blocks, [&](int i, int j, double v) { Qs[(size_t)i * Lq + j] = v; }, stage);
         }
         __syncthreads();
         // g, h (global rows k, k + 1 of Qs, and staged in A: T2 is no longer needed)
@@ -540,10 +471,13 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
             for (int i0 = 0; i0 < k; i0 += 8) {
                 double v[8];
 #pragma unroll
-                for (int t = 0; t < 8; ++t) v[t] = i0 + t < k ? Qs[(size_t)(i0 + t) * Lq + j] : 0.0;
+                for (int t = 0; t < 8; ++t) {
+                    const double q = Qs[(size_t)min(i0 + t, k - 1) * Lq + j];
+                    v[t] = i0 + t < k ? q : 0.0;
+                }
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
-                    g = fma(v[t], i0 + t < k ? (double)s_rat[i0 + t] : 0.0, g);
+                    g = fma(v[t], (double)s_rat[min(i0 + t, k - 1)], g);   // v[t] = 0 past k
                     h += v[t];
                 }
             }
@@ -561,7 +495,10 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
             for (int j0 = 0; j0 < Lq; j0 += 8) {
                 double v[8];
 #pragma unroll
-                for (int t = 0; t < 8; ++t) v[t] = j0 + t < Lq ? qi[j0 + t] : 0.0;
+                for (int t = 0; t < 8; ++t) {
+                    const double q = qi[min(j0 + t, Lq - 1)];
+                    v[t] = j0 + t < Lq ? q : 0.0;
+                }
 #pragma unroll
                 for (int t = 0; t < 8; ++t)
                     if (j0 + t < Lq) {
@@ -572,7 +509,16 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
             }
         }
         double* Pm = Q1;   // U T1 is consumed: P = Q Q^T takes its place
-        if (Lq > 0) row_gram_tiles(Qs, Lq, k, Pm);
+        if (Lq > 0)
+            block_gemm<true, true>(
+                k, k, [&](int i, int l) { return Qs[(size_t)i * Lq + l]; }, as_double,
+                [&](int l, int j) { return Qs[(size_t)j * Lq + l]; }, as_double, [&](int) { return Lq; }, lower_blocks,
+                [&](int i, int j, double v) {
+                    if (j > i) return;
+                    Pm[(size_t)i * k + j] = v;
+                    Pm[(size_t)j * k + i] = v;
+                },
+                stage);
         __syncthreads();
         PHASE_STAMP(1);
 
@@ -589,7 +535,8 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
 #pragma unroll
                 for (int t = 0; t < 3; ++t) {
                     const int i = 64 * t + lane;
-                    gv[t] = (rr < k && i < k) ? nrow[s_item[i]] : 0.0f;
+                    const float v = nrow[s_item[min(i, k - 1)]];   // unconditional (see block_gemm)
+                    gv[t] = (rr < k && i < k) ? v : 0.0f;
                 }
             };
             load_graph_row(wave, gv_next);
@@ -615,6 +562,8 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                 const int c = k - nc;
                 const int lim = s_lim[r];
                 bool slow = c == 0 || nc > a.ncw || lim > Lq || m < 2;
+                // too many complement rows for one wave: the block-wide K path (bit 16)
+                const bool wide = !(c == 0 || lim > Lq || m < 2) && nc > a.ncw;
                 WAVE_SYNC();
                 if (!slow) {
                     // column j < lim is dropped (:284-304) iff every row with
@@ -631,13 +580,13 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                     slow = __ballot(drop) != 0ull;
                 }
                 if (slow) {
-                    if (lane == 0) s_slow[atomicAdd(&s_cnt[7], 1)] = r;
+                    if (lane == 0) s_slow[atomicAdd(&s_cnt[7], 1)] = r | (wide ? 0x10000 : 0);
                     continue;
                 }
                 const double mu = (sum_all - sc) / (double)c;   // mean over C (:311)
                 if (a.phase_cycles && tid == 0) {
                     const unsigned long long now = __builtin_amdgcn_s_memtime();
-                    ph_acc[6] += now - t_w0;
+                    (void)now;
                     t_w0 = now;
                 }
 
@@ -659,7 +608,7 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
                     Ew[e] = v;
                 }
                 WAVE_SYNC();
-                if (a.phase_cycles && tid == 0) ph_acc[7] += __builtin_amdgcn_s_memtime() - t_w0;
+
                 // Border rows: row nc = P_{r,Cbar} (already in place), row nc + 1 := b.
                 // a_r on lane 63 (never a border lane's register).
                 const double2* pgh_lim = reinterpret_cast<const double2*>(PGH) + lim;
@@ -733,9 +682,10 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
         }
         PHASE_STAMP(2);
 
-        // ---- dense path: block-wide, the rating's own bordered Gram matrix ----------------
+        // ---- block-wide paths: the K system of the fast path for large complements, and
+        // the rating's own bordered Gram matrix (dense) for everything else ---------------
         for (int si = 0; si < nslow; ++si) {
-            const int r = s_slow[si];
+            const int r = s_slow[si] & 0xffff;
             // connected set C: the user's items that are out-neighbours of movie r (:254-265)
             const float* nrow = a.graph + (size_t)s_item[r] * a.n_items;
             const bool conn = tid < k && (double)nrow[s_item[tid < k ? tid : 0]] > 0.1;
@@ -743,6 +693,98 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32
             const int nc = block_compact(tid < k && !conn, tid, s_nconn, s_cnt);
             const bool use_complement = nc < c;
             const int lim = s_lim[r];
+
+            bool wide = (s_slow[si] >> 16) != 0;
+            const unsigned long long tw0 = (a.phase_cycles && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
+            if (wide) {   // block-uniform
+                bool drop = false;   // the column filter, as in the fast path
+                if (tid < lim && s_cpos[tid] <= nc) {
+                    int hit = 0;
+                    for (int q = 0; q < nc; ++q) hit += (double)U[(size_t)s_nconn[q] * m + tid] >= 0.0001;
+                    drop = hit == s_cpos[tid];
+                }
+                wide = !__syncthreads_or(drop);
+            }
+            if (wide) {
+                // E = P_S over the rows [Cbar..., r] into A (packed), then the bordered K
+                // system exactly as in the fast path, factored by the blocked LDL^T.
+                const int np = nc + 1;
+                for (int e = tid; e < np * (np + 1) / 2; e += kThreads) {
+                    int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+                    while (ra * (ra + 1) / 2 > e) --ra;
+                    while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
+                    const int rb = e - ra * (ra + 1) / 2;
+                    const int ia = ra < nc ? s_nconn[ra] : r;
+                    const int ib = rb < nc ? s_nconn[rb] : r;
+                    double v = Pm[(size_t)ia * k + ib];
+                    const double* xa = Qs + (size_t)ia * Lq;
+                    const double* xb = Qs + (size_t)ib * Lq;
+                    for (int j = lim; j < Lq; ++j) v = fma(-xa[j], xb[j], v);
+                    A[e] = v;
+                }
+                if (wave == 0) {
+                    double sc = 0.0;
+                    for (int q = lane; q < nc; q += 64) sc += (double)s_rat[s_nconn[q]];
+                    sc = wave_sum(sc);
+                    if (lane == 0) s_misc[0] = (s_misc[1] - sc) / (double)c;
+                }
+                __syncthreads();
+                const double mu = s_misc[0];
+                const double2* pgh_lim = reinterpret_cast<const double2*>(PGH) + lim;
+                double bl = 0.0;
+                if (tid < nc) {
+                    const double2 py = pgh_lim[(size_t)s_nconn[tid] * (Lq + 1)];
+                    bl = py.x - mu * py.y;
+                    for (int q = 0; q < nc; ++q) {
+                        const double eq = q <= tid ? A[tri(tid, q)] : A[tri(q, tid)];
+                        bl = fma(-eq, (double)s_rat[s_nconn[q]] - mu, bl);
+                    }
+                }
+                if (tid == kThreads - 1) {   // a_r (k <= 192 < 255: never a row thread)
+                    const double2 py = pgh_lim[(size_t)r * (Lq + 1)];
+                    double ar = py.x - mu * py.y;
+                    for (int q = 0; q < nc; ++q) ar = fma(-A[tri(nc, q)], (double)s_rat[s_nconn[q]] - mu, ar);
+                    s_misc[2] = ar;
+                }
+                __syncthreads();
+                if (tid < nc) A[tri(nc + 1, tid)] = bl;
+                for (int e = tid; e < nc * (nc + 1) / 2; e += kThreads) {
+                    int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+                    while (ra * (ra + 1) / 2 > e) --ra;
+                    while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
+                    A[e] = (e == tri(ra, ra) ? 1.0 : 0.0) - A[e];   // K = I - P_CbarCbar
+                }
+                __syncthreads();
+                ldlt_bordered(A, nc, nc + 2);
+                if (wave == 0) {
+                    double minpiv = 1.0, dot = 0.0;
+                    for (int j = lane; j < nc; j += 64) {
+                        const double dj = A[tri(j, j)];
+                        minpiv = fmin(minpiv, dj);
+                        dot = fma(A[tri(nc, j)] * A[tri(nc + 1, j)], dj, dot);
+                    }
+                    dot = wave_sum(dot);
+                    for (int off = 32; off >= 1; off >>= 1) minpiv = fmin(minpiv, __shfl_xor(minpiv, off));
+                    if (lane == 0) {
+                        s_misc[3] = dot;
+                        s_cnt[4] = minpiv >= kPivMin ? 1 : 0;
+                    }
+                }
+                __syncthreads();
+                wide = !(s_cnt[4] == 0 && c >= lim);   // ill-conditioned full rank: dense
+                if (wide && tid == 0) {
+                    double pred = mu + s_misc[2] + s_misc[3];
+                    if (pred > 5) pred = 5;
+                    if (pred < 1) pred = 1;
+                    const double d = (double)s_rat[r] - pred;
+                    a.mse[base + r] = (float)(d * d);
+                    a.kk[base + r] = c;
+                    if (a.pred) a.pred[base + r] = pred;
+                }
+                __syncthreads();
+                if (a.phase_cycles && tid == 0) ph_acc[7] += __builtin_amdgcn_s_memtime() - tw0;
+                if (wide) continue;
+            }
 
             // zero-column filter: keep column j < lim iff some U(C, j) >= 1e-4 (:284-304)
             bool keep = false;
@@ -891,7 +933,7 @@ int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lma
     args.lmax = lmax;
     args.ncw = std::min(kNcMax, lmax);
     args.ew = (args.ncw + 2) * (args.ncw + 3) / 2;
-    args.a_elems = std::max((lmax + 2) * (lmax + 3) / 2, kWaves * args.ew);
+    args.a_elems = std::max({(lmax + 2) * (lmax + 3) / 2, kWaves * args.ew, kStageElems});
     const size_t lds = sizeof(double) * ((size_t)args.a_elems + 4) +
                        CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 6 * sizeof(int)) + 8 * sizeof(int);
     if (lds > 163840) return cf_set_error(ctx, CF_ERANGE, "predict bucket exceeds LDS");

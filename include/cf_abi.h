@@ -62,9 +62,9 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
  * steps} (cycles: s_memtime of thread 0).  enable == 0 frees them. */
 int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out8);
 /* Diagnostics: predictor phase totals (s_memtime cycles, thread 0 of each block):
- * {per-user setup, basis Q, fast-path ratings, dense-path ratings} cycles, then the
- * number of ratings taken by the fast and by the dense path, then wave 0's cycles in
- * the fast path's connected-set gather and in its projector entries. */
+ * {per-user setup, basis, fast-path ratings, block-wide ratings} cycles, the number of
+ * ratings taken by the fast path and by the block-wide paths, then the cycles of the
+ * per-user Gbar GEMM and of the block-wide K path (a subset of the block-wide cycles). */
 int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out8);
 
 /* ---- item graph (out_fin_) ---------------------------------------------------

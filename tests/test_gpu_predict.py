@@ -131,3 +131,37 @@ def test_predict_device_f32_path_matches_f64(gpu_ctx):
     assert np.array_equal(np.isnan(a), np.isnan(b))
     ok = ~np.isnan(b)
     assert np.allclose(a[ok], b[ok], rtol=1e-6, atol=1e-6)
+
+
+def test_predict_wide_complement_full_rank(gpu_ctx):
+    """Ratings whose complement Cbar exceeds one wave's K system (nc > 62) while the
+    Gram matrix keeps full rank (c >= lim): the block-wide K path must match the
+    oracle like the per-wave one.  A low w_lim (0.3) keeps lim small."""
+    ks = [150, 140, 130]
+    W, off, items, rat, m, sigs, evals, evec_off, evecs, blocks = build_case(0.5, ks, seed=70)
+    sigtab = np.full_like(sigs, 0.3)
+    gpu_ctx.upload_graph_dense(W)
+    mse_g, kk_g, _ = gpu_ctx.predict_precomp(off, items, rat, m, evals, evec_off, evecs, sigtab,
+                                             sig_mode=CF_SIGS_OWN, want_pred=True)
+    n_wide = 0
+    bad = []
+    for u in range(len(ks)):
+        b, e = int(off[u]), int(off[u + 1])
+        it = items[b:e].astype(np.int64)
+        ev, U = blocks[u]
+        ev_full = np.zeros(m[u])
+        ev_full[: min(m[u], e - b)] = ev[: min(m[u], e - b)]
+        tab = sigtab[b:e]
+        mse_o, kk_o, _ = orc.predict_user(it, rat[b:e], ev_full, U, tab, W)
+        for r in range(e - b):
+            g = b + r
+            assert kk_g[g] == kk_o[r]
+            if (e - b) - kk_o[r] <= 62 or kk_o[r] == 0:
+                continue
+            if gram_cond(it, ev_full, U, tab[r], W, r) > 1e8:
+                continue
+            n_wide += 1
+            if abs(float(mse_g[g]) - float(mse_o[r])) > 1e-6 * max(1.0, float(mse_o[r])):
+                bad.append((u, r, float(mse_g[g]), float(mse_o[r])))
+    assert not bad, bad[:10]
+    assert n_wide > 20, n_wide

@@ -28,9 +28,9 @@ t = time.perf_counter(); pred(); torch.cuda.synchronize(); dt = time.perf_counte
 print(f"predict {n} ratings in {dt*1e3:.1f} ms -> {n/dt:.0f}/s", flush=True)
 ctx.debug_phases(True); pred(); torch.cuda.synchronize()
 ph = ctx.debug_phases(True, read=True)
-cyc = {k_: v for k_, v in ph.items() if not k_.startswith("n_") and not k_.startswith("w0")}
-print("wave0 fast-path cycles per rating: conn", ph["w0_conn"] / max(ph["n_fast"] / 4, 1),
-      "entries", ph["w0_entries"] / max(ph["n_fast"] / 4, 1))
+cyc = {k_: ph[k_] for k_ in ("setup", "basis", "fast", "dense")}
+print("per user: gram", ph["gram"] / users, "setup", ph["setup"] / users, "basis", ph["basis"] / users,
+      "| block-wide ratings", ph["n_dense"], "wide-K share of block-wide cycles", ph["wide"] / max(ph["dense"], 1))
 tot = sum(cyc.values())
 print({k_: f"{v/tot*100:.1f}%" for k_, v in cyc.items()}, "cycles/prediction:", tot / n,
       "fast", ph["n_fast"], "dense", ph["n_dense"])
