@@ -239,29 +239,36 @@ __device__ void ldlt_bordered(double* A, int L, int nrows) {
 // a formula, so the loads of the next 16-deep chunk stay in flight (raw, in registers)
 // while the current chunk -- staged in LDS as fp64 (`stage`: kStageElems doubles) with
 // coalesced loads -- is consumed; the conversions run when the chunk is written to LDS.
-// A_LFAST / B_LFAST say whether l is the operand's contiguous index in memory.  Each
-// thread owns a 4 x 4 register tile.  Called by the whole block; the caller
-// synchronises before reading C.
-constexpr int kStageLd = 65;                       // odd stride: conflict-free staging writes
+// A_LFAST / B_LFAST say whether l is the operand's contiguous index in memory.  The
+// products run on the fp64 matrix cores: wave w owns the 32 x 32 quadrant (w >> 1,
+// w & 1) of the block as 2 x 2 v_mfma_f64_16x16x4_f64 tiles (A lane l = A[l&15][l>>4],
+// B lane l = B[l>>4][l&15], result q of lane l = C[(l>>4) + 4q][l&15]; checked by
+// tools/mfma_f64_probe.hip), so a 16-deep chunk costs each wave 16 LDS fragment reads for
+// 16 MFMAs -- an eighth of the LDS traffic of 4 x 4 VALU register tiles.  Called by the
+// whole block; the caller synchronises before reading C.
+constexpr int kStageLd = 80;                       // == 16 (mod 32): the four 16-lane row
+                                                   // groups of a fragment read hit disjoint banks
 constexpr int kStageElems = 2 * 16 * kStageLd;
+using f64x4 = __attribute__((ext_vector_type(4))) double;
 template <bool A_LFAST, bool B_LFAST, class LA, class XA, class LB, class XB, class FK, class FW, class FO>
 __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK kend, FW want, FO out,
                            double* stage) {
     double* As = stage;
     double* Bs = stage + 16 * kStageLd;
     const int tid = threadIdx.x;
-    const int tx = tid & 15, ty = tid >> 4;
+    const int lane = tid & 63;
+    const int wr = (tid >> 6) >> 1, wc = (tid >> 6) & 1;   // this wave's 32 x 32 quadrant
     using RA = decltype(loadA(0, 0));
     using RB = decltype(loadB(0, 0));
     for (int i0 = 0; i0 < M; i0 += 64)
         for (int j0 = 0; j0 < N; j0 += 64) {
             if (!want(i0, j0)) continue;
             const int K = kend(j0);
-            double acc[4][4];
+            f64x4 acc[2][2];
 #pragma unroll
-            for (int x = 0; x < 4; ++x)
+            for (int x = 0; x < 2; ++x)
 #pragma unroll
-                for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+                for (int y = 0; y < 2; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
             RA ra[4];
             RB rb[4];
             // unconditional loads from clamped indices: a guarded load would become a
@@ -291,32 +298,37 @@ __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK ke
                 }
                 __syncthreads();
                 if (l0 + 16 < K) fetch(l0 + 16);
-#pragma unroll 4
-                for (int l = 0; l < 16; ++l) {
-                    double av[4], bv[4];
 #pragma unroll
-                    for (int x = 0; x < 4; ++x) {
-                        av[x] = As[l * kStageLd + 4 * ty + x];
-                        bv[x] = Bs[l * kStageLd + 4 * tx + x];
+                for (int ks = 0; ks < 4; ++ks) {
+                    const int row = (4 * ks + (lane >> 4)) * kStageLd + (lane & 15);
+                    double av[2], bv[2];
+#pragma unroll
+                    for (int x = 0; x < 2; ++x) {
+                        av[x] = As[row + 32 * wr + 16 * x];
+                        bv[x] = Bs[row + 32 * wc + 16 * x];
                     }
 #pragma unroll
-                    for (int x = 0; x < 4; ++x)
+                    for (int x = 0; x < 2; ++x)
 #pragma unroll
-                        for (int y = 0; y < 4; ++y) acc[x][y] = fma(av[x], bv[y], acc[x][y]);
+                        for (int y = 0; y < 2; ++y)
+                            acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
                 }
             }
 #pragma unroll
-            for (int x = 0; x < 4; ++x)
+            for (int x = 0; x < 2; ++x)
 #pragma unroll
-                for (int y = 0; y < 4; ++y) {
-                    const int i = i0 + 4 * ty + x, j = j0 + 4 * tx + y;
-                    if (i < M && j < N) out(i, j, acc[x][y]);
-                }
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int i = i0 + 32 * wr + 16 * x + (lane >> 4) + 4 * q;
+                        const int j = j0 + 32 * wc + 16 * y + (lane & 15);
+                        if (i < M && j < N) out(i, j, acc[x][y][q]);
+                    }
         }
 }
 
 template <typename T>
-__global__ __launch_bounds__(kThreads) void predict_kernel(PredArgs<T> a, uint32_t count) {
+__global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uint32_t count) {
     extern __shared__ double dsm[];
     const int lmax = a.lmax;
     // A: the factorisation region.  Per user it holds Gbar's LDL^T, then the per-wave
