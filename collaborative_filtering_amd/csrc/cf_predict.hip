@@ -129,7 +129,11 @@ constexpr int kNB = 16;   // LDL^T panel width
 // Blocked right-looking LDL^T of the leading L x L block of the packed lower triangle
 // A (rows [0, nrows), nrows >= L), carrying rows [L, nrows) as border rows: on return
 // A holds unit-lower L below the diagonal, D on it, and border row i holds
-// (L^-1 a_i)_j / D_j.  Called by the whole block; starts and ends synchronised.
+// (L^-1 a_i)_j / D_j.  An exactly zero pivot is skipped (its column of L is 0), as
+// Eigen's LU skips a zero pivot column: a structurally singular matrix whose trailing
+// block has cancelled to exact zeros gives finite, clamped garbage like the
+// reference's, not inf - inf = NaN.  Called by the whole block; starts and ends
+// synchronised.
 __device__ void ldlt_bordered(double* A, int L, int nrows) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -149,7 +153,7 @@ __device__ void ldlt_bordered(double* A, int L, int nrows) {
                 if (j < b) {
                     const double dj = __shfl(rowv[j], j);
                     const double w = (i > j) ? rowv[j] : 0.0;   // unscaled a_ij
-                    const double lij = w / dj;
+                    const double lij = dj != 0.0 ? w / dj : 0.0;   // exact-zero pivot: skipped
 #pragma unroll
                     for (int q = j + 1; q < kNB; ++q) {
                         const double wq = __shfl(w, q);
@@ -176,7 +180,7 @@ __device__ void ldlt_bordered(double* A, int L, int nrows) {
                     double sacc = x[jj];
 #pragma unroll
                     for (int q = 0; q < jj; ++q) sacc = fma(-x[q] * A[tri(kb + q, kb + q)], Aj[q], sacc);
-                    x[jj] = sacc / Aj[jj];
+                    x[jj] = Aj[jj] != 0.0 ? sacc / Aj[jj] : 0.0;
                 }
             }
 #pragma unroll
@@ -651,7 +655,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                     const double dj = Ew[tri(j, j)];
                     minpiv = fmin(minpiv, dj);
                     const bool mine = lane > j && lane < nc + 2;
-                    const double lij = mine ? Ew[tri(lane, j)] / dj : 0.0;
+                    const double lij = (mine && dj != 0.0) ? Ew[tri(lane, j)] / dj : 0.0;
                     if (mine) {
                         const int qend = min(lane, nc - 1);
                         for (int q = j + 1; q <= qend; ++q)

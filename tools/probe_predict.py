@@ -105,3 +105,6 @@ for u in range(users):
     e_by += np.histogram(nc_u, bins=bins, weights=w)[0]
 print("entry FMA per rating", tot_e / nr, "mean lim", tot_lim / nr, "mean tail Lu-lim", tot_tail / nr)
 print("entry-work share by nc bins", dict(zip([f"<{b}" for b in bins[1:]], np.round(e_by / e_by.sum(), 3))))
+mse_h = d["mse"].cpu().numpy()
+print("NaN mse: total", int(np.isnan(mse_h).sum()), "with c=0", int((np.isnan(mse_h) & (kk == 0)).sum()),
+      "with c>0", int((np.isnan(mse_h) & (kk > 0)).sum()))
