@@ -12,8 +12,9 @@
 //      (:164); the shift makes B positive definite (spectrum of L2 is in [0,2]) so
 //      its singular values are its eigenvalues and the rotated columns of B are the
 //      eigenvectors scaled by (lambda + 1);
-//   4. one-sided (Hestenes) Jacobi sweeps in LDS: each step of a round-robin
-//      tournament rotates k/2 disjoint column pairs; a pair is owned by 8 lanes
+//   4. one-sided (Hestenes) Jacobi sweeps in LDS: each step rotates up to k/2 disjoint
+//      column pairs in a recursive-halving ordering that keeps one column of every pair
+//      in registers for a whole level (see the loop); a pair is owned by 8 lanes
 //      (float2 = ds_read_b64 per row pair, packed v_pk_fma_f32), whose three dot
 //      products are reduced with three DPP steps.  Each step reads and writes the
 //      whole k x k matrix, so the sweep is bound by LDS bandwidth (128 B/clk/CU),
@@ -165,69 +166,99 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     __syncthreads();
 
     if (a.stats && tid == 0) t_phase1 = __builtin_amdgcn_s_memtime();
-    // ---- 4. one-sided Jacobi --------------------------------------------------------
-    const int n = (k + 1) & ~1;          // players in the round-robin tournament
-    const int npairs = n >> 1;
+    // ---- 4. one-sided Jacobi, recursive-halving ordering --------------------------------
+    // Level L splits the n columns into 2^L segments (halving each parent, first half
+    // rounded up).  In a segment of size s the first f = ceil(s/2) columns are *fixed* --
+    // each held by one lane group in registers for the whole level -- and the other
+    // s - f *travel*: at step j fixed column i meets traveling column (i + j) mod f.  Every
+    // pair of columns meets exactly once per sweep (n - 1 + O(log n) steps), and a step
+    // moves one column through LDS instead of two (read, and write back if rotated).
+    // Group budget: 2^L * ceil(ceil(n / 2^L) / 2) <= NG for every n <= NR (checked
+    // offline for every bucket).
+    const int n = (k + 1) & ~1;          // columns incl. the padding column k when k is odd
     const int g = tid / kGroup;
     const int lig = tid % kGroup;
     const float tol = a.tol_scale * sqrtf((float)k) * 2.384185791015625e-07f;  // sqrt(k) * 2^-22
     const float tol2 = tol * tol;
     int sweep = 0;
     for (; sweep < a.max_sweeps && k > 1; ++sweep) {
-        for (int step = 0; step < n - 1; ++step) {
-            for (int pi = g; pi < npairs; pi += NG) {
-                int p, q;
-                if (pi == 0) {
-                    p = n - 1;
-                    q = step;
-                } else {
-                    p = step + pi;
-                    if (p >= n - 1) p -= n - 1;
-                    q = step - pi;
-                    if (q < 0) q += n - 1;
-                }
-                if (p >= k || q >= k) continue;
-                f2* bp = reinterpret_cast<f2*>(B + p * LD) + lig;
-                f2* bq = reinterpret_cast<f2*>(B + q * LD) + lig;
-                f2 xp[E2], xq[E2];
-                f2 al2 = {0.f, 0.f}, be2 = {0.f, 0.f}, ga2 = {0.f, 0.f};
+        for (int L = 0;; ++L) {
+            const int segmax = (n + (1 << L) - 1) >> L;
+            if (segmax < 2) break;
+            const int FL = (segmax + 1) >> 1;   // steps of this level
+            const int sigma = g / FL, fi = g - sigma * FL;
+            int s0 = 0, s1 = n;
+            for (int bit = L - 1; bit >= 0; --bit) {
+                const int half = (s1 - s0 + 1) >> 1;
+                if ((sigma >> bit) & 1) s0 += half;
+                else s1 = s0 + half;
+            }
+            const int f = (s1 - s0 + 1) >> 1, t = (s1 - s0) - f;
+            const int p = s0 + fi;
+            const bool fixed = sigma < (1 << L) && fi < f && p < k;
+            f2* bp = reinterpret_cast<f2*>(B + (fixed ? p : 0) * LD) + lig;
+            f2 xp[E2];
+            float devp = 0.0f;
+            bool pmod = false;
+            if (fixed) {
 #pragma unroll
-                for (int t = 0; t < E2; ++t) {
-                    xp[t] = bp[kGroup * t];
-                    xq[t] = bq[kGroup * t];
-                    al2 = __builtin_elementwise_fma(xp[t], xp[t], al2);
-                    be2 = __builtin_elementwise_fma(xq[t], xq[t], be2);
-                    ga2 = __builtin_elementwise_fma(xp[t], xq[t], ga2);
-                }
-                const float al = pair_sum(al2.x + al2.y);
-                const float be = pair_sum(be2.x + be2.y);
-                const float ga = pair_sum(ga2.x + ga2.y);
-                if (ga * ga > tol2 * (al * be)) {
-                    // Hardware rcp/rsq/sqrt: the rotation only has to annihilate ga well
-                    // enough; its scale error (c^2 + s^2 != 1) is tracked exactly below.
-                    const float zeta = (be - al) * __builtin_amdgcn_rcpf(2.0f * ga);
-                    const float az = fabsf(zeta);
-                    const float t = copysignf(__builtin_amdgcn_rcpf(az + __builtin_amdgcn_sqrtf(fmaf(az, az, 1.0f))),
-                                              zeta);
-                    const float c = __builtin_amdgcn_rsqf(fmaf(t, t, 1.0f));
-                    const float s = c * t;
-                    const f2 c2 = {c, c}, s2 = {s, s}, ns2 = {-s, -s};
+                for (int e = 0; e < E2; ++e) xp[e] = bp[kGroup * e];
+                devp = s_dev[p];
+            }
+            for (int step = 0; step < FL; ++step) {
+                int ti = fi + step;
+                if (ti >= f) ti -= f;
+                const int q = s0 + f + ti;
+                if (fixed && step < f && ti < t && q < k) {
+                    f2* bq = reinterpret_cast<f2*>(B + q * LD) + lig;
+                    f2 xq[E2];
+                    f2 al2 = {0.f, 0.f}, be2 = {0.f, 0.f}, ga2 = {0.f, 0.f};
 #pragma unroll
                     for (int e = 0; e < E2; ++e) {
-                        bp[kGroup * e] = __builtin_elementwise_fma(ns2, xq[e], c2 * xp[e]);
-                        bq[kGroup * e] = __builtin_elementwise_fma(s2, xp[e], c2 * xq[e]);
+                        xq[e] = bq[kGroup * e];
+                        al2 = __builtin_elementwise_fma(xp[e], xp[e], al2);
+                        be2 = __builtin_elementwise_fma(xq[e], xq[e], be2);
+                        ga2 = __builtin_elementwise_fma(xp[e], xq[e], ga2);
                     }
-                    // c^2 + s^2 = 1 + delta: track each column's accumulated scale so
-                    // lambda = ||b_j|| / ||v_j|| - 1 carries no rotation drift.
-                    const float delta = fmaf(s, s, fmaf(c, c, -1.0f));
-                    const float dp = s_dev[p], dq = s_dev[q];
-                    const float cc = c * c, ss = s * s;
-                    if (lig == 0) {
-                        s_dev[p] = delta + fmaf(cc, dp, ss * dq);
-                        s_dev[q] = delta + fmaf(ss, dp, cc * dq);
-                        s_flag[0] = 1;
+                    const float al = pair_sum(al2.x + al2.y);
+                    const float be = pair_sum(be2.x + be2.y);
+                    const float ga = pair_sum(ga2.x + ga2.y);
+                    if (ga * ga > tol2 * (al * be)) {
+                        // Hardware rcp/rsq/sqrt: the rotation only has to annihilate ga well
+                        // enough; its scale error (c^2 + s^2 != 1) is tracked exactly below.
+                        const float zeta = (be - al) * __builtin_amdgcn_rcpf(2.0f * ga);
+                        const float az = fabsf(zeta);
+                        const float tt = copysignf(
+                            __builtin_amdgcn_rcpf(az + __builtin_amdgcn_sqrtf(fmaf(az, az, 1.0f))), zeta);
+                        const float c = __builtin_amdgcn_rsqf(fmaf(tt, tt, 1.0f));
+                        const float sn = c * tt;
+                        const f2 c2 = {c, c}, s2 = {sn, sn}, ns2 = {-sn, -sn};
+#pragma unroll
+                        for (int e = 0; e < E2; ++e) {
+                            const f2 np = __builtin_elementwise_fma(ns2, xq[e], c2 * xp[e]);
+                            bq[kGroup * e] = __builtin_elementwise_fma(s2, xp[e], c2 * xq[e]);
+                            xp[e] = np;
+                        }
+                        // c^2 + s^2 = 1 + delta: track each column's accumulated scale so
+                        // lambda = ||b_j|| / ||v_j|| - 1 carries no rotation drift.
+                        const float delta = fmaf(sn, sn, fmaf(c, c, -1.0f));
+                        const float dq = s_dev[q];
+                        const float cc = c * c, ss = sn * sn;
+                        const float ndp = delta + fmaf(cc, devp, ss * dq);
+                        if (lig == 0) {
+                            s_dev[q] = delta + fmaf(ss, devp, cc * dq);
+                            s_flag[0] = 1;
+                        }
+                        devp = ndp;
+                        pmod = true;
                     }
                 }
+                __syncthreads();
+            }
+            if (pmod) {
+#pragma unroll
+                for (int e = 0; e < E2; ++e) bp[kGroup * e] = xp[e];
+                if (lig == 0) s_dev[p] = devp;
             }
             __syncthreads();
         }
@@ -300,7 +331,9 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
         atomicAdd(&a.stats[4], t_phase1 - t_phase0);
         atomicAdd(&a.stats[5], t_phase2 - t_phase1);
         atomicAdd(&a.stats[6], t3 - t_phase2);
-        atomicAdd(&a.stats[7], (unsigned long long)((sweep + 1) * (((k + 1) & ~1) - 1)));
+        int steps = 0;   // steps per sweep of the recursive-halving ordering
+        for (int L = 0; ((n + (1 << L) - 1) >> L) >= 2; ++L) steps += (((n + (1 << L) - 1) >> L) + 1) >> 1;
+        atomicAdd(&a.stats[7], (unsigned long long)((sweep + 1) * steps));
     }
 }
 
