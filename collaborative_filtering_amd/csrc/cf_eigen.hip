@@ -278,15 +278,21 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
 
     // ---- 5. eigenvalues, ordering, lim, output ----------------------------------------
     // ||b_j|| accumulated in fp64: a k-term fp32 sum would cost ~k ulps (3e-5 at k=192).
+    // Sign convention: sum_i v_ij >= 0.  Eigenvector signs are arbitrary (the reference's
+    // come out of Eigen's internals), but the predictor's column filter is signed
+    // (local_calc_precomp.cpp:284-304): a fixed convention makes the all-positive
+    // lambda = 0 eigenvector of a connected subgraph survive it instead of being dropped
+    // from every rating of the user by the luck of the rotation order.
     for (int j = tid; j < k; j += NT) {
-        double acc = 0.0;
+        double acc = 0.0, sum = 0.0;
         for (int i = 0; i < k; ++i) {
             const double v = (double)B[j * LD + i];
             acc = fma(v, v, acc);
+            sum += v;
         }
         const double nrm = sqrt(acc);
         s_mu[j] = (float)(nrm / sqrt(1.0 + (double)s_dev[j]));   // lambda_j + 1
-        s_s[j] = (float)(1.0 / nrm);                             // unit-normalises v_j
+        s_s[j] = (float)((sum < 0.0 ? -1.0 : 1.0) / nrm);        // unit-normalises v_j
     }
     __syncthreads();
     for (int j = tid; j < k; j += NT) {

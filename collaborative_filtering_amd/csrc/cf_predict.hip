@@ -61,7 +61,11 @@ constexpr int kNcMax = 62;            // fast path: complement rows (nc + 2 bord
 // eigenvalue of U_CS^T U_CS in the Q basis, so this admits cond <~ 1e10, where the
 // reference's own explicit inverse is accurate to ~cond * eps; parity is tested to 1e8)
 constexpr double kPivMin = 1e-10;
-constexpr double kOrthoMax = 1e-5;    // max |Gbar - I| for the two-step basis (error ~ 1e-20)
+// max |Gbar - I| for a basis: each correction step squares the orthogonality error, and
+// steps repeat (up to 4) until the last Gram is within kOrthoDone, so Q is orthonormal to
+// ~1e-16 for any U within kOrthoMax of orthonormal
+constexpr double kOrthoMax = 1e-2;
+constexpr float kOrthoDone = 1e-8f;
 
 template <typename T>
 struct PredArgs {
@@ -453,30 +457,56 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
         const int Lq = (__int_as_float(s_cnt[6]) <= (float)kOrthoMax) ? Lu : 0;
         PHASE_STAMP(0);
 
-        // Q = (U T1) T2, T(l, j) = -G(l, j) (l < j), 1.5 - G(j, j) / 2 (l = j), 0 (l > j),
-        // T1 from Gbar, T2 from G2 = (U T1)^T (U T1) (held in the PGH buffer until the
-        // prefix tables are built).
+        // Q = U T1 T2 ..., T(l, j) = -G(l, j) (l < j), 1.5 - G(j, j) / 2 (l = j), 0 (l > j),
+        // T1 from Gbar, each further T from the Gram of the previous product (held in the
+        // PGH buffer until the prefix tables are built); stop once that Gram is within
+        // kOrthoDone of I (two steps for eigenvectors, |Gbar - I| ~ 1e-6).
         double* Q1 = a.q1 + (size_t)blockIdx.x * lmax * lmax;
         double* G2 = PGH;
         if (Lq > 0) {
             const auto tri_end = [&](int j0) { return min(Lq, j0 + 64); };
             block_gemm<true, false>(
                 k, Lq, [&](int i, int l) { return U[(size_t)i * m + l]; }, as_double,
-                [&](int l, int j) { return Gb[(size_t)l * lmax + j]; }, tri_T, tri_end, all_blocks, [&](int i, int j, double v) { Q1[(size_t)i * Lq + j] = v; }, stage);
-            __syncthreads();
-            block_gemm<false, false>(
-                Lq, Lq, [&](int i, int l) { return Q1[(size_t)l * Lq + i]; }, as_double,
-                [&](int l, int j) { return Q1[(size_t)l * Lq + j]; }, as_double, [&](int) { return k; }, lower_blocks,
-                [&](int i, int j, double v) {
-                    if (j > i) return;
-                    G2[(size_t)i * Lq + j] = v;
-                    G2[(size_t)j * Lq + i] = v;
-                },
-                stage);
-            __syncthreads();
-            block_gemm<true, false>(
-                k, Lq, [&](int i, int l) { return Q1[(size_t)i * Lq + l]; }, as_double,
-                [&](int l, int j) { return G2[(size_t)l * Lq + j]; }, tri_T, tri_end, all_blocks, [&](int i, int j, double v) { Qs[(size_t)i * Lq + j] = v; }, stage);
+                [&](int l, int j) { return Gb[(size_t)l * lmax + j]; }, tri_T, tri_end, all_blocks,
+                [&](int i, int j, double v) { Q1[(size_t)i * Lq + j] = v; }, stage);
+            double* X = Q1;
+            double* Y = Qs;
+            for (int it = 0; it < 3; ++it) {
+                __syncthreads();
+                if (tid == 0) s_cnt[6] = 0;
+                __syncthreads();
+                float dv = 0.0f;
+                block_gemm<false, false>(
+                    Lq, Lq, [&](int i, int l) { return X[(size_t)l * Lq + i]; }, as_double,
+                    [&](int l, int j) { return X[(size_t)l * Lq + j]; }, as_double, [&](int) { return k; },
+                    lower_blocks,
+                    [&](int i, int j, double v) {
+                        if (j > i) return;
+                        G2[(size_t)i * Lq + j] = v;
+                        G2[(size_t)j * Lq + i] = v;
+                        const float d = (float)fabs(v - (i == j ? 1.0 : 0.0));
+                        dv = fmaxf(dv, d == d ? d : 3.0e38f);
+                    },
+                    stage);
+                for (int off = 32; off >= 1; off >>= 1) dv = fmaxf(dv, __shfl_xor(dv, off));
+                if (lane == 0) atomicMax(&s_cnt[6], __float_as_int(dv));
+                __syncthreads();
+                const bool last = it == 2 || __int_as_float(s_cnt[6]) <= kOrthoDone;
+                block_gemm<true, false>(
+                    k, Lq, [&](int i, int l) { return X[(size_t)i * Lq + l]; }, as_double,
+                    [&](int l, int j) { return G2[(size_t)l * Lq + j]; }, tri_T, tri_end, all_blocks,
+                    [&](int i, int j, double v) { Y[(size_t)i * Lq + j] = v; }, stage);
+                if (last) {
+                    if (Y != Qs) {
+                        __syncthreads();
+                        for (int e = tid; e < k * Lq; e += kThreads) Qs[e] = Y[e];
+                    }
+                    break;
+                }
+                double* tmp = X;
+                X = Y;
+                Y = tmp;
+            }
         }
         __syncthreads();
         // g, h (global rows k, k + 1 of Qs, and staged in A: T2 is no longer needed)
