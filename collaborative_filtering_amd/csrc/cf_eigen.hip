@@ -77,6 +77,7 @@ struct EigenGeom {
     static constexpr int LD = (NR * (NR + ((16 - NR) % 64 + 64) % 64) + 9 * NR <= 40960 - 4)
                                   ? NR + ((16 - NR) % 64 + 64) % 64 : NR + 8;
     static constexpr int NT = (NR > 128) ? 1024 : 512;         // 1 pass per step up to NT/8 pairs
+
     static constexpr size_t bytes() {
         return sizeof(float) * (size_t)NR * LD     // B
                + sizeof(uint32_t) * NR             // items
@@ -91,6 +92,9 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     using G = EigenGeom<EMAX>;
     constexpr int NR = G::NR;
     constexpr int LD = G::LD;
+    // element (row i, column j) of B.  (A row swizzle for the LD == 8 (mod 64) bucket,
+    // to undo its 2-way bank conflicts, measured 12% slower: the modulo costs more.)
+    auto bidx = [](int i, int j) { return j * LD + i; };
     constexpr int E2 = G::E2;
     constexpr int NT = G::NT;
     constexpr int NG = NT / kGroup;
@@ -126,25 +130,25 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     __syncthreads();
     for (int i = wave; i < k; i += NW) {
         const float* row = a.graph + (size_t)s_item[i] * a.n_items;
-        for (int j = lane; j < k; j += 64) B[j * LD + i] = row[s_item[j]];
+        for (int j = lane; j < k; j += 64) B[bidx(i, j)] = row[s_item[j]];
     }
     __syncthreads();
 
     // ---- 2. degrees, D^-1/2, diagonal of L2, sig_min -------------------------------
     for (int i = tid; i < k; i += NT) {
         double d = 0.0;
-        for (int j = 0; j < k; ++j) d += (double)B[j * LD + i];
+        for (int j = 0; j < k; ++j) d += (double)B[bidx(i, j)];
         if (d == 0.0) d = 1.0;                      // (:137-140)
         const double s = sqrt(1.0 / d);             // inverse, then sqrt (:149-153)
         s_s[i] = (float)s;
-        s_l2d[i] = (float)((s * (d - (double)B[i * LD + i])) * s);
+        s_l2d[i] = (float)((s * (d - (double)B[bidx(i, i)])) * s);
     }
     __syncthreads();
     for (int i = tid; i < k; i += NT) {
         const float si = s_s[i];
         float acc = 0.0f;
         for (int j = 0; j < k; ++j) {
-            const float l2 = (j == i) ? s_l2d[i] : -(si * B[j * LD + i]) * s_s[j];
+            const float l2 = (j == i) ? s_l2d[i] : -(si * B[bidx(i, j)]) * s_s[j];
             acc = fmaf(l2, l2, acc);
         }
         s_sig[i] = sqrtf(acc);                      // (:172-176)
@@ -155,11 +159,11 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     for (int i = wave; i < k; i += NW) {
         const float si = s_s[i];
         for (int j = lane; j < i; j += 64) {
-            const float v = -(si * B[j * LD + i]) * s_s[j];
-            B[j * LD + i] = v;   // (i,j), lower
-            B[i * LD + j] = v;   // (j,i), mirrored
+            const float v = -(si * B[bidx(i, j)]) * s_s[j];
+            B[bidx(i, j)] = v;   // (i,j), lower
+            B[bidx(j, i)] = v;   // (j,i), mirrored
         }
-        if (lane == 0) B[i * LD + i] = s_l2d[i] + 1.0f;
+        if (lane == 0) B[bidx(i, i)] = s_l2d[i] + 1.0f;
     }
     for (int i = tid; i < k; i += NT) s_dev[i] = 0.0f;
     if (tid == 0) s_flag[0] = 0;
@@ -196,13 +200,14 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
             const int f = (s1 - s0 + 1) >> 1, t = (s1 - s0) - f;
             const int p = s0 + fi;
             const bool fixed = sigma < (1 << L) && fi < f && p < k;
-            f2* bp = reinterpret_cast<f2*>(B + (fixed ? p : 0) * LD) + lig;
+            auto slot = [&](int, int e) { return kGroup * e + lig; };   // float2 of lane lig, chunk e
+            f2* bp = reinterpret_cast<f2*>(B + (fixed ? p : 0) * LD);
             f2 xp[E2];
             float devp = 0.0f;
             bool pmod = false;
             if (fixed) {
 #pragma unroll
-                for (int e = 0; e < E2; ++e) xp[e] = bp[kGroup * e];
+                for (int e = 0; e < E2; ++e) xp[e] = bp[slot(p, e)];
                 devp = s_dev[p];
             }
             for (int step = 0; step < FL; ++step) {
@@ -210,12 +215,13 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
                 if (ti >= f) ti -= f;
                 const int q = s0 + f + ti;
                 if (fixed && step < f && ti < t && q < k) {
-                    f2* bq = reinterpret_cast<f2*>(B + q * LD) + lig;
+                    f2* bq = reinterpret_cast<f2*>(B + q * LD);
+                    const float dq = s_dev[q];   // issued with the column loads
                     f2 xq[E2];
                     f2 al2 = {0.f, 0.f}, be2 = {0.f, 0.f}, ga2 = {0.f, 0.f};
 #pragma unroll
                     for (int e = 0; e < E2; ++e) {
-                        xq[e] = bq[kGroup * e];
+                        xq[e] = bq[slot(q, e)];
                         al2 = __builtin_elementwise_fma(xp[e], xp[e], al2);
                         be2 = __builtin_elementwise_fma(xq[e], xq[e], be2);
                         ga2 = __builtin_elementwise_fma(xp[e], xq[e], ga2);
@@ -236,13 +242,12 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
 #pragma unroll
                         for (int e = 0; e < E2; ++e) {
                             const f2 np = __builtin_elementwise_fma(ns2, xq[e], c2 * xp[e]);
-                            bq[kGroup * e] = __builtin_elementwise_fma(s2, xp[e], c2 * xq[e]);
+                            bq[slot(q, e)] = __builtin_elementwise_fma(s2, xp[e], c2 * xq[e]);
                             xp[e] = np;
                         }
                         // c^2 + s^2 = 1 + delta: track each column's accumulated scale so
                         // lambda = ||b_j|| / ||v_j|| - 1 carries no rotation drift.
                         const float delta = fmaf(sn, sn, fmaf(c, c, -1.0f));
-                        const float dq = s_dev[q];
                         const float cc = c * c, ss = sn * sn;
                         const float ndp = delta + fmaf(cc, devp, ss * dq);
                         if (lig == 0) {
@@ -257,7 +262,7 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
             }
             if (pmod) {
 #pragma unroll
-                for (int e = 0; e < E2; ++e) bp[kGroup * e] = xp[e];
+                for (int e = 0; e < E2; ++e) bp[slot(p, e)] = xp[e];
                 if (lig == 0) s_dev[p] = devp;
             }
             __syncthreads();
@@ -286,7 +291,7 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     for (int j = tid; j < k; j += NT) {
         double acc = 0.0, sum = 0.0;
         for (int i = 0; i < k; ++i) {
-            const double v = (double)B[j * LD + i];
+            const double v = (double)B[bidx(i, j)];
             acc = fma(v, v, acc);
             sum += v;
         }
@@ -328,7 +333,7 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
         float v = 0.0f;
         if (r < k) {
             const int j = s_perm[r];
-            v = B[j * LD + i] * s_s[j];
+            v = B[bidx(i, j)] * s_s[j];
         }
         out[idx] = v;
     }
