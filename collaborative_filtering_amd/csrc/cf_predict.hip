@@ -640,18 +640,36 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                 // from P, minus the tail sum_{j in [lim, Lq)} Q_aj Q_bj when lim < Lq.
                 const int np = nc + 1;
                 const int nent = np * (np + 1) / 2;
-                for (int e = lane; e < nent; e += 64) {
+                auto entry_rows = [&](int e, int& ia, int& ib) {
                     int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
                     while (ra * (ra + 1) / 2 > e) --ra;
                     while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
                     const int rb = e - ra * (ra + 1) / 2;
-                    const int ia = ra < nc ? cb[ra] : r;
-                    const int ib = rb < nc ? cb[rb] : r;
-                    double v = Pm[(size_t)ia * k + ib];
-                    const double* xa = Qs + (size_t)ia * Lq;
-                    const double* xb = Qs + (size_t)ib * Lq;
-                    for (int j = lim; j < Lq; ++j) v = fma(-xa[j], xb[j], v);
-                    Ew[e] = v;
+                    ia = ra < nc ? cb[ra] : r;
+                    ib = rb < nc ? cb[rb] : r;
+                };
+                for (int e0 = 0; e0 < nent; e0 += 4 * 64) {   // four gathers in flight per lane
+                    double v[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        int ia, ib;
+                        entry_rows(min(e0 + 64 * t + lane, nent - 1), ia, ib);
+                        v[t] = Pm[(size_t)ia * k + ib];
+                    }
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        if (e0 + 64 * t + lane < nent) Ew[e0 + 64 * t + lane] = v[t];
+                }
+                if (lim < Lq) {   // rare (mean Lu - lim = 0.08): the tail of P_S
+                    for (int e = lane; e < nent; e += 64) {
+                        int ia, ib;
+                        entry_rows(e, ia, ib);
+                        const double* xa = Qs + (size_t)ia * Lq;
+                        const double* xb = Qs + (size_t)ib * Lq;
+                        double v = Ew[e];
+                        for (int j = lim; j < Lq; ++j) v = fma(-xa[j], xb[j], v);
+                        Ew[e] = v;
+                    }
                 }
                 WAVE_SYNC();
 
@@ -688,6 +706,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                     const double lij = (mine && dj != 0.0) ? Ew[tri(lane, j)] / dj : 0.0;
                     if (mine) {
                         const int qend = min(lane, nc - 1);
+#pragma unroll 4
                         for (int q = j + 1; q <= qend; ++q)
                             Ew[tri(lane, q)] = fma(-lij, Ew[tri(q, j)], Ew[tri(lane, q)]);
                     }
