@@ -697,21 +697,44 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                 }
                 WAVE_SYNC();
                 // LDL^T of K (nc columns), border rows nc (P_{r,Cbar}) and nc + 1 (b);
-                // lane i owns row i.
+                // lane i owns row i.  Panels of 4 columns: the panel is factored column
+                // by column (updates confined to the panel), then one rank-4 update
+                // sum_t l_it d_t l_qt hits the trailing rows -- a quarter of the serial
+                // LDS read-modify-writes of rank-1 steps.
                 double minpiv = 1.0;
-                for (int j = 0; j < nc; ++j) {
-                    const double dj = Ew[tri(j, j)];
-                    minpiv = fmin(minpiv, dj);
-                    const bool mine = lane > j && lane < nc + 2;
-                    const double lij = (mine && dj != 0.0) ? Ew[tri(lane, j)] / dj : 0.0;
-                    if (mine) {
-                        const int qend = min(lane, nc - 1);
-#pragma unroll 4
-                        for (int q = j + 1; q <= qend; ++q)
-                            Ew[tri(lane, q)] = fma(-lij, Ew[tri(q, j)], Ew[tri(lane, q)]);
+                for (int j0 = 0; j0 < nc; j0 += 4) {
+                    const int pw = min(4, nc - j0);
+                    for (int jj = 0; jj < pw; ++jj) {
+                        const int j = j0 + jj;
+                        const double dj = Ew[tri(j, j)];
+                        minpiv = fmin(minpiv, dj);
+                        const bool mine = lane > j && lane < nc + 2;
+                        const double lij = (mine && dj != 0.0) ? Ew[tri(lane, j)] / dj : 0.0;
+                        if (mine) {
+                            const int qend = min(lane, j0 + pw - 1);
+                            for (int q = j + 1; q <= qend; ++q)
+                                Ew[tri(lane, q)] = fma(-lij, Ew[tri(q, j)], Ew[tri(lane, q)]);
+                        }
+                        WAVE_SYNC();
+                        if (mine) Ew[tri(lane, j)] = lij;
+                        WAVE_SYNC();
                     }
-                    WAVE_SYNC();
-                    if (mine) Ew[tri(lane, j)] = lij;
+                    if (lane >= j0 + pw && lane < nc + 2) {
+                        double ld[4];   // l_it d_t of this row's panel columns
+#pragma unroll
+                        for (int t = 0; t < 4; ++t)
+                            ld[t] = t < pw ? Ew[tri(lane, j0 + t)] * Ew[tri(j0 + t, j0 + t)] : 0.0;
+                        const int qend = min(lane, nc - 1);
+#pragma unroll 2
+                        for (int q = j0 + pw; q <= qend; ++q) {
+                            const double* lq = Ew + tri(q, j0);   // l_q,j0.. (contiguous)
+                            double acc = Ew[tri(lane, q)];
+#pragma unroll
+                            for (int t = 0; t < 4; ++t)
+                                if (t < pw) acc = fma(-ld[t], lq[t], acc);
+                            Ew[tri(lane, q)] = acc;
+                        }
+                    }
                     WAVE_SYNC();
                 }
                 double dot = 0.0;
