@@ -197,6 +197,25 @@ class Context:
                                           ptr(pred), ptr(mse), ptr(cnt)), "cf_knn_predict")
         return pred, mse, cnt
 
+    def local_calc(self, movie_off, movie_items, test_off, test_user, test_rating):
+        """local_calc (a8).  Returns per test entry (mse float32, kk, pred, w_lim, lim);
+        entries of movies that are not processed keep mse = NaN, kk = -1."""
+        movie_off = np.ascontiguousarray(movie_off, dtype=np.uint64)
+        movie_items = np.ascontiguousarray(movie_items, dtype=np.uint32)
+        test_off = np.ascontiguousarray(test_off, dtype=np.uint64)
+        test_user = np.ascontiguousarray(test_user, dtype=np.uint32)
+        test_rating = np.ascontiguousarray(test_rating, dtype=np.float32)
+        n = int(test_off[-1])
+        mse = np.full(n, np.nan, dtype=np.float32)
+        kk = np.full(n, -1, dtype=np.int32)
+        pred = np.full(n, np.nan)
+        wlim = np.full(n, np.nan, dtype=np.float32)
+        lim = np.full(n, -1, dtype=np.int32)
+        self._chk(self.lib.cf_local_calc(self.h, len(movie_off) - 1, ptr(movie_off), ptr(movie_items), ptr(test_off),
+                                         ptr(test_user), ptr(test_rating), ptr(mse), ptr(kk), ptr(pred), ptr(wlim),
+                                         ptr(lim)), "cf_local_calc")
+        return mse, kk, pred, wlim, lim
+
     # -- device-resident paths (torch CUDA tensors) -------------------------------
     def plan(self, item_off_host) -> "Plan":
         return Plan(self, item_off_host)

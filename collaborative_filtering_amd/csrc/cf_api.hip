@@ -32,31 +32,7 @@ __global__ void dense_scatter_kernel(uint32_t n_items, const uint64_t* row_ptr, 
 }
 
 // RAII device buffer used by the host-pointer wrappers.
-struct DevBuf {
-    void* p = nullptr;
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
-    }
-};
 
-int dev_alloc(cf_ctx* ctx, DevBuf& b, size_t bytes) {
-    if (bytes == 0) bytes = 16;
-    hipError_t e = hipMalloc(&b.p, bytes);
-    if (e != hipSuccess)
-        return cf_set_error(ctx, CF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
-    return CF_OK;
-}
-
-int set_device(cf_ctx* ctx) {
-    CF_HIP_CHECK(ctx, hipSetDevice(ctx->device));
-    return CF_OK;
-}
-
-#define CF_TRY(expr)              \
-    do {                          \
-        int _rc = (expr);         \
-        if (_rc != CF_OK) return _rc; \
-    } while (0)
 
 }  // namespace
 

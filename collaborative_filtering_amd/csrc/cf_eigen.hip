@@ -47,7 +47,16 @@ __device__ __forceinline__ float pair_sum(float x) {
     return x;
 }
 
+// Launch modes (uniform per launch):
+//   kUser  : a2-a4, one user's item subgraph (compute_eigens, precompute_local_threads.cpp)
+//   kLocal : a8, one movie's local graph (local_calc.cpp:268-378): star-shaped W, w > 0.1,
+//            no 0 -> 1 degree rule, all n eigenpairs, full L2 written out
+//   kSigma : a8 w_lim (local_calc.cpp:402-436) of one (movie, test user) pair: the singular
+//            values of the unrated rows of the movie's L2, by the same one-sided Jacobi
+enum EigenMode : int { kUser = 0, kLocal = 1, kSigma = 2 };
+
 struct EigenArgs {
+    int mode;
     const uint32_t* order;
     uint32_t first;
     const uint64_t* item_off;
@@ -62,7 +71,30 @@ struct EigenArgs {
     float tol_scale;
     int max_sweeps;
     unsigned long long* stats;
+    // kLocal / kSigma
+    float* l2;                  // per movie n x n row-major L2 (kLocal writes, kSigma reads)
+    const uint64_t* l2_off;
+    const uint32_t* pair_movie; // kSigma: unit -> (movie unit, test user)
+    const uint32_t* pair_user;
+    const uint64_t* test_off;   // test ratings CSR over compact item ids, users ascending
+    const uint32_t* test_user;
+    const float* test_rating;
+    float* wlim;                // kSigma output per pair
 };
+
+// Test rating of `user` for compact item `movie` (0 if absent): binary search of the
+// ascending user list (the reference's map lookup with a default of 0, local_calc.cpp:318).
+__device__ __forceinline__ float test_rating(const EigenArgs& a, uint32_t movie, uint32_t user) {
+    uint64_t lo = a.test_off[movie];
+    const uint64_t end = a.test_off[movie + 1];
+    uint64_t hi = end;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (a.test_user[mid] < user) lo = mid + 1;
+        else hi = mid;
+    }
+    return (lo < end && a.test_user[lo] == user) ? a.test_rating[lo] : 0.0f;
+}
 
 // Bucket geometry: k <= NR = 16 * EMAX rows.  A column is read/written as float2
 // (ds_read_b64 / ds_write_b64): lane l of a pair owns rows 16t + 2l, 16t + 2l + 1.
@@ -97,7 +129,6 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     auto bidx = [](int i, int j) { return j * LD + i; };
     constexpr int E2 = G::E2;
     constexpr int NT = G::NT;
-    constexpr int NG = NT / kGroup;
     extern __shared__ float smem[];
     float* B = smem;
     uint32_t* s_item = reinterpret_cast<uint32_t*>(B + (size_t)NR * LD);
@@ -116,21 +147,62 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     // diagnostics (stats != null): s_memtime per phase, thread 0, summed into stats[4..6]
     unsigned long long t_phase0 = (a.stats && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
     unsigned long long t_phase1 = 0, t_phase2 = 0;
-    const uint32_t u = a.order[a.first + blockIdx.x];
+    const int mode = a.mode;
+    const uint32_t unit = a.order[a.first + blockIdx.x];
+    const uint32_t u = (mode == kSigma) ? a.pair_movie[unit] : unit;   // the graph's unit
     const uint64_t base = a.item_off[u];
-    const int k = (int)(a.item_off[u + 1] - base);
-    if (k <= 0 || k > NR) {
-        if (tid == 0) a.m_out[u] = (k <= 0) ? 0 : -1;
+    const int nrows = (int)(a.item_off[u + 1] - base);
+    int k = nrows;   // columns of B (kSigma: the unrated rows, set below)
+    if (nrows <= 0 || nrows > NR) {
+        if (tid == 0) {
+            if (mode == kSigma) a.wlim[unit] = __int_as_float(0x7fc00000);
+            else a.m_out[u] = (nrows <= 0) ? 0 : -1;
+        }
         return;
     }
 
-    // ---- 1. gather W_u (column-major, B[j*LD + i] = W(i,j)) ----------------------
-    for (int i = tid; i < k; i += NT) s_item[i] = a.items[base + i];
+    for (int i = tid; i < nrows; i += NT) s_item[i] = a.items[base + i];
     for (int idx = tid; idx < NR * LD; idx += NT) B[idx] = 0.0f;
     __syncthreads();
+    if (mode == kSigma) {
+        // ---- 1s. B's columns = the unrated rows of the movie's L2 (row 0 counts as
+        // unrated, :405-413), in row order (ordered ballot compaction into s_perm)
+        const uint32_t user = a.pair_user[unit];
+        const bool unr = tid < nrows && (tid == 0 || test_rating(a, s_item[tid], user) == 0.0f);
+        const unsigned long long bal = __ballot(unr);
+        if (lane == 0) s_perm[NR - 1 - wave] = __popcll(bal);   // per-wave counts (NW <= 16)
+        __syncthreads();
+        int off = 0;
+        for (int w = 0; w < wave; ++w) off += s_perm[NR - 1 - w];
+        int h = 0;
+        for (int w = 0; w < NW; ++w) h += s_perm[NR - 1 - w];
+        __syncthreads();
+        if (unr) s_perm[off + __popcll(bal & ((1ull << lane) - 1ull))] = tid;
+        __syncthreads();
+        k = h;
+        const float* L2m = a.l2 + a.l2_off[u];
+        for (int c = wave; c < k; c += NW) {
+            const float* row = L2m + (size_t)s_perm[c] * nrows;
+            for (int j = lane; j < nrows; j += 64) B[bidx(j, c)] = row[j];
+        }
+        for (int i = tid; i < k; i += NT) s_dev[i] = 0.0f;
+        if (tid == 0) s_flag[0] = 0;
+        __syncthreads();
+    } else {
+    // ---- 1. gather W (column-major, B[j*LD + i] = W(i,j)) --------------------------
+    // kLocal: W(i, j) = w(item_i -> item_j) if > 0.1 (graph_loader, local_calc.cpp:113);
+    // column 0 mirrors row 0: W(i, 0) = w(movie -> item_i) (:331-333); W(0, 0) = 0.
     for (int i = wave; i < k; i += NW) {
         const float* row = a.graph + (size_t)s_item[i] * a.n_items;
-        for (int j = lane; j < k; j += 64) B[bidx(i, j)] = row[s_item[j]];
+        const float* row0 = a.graph + (size_t)s_item[0] * a.n_items;
+        for (int j = lane; j < k; j += 64) {
+            float w = row[s_item[j]];
+            if (mode == kLocal) {
+                if (j == 0) w = (i == 0) ? 0.0f : row0[s_item[i]];
+                if (!((double)w > 0.1)) w = 0.0f;
+            }
+            B[bidx(i, j)] = w;
+        }
     }
     __syncthreads();
 
@@ -138,7 +210,7 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     for (int i = tid; i < k; i += NT) {
         double d = 0.0;
         for (int j = 0; j < k; ++j) d += (double)B[bidx(i, j)];
-        if (d == 0.0) d = 1.0;                      // (:137-140)
+        if (d == 0.0 && mode == kUser) d = 1.0;     // (:137-140); local_calc has no guard (:354-360)
         const double s = sqrt(1.0 / d);             // inverse, then sqrt (:149-153)
         s_s[i] = (float)s;
         s_l2d[i] = (float)((s * (d - (double)B[bidx(i, i)])) * s);
@@ -152,6 +224,14 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
             acc = fmaf(l2, l2, acc);
         }
         s_sig[i] = sqrtf(acc);                      // (:172-176)
+    }
+    if (mode == kLocal) {   // the full, unsymmetrised L2 for the w_lim pass (:374, :425-431)
+        float* L2m = a.l2 + a.l2_off[u];
+        for (int i = wave; i < k; i += NW) {
+            const float si = s_s[i];
+            for (int j = lane; j < k; j += 64)
+                L2m[(size_t)i * k + j] = (j == i) ? s_l2d[i] : -(si * B[bidx(i, j)]) * s_s[j];
+        }
     }
     __syncthreads();
 
@@ -168,6 +248,7 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     for (int i = tid; i < k; i += NT) s_dev[i] = 0.0f;
     if (tid == 0) s_flag[0] = 0;
     __syncthreads();
+    }   // mode != kSigma
 
     if (a.stats && tid == 0) t_phase1 = __builtin_amdgcn_s_memtime();
     // ---- 4. one-sided Jacobi, recursive-halving ordering --------------------------------
@@ -290,7 +371,7 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     // from every rating of the user by the luck of the rotation order.
     for (int j = tid; j < k; j += NT) {
         double acc = 0.0, sum = 0.0;
-        for (int i = 0; i < k; ++i) {
+        for (int i = 0; i < nrows; ++i) {
             const double v = (double)B[bidx(i, j)];
             acc = fma(v, v, acc);
             sum += v;
@@ -300,6 +381,14 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
         s_s[j] = (float)((sum < 0.0 ? -1.0 : 1.0) / nrm);        // unit-normalises v_j
     }
     __syncthreads();
+    if (mode == kSigma) {   // w_lim = sqrt(lambda_min(L2_h L2_h^T)) = sigma_min(L2_h) (:435-436)
+        if (tid == 0) {
+            float smin = s_mu[0];
+            for (int j = 1; j < k; ++j) smin = fminf(smin, s_mu[j]);
+            a.wlim[unit] = smin;
+        }
+        return;
+    }
     for (int j = tid; j < k; j += NT) {
         const float mj = s_mu[j];
         int rank = 0;
@@ -311,20 +400,23 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     }
     __syncthreads();
     if (tid == 0) {
-        float smm = 0.0f;
-        for (int i = 0; i < k; ++i)
-            if (smm < s_sig[i]) smm = s_sig[i];
-        smm = (float)((double)smm + 0.01);          // (:182)
-        int lim = 0;
-        for (; lim < k; ++lim)
-            if ((double)(s_mu[s_perm[lim]] - 1.0f) > (double)smm) break;  // (:186-188)
-        if (lim < 2) lim = 2;                        // (:190-191)
+        int lim = k;   // kLocal keeps every eigenpair (es(ll2), local_calc.cpp:378)
+        if (mode == kUser) {
+            float smm = 0.0f;
+            for (int i = 0; i < k; ++i)
+                if (smm < s_sig[i]) smm = s_sig[i];
+            smm = (float)((double)smm + 0.01);          // (:182)
+            for (lim = 0; lim < k; ++lim)
+                if ((double)(s_mu[s_perm[lim]] - 1.0f) > (double)smm) break;  // (:186-188)
+            if (lim < 2) lim = 2;                        // (:190-191)
+        }
         s_flag[1] = lim;
         a.m_out[u] = lim;
     }
     __syncthreads();
     const int m = s_flag[1];
-    for (int i = tid; i < k; i += NT) a.sigs[base + i] = (float)((double)s_sig[i] + 0.01);
+    if (mode == kUser)
+        for (int i = tid; i < k; i += NT) a.sigs[base + i] = (float)((double)s_sig[i] + 0.01);
     for (int r = tid; r < m && r < k; r += NT) a.evals[base + r] = s_mu[s_perm[r]] - 1.0f;
     float* out = a.evecs + a.evec_off[u];
     for (int idx = tid; idx < k * m; idx += NT) {
@@ -365,23 +457,8 @@ int launch_bucket(cf_ctx* ctx, const EigenArgs& args, uint32_t count, hipStream_
 
 }  // namespace
 
-int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
-                    const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m,
-                    float* d_sigs, float* d_evals, float* d_evecs, hipStream_t stream) {
-    EigenArgs args{};
-    args.order = plan->d_order;
-    args.item_off = d_item_off;
-    args.items = d_items;
-    args.graph = ctx->d_graph;
-    args.n_items = ctx->n_items;
-    args.evec_off = d_evec_off;
-    args.m_out = d_m;
-    args.sigs = d_sigs;
-    args.evals = d_evals;
-    args.evecs = d_evecs;
-    args.tol_scale = ctx->tol_scale;
-    args.max_sweeps = ctx->max_sweeps;
-    args.stats = ctx->d_stats;
+namespace {
+int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStream_t stream) {
     for (const cf_bucket& b : plan->buckets) {
         if (b.count == 0) continue;
         args.first = b.first;
@@ -404,4 +481,71 @@ int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off
         if (rc != CF_OK) return rc;
     }
     return CF_OK;
+}
+}  // namespace
+
+int cf_launch_local_eigen(cf_ctx* ctx, const cf_plan* movie_plan, const uint64_t* d_item_off,
+                          const uint32_t* d_items, const uint64_t* d_evec_off, float* d_evals,
+                          float* d_evecs, float* d_l2, const uint64_t* d_l2_off, int32_t* d_n_out,
+                          hipStream_t stream) {
+    EigenArgs args{};
+    args.mode = kLocal;
+    args.order = movie_plan->d_order;
+    args.item_off = d_item_off;
+    args.items = d_items;
+    args.graph = ctx->d_graph;
+    args.n_items = ctx->n_items;
+    args.evec_off = d_evec_off;
+    args.m_out = d_n_out;
+    args.evals = d_evals;
+    args.evecs = d_evecs;
+    args.l2 = d_l2;
+    args.l2_off = d_l2_off;
+    args.tol_scale = ctx->tol_scale;
+    args.max_sweeps = ctx->max_sweeps;
+    return launch_all_buckets(ctx, movie_plan, args, stream);
+}
+
+int cf_launch_local_sigma(cf_ctx* ctx, const cf_plan* pair_plan, const uint64_t* d_item_off,
+                          const uint32_t* d_items, const uint32_t* d_pair_movie,
+                          const uint32_t* d_pair_user, const float* d_l2, const uint64_t* d_l2_off,
+                          const uint64_t* d_test_off, const uint32_t* d_test_user,
+                          const float* d_test_rating, float* d_wlim, hipStream_t stream) {
+    EigenArgs args{};
+    args.mode = kSigma;
+    args.order = pair_plan->d_order;
+    args.item_off = d_item_off;
+    args.items = d_items;
+    args.pair_movie = d_pair_movie;
+    args.pair_user = d_pair_user;
+    args.l2 = const_cast<float*>(d_l2);
+    args.l2_off = d_l2_off;
+    args.test_off = d_test_off;
+    args.test_user = d_test_user;
+    args.test_rating = d_test_rating;
+    args.wlim = d_wlim;
+    args.tol_scale = ctx->tol_scale;
+    args.max_sweeps = ctx->max_sweeps;
+    return launch_all_buckets(ctx, pair_plan, args, stream);
+}
+
+int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
+                    const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m,
+                    float* d_sigs, float* d_evals, float* d_evecs, hipStream_t stream) {
+    EigenArgs args{};
+    args.mode = kUser;
+    args.order = plan->d_order;
+    args.item_off = d_item_off;
+    args.items = d_items;
+    args.graph = ctx->d_graph;
+    args.n_items = ctx->n_items;
+    args.evec_off = d_evec_off;
+    args.m_out = d_m;
+    args.sigs = d_sigs;
+    args.evals = d_evals;
+    args.evecs = d_evecs;
+    args.tol_scale = ctx->tol_scale;
+    args.max_sweeps = ctx->max_sweeps;
+    args.stats = ctx->d_stats;
+    return launch_all_buckets(ctx, plan, args, stream);
 }

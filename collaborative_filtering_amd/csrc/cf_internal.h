@@ -56,7 +56,45 @@ int cf_set_error(cf_ctx* ctx, int code, const std::string& msg);
                                 std::string(#expr) + ": " + hipGetErrorString(_e));      \
     } while (0)
 
+// RAII device buffer used by the host-pointer wrappers.
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+inline int dev_alloc(cf_ctx* ctx, DevBuf& b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess)
+        return cf_set_error(ctx, CF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return CF_OK;
+}
+
+inline int set_device(cf_ctx* ctx) {
+    CF_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    return CF_OK;
+}
+
+#define CF_TRY(expr)              \
+    do {                          \
+        int _rc = (expr);         \
+        if (_rc != CF_OK) return _rc; \
+    } while (0)
+
 // Launchers implemented in the .hip translation units.
+// a8 (local_calc): kLocal / kSigma modes of the eigen kernel (cf_eigen.hip).
+int cf_launch_local_eigen(cf_ctx* ctx, const cf_plan* movie_plan, const uint64_t* d_item_off,
+                          const uint32_t* d_items, const uint64_t* d_evec_off, float* d_evals,
+                          float* d_evecs, float* d_l2, const uint64_t* d_l2_off, int32_t* d_n_out,
+                          hipStream_t stream);
+int cf_launch_local_sigma(cf_ctx* ctx, const cf_plan* pair_plan, const uint64_t* d_item_off,
+                          const uint32_t* d_items, const uint32_t* d_pair_movie,
+                          const uint32_t* d_pair_user, const float* d_l2, const uint64_t* d_l2_off,
+                          const uint64_t* d_test_off, const uint32_t* d_test_user,
+                          const float* d_test_rating, float* d_wlim, hipStream_t stream);
+
 int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
                     const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m,
                     float* d_sigs, float* d_evals, float* d_evecs, hipStream_t stream);

@@ -1,0 +1,318 @@
+// cf_local.hip -- local_calc (a8) on gfx950: the per-movie graph-signal predictor.
+//
+// Replaces vertex_program::apply of local_calc.cpp:262-526.  For each movie vertex m
+// with n = 1 + #out-neighbours >= 3 (:269-272):
+//   1. eigen_kernel<kLocal>: the local graph's W (star-shaped, w > 0.1), L2 without the
+//      0 -> 1 degree rule, all n eigenpairs, and the full L2 kept in HBM (:276-378);
+//   2. eigen_kernel<kSigma>, one workgroup per (movie, test user): w_lim =
+//      sqrt(lambda_min(L2_h L2_h^T)) = sigma_min(L2_h) over the user's unrated rows h,
+//      by the same one-sided Jacobi on the columns L2_h^T (:402-436);
+//   3. local_predict_kernel, one workgroup per pair: lim = first eigenvalue > w_lim (>= 2,
+//      :444-451), the bordered Gram M = U_C^T U_C of the rated rows C (no zero-column
+//      filter, :455-485) factored by the blocked LDL^T of cf_ldlt.hpp, pred = v^T M^-1
+//      U_C^T (r - mean) + mean, clamp, mse (float), kk = |C| (:487-521).
+// Test ratings are looked up in a CSR over compact item ids (users ascending).
+
+#include <algorithm>
+#include <vector>
+
+#include "cf_internal.h"
+#include "cf_ldlt.hpp"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+struct LocalPredArgs {
+    const uint32_t* pair_movie;   // pair -> movie unit
+    const uint32_t* pair_user;    // pair -> test user
+    const uint64_t* pair_out;     // pair -> output slot (its test-rating entry)
+    const uint64_t* item_off;     // movie unit -> [m, out-neighbours...]
+    const uint32_t* items;
+    const float* evals;           // per movie unit at item_off, n values ascending
+    const uint64_t* evec_off;     // per movie unit, n x n row-major
+    const float* evecs;
+    const float* wlim;            // per pair
+    const uint64_t* test_off;
+    const uint32_t* test_user;
+    const float* test_rating;
+    float* mse;
+    int32_t* kk;
+    double* pred;
+    int32_t* lim_out;
+    int lmax;
+};
+
+__device__ float lookup_rating(const LocalPredArgs& a, uint32_t movie, uint32_t user) {
+    uint64_t lo = a.test_off[movie];
+    const uint64_t end = a.test_off[movie + 1];
+    uint64_t hi = end;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (a.test_user[mid] < user) lo = mid + 1;
+        else hi = mid;
+    }
+    return (lo < end && a.test_user[lo] == user) ? a.test_rating[lo] : 0.0f;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+__global__ __launch_bounds__(kThreads) void local_predict_kernel(LocalPredArgs a, uint32_t n_pairs) {
+    extern __shared__ double dsm[];
+    const int lmax = a.lmax;
+    double* A = dsm;                                                   // (lmax+2)(lmax+3)/2
+    double* s_misc = A + (size_t)(lmax + 2) * (lmax + 3) / 2;          // [0] mean [1] real
+    float* s_rat = reinterpret_cast<float*>(s_misc + 4);
+    int* s_c = reinterpret_cast<int*>(s_rat + CF_MAX_K);
+    int* s_cnt = s_c + CF_MAX_K;                                       // [0..3] waves, [4] lim
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+
+    for (uint32_t p = blockIdx.x; p < n_pairs; p += gridDim.x) {
+        const uint32_t mv = a.pair_movie[p];
+        const uint32_t user = a.pair_user[p];
+        const uint64_t base = a.item_off[mv];
+        const int n = (int)(a.item_off[mv + 1] - base);
+        const float* U = a.evecs + a.evec_off[mv];
+        __syncthreads();
+        // ratings of the local graph's rows by this user; row 0 is the unknown (:400-405)
+        float r = 0.0f;
+        if (tid < n) {
+            const float v = lookup_rating(a, a.items[base + tid], user);
+            if (tid == 0) s_misc[1] = (double)v;
+            r = tid == 0 ? 0.0f : v;
+            s_rat[tid] = r;
+        }
+        // rated rows C in row order (:470-479), ordered ballot compaction
+        const bool rated = tid < n && r != 0.0f;
+        const unsigned long long bal = __ballot(rated);
+        if (lane == 0) s_cnt[wave] = __popcll(bal);
+        __syncthreads();
+        int off = 0;
+        for (int w = 0; w < wave; ++w) off += s_cnt[w];
+        const int c = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+        if (rated) s_c[off + __popcll(bal & ((1ull << lane) - 1ull))] = tid;
+        if (tid == 0) {
+            // lim = first eigenvalue above w_lim, >= 2 (:444-451)
+            const double wl = (double)a.wlim[p];
+            int lim = 0;
+            for (; lim < n; ++lim)
+                if ((double)a.evals[base + lim] > wl) break;
+            if (lim < 2) lim = 2;
+            s_cnt[4] = lim;
+        }
+        __syncthreads();
+        const int L = s_cnt[4];
+        if (wave == 0) {
+            double sum = 0.0;
+            for (int i = lane; i < c; i += 64) sum += (double)s_rat[s_c[i]];
+            sum = wave_sum(sum);
+            if (lane == 0) s_misc[0] = sum / (double)c;   // 0/0 = NaN when nothing is rated (:487)
+        }
+        __syncthreads();
+        const double mean = s_misc[0];
+        // bordered Gram: A[a][b] = (U_C^T U_C)_ab (b <= a < L), A[L][b] = t_b, A[L+1][b] = v_b
+        for (int e = tid; e < L * (L + 1) / 2; e += kThreads) {
+            int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+            while (ra * (ra + 1) / 2 > e) --ra;
+            while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
+            const int rb = e - ra * (ra + 1) / 2;
+            double g = 0.0;
+            for (int i = 0; i < c; ++i) {
+                const float* row = U + (size_t)s_c[i] * n;
+                g = fma((double)row[ra], (double)row[rb], g);
+            }
+            A[e] = g;
+        }
+        for (int b = tid; b < L; b += kThreads) {
+            double t = 0.0;
+            for (int i = 0; i < c; ++i) {
+                const int ri = s_c[i];
+                t = fma((double)U[(size_t)ri * n + b], (double)s_rat[ri] - mean, t);
+            }
+            A[tri(L, b)] = t;
+            A[tri(L + 1, b)] = (double)U[b];   // vv = row 0 (:465-466)
+        }
+        __syncthreads();
+        ldlt_bordered<kThreads>(A, L, L + 2);
+        if (wave == 0) {
+            double dot = 0.0;
+            for (int j = lane; j < L; j += 64) dot = fma(A[tri(L, j)] * A[tri(L + 1, j)], A[tri(j, j)], dot);
+            dot = wave_sum(dot);
+            if (lane == 0) {
+                double pred = dot + mean;
+                if (pred > 5) pred = 5;   // (:494-497)
+                if (pred < 1) pred = 1;
+                const double d = s_misc[1] - pred;
+                const uint64_t o = a.pair_out[p];
+                a.mse[o] = (float)(d * d);
+                a.kk[o] = c;
+                if (a.pred) a.pred[o] = pred;
+                if (a.lim_out) a.lim_out[o] = L;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* movie_off,
+                             const uint32_t* movie_items, const uint64_t* test_off,
+                             const uint32_t* test_user, const float* test_rating, float* mse,
+                             int32_t* kk, double* pred, float* wlim, int32_t* lim) {
+    if (!ctx || (n_movies && (!movie_off || !movie_items)) || !test_off || !mse || !kk)
+        return cf_set_error(ctx, CF_EINVAL, "cf_local_calc: null argument");
+    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_local_calc: no item graph uploaded");
+    CF_TRY(set_device(ctx));
+    const uint32_t n_items = ctx->n_items;
+    const uint64_t n_test = test_off[n_items];
+    // units with n >= 3 and their (movie, test user) pairs (:269-272, :394)
+    std::vector<uint64_t> sq_off(n_movies + 1, 0);
+    std::vector<uint32_t> pair_movie, pair_user;
+    std::vector<uint64_t> pair_out, pair_k;
+    for (uint32_t v = 0; v < n_movies; ++v) {
+        const uint64_t n = movie_off[v + 1] - movie_off[v];
+        if (n > CF_MAX_K)
+            return cf_set_error(ctx, CF_ERANGE, "cf_local_calc: movie unit " + std::to_string(v) + " has " +
+                                                    std::to_string(n - 1) +
+                                                    " out-neighbours; the LDS path supports n <= 192");
+        sq_off[v + 1] = sq_off[v] + n * n;
+        if (n < 3) continue;
+        const uint32_t m = movie_items[movie_off[v]];
+        if (m >= n_items) return cf_set_error(ctx, CF_EINVAL, "cf_local_calc: movie id out of range");
+        for (uint64_t t = test_off[m]; t < test_off[m + 1]; ++t) {
+            pair_movie.push_back(v);
+            pair_user.push_back(test_user[t]);
+            pair_out.push_back(t);
+            pair_k.push_back(n);
+        }
+    }
+    const uint32_t n_pairs = (uint32_t)pair_movie.size();
+    // movie plan (units with n < 3 are excluded by giving them k = 0)
+    std::vector<uint64_t> plan_off(n_movies + 1, 0);
+    for (uint32_t v = 0; v < n_movies; ++v) {
+        const uint64_t n = movie_off[v + 1] - movie_off[v];
+        plan_off[v + 1] = plan_off[v] + (n >= 3 ? n : 0);
+    }
+    std::vector<uint64_t> pplan_off(n_pairs + 1, 0);
+    for (uint32_t p = 0; p < n_pairs; ++p) pplan_off[p + 1] = pplan_off[p] + pair_k[p];
+    cf_plan* mplan = nullptr;
+    cf_plan* pplan = nullptr;
+    CF_TRY(cf_plan_create(ctx, n_movies, plan_off.data(), &mplan));
+    int rc = cf_plan_create(ctx, n_pairs, pplan_off.data(), &pplan);
+    if (rc != CF_OK) {
+        cf_plan_destroy(mplan);
+        return rc;
+    }
+    auto cleanup = [&]() {
+        cf_plan_destroy(mplan);
+        cf_plan_destroy(pplan);
+    };
+    const uint64_t n_entries = movie_off[n_movies];
+    DevBuf d_moff, d_mitems, d_sqoff, d_evals, d_evecs, d_l2, d_nout, d_toff, d_tuser, d_trat, d_pm, d_pu,
+        d_po, d_wlim, d_mse, d_kk, d_pred, d_lim;
+    auto alloc_copy = [&](DevBuf& b, const void* h, size_t bytes) -> int {
+        CF_TRY(dev_alloc(ctx, b, bytes));
+        if (h && bytes) CF_HIP_CHECK(ctx, hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice));
+        return CF_OK;
+    };
+    rc = CF_OK;
+    do {
+        if ((rc = alloc_copy(d_moff, movie_off, sizeof(uint64_t) * (n_movies + 1)))) break;
+        if ((rc = alloc_copy(d_mitems, movie_items, sizeof(uint32_t) * n_entries))) break;
+        if ((rc = alloc_copy(d_sqoff, sq_off.data(), sizeof(uint64_t) * (n_movies + 1)))) break;
+        if ((rc = alloc_copy(d_evals, nullptr, sizeof(float) * n_entries))) break;
+        if ((rc = alloc_copy(d_evecs, nullptr, sizeof(float) * sq_off[n_movies]))) break;
+        if ((rc = alloc_copy(d_l2, nullptr, sizeof(float) * sq_off[n_movies]))) break;
+        if ((rc = alloc_copy(d_nout, nullptr, sizeof(int32_t) * n_movies))) break;
+        if ((rc = alloc_copy(d_toff, test_off, sizeof(uint64_t) * (n_items + 1)))) break;
+        if ((rc = alloc_copy(d_tuser, test_user, sizeof(uint32_t) * n_test))) break;
+        if ((rc = alloc_copy(d_trat, test_rating, sizeof(float) * n_test))) break;
+        if ((rc = alloc_copy(d_pm, pair_movie.data(), sizeof(uint32_t) * n_pairs))) break;
+        if ((rc = alloc_copy(d_pu, pair_user.data(), sizeof(uint32_t) * n_pairs))) break;
+        if ((rc = alloc_copy(d_po, pair_out.data(), sizeof(uint64_t) * n_pairs))) break;
+        if ((rc = alloc_copy(d_wlim, nullptr, sizeof(float) * n_pairs))) break;
+        if ((rc = alloc_copy(d_mse, mse, sizeof(float) * n_test))) break;
+        if ((rc = alloc_copy(d_kk, kk, sizeof(int32_t) * n_test))) break;
+        if (pred && (rc = alloc_copy(d_pred, pred, sizeof(double) * n_test))) break;
+        if (lim && (rc = alloc_copy(d_lim, lim, sizeof(int32_t) * n_test))) break;
+        const auto* moff = static_cast<const uint64_t*>(d_moff.p);
+        const auto* mit = static_cast<const uint32_t*>(d_mitems.p);
+        const auto* sqo = static_cast<const uint64_t*>(d_sqoff.p);
+        if ((rc = cf_launch_local_eigen(ctx, mplan, moff, mit, sqo, static_cast<float*>(d_evals.p),
+                                        static_cast<float*>(d_evecs.p), static_cast<float*>(d_l2.p), sqo,
+                                        static_cast<int32_t*>(d_nout.p), 0)))
+            break;
+        if ((rc = cf_launch_local_sigma(ctx, pplan, moff, mit, static_cast<const uint32_t*>(d_pm.p),
+                                        static_cast<const uint32_t*>(d_pu.p), static_cast<const float*>(d_l2.p),
+                                        sqo, static_cast<const uint64_t*>(d_toff.p),
+                                        static_cast<const uint32_t*>(d_tuser.p),
+                                        static_cast<const float*>(d_trat.p), static_cast<float*>(d_wlim.p), 0)))
+            break;
+        if (n_pairs) {
+            LocalPredArgs la{};
+            la.pair_movie = static_cast<const uint32_t*>(d_pm.p);
+            la.pair_user = static_cast<const uint32_t*>(d_pu.p);
+            la.pair_out = static_cast<const uint64_t*>(d_po.p);
+            la.item_off = moff;
+            la.items = mit;
+            la.evals = static_cast<const float*>(d_evals.p);
+            la.evec_off = sqo;
+            la.evecs = static_cast<const float*>(d_evecs.p);
+            la.wlim = static_cast<const float*>(d_wlim.p);
+            la.test_off = static_cast<const uint64_t*>(d_toff.p);
+            la.test_user = static_cast<const uint32_t*>(d_tuser.p);
+            la.test_rating = static_cast<const float*>(d_trat.p);
+            la.mse = static_cast<float*>(d_mse.p);
+            la.kk = static_cast<int32_t*>(d_kk.p);
+            la.pred = pred ? static_cast<double*>(d_pred.p) : nullptr;
+            la.lim_out = lim ? static_cast<int32_t*>(d_lim.p) : nullptr;
+            uint64_t nmax = 3;
+            for (uint64_t k : pair_k) nmax = std::max(nmax, k);
+            la.lmax = (int)nmax;
+            const size_t lds = sizeof(double) * ((size_t)(nmax + 2) * (nmax + 3) / 2 + 4) +
+                               CF_MAX_K * (sizeof(float) + sizeof(int)) + 8 * sizeof(int);
+            if (lds > 163840) {
+                rc = cf_set_error(ctx, CF_ERANGE, "local predict exceeds LDS");
+                break;
+            }
+            if (hipFuncSetAttribute((const void*)local_predict_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds) != hipSuccess) {
+                rc = cf_set_error(ctx, CF_EHIP, "local predict LDS attribute");
+                break;
+            }
+            const uint32_t blocks = std::min<uint32_t>(n_pairs, 4096u);
+            hipLaunchKernelGGL(local_predict_kernel, dim3(blocks), dim3(kThreads), lds, 0, la, n_pairs);
+            if (hipGetLastError() != hipSuccess) {
+                rc = cf_set_error(ctx, CF_EHIP, "local_predict_kernel launch");
+                break;
+            }
+        }
+        if (hipDeviceSynchronize() != hipSuccess) {
+            rc = cf_set_error(ctx, CF_EHIP, "cf_local_calc: device synchronize");
+            break;
+        }
+        if (hipMemcpy(mse, d_mse.p, sizeof(float) * n_test, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(kk, d_kk.p, sizeof(int32_t) * n_test, hipMemcpyDeviceToHost) != hipSuccess ||
+            (pred && hipMemcpy(pred, d_pred.p, sizeof(double) * n_test, hipMemcpyDeviceToHost) != hipSuccess) ||
+            (lim && hipMemcpy(lim, d_lim.p, sizeof(int32_t) * n_test, hipMemcpyDeviceToHost) != hipSuccess)) {
+            rc = cf_set_error(ctx, CF_EHIP, "cf_local_calc: copy out");
+            break;
+        }
+        if (wlim) {
+            std::vector<float> w(n_pairs);
+            if (n_pairs && hipMemcpy(w.data(), d_wlim.p, sizeof(float) * n_pairs, hipMemcpyDeviceToHost) != hipSuccess) {
+                rc = cf_set_error(ctx, CF_EHIP, "cf_local_calc: copy w_lim");
+                break;
+            }
+            for (uint32_t p = 0; p < n_pairs; ++p) wlim[pair_out[p]] = w[p];
+        }
+    } while (false);
+    cleanup();
+    return rc;
+}

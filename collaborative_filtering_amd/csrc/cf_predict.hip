@@ -51,6 +51,7 @@
 // garbage as the reference's inverse (:314) instead of a NaN.
 
 #include "cf_internal.h"
+#include "cf_ldlt.hpp"
 
 namespace {
 
@@ -117,128 +118,6 @@ __device__ int block_compact(bool flag, int idx, int* out, int* s_cnt) {
     const int total = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
     __syncthreads();
     return total;
-}
-
-// Packed lower-triangular index (row-major rows of increasing length).
-__device__ __forceinline__ int tri(int i, int j) { return (i * (i + 1)) / 2 + j; }
-
-#define WAVE_SYNC()                                              \
-    do {                                                         \
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   \
-        __builtin_amdgcn_wave_barrier();                         \
-    } while (0)
-
-constexpr int kNB = 16;   // LDL^T panel width
-
-// Blocked right-looking LDL^T of the leading L x L block of the packed lower triangle
-// A (rows [0, nrows), nrows >= L), carrying rows [L, nrows) as border rows: on return
-// A holds unit-lower L below the diagonal, D on it, and border row i holds
-// (L^-1 a_i)_j / D_j.  An exactly zero pivot is skipped (its column of L is 0), as
-// Eigen's LU skips a zero pivot column: a structurally singular matrix whose trailing
-// block has cancelled to exact zeros gives finite, clamped garbage like the
-// reference's, not inf - inf = NaN.  Called by the whole block; starts and ends
-// synchronised.
-__device__ void ldlt_bordered(double* A, int L, int nrows) {
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    for (int kb = 0; kb < L; kb += kNB) {
-        const int b = min(kNB, L - kb);
-        // (1) diagonal block, unblocked LDL^T, in wave 0's registers: lane i < b holds
-        //     row kb + i; column j is broadcast by shuffles.
-        if (wave == 0) {
-            double rowv[kNB];
-            const int i = lane;
-            const bool live = i < b;
-#pragma unroll
-            for (int q = 0; q < kNB; ++q) rowv[q] = (live && q <= i) ? A[tri(kb + i, kb + q)] : 0.0;
-#pragma unroll
-            for (int j = 0; j < kNB; ++j) {
-                if (j < b) {
-                    const double dj = __shfl(rowv[j], j);
-                    const double w = (i > j) ? rowv[j] : 0.0;   // unscaled a_ij
-                    const double lij = dj != 0.0 ? w / dj : 0.0;   // exact-zero pivot: skipped
-#pragma unroll
-                    for (int q = j + 1; q < kNB; ++q) {
-                        const double wq = __shfl(w, q);
-                        if (q <= i) rowv[q] = fma(-lij, wq, rowv[q]);
-                    }
-                    if (i > j) rowv[j] = lij;
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < kNB; ++q)
-                if (live && q <= i) A[tri(kb + i, kb + q)] = rowv[q];
-        }
-        __syncthreads();
-        // (2) panel: rows below the block (incl. the border rows) solve against L11^T
-        for (int i = kb + b + tid; i < nrows; i += kThreads) {
-            double* Ai = A + tri(i, kb);
-            double x[kNB];
-#pragma unroll
-            for (int jj = 0; jj < kNB; ++jj) x[jj] = jj < b ? Ai[jj] : 0.0;
-#pragma unroll
-            for (int jj = 0; jj < kNB; ++jj) {
-                if (jj < b) {
-                    const double* Aj = A + tri(kb + jj, kb);
-                    double sacc = x[jj];
-#pragma unroll
-                    for (int q = 0; q < jj; ++q) sacc = fma(-x[q] * A[tri(kb + q, kb + q)], Aj[q], sacc);
-                    x[jj] = Aj[jj] != 0.0 ? sacc / Aj[jj] : 0.0;
-                }
-            }
-#pragma unroll
-            for (int jj = 0; jj < kNB; ++jj)
-                if (jj < b) Ai[jj] = x[jj];
-        }
-        __syncthreads();
-        // (3) trailing update A22 -= L21 D L21^T over rows [kb+b, nrows), columns [kb+b, L)
-        {
-            const int r0 = kb + b;
-            const int nr = nrows - r0;
-            const int nc = L - r0;
-            if (nc > 0) {
-                const int tr = (nr + 3) >> 2, tcn = (nc + 3) >> 2;
-                for (int tix = tid; tix < tr * tcn; tix += kThreads) {
-                    const int ti = tix / tcn, tq = tix - ti * tcn;
-                    if (tq > ti) continue;   // strictly above the diagonal tiles
-                    double acc[4][4];
-#pragma unroll
-                    for (int x = 0; x < 4; ++x)
-#pragma unroll
-                        for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
-                    const double* Ar[4];
-                    const double* Aq[4];
-#pragma unroll
-                    for (int x = 0; x < 4; ++x) {
-                        Ar[x] = A + tri(min(r0 + 4 * ti + x, nrows - 1), 0);
-                        Aq[x] = A + tri(min(r0 + 4 * tq + x, L - 1), 0);
-                    }
-                    for (int j = kb; j < kb + b; ++j) {
-                        double vr[4], vq[4];
-                        const double dj = A[tri(j, j)];
-#pragma unroll
-                        for (int x = 0; x < 4; ++x) {
-                            vr[x] = Ar[x][j] * dj;
-                            vq[x] = Aq[x][j];
-                        }
-#pragma unroll
-                        for (int x = 0; x < 4; ++x)
-#pragma unroll
-                            for (int y = 0; y < 4; ++y) acc[x][y] = fma(vr[x], vq[y], acc[x][y]);
-                    }
-#pragma unroll
-                    for (int x = 0; x < 4; ++x)
-#pragma unroll
-                        for (int y = 0; y < 4; ++y) {
-                            const int gi = r0 + 4 * ti + x, gq = r0 + 4 * tq + y;
-                            if (gi < nrows && gq < L && gq <= gi) A[tri(gi, gq)] -= acc[x][y];
-                        }
-                }
-            }
-        }
-        __syncthreads();
-    }
 }
 
 // Block-level GEMM on 64 x 64 output blocks: C(i, j) = sum_{l < kend(j0)} A(i, l) B(l, j)
@@ -587,7 +466,6 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
             };
             load_graph_row(wave, gv_next);
             for (int r = wave; r < k; r += kWaves) {
-                unsigned long long t_w0 = (a.phase_cycles && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
                 float gv[3] = {gv_next[0], gv_next[1], gv_next[2]};
                 load_graph_row(r + kWaves, gv_next);
                 int nc = 0;
@@ -630,11 +508,6 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                     continue;
                 }
                 const double mu = (sum_all - sc) / (double)c;   // mean over C (:311)
-                if (a.phase_cycles && tid == 0) {
-                    const unsigned long long now = __builtin_amdgcn_s_memtime();
-                    (void)now;
-                    t_w0 = now;
-                }
 
                 // E = P_S over the rows [Cbar..., r] (np rows, packed lower): gathers
                 // from P, minus the tail sum_{j in [lim, Lq)} Q_aj Q_bj when lim < Lq.
@@ -843,7 +716,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                     A[e] = (e == tri(ra, ra) ? 1.0 : 0.0) - A[e];   // K = I - P_CbarCbar
                 }
                 __syncthreads();
-                ldlt_bordered(A, nc, nc + 2);
+                ldlt_bordered<kThreads>(A, nc, nc + 2);
                 if (wave == 0) {
                     double minpiv = 1.0, dot = 0.0;
                     for (int j = lane; j < nc; j += 64) {
@@ -989,7 +862,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
             }
             __syncthreads();
 
-            ldlt_bordered(A, L, L + 2);
+            ldlt_bordered<kThreads>(A, L, L + 2);
 
             // pred = v^T M^-1 t + mean = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean (:314-327)
             if (wave == 0) {

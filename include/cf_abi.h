@@ -24,6 +24,8 @@
  *                                  local_calc_precomp.cpp:217-380 (per (movie,user) rating)
  *   cf_item_cosine               : weights_calc() via graph.transform_edges, knn2.cpp:127-146,206
  *                                  plus the w > 0.01 writer filter knn2.cpp:155-163
+ *   cf_local_calc                : vertex_program::apply of local_calc.cpp:262-526 (per
+ *                                  movie local graph, eigensolve, per-user w_lim, predict)
  *   cf_knn_predict               : knn_program gather/apply + error_vertex_data,
  *                                  knn3.cpp:185-256
  */
@@ -150,6 +152,20 @@ int cf_item_cosine_run(cf_ctx* ctx, uint32_t n_users, uint32_t n_items,
                        const uint64_t* d_user_off, const uint32_t* d_item, const float* d_rating,
                        int integer_ratings, float w_min, int cnt_min, float* d_w_out,
                        void* stream);
+/* local_calc vertex_program::apply (local_calc.cpp:262-526) on the uploaded graph (raw
+ * out_fin_ weights; edges count iff w > 0.1, graph_loader :113).  Movie unit v lists
+ * movie_items[movie_off[v] .. movie_off[v+1]) = [m, the out-neighbours of m with w > 0.1]
+ * (compact ids, any order: results are permutation-equivariant).  Units with fewer than 2
+ * out-neighbours are skipped (:271-272); more than 191 is CF_ERANGE (LDS path).
+ * Test ratings: CSR over all n_items compact ids, test_off[n_items + 1], users ascending
+ * within an item.  For every test entry t of a processed movie m (test_off[m] <= t <
+ * test_off[m+1]): mse[t] (float, :499), kk[t] (rated rows of the local graph), and when
+ * non-null pred[t] (clamped), wlim[t] (= sqrt(lambda_min(L2_h L2_h^T)), :436) and lim[t].
+ * Entries of movies not processed are left untouched. */
+int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* movie_off,
+                  const uint32_t* movie_items, const uint64_t* test_off, const uint32_t* test_user,
+                  const float* test_rating, float* mse, int32_t* kk, double* pred, float* wlim,
+                  int32_t* lim);
 /* knn3 knn_program + error_vertex_data (knn3.cpp:185-256) on the uploaded graph:
  * per test rating (user u, movie items[e]) pred[e] = sum w*r / sum w over u's test
  * items j with w(movie, j) > 0.1 (0 when none); per movie (compact id)

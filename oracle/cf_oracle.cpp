@@ -474,6 +474,117 @@ int cfo_predict_user(int k, int m, const int32_t* items, const double* ratings,
     return 0;
 }
 
+// a8 assembly: the local graph of movie m (local_calc.cpp:268-334).  Row/column 0 is
+// the movie, rows 1..deg its out-neighbours nbrs[] (compact ids, w > 0.1, ascending:
+// the reference iterates a boost::unordered_map, so its row order is unpinned and the
+// results are permutation-equivariant).  Graph edges exist only for w > 0.1
+// (graph_loader :113).  W(i, j) = w(nb_i -> nb_j) for i, j >= 1 (:326-330; an
+// out-neighbour outside the local graph aliases to column 0 and is overwritten by
+// :333), W(0, j) = W(j, 0) = w(m -> nb_j) (:331-333), W(0, 0) = 0.
+//   G: n_items x n_items raw weights (float); W: n x n row-major, n = deg + 1.
+int cfo_local_graph(int m, int deg, const int32_t* nbrs, const float* G, int64_t n_items, double* W) {
+    const int n = deg + 1;
+    auto w = [&](int a, int b) {
+        const float v = G[(size_t)a * n_items + b];
+        return (double)v > 0.1 ? (double)v : 0.0;
+    };
+    for (int i = 0; i < n * n; ++i) W[i] = 0.0;
+    for (int i = 1; i < n; ++i)
+        for (int j = 1; j < n; ++j) W[(size_t)i * n + j] = w(nbrs[i - 1], nbrs[j - 1]);
+    for (int j = 1; j < n; ++j) {
+        W[j] = w(m, nbrs[j - 1]);
+        W[(size_t)j * n] = w(m, nbrs[j - 1]);
+    }
+    return n;
+}
+
+// a8: vertex_program::apply for one movie (local_calc.cpp:346-521).
+//   W  : n x n local adjacency (cfo_local_graph)
+//   R  : n x nu row-major test ratings; column u = one test user of the movie, row 0 its
+//        rating of the movie, row i >= 1 its test rating of neighbour i (0 = unrated)
+//   out: per user mse (float, :499,519), kk (= #rated rows), pred, w_lim, lim
+// D has no 0 -> 1 guard (:354-360); L2 = (s_i L_ij) s_j with s = sqrt(1/d) (:368-374),
+// full and unsymmetrised; the eigensolver reads its lower triangle (:378).  Per user:
+// row 0 counts as unrated (:405); w_lim = sqrt(lambda_min(L2_h L2_h^T)) over the unrated
+// rows h (:417-436); lim = first eigenvalue > w_lim, >= 2 (:444-451); no zero-column
+// filter; pred = v^T (mm^-1 (U_C^T (r - mean))) + mean with mm = U_C^T U_C inverted by
+// partial-pivot LU (:484-491), clamped to [1, 5] (:494-497).
+int cfo_local_calc(int n, const double* W, int nu, const double* R, float* mse_out, int32_t* kk_out,
+                   double* pred_out, double* wlim_out, int32_t* lim_out) {
+    std::vector<double> d(n), L((size_t)n * n), L2((size_t)n * n), ev(n), V((size_t)n * n);
+    for (int i = 0; i < n; ++i) {
+        double count = 0;
+        for (int j = 0; j < n; ++j) count += W[(size_t)i * n + j];
+        d[i] = count;
+    }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) L[(size_t)i * n + j] = (i == j ? d[i] : 0.0) - W[(size_t)i * n + j];
+    for (int i = 0; i < n; ++i) {
+        const double si = std::sqrt(1.0 / d[i]);
+        for (int j = 0; j < n; ++j) L2[(size_t)i * n + j] = (si * L[(size_t)i * n + j]) * std::sqrt(1.0 / d[j]);
+    }
+    cfo_eigh(n, L2.data(), ev.data(), V.data());
+    std::vector<int> hrows, crows;
+    for (int u = 0; u < nu; ++u) {
+        std::vector<double> r(n);
+        for (int i = 0; i < n; ++i) r[i] = R[(size_t)i * nu + u];
+        const double rat_real = r[0];
+        r[0] = 0;
+        hrows.clear();
+        crows.clear();
+        for (int i = 0; i < n; ++i) (r[i] == 0 ? hrows : crows).push_back(i);
+        const int h = (int)hrows.size(), c = (int)crows.size();
+        // w_lim = sqrt(lambda_min(L2_h L2_h^T))
+        std::vector<double> S((size_t)h * h), sev(h), svec((size_t)h * h);
+        for (int a = 0; a < h; ++a)
+            for (int b = 0; b < h; ++b) {
+                double acc = 0;
+                for (int j = 0; j < n; ++j) acc += L2[(size_t)hrows[a] * n + j] * L2[(size_t)hrows[b] * n + j];
+                S[(size_t)a * h + b] = acc;
+            }
+        cfo_eigh(h, S.data(), sev.data(), svec.data());
+        double emin = sev[0];
+        for (int a = 1; a < h; ++a) emin = std::min(emin, sev[a]);
+        const double w_lim = std::sqrt(emin);
+        int lim;
+        for (lim = 0; lim < n; ++lim)
+            if (ev[lim] > w_lim) break;
+        if (lim < 2) lim = 2;
+        // prediction over the rated rows (:455-491)
+        double sum = 0;
+        for (int i = 0; i < c; ++i) sum += r[crows[i]];
+        const double mean = sum / c;
+        std::vector<double> mm((size_t)lim * lim), inv((size_t)lim * lim), tv(lim), x(lim);
+        for (int a = 0; a < lim; ++a) {
+            double t = 0;
+            for (int i = 0; i < c; ++i) t += V[(size_t)crows[i] * n + a] * (r[crows[i]] - mean);
+            tv[a] = t;
+            for (int b = 0; b < lim; ++b) {
+                double g = 0;
+                for (int i = 0; i < c; ++i) g += V[(size_t)crows[i] * n + a] * V[(size_t)crows[i] * n + b];
+                mm[(size_t)a * lim + b] = g;
+            }
+        }
+        lu_inverse(lim, mm.data(), inv.data());
+        for (int a = 0; a < lim; ++a) {
+            double t = 0;
+            for (int b = 0; b < lim; ++b) t += inv[(size_t)a * lim + b] * tv[b];
+            x[a] = t;
+        }
+        double pred = 0;
+        for (int a = 0; a < lim; ++a) pred += V[a] * x[a];   // vv = row 0 of U
+        pred += mean;
+        if (pred > 5) pred = 5;
+        if (pred < 1) pred = 1;
+        mse_out[u] = (float)std::pow(rat_real - pred, 2);
+        kk_out[u] = c;
+        if (pred_out) pred_out[u] = pred;
+        if (wlim_out) wlim_out[u] = w_lim;
+        if (lim_out) lim_out[u] = lim;
+    }
+    return 0;
+}
+
 // a10: weights_calc for every ordered item pair (knn2.cpp:127-146) + the writer's
 // w > 0.01 filter (:157).  Train ratings come per user (CSR); each item's map is
 // built in ascending user order (the reference iterates a boost::unordered_map, so

@@ -35,6 +35,9 @@ def lib():
         L.cfo_predict_user.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, ctypes.c_int64, ci, vp, vp, vp, vp]
         L.cfo_knn2.argtypes = [ci, vp, vp, vp, ci, vp, vp]
         L.cfo_knn3.argtypes = [ci, vp, vp, vp, vp, vp, vp]
+        L.cfo_local_graph.argtypes = [ci, ci, vp, vp, ctypes.c_int64, vp]
+        L.cfo_local_graph.restype = ci
+        L.cfo_local_calc.argtypes = [ci, vp, ci, vp, vp, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -131,6 +134,43 @@ def knn3(W, movie_off, user, rating):
     mse = np.zeros(W.shape[0], dtype=np.float32)
     lib().cfo_knn3(W.shape[0], _p(W), _p(movie_off), _p(user), _p(rating), _p(pred), _p(mse))
     return pred[: int(movie_off[-1])], mse
+
+
+def local_graph(m, nbrs, G):
+    """local_calc.cpp:268-334: the (deg+1) x (deg+1) local adjacency of movie m."""
+    nbrs = np.ascontiguousarray(nbrs, dtype=np.int32)
+    G = np.ascontiguousarray(G, dtype=np.float32)
+    n = len(nbrs) + 1
+    W = np.zeros((n, n))
+    lib().cfo_local_graph(int(m), len(nbrs), _p(nbrs), _p(G), G.shape[0], _p(W))
+    return W
+
+
+def local_calc(W, R):
+    """vertex_program::apply for one movie: (mse float32, kk, pred, w_lim, lim) per user."""
+    W = np.ascontiguousarray(W, dtype=np.float64)
+    R = np.ascontiguousarray(R, dtype=np.float64)
+    n, nu = R.shape
+    mse = np.zeros(nu, dtype=np.float32)
+    kk = np.zeros(nu, dtype=np.int32)
+    pred = np.zeros(nu)
+    wlim = np.zeros(nu)
+    lim = np.zeros(nu, dtype=np.int32)
+    lib().cfo_local_calc(n, _p(W), nu, _p(R), _p(mse), _p(kk), _p(pred), _p(wlim), _p(lim))
+    return mse, kk, pred, wlim, lim
+
+
+def local_ratings(m, nbrs, test):
+    """The rat matrix of local_calc.cpp:305-323: rows = [m, nbrs...], columns = the movie's
+    test users (ascending); test = {movie: {user: rating}}."""
+    users = sorted(test.get(m, {}))
+    rows = [m] + list(nbrs)
+    R = np.zeros((len(rows), len(users)))
+    for i, mv in enumerate(rows):
+        tr = test.get(mv, {})
+        for j, u in enumerate(users):
+            R[i, j] = tr.get(u, 0.0)
+    return users, R
 
 
 # ---------------------------------------------------------------------------
