@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-steps-only", action="store_true", help="skip CPU baseline (for rocprof runs)")
+    p.add_argument("--pmc", choices=["auto", "off"], default="auto",
+                   help="N=1: measure HBM traffic with two rocprofv3 --pmc child passes (FETCH_SIZE, WRITE_SIZE)")
+    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)   # one pass, no output
     return p.parse_args()
 
 
@@ -112,6 +115,11 @@ def main():
             ev[2].synchronize()
             eig_ms.append(ev[0].elapsed_time(ev[1]))
             pred_ms.append(ev[1].elapsed_time(ev[2]))
+
+    if args.pmc_child:   # one eigen + one predict pass for the PMC collector, then exit
+        step(False)
+        torch.cuda.synchronize(dev)
+        return
 
     for _ in range(args.warmup):
         step(False)
@@ -253,6 +261,25 @@ def main():
         "nan_predictions": int(np.isnan(mse_h).sum()),
     }
 
+    # ---- HBM traffic (rank 0, N=1): two rocprofv3 --pmc passes over one child step ------
+    if rank == 0 and world == 1 and args.pmc == "auto" and not args.profile_steps_only:
+        tr = pmc_traffic(args)
+        if tr is not None:
+            for key, roof in (("predict", roof_pred), ("eigen", roof_eigen)):
+                fetch, write = tr[key]
+                roof["traffic"] = 2.0 * fetch + write
+                roof["traffic_fetch_bytes_raw"] = fetch
+                roof["traffic_write_bytes"] = write
+                roof["traffic_note"] = ("HBM bytes per stage pass from rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE "
+                                        "(separate passes over one child step of the same workload); "
+                                        "traffic = 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of "
+                                        "MI355X_MICROARCH.md (calibrated for 16 B/lane streaming reads; this "
+                                        "kernel's narrower gathers are uncalibrated); Infinity-Cache hits count")
+                stage_s = pred_s if key == "predict" else eig_s
+                roof["traffic_GBps"] = roof["traffic"] / stage_s / 1e9
+        else:
+            result["pmc"] = "unavailable (rocprofv3 missing or the collector failed)"
+
     # ---- CPU baseline (rank 0, N=1): the oracle in precompute_local_threads form ---------
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_steps_only:
         result["cpu_baseline"] = cpu_baseline(args, off, items, ratings, W, k)
@@ -261,6 +288,43 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(args):
+    """FETCH_SIZE and WRITE_SIZE (bytes) summed over the predict_kernel and eigen_kernel
+    launches of one child pass, each counter in its own rocprofv3 run (MI355X_MICROARCH.md:
+    FETCH_SIZE costs 3 TCC slots, WRITE_SIZE 2, so they cannot share a pass)."""
+    import csv
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None
+    out = {"predict": [0.0, 0.0], "eigen": [0.0, 0.0]}
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--users", str(args.users),
+             "--items", str(args.items), "--k-median", str(args.k_median), "--seed", str(args.seed)]
+    env = dict(os.environ, TMPDIR="/tmp")
+    for slot, counter in enumerate(("FETCH_SIZE", "WRITE_SIZE")):
+        d = tempfile.mkdtemp(prefix="cf_pmc_", dir="/tmp")
+        cmd = [prof, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--", *child]
+        try:
+            subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           timeout=600, check=True)
+            path = os.path.join(d, "run_counter_collection.csv")
+            for r in csv.DictReader(open(path)):
+                name = r["Kernel_Name"]
+                key = "predict" if re.search(r"predict_kernel<", name) else \
+                      "eigen" if re.search(r"eigen_kernel<", name) else None
+                if key and r["Counter_Name"] == counter:
+                    out[key][slot] += float(r["Counter_Value"]) * 1024.0   # the counter is in KiB
+        except (subprocess.SubprocessError, OSError, KeyError, ValueError):
+            return None
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    return out
 
 
 def predictor_flops(off, k, m, kk, evals, sigtab):
