@@ -570,42 +570,100 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                 }
                 WAVE_SYNC();
                 // LDL^T of K (nc columns), border rows nc (P_{r,Cbar}) and nc + 1 (b);
-                // lane i owns row i.  Panels of 4 columns: the panel is factored column
-                // by column (updates confined to the panel), then one rank-4 update
-                // sum_t l_it d_t l_qt hits the trailing rows -- a quarter of the serial
-                // LDS read-modify-writes of rank-1 steps.
+                // lane i owns row i.  Panels of 4 columns, no per-column sync:
+                //  1. every lane factors the 4x4 diagonal block redundantly in registers;
+                //  2. each row below it solves against that block (its 4 entries of L);
+                //  3. the rank-4 trailing update A22 -= L21 D L21^T is one
+                //     v_mfma_f64_16x16x4 per 16x16 lower tile (k = 4 = the panel width).
+                // An exactly zero pivot is skipped (its column of L is 0), as in cf_ldlt.hpp.
+                const int nrows = nc + 2;
                 double minpiv = 1.0;
+                const int li = lane & 15, lk = lane >> 4;
                 for (int j0 = 0; j0 < nc; j0 += 4) {
                     const int pw = min(4, nc - j0);
-                    for (int jj = 0; jj < pw; ++jj) {
-                        const int j = j0 + jj;
-                        const double dj = Ew[tri(j, j)];
-                        minpiv = fmin(minpiv, dj);
-                        const bool mine = lane > j && lane < nc + 2;
-                        const double lij = (mine && dj != 0.0) ? Ew[tri(lane, j)] / dj : 0.0;
-                        if (mine) {
-                            const int qend = min(lane, j0 + pw - 1);
-                            for (int q = j + 1; q <= qend; ++q)
-                                Ew[tri(lane, q)] = fma(-lij, Ew[tri(q, j)], Ew[tri(lane, q)]);
-                        }
-                        WAVE_SYNC();
-                        if (mine) Ew[tri(lane, j)] = lij;
-                        WAVE_SYNC();
-                    }
-                    if (lane >= j0 + pw && lane < nc + 2) {
-                        double ld[4];   // l_it d_t of this row's panel columns
+                    double Lm[4][4], Dv[4];
 #pragma unroll
-                        for (int t = 0; t < 4; ++t)
-                            ld[t] = t < pw ? Ew[tri(lane, j0 + t)] * Ew[tri(j0 + t, j0 + t)] : 0.0;
-                        const int qend = min(lane, nc - 1);
-#pragma unroll 2
-                        for (int q = j0 + pw; q <= qend; ++q) {
-                            const double* lq = Ew + tri(q, j0);   // l_q,j0.. (contiguous)
-                            double acc = Ew[tri(lane, q)];
+                    for (int t = 0; t < 4; ++t) {
+                        // unconditional (clamped) broadcast reads, then select
+                        double at[4];
+#pragma unroll
+                        for (int u = 0; u <= t; ++u)
+                            at[u] = Ew[tri(j0 + min(t, pw - 1), j0 + min(u, pw - 1))];
+#pragma unroll
+                        for (int u = 0; u <= t; ++u)
+                            at[u] = t < pw ? at[u] : (u == t ? 1.0 : 0.0);
+                        // row t of the block against the rows above it (left-looking)
+#pragma unroll
+                        for (int u = 0; u < t; ++u) {
+                            double x = at[u];
+#pragma unroll
+                            for (int s2 = 0; s2 < u; ++s2) x = fma(-Lm[t][s2] * Dv[s2], Lm[u][s2], x);
+                            Lm[t][u] = Dv[u] != 0.0 ? x / Dv[u] : 0.0;
+                        }
+                        double d = at[t];
+#pragma unroll
+                        for (int s2 = 0; s2 < t; ++s2) d = fma(-Lm[t][s2] * Dv[s2], Lm[t][s2], d);
+                        Dv[t] = d;
+                    }
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        if (t < pw) minpiv = fmin(minpiv, Dv[t]);
+                    if (lane >= j0 && lane < nrows) {
+                        if (lane < j0 + pw) {   // a row of the block: L and D from the factor
 #pragma unroll
                             for (int t = 0; t < 4; ++t)
-                                if (t < pw) acc = fma(-ld[t], lq[t], acc);
-                            Ew[tri(lane, q)] = acc;
+                                if (lane - j0 == t) {
+#pragma unroll
+                                    for (int u = 0; u < t; ++u) Ew[tri(lane, j0 + u)] = Lm[t][u];
+                                    Ew[tri(lane, lane)] = Dv[t];
+                                }
+                        } else {   // a row below: z L11^T = a_i, l_i = z / D
+                            double z[4];
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) z[t] = Ew[tri(lane, j0 + min(t, pw - 1))];
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) {
+                                z[t] = t < pw ? z[t] : 0.0;
+#pragma unroll
+                                for (int s2 = 0; s2 < t; ++s2) z[t] = fma(-z[s2], Lm[t][s2], z[t]);
+                            }
+#pragma unroll
+                            for (int t = 0; t < 4; ++t)
+                                if (t < pw) Ew[tri(lane, j0 + t)] = Dv[t] != 0.0 ? z[t] / Dv[t] : 0.0;
+                        }
+                    }
+                    WAVE_SYNC();
+                    const int r0 = j0 + pw;
+                    if (r0 < nc) {
+                        const int ntr = (nrows - r0 + 15) >> 4, ntc = (nc - r0 + 15) >> 4;
+                        const double dk = lk == 0 ? Dv[0] : lk == 1 ? Dv[1] : lk == 2 ? Dv[2] : Dv[3];
+                        const int kc = j0 + min(lk, pw - 1);
+                        for (int ti = 0; ti < ntr; ++ti) {
+                            const int arow = r0 + 16 * ti + li;
+                            const double av = Ew[tri(min(arow, nrows - 1), kc)];
+                            const double aop = (arow < nrows && lk < pw) ? -av * dk : 0.0;
+                            for (int tq = 0; tq <= min(ti, ntc - 1); ++tq) {
+                                const int col = r0 + 16 * tq + li;
+                                const double bv = Ew[tri(min(col, nc - 1), kc)];
+                                const double bop = (col < nc && lk < pw) ? bv : 0.0;
+                                f64x4 acc;
+                                int idx[4];
+                                bool ok[4];
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) {
+                                    const int row = r0 + 16 * ti + lk + 4 * q;
+                                    const int rc = min(row, nrows - 1);
+                                    ok[q] = row < nrows && col < nc && col <= row;
+                                    idx[q] = tri(rc, min(col, rc));
+                                    acc[q] = Ew[idx[q]];
+                                }
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) acc[q] = ok[q] ? acc[q] : 0.0;
+                                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(aop, bop, acc, 0, 0, 0);
+#pragma unroll
+                                for (int q = 0; q < 4; ++q)
+                                    if (ok[q]) Ew[idx[q]] = acc[q];
+                            }
                         }
                     }
                     WAVE_SYNC();
