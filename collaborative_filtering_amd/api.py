@@ -101,10 +101,12 @@ class Context:
 
     def debug_phases(self, enable: bool = True, read: bool = False):
         """Predictor phase cycles {setup, basis, fast, block} and rating counts; see cf_abi.h."""
-        out = np.zeros(8, dtype=np.uint64) if read else None
+        out = np.zeros(16, dtype=np.uint64) if read else None
         self._chk(self.lib.cf_debug_phases(self.h, int(enable), ptr(out)), "cf_debug_phases")
         if read:
-            return dict(zip(["setup", "basis", "fast", "dense", "n_fast", "n_dense", "gram", "wide"], map(int, out)))
+            names = ["setup", "basis", "fast", "dense", "n_fast", "n_dense", "gram", "wide",
+                     "w_gather", "w_ldlt", "w_fast", "cyc_nc4", "cyc_nc16", "cyc_ncbig", "n_nc4", "n_nc16"]
+            return dict(zip(names, map(int, out)))
         return None
 
     # -- item graph (out_fin_) ---------------------------------------------------

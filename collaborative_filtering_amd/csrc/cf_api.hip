@@ -81,18 +81,18 @@ void cf_destroy(cf_ctx* ctx) {
     delete ctx;
 }
 
-int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out8) {
+int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out16) {
     if (!ctx) return CF_EINVAL;
     CF_TRY(set_device(ctx));
     if (enable && !ctx->d_phase) {
-        if (hipMalloc(&ctx->d_phase, 8 * sizeof(unsigned long long)) != hipSuccess)
+        if (hipMalloc(&ctx->d_phase, 16 * sizeof(unsigned long long)) != hipSuccess)
             return cf_set_error(ctx, CF_ENOMEM, "phase counters");
-        CF_HIP_CHECK(ctx, hipMemset(ctx->d_phase, 0, 8 * sizeof(unsigned long long)));
+        CF_HIP_CHECK(ctx, hipMemset(ctx->d_phase, 0, 16 * sizeof(unsigned long long)));
     }
-    if (out8 && ctx->d_phase) {
+    if (out16 && ctx->d_phase) {
         CF_HIP_CHECK(ctx, hipDeviceSynchronize());
-        CF_HIP_CHECK(ctx, hipMemcpy(out8, ctx->d_phase, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-        CF_HIP_CHECK(ctx, hipMemset(ctx->d_phase, 0, 8 * sizeof(unsigned long long)));
+        CF_HIP_CHECK(ctx, hipMemcpy(out16, ctx->d_phase, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        CF_HIP_CHECK(ctx, hipMemset(ctx->d_phase, 0, 16 * sizeof(unsigned long long)));
     }
     if (!enable && ctx->d_phase) {
         (void)hipFree(ctx->d_phase);

@@ -20,7 +20,7 @@ struct cf_ctx {
     int max_sweeps = 30;
     // Optional device counters: [0] sum of sweeps, [1] users, [2] max sweeps, [3] capped users.
     unsigned long long* d_stats = nullptr;
-    // Optional predictor phase-cycle counters (6 phases), see cf_debug_phases.
+    // Optional predictor phase-cycle counters (16 slots), see cf_debug_phases.
     unsigned long long* d_phase = nullptr;
     // Device scratch owned by the context (predictor per-block U^T U), grown on demand.
     void* d_scratch = nullptr;

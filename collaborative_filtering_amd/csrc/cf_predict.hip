@@ -232,7 +232,12 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
     int* s_cpos = s_lim + CF_MAX_K;                        // #rows with U(i, j) >= 1e-4
     int* s_slow = s_cpos + CF_MAX_K;                       // rows left to the dense path
     int* s_cnt = s_slow + CF_MAX_K;                        // [0..3] compaction, [4] lim,
-                                                           // [5] Lu, [6] Lq, [7] #dense rows
+                                                           // [5] Lu, [6] Lq, [7] #dense rows,
+                                                           // [8] next fast-path rating
+    // complement masks: bit i of word 3r + (i >> 6) = item i is NOT an out-neighbour of
+    // item r with w > 0.1 (:254-265); fast-path rating order (largest nc first)
+    uint64_t* s_cmask = reinterpret_cast<uint64_t*>(s_cnt + 12);
+    int* s_order = reinterpret_cast<int*>(s_cmask + 3 * CF_MAX_K);
     int* s_cbar = s_conn;   // fast path: per-wave complement lists (kWaves x 64), aliases s_conn/s_keep
     double* Gb = a.gbar + (size_t)blockIdx.x * lmax * lmax;
     double* Qs = a.qs + (size_t)blockIdx.x * (lmax + 2) * lmax;
@@ -265,6 +270,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
         if (tid == 0) {
             s_cnt[5] = 0;
             s_cnt[7] = 0;
+            s_cnt[8] = 0;
         }
         for (int j = tid; j < m; j += kThreads) A[j] = (double)ev[j];   // evals staged in A
         __syncthreads();
@@ -291,6 +297,41 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
         }
         __syncthreads();
         const int Lu = s_cnt[5];
+        // complement masks, four graph rows in flight per wave (unconditional clamped
+        // loads, see block_gemm), then nc of every row in s_slow (free until the fast path)
+        for (int r0 = 4 * wave; r0 < k; r0 += 4 * kWaves) {
+            float gv[4][3];
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+                const float* nrow = a.graph + (size_t)s_item[min(r0 + x, k - 1)] * a.n_items;
+#pragma unroll
+                for (int t = 0; t < 3; ++t) gv[x][t] = nrow[s_item[min(64 * t + lane, k - 1)]];
+            }
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+                int nc = 0;
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    const int i = 64 * t + lane;
+                    const unsigned long long bal = __ballot(i < k && !((double)gv[x][t] > 0.1));   // (:259)
+                    nc += __popcll(bal);
+                    if (lane == 0 && r0 + x < k) s_cmask[3 * (r0 + x) + t] = bal;
+                }
+                if (lane == 0 && r0 + x < k) s_slow[r0 + x] = nc;
+            }
+        }
+        __syncthreads();
+        // fast-path order: descending nc (ties by row), so the waves that claim ratings
+        // dynamically finish together (longest first)
+        for (int i = tid; i < k; i += kThreads) {
+            const int ni = s_slow[i];
+            int rank = 0;
+            for (int j = 0; j < k; ++j) {
+                const int nj = s_slow[j];
+                rank += (nj > ni) || (nj == ni && j < i);
+            }
+            s_order[rank] = i;
+        }
 
         // Gbar = U^T U over the columns [0, Lu), all k rows: full copy in Gb (the dense
         // path's complement form reads it); max |Gbar - I| (non-negative floats order
@@ -452,29 +493,27 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
             double* Ew = A + (size_t)wave * a.ew;
             int* cb = s_cbar + wave * 64;
             const double sum_all = s_misc[1];
-            // graph(movie_r, item_i) for this wave's next rating, loaded one rating ahead
-            // (k <= 192: three loads per lane)
-            float gv_next[3];
-            auto load_graph_row = [&](int rr, float* gv) {
-                const float* nrow = a.graph + (size_t)s_item[rr < k ? rr : 0] * a.n_items;
-#pragma unroll
-                for (int t = 0; t < 3; ++t) {
-                    const int i = 64 * t + lane;
-                    const float v = nrow[s_item[min(i, k - 1)]];   // unconditional (see block_gemm)
-                    gv[t] = (rr < k && i < k) ? v : 0.0f;
-                }
+            // ratings are claimed from s_order one ahead (LDS counter)
+            auto claim = [&]() {
+                int v = 0;
+                if (lane == 0) v = atomicAdd(&s_cnt[8], 1);
+                return __shfl(v, 0);
             };
-            load_graph_row(wave, gv_next);
-            for (int r = wave; r < k; r += kWaves) {
-                float gv[3] = {gv_next[0], gv_next[1], gv_next[2]};
-                load_graph_row(r + kWaves, gv_next);
+            const unsigned long long fw0 = a.phase_cycles ? __builtin_amdgcn_s_memtime() : 0ull;
+            // diagnostics, summed over this wave's ratings of the user (wave-uniform)
+            unsigned long long wacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            int idx = claim();
+            while (idx < k) {
+                const int r = s_order[idx];
+                idx = claim();
+                const unsigned long long rt0 = a.phase_cycles ? __builtin_amdgcn_s_memtime() : 0ull;
                 int nc = 0;
                 double sc = 0.0;
 #pragma unroll
                 for (int t = 0; t < 3; ++t) {
                     const int i = 64 * t + lane;
-                    const bool out = i < k && !((double)gv[t] > 0.1);   // (:259)
-                    const unsigned long long bal = __ballot(out);
+                    const unsigned long long bal = s_cmask[3 * r + t];
+                    const bool out = (bal >> lane) & 1ull;
                     if (out) {
                         const int pos = nc + __popcll(bal & ((1ull << lane) - 1ull));
                         if (pos < 64) cb[pos] = i;
@@ -508,11 +547,18 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                     continue;
                 }
                 const double mu = (sum_all - sc) / (double)c;   // mean over C (:311)
+                const unsigned long long sp0 = a.phase_cycles ? __builtin_amdgcn_s_memtime() : 0ull;
 
                 // E = P_S over the rows [Cbar..., r] (np rows, packed lower): gathers
                 // from P, minus the tail sum_{j in [lim, Lq)} Q_aj Q_bj when lim < Lq.
                 const int np = nc + 1;
                 const int nent = np * (np + 1) / 2;
+                // border-row inputs, issued ahead of the P gathers: (PG, PH)(i, lim) of row
+                // cb[lane] (lane < nc) or r (lane 63), and y_q = r_q - mu of the complement
+                const double2* pgh_lim = reinterpret_cast<const double2*>(PGH) + lim;
+                const double2 py = pgh_lim[(size_t)(lane < nc ? cb[lane] : r) * (Lq + 1)];
+                double* sy = Ew + (a.ew - 64);
+                if (lane < nc) sy[lane] = (double)s_rat[cb[lane]] - mu;
                 auto entry_rows = [&](int e, int& ia, int& ib) {
                     int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
                     while (ra * (ra + 1) / 2 > e) --ra;
@@ -548,20 +594,17 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
 
                 // Border rows: row nc = P_{r,Cbar} (already in place), row nc + 1 := b.
                 // a_r on lane 63 (never a border lane's register).
-                const double2* pgh_lim = reinterpret_cast<const double2*>(PGH) + lim;
                 double bl = 0.0, ar = 0.0;
                 if (lane < nc) {
-                    const double2 py = pgh_lim[(size_t)cb[lane] * (Lq + 1)];
                     bl = py.x - mu * py.y;
                     for (int q = 0; q < nc; ++q) {
                         const double eq = q <= lane ? Ew[tri(lane, q)] : Ew[tri(q, lane)];
-                        bl = fma(-eq, (double)s_rat[cb[q]] - mu, bl);
+                        bl = fma(-eq, sy[q], bl);
                     }
                 }
                 if (lane == 63) {
-                    const double2 py = pgh_lim[(size_t)r * (Lq + 1)];
                     ar = py.x - mu * py.y;
-                    for (int q = 0; q < nc; ++q) ar = fma(-Ew[tri(nc, q)], (double)s_rat[cb[q]] - mu, ar);
+                    for (int q = 0; q < nc; ++q) ar = fma(-Ew[tri(nc, q)], sy[q], ar);
                 }
                 WAVE_SYNC();
                 if (lane < nc) {
@@ -569,6 +612,8 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                     for (int q = 0; q <= lane; ++q) Ew[tri(lane, q)] = (q == lane ? 1.0 : 0.0) - Ew[tri(lane, q)];
                 }
                 WAVE_SYNC();
+                const unsigned long long sp1 = a.phase_cycles ? __builtin_amdgcn_s_memtime() : 0ull;
+                if (a.phase_cycles) wacc[0] += sp1 - sp0;
                 // LDL^T of K (nc columns), border rows nc (P_{r,Cbar}) and nc + 1 (b);
                 // lane i owns row i.  Panels of 4 columns, no per-column sync:
                 //  1. every lane factors the 4x4 diagonal block redundantly in registers;
@@ -581,7 +626,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                 const int li = lane & 15, lk = lane >> 4;
                 for (int j0 = 0; j0 < nc; j0 += 4) {
                     const int pw = min(4, nc - j0);
-                    double Lm[4][4], Dv[4];
+                    double Lm[4][4], Dv[4], Di[4];
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
                         // unconditional (clamped) broadcast reads, then select
@@ -598,12 +643,13 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                             double x = at[u];
 #pragma unroll
                             for (int s2 = 0; s2 < u; ++s2) x = fma(-Lm[t][s2] * Dv[s2], Lm[u][s2], x);
-                            Lm[t][u] = Dv[u] != 0.0 ? x / Dv[u] : 0.0;
+                            Lm[t][u] = x * Di[u];
                         }
                         double d = at[t];
 #pragma unroll
                         for (int s2 = 0; s2 < t; ++s2) d = fma(-Lm[t][s2] * Dv[s2], Lm[t][s2], d);
                         Dv[t] = d;
+                        Di[t] = d != 0.0 ? 1.0 / d : 0.0;   // exact-zero pivot: column skipped
                     }
 #pragma unroll
                     for (int t = 0; t < 4; ++t)
@@ -629,7 +675,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                             }
 #pragma unroll
                             for (int t = 0; t < 4; ++t)
-                                if (t < pw) Ew[tri(lane, j0 + t)] = Dv[t] != 0.0 ? z[t] / Dv[t] : 0.0;
+                                if (t < pw) Ew[tri(lane, j0 + t)] = z[t] * Di[t];
                         }
                     }
                     WAVE_SYNC();
@@ -642,32 +688,42 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                             const int arow = r0 + 16 * ti + li;
                             const double av = Ew[tri(min(arow, nrows - 1), kc)];
                             const double aop = (arow < nrows && lk < pw) ? -av * dk : 0.0;
-                            for (int tq = 0; tq <= min(ti, ntc - 1); ++tq) {
-                                const int col = r0 + 16 * tq + li;
-                                const double bv = Ew[tri(min(col, nc - 1), kc)];
-                                const double bop = (col < nc && lk < pw) ? bv : 0.0;
-                                f64x4 acc;
-                                int idx[4];
-                                bool ok[4];
+                            const int tmax = min(ti, ntc - 1);
+                            // two tiles of the row at a time: loads, then MFMAs, then stores
+                            for (int tq0 = 0; tq0 <= tmax; tq0 += 2) {
+                                f64x4 acc[2];
+                                double bop[2];
 #pragma unroll
-                                for (int q = 0; q < 4; ++q) {
-                                    const int row = r0 + 16 * ti + lk + 4 * q;
-                                    const int rc = min(row, nrows - 1);
-                                    ok[q] = row < nrows && col < nc && col <= row;
-                                    idx[q] = tri(rc, min(col, rc));
-                                    acc[q] = Ew[idx[q]];
+                                for (int x = 0; x < 2; ++x) {
+                                    const int col = r0 + 16 * (tq0 + x) + li;
+                                    const double bv = Ew[tri(min(col, nc - 1), kc)];
+                                    bop[x] = (col < nc && lk < pw) ? bv : 0.0;
+#pragma unroll
+                                    for (int q = 0; q < 4; ++q) {
+                                        const int row = r0 + 16 * ti + lk + 4 * q;
+                                        const int rc = min(row, nrows - 1);
+                                        const double v = Ew[tri(rc, min(col, rc))];
+                                        acc[x][q] = (tq0 + x <= tmax && row < nrows && col < nc && col <= row) ? v : 0.0;
+                                    }
                                 }
+                                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop, bop[0], acc[0], 0, 0, 0);
+                                if (tq0 + 1 <= tmax) acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop, bop[1], acc[1], 0, 0, 0);
 #pragma unroll
-                                for (int q = 0; q < 4; ++q) acc[q] = ok[q] ? acc[q] : 0.0;
-                                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(aop, bop, acc, 0, 0, 0);
+                                for (int x = 0; x < 2; ++x) {
+                                    const int col = r0 + 16 * (tq0 + x) + li;
 #pragma unroll
-                                for (int q = 0; q < 4; ++q)
-                                    if (ok[q]) Ew[idx[q]] = acc[q];
+                                    for (int q = 0; q < 4; ++q) {
+                                        const int row = r0 + 16 * ti + lk + 4 * q;
+                                        if (tq0 + x <= tmax && row < nrows && col < nc && col <= row)
+                                            Ew[tri(row, col)] = acc[x][q];
+                                    }
+                                }
                             }
                         }
                     }
                     WAVE_SYNC();
                 }
+                if (a.phase_cycles) wacc[1] += __builtin_amdgcn_s_memtime() - sp1;
                 double dot = 0.0;
                 if (lane < nc) dot = Ew[tri(nc, lane)] * Ew[tri(nc + 1, lane)] * Ew[tri(lane, lane)];
                 dot = wave_sum(dot);
@@ -691,6 +747,23 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                     a.kk[base + r] = c;
                     if (a.pred) a.pred[base + r] = pred;
                 }
+                if (a.phase_cycles) {   // per nc class: cycles, count (wave-uniform)
+                    const unsigned long long dt = __builtin_amdgcn_s_memtime() - rt0;
+                    if (nc <= 4) {
+                        wacc[3] += dt;
+                        wacc[6] += 1;
+                    } else if (nc <= 16) {
+                        wacc[4] += dt;
+                        wacc[7] += 1;
+                    } else {
+                        wacc[5] += dt;
+                    }
+                }
+            }
+            if (a.phase_cycles) {
+                wacc[2] += __builtin_amdgcn_s_memtime() - fw0;
+                if (lane == 0)
+                    for (int x = 0; x < 8; ++x) atomicAdd(&a.phase_cycles[8 + x], wacc[x]);
             }
         }
         __syncthreads();
@@ -943,6 +1016,8 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
         }
         PHASE_STAMP(3);
     }
+    // slots 0-7 (thread 0 of the block); 8-10 are added per rating / user by lane 0 of
+    // every wave
     if (a.phase_cycles && tid == 0)
         for (int ph = 0; ph < 8; ++ph) atomicAdd(&a.phase_cycles[ph], ph_acc[ph]);
 }
@@ -951,10 +1026,11 @@ template <typename T>
 int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lmax, hipStream_t stream) {
     args.lmax = lmax;
     args.ncw = std::min(kNcMax, lmax);
-    args.ew = (args.ncw + 2) * (args.ncw + 3) / 2;
+    args.ew = (args.ncw + 2) * (args.ncw + 3) / 2 + 64;   // + y of the complement rows
     args.a_elems = std::max({(lmax + 2) * (lmax + 3) / 2, kWaves * args.ew, kStageElems});
     const size_t lds = sizeof(double) * ((size_t)args.a_elems + 4) +
-                       CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 6 * sizeof(int)) + 8 * sizeof(int);
+                       CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 6 * sizeof(int)) + 12 * sizeof(int) +
+                       CF_MAX_K * (3 * sizeof(uint64_t) + sizeof(int));   // s_cmask, s_order
     if (lds > 163840) return cf_set_error(ctx, CF_ERANGE, "predict bucket exceeds LDS");
     int blocks = (int)std::min<uint32_t>(count, 2048u);
     const size_t per_block = (size_t)lmax * lmax + (size_t)(lmax + 2) * lmax + (size_t)lmax * (lmax + 1) * 2 +

@@ -63,11 +63,15 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
  * hit the sweep cap, assembly cycles, Jacobi cycles, epilogue cycles, tournament
  * steps} (cycles: s_memtime of thread 0).  enable == 0 frees them. */
 int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out8);
-/* Diagnostics: predictor phase totals (s_memtime cycles, thread 0 of each block):
- * {per-user setup, basis, fast-path ratings, block-wide ratings} cycles, the number of
- * ratings taken by the fast path and by the block-wide paths, then the cycles of the
- * per-user Gbar GEMM and of the block-wide K path (a subset of the block-wide cycles). */
-int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out8);
+/* Diagnostics: predictor phase totals in s_memtime cycles.  out16[0..7], thread 0 of
+ * each block: {per-user setup, basis, fast-path ratings, block-wide ratings} cycles,
+ * the number of ratings taken by the fast path and by the block-wide paths, then the
+ * cycles of the per-user Gbar GEMM and of the block-wide K path (a subset of the
+ * block-wide cycles).  out16[8..15], summed over every wave: fast-path cycles in
+ * {P/PG/PH gathers and border rows, LDL^T of K, the whole fast phase}, the cycles of
+ * completed fast-path ratings with nc <= 4, 5..16 and > 16, and the counts of the first
+ * two classes. */
+int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out16);
 
 /* ---- item graph (out_fin_) ---------------------------------------------------
  * Directed weighted graph exactly as parsed: w(a,b) and w(b,a) are independent.

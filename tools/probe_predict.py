@@ -35,6 +35,12 @@ tot = sum(cyc.values())
 print({k_: f"{v/tot*100:.1f}%" for k_, v in cyc.items()}, "cycles/prediction:", tot / n,
       "fast", ph["n_fast"], "dense", ph["n_dense"])
 m = d["m"].cpu().numpy(); kk = d["kk"].cpu().numpy()
+wf = max(ph["w_fast"], 1)
+print("fast path, summed over waves: gathers+border", f"{ph['w_gather']/wf*100:.1f}%", "LDL^T", f"{ph['w_ldlt']/wf*100:.1f}%",
+      "rest", f"{(wf-ph['w_gather']-ph['w_ldlt'])/wf*100:.1f}%", "wave-cycles per fast rating", wf / max(ph["n_fast"], 1))
+nbig = max(ph["n_fast"] - ph["n_nc4"] - ph["n_nc16"], 1)
+print("completed fast ratings: nc<=4", ph["n_nc4"], "cyc/rating", ph["cyc_nc4"] / max(ph["n_nc4"], 1),
+      "| 5..16", ph["n_nc16"], ph["cyc_nc16"] / max(ph["n_nc16"], 1), "| >16", nbig, ph["cyc_ncbig"] / nbig)
 print("m mean", m.mean(), "kk mean", kk.mean(), "k mean", k.mean())
 # lim distribution (compat sig table: w_lim of row r is sigs[r] of the global table)
 ev = d["evals"].cpu().numpy(); sg = d["sigs"].cpu().numpy()
