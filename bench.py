@@ -46,6 +46,11 @@ def parse():
     p.add_argument("--pmc", choices=["auto", "off"], default="auto",
                    help="N=1: measure HBM traffic with two rocprofv3 --pmc child passes (FETCH_SIZE, WRITE_SIZE)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)   # one pass, no output
+    p.add_argument("--knn2", choices=["auto", "off", "only"], default="auto",
+                   help="BASELINE config 3 knn2 leg (N=1, rank 0): int8 MFMA item cosine, 20k items x 500k users")
+    p.add_argument("--knn2-users", type=int, default=500_000)
+    p.add_argument("--knn2-items", type=int, default=20_000)
+    p.add_argument("--knn2-reps", type=int, default=3)
     return p.parse_args()
 
 
@@ -70,6 +75,11 @@ def main():
 
     from collaborative_filtering_amd import synth
     from collaborative_filtering_amd.api import CF_SIGS_COMPAT, Context, evec_offsets
+
+    if args.knn2 == "only":
+        with Context(dev_index) as kctx:
+            print(json.dumps(knn2_leg(args, kctx, dev, torch)), flush=True)
+        return
 
     # ---- workload (untimed setup) -------------------------------------------------
     t_setup = time.time()
@@ -280,6 +290,10 @@ def main():
         else:
             result["pmc"] = "unavailable (rocprofv3 missing or the collector failed)"
 
+    # ---- knn2 leg (BASELINE config 3; rank 0, N=1; not part of `value`) ----------------
+    if rank == 0 and world == 1 and args.knn2 == "auto" and not args.profile_steps_only:
+        result["knn2"] = knn2_leg(args, ctx, dev, torch)
+
     # ---- CPU baseline (rank 0, N=1): the oracle in precompute_local_threads form ---------
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_steps_only:
         result["cpu_baseline"] = cpu_baseline(args, off, items, ratings, W, k)
@@ -288,6 +302,107 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+INT8_PEAK_TOPS = 5000.0    # MI355X int8 MFMA dense (2x bf16 2.5 PF), MI355X_MICROARCH.md
+
+
+def knn2_leg(args, ctx, dev, torch):
+    """BASELINE config 3: knn2 weights_calc (knn2.cpp:127-164) over I items x U train users,
+    integer ratings 1..5, on the int8 MFMA path; the dense item-weight matrix stays in HBM.
+    Timed with HIP events on the launch stream: the whole call (rating scan, plane build,
+    similarity kernel) and, from cf_knn2_timing, the similarity kernel alone.  Parity at
+    full size: rows sampled for the CPU baseline are compared bit-exactly with the oracle."""
+    from collaborative_filtering_amd import synth
+
+    seed = 2026101503
+    n_items, n_users = args.knn2_items, args.knn2_users
+    kd = synth.degrees(seed, n_users, k_median=89.0, sigma=0.5, kmin=20, kmax=2000)   # mean ~100
+    off, items, rats = synth.user_items(seed, kd, n_items, threads=16)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    d_off, d_items, d_rat = T(off.view(np.int64)), T(items.view(np.int32)), T(rats)
+    d_W = torch.empty(n_items * n_items, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    call_ms, plane_ms, gemm_ms = [], [], []
+    path = 0
+    for rep in range(1 + args.knn2_reps):
+        e0.record(stream)
+        ctx.item_cosine_run(n_users, n_items, d_off, d_items, d_rat, 1, d_W, stream=sp)
+        e1.record(stream)
+        e1.synchronize()
+        pm, gm, path = ctx.knn2_timing()
+        if rep:
+            call_ms.append(e0.elapsed_time(e1))
+            plane_ms.append(pm)
+            gemm_ms.append(gm)
+    call_s, gemm_s = float(np.median(call_ms)) / 1e3, float(np.median(gemm_ms)) / 1e3
+    I, U = float(n_items), float(n_users)
+    ops = 2.0 * 4.0 * U * I * (I + 1) / 2                      # 4 products, MAC = 2 ops, upper triangle
+    nt = -(-n_items // 128)
+    ldu = -(-n_users // 128) * 128
+    ops_exec = 2.0 * 4.0 * ldu * (nt * (nt + 1) / 2) * 128.0 * 128.0
+    bytes_alg = float(n_items) * ldu + 4.0 * I * I              # code plane read once + weights written
+    W_s = d_W.view(n_items, n_items)
+    sym = bool(torch.equal(W_s, W_s.t()))
+    nnz = int((W_s > 0).sum().item())
+    out = {
+        "workload": f"BASELINE config 3: knn2 item cosine, {n_items} items x {n_users} train users, "
+                    f"mean deg {float(kd.mean()):.1f}, integer ratings 1..5 (Zipf(1) items, seed {seed})",
+        "path": {1: "int8 MFMA, one code plane", 2: "int8 MFMA, three planes", 3: "fp32 MFMA"}.get(path, path),
+        "call_ms": call_s * 1e3,
+        "plane_build_ms": float(np.median(plane_ms)),
+        "kernel_ms": gemm_s * 1e3,
+        "item_pairs_per_s": I * (I - 1) / 2 / call_s,
+        "useful_pair_updates": float(np.sum(kd.astype(np.float64) ** 2)),
+        "edges_w_gt_0.01": nnz,
+        "symmetric": sym,
+        "roofline": {
+            "bound": "mfma",
+            "kernel": "knn2_code_kernel (v_mfma_i32_32x32x32_i8)",
+            "achieved": ops / gemm_s / 1e12,
+            "peak": INT8_PEAK_TOPS,
+            "unit": "TOPS",
+            "frac": ops / gemm_s / 1e12 / INT8_PEAK_TOPS,
+            "traffic": None,
+            "algorithmic_ops": ops,
+            "executed_ops": ops_exec,
+            "executed_frac": ops_exec / gemm_s / 1e12 / INT8_PEAK_TOPS,
+            "algorithmic_bytes": bytes_alg,
+            "algorithmic_GBps": bytes_alg / gemm_s / 1e9,
+            "note": "ops = 2 x 4 products x U x I(I+1)/2 (SURVEY 8d: num=R^T R, den1=S^T B, den2=B^T S, "
+                    "cnt=B^T B on the upper triangle); executed counts the 128-item tile and 128-user padding",
+        },
+    }
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_ref as orc
+
+        rng = np.random.default_rng(3)
+        cal = rng.choice(n_items, size=2, replace=False).astype(np.int32)
+        t = time.perf_counter()
+        orc.knn2_rows(off.astype(np.int64), items.astype(np.int32), rats.astype(np.float64), n_items, cal)
+        per = (time.perf_counter() - t) / 2
+        n_rows = int(max(2, min(200, args.cpu_seconds / max(per, 1e-3))))
+        rows = np.sort(rng.choice(n_items, size=n_rows, replace=False)).astype(np.int32)
+        t = time.perf_counter()
+        Wr = orc.knn2_rows(off.astype(np.int64), items.astype(np.int32), rats.astype(np.float64), n_items, rows)
+        cpu_s = time.perf_counter() - t
+        Wg = W_s[torch.from_numpy(rows.astype(np.int64)).to(dev)].cpu().numpy()
+        out["parity_rows_bit_exact"] = bool(np.array_equal(Wg, Wr))
+        out["parity_rows"] = n_rows
+        out["cpu_baseline"] = {
+            "value": n_rows * (I - 1) / cpu_s,
+            "unit": "item-pair similarities/s",
+            "cores": 1,
+            "kind": "port",
+            "sample": f"{n_rows} random rows x {n_items} items of the same workload, oracle weights_calc "
+                      f"(sorted-list intersection per pair, float accumulators as knn2.cpp:127-146), 1 thread",
+        }
+    del d_W
+    torch.cuda.empty_cache()
+    return out
 
 
 def pmc_traffic(args):

@@ -51,6 +51,7 @@ SIGNATURES = {
                                c_void_p]),
     "cf_item_cosine_run": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_int, c_float,
                                    c_int, c_void_p, c_void_p]),
+    "cf_knn2_timing": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "cf_knn_predict": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "cf_local_calc": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -6,7 +6,7 @@ Inputs are numpy arrays (host) or torch CUDA tensors for the *_run device paths.
 """
 from __future__ import annotations
 
-from ctypes import byref, c_uint32, c_void_p
+from ctypes import byref, c_float, c_int, c_uint32, c_void_p
 from dataclasses import dataclass
 
 import numpy as np
@@ -184,6 +184,20 @@ class Context:
         if adopt:
             self.n_items = n_items
         return W
+
+    def item_cosine_run(self, n_users, n_items, d_user_off, d_item, d_rating, integer, d_w_out,
+                        w_min=0.01, cnt_min=5, stream=None):
+        """Device-pointer knn2 (cf_item_cosine_run) on torch CUDA tensors."""
+        self._chk(self.lib.cf_item_cosine_run(self.h, n_users, n_items, ptr(d_user_off), ptr(d_item),
+                                              ptr(d_rating), int(integer), float(w_min), int(cnt_min),
+                                              ptr(d_w_out), c_void_p(stream or 0)), "cf_item_cosine_run")
+
+    def knn2_timing(self):
+        """(plane_ms, gemm_ms, path) of the last knn2 launch (waits for it)."""
+        a, b, c = c_float(), c_float(), c_int()
+        self._chk(self.lib.cf_knn2_timing(self.h, byref(a), byref(b), byref(c)),
+                  "cf_knn2_timing")
+        return a.value, b.value, c.value
 
     # -- knn_program + error_vertex_data (knn3.cpp:185-256) ------------------------
     def knn_predict(self, user_off, items, ratings):

@@ -78,6 +78,8 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_phase) (void)hipFree(ctx->d_phase);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_knn) (void)hipFree(ctx->d_knn);
+    for (hipEvent_t& e : ctx->knn_ev)
+        if (e) (void)hipEventDestroy(e);
     delete ctx;
 }
 
@@ -433,6 +435,20 @@ int cf_item_cosine_run(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const ui
     CF_TRY(set_device(ctx));
     return cf_launch_knn2(ctx, n_users, n_items, d_user_off, d_item, d_rating, integer_ratings, w_min, cnt_min,
                           d_w_out, (hipStream_t)stream);
+}
+
+int cf_knn2_timing(cf_ctx* ctx, float* plane_ms, float* gemm_ms, int* path) {
+    if (!ctx) return CF_EINVAL;
+    if (!ctx->knn_ev[2]) return cf_set_error(ctx, CF_ESTATE, "cf_knn2_timing: no knn2 launch yet");
+    CF_TRY(set_device(ctx));
+    CF_HIP_CHECK(ctx, hipEventSynchronize(ctx->knn_ev[2]));
+    float a = 0.0f, b = 0.0f;
+    CF_HIP_CHECK(ctx, hipEventElapsedTime(&a, ctx->knn_ev[0], ctx->knn_ev[1]));
+    CF_HIP_CHECK(ctx, hipEventElapsedTime(&b, ctx->knn_ev[1], ctx->knn_ev[2]));
+    if (plane_ms) *plane_ms = a;
+    if (gemm_ms) *gemm_ms = b;
+    if (path) *path = ctx->knn_path;
+    return CF_OK;
 }
 
 int cf_item_cosine(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64_t* user_off,

@@ -28,6 +28,9 @@ struct cf_ctx {
     // knn2 rating planes (R, S, B), grown on demand.
     void* d_knn = nullptr;
     size_t knn_bytes = 0;
+    // knn2 stage events (plane build start, GEMM start, GEMM end) of the last launch.
+    hipEvent_t knn_ev[3] = {nullptr, nullptr, nullptr};
+    int knn_path = 0;   // 1 code plane, 2 three int8 planes, 3 fp32 planes
 };
 
 // One launch of the eigen / predict kernels covers the users of one k-bucket.

@@ -18,6 +18,8 @@
 // w(m, j) > 0.1 (the out-neighbours of m that hold a test rating of u); the squared
 // error of round(pred) (0 if pred < 0.1) is accumulated per movie exactly in int64.
 
+#include <algorithm>
+
 #include "cf_internal.h"
 
 namespace {
@@ -158,6 +160,171 @@ __global__ __launch_bounds__(256) void knn2_f32_kernel(Knn2Args a) {
     knn2_store(a, a0, b0, ta == tb, num, den1, den2, cnt);
 }
 
+// ---- knn2 on one code plane ----------------------------------------------------------
+// MovieLens-style data has few distinct integer ratings (1..5, plus 0 for .predict
+// entries).  With at most 7 distinct values v_1 < ... < v_n, one int8 plane holds
+// code = present ? 1 + index(r) : 0 and the three MFMA operands are rebuilt in
+// registers with one v_perm_b32 byte lookup per 4 users each:
+//     R = tR[code], S = tS[code] = tR[code]^2, B = tB[code] (presence).
+// That is a third of the HBM / L2 bytes of the three-plane form.
+//
+// Tiling: one 256-thread workgroup (4 waves, one per SIMD) per 128 x 128 item tile of
+// the upper triangle; wave (wy, wx) owns 64 x 64 = 2 x 2 blocks of 32 x 32, i.e. 16
+// int32 accumulators (4 products x 4 blocks, 256 registers).  Users are staged 128 at
+// a time through double-buffered LDS (rows padded to 144 B: conflict-free
+// ds_read_b128 / ds_write_b128), one barrier per stage.  Per stage a wave issues 64
+// MFMAs (2048 SIMD cycles) against 8 KB of staged codes per operand.
+//
+// Tile order is XCD-aware: 256 consecutive workgroup ids cover a 16 x 16 super-block
+// of tiles, and the 32 ids of one XCD (id % 8) a 4 x 8 sub-block, so the tiles that
+// run together on one XCD share 12 row bands (1536 items) in its L2.
+constexpr int KC_T = 128;            // items per tile side
+constexpr int KC_U = 128;            // users per LDS stage
+constexpr int KC_ROW = KC_U + 16;    // padded LDS row, bytes
+
+struct Knn2CodeArgs {
+    const int8_t* C;
+    uint64_t ldu;        // users per plane row (multiple of KC_U)
+    uint32_t n_items;
+    uint32_t n_tiles;    // tiles per side
+    uint32_t n_super;    // super-blocks (16 tiles) per side
+    uint32_t tR_lo, tR_hi, tS_lo, tS_hi, tB_lo, tB_hi;   // byte tables, codes 0..3 / 4..7
+    float w_min;
+    int cnt_min;
+    float* w_out;
+};
+
+__device__ __forceinline__ bool code_tile(uint32_t b, uint32_t nt, uint32_t nsb, uint32_t& ta, uint32_t& tb) {
+    const uint32_t sbi = b >> 8, r = b & 255, x = r & 7, j = r >> 3;
+    uint32_t sa, sb;
+    tile_pair(sbi, nsb, sa, sb);
+    ta = sa * 16 + (x >> 1) * 4 + (j >> 3);
+    tb = sb * 16 + (x & 1) * 8 + (j & 7);
+    return ta < nt && tb < nt && ta <= tb;
+}
+
+__device__ __forceinline__ v4i perm4(uint32_t hi, uint32_t lo, v4i c) {
+    v4i o;
+    o.x = (int)__builtin_amdgcn_perm(hi, lo, (uint32_t)c.x);
+    o.y = (int)__builtin_amdgcn_perm(hi, lo, (uint32_t)c.y);
+    o.z = (int)__builtin_amdgcn_perm(hi, lo, (uint32_t)c.z);
+    o.w = (int)__builtin_amdgcn_perm(hi, lo, (uint32_t)c.w);
+    return o;
+}
+
+__global__ __launch_bounds__(256, 1) void knn2_code_kernel(Knn2CodeArgs a) {
+    __shared__ __attribute__((aligned(16))) int8_t lds[2][2][KC_T * KC_ROW];   // [buf][A|B], 73,728 B
+    uint32_t ta, tb;
+    if (!code_tile(blockIdx.x, a.n_tiles, a.n_super, ta, tb)) return;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wy = wave >> 1, wx = wave & 1, r = lane & 31, h = lane >> 5;
+
+    // staging: piece q = t + 256 i (i < 4) of each operand is row q >> 3, 16-byte segment q & 7
+    const int8_t* srcA[4];
+    const int8_t* srcB[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t row = (t >> 3) + 32 * i;
+        const uint32_t ra = min(ta * KC_T + row, a.n_items - 1), rb = min(tb * KC_T + row, a.n_items - 1);
+        srcA[i] = a.C + (size_t)ra * a.ldu + 16 * (t & 7);
+        srcB[i] = a.C + (size_t)rb * a.ldu + 16 * (t & 7);
+    }
+    const int st_off = (t >> 3) * KC_ROW + 16 * (t & 7);     // + 32 rows per piece
+    v4i stA[4], stB[4];
+    auto gload = [&](uint64_t k0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            stA[i] = *(const v4i*)(srcA[i] + k0);
+            stB[i] = *(const v4i*)(srcB[i] + k0);
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            *(v4i*)(&lds[buf][0][st_off + 32 * i * KC_ROW]) = stA[i];
+            *(v4i*)(&lds[buf][1][st_off + 32 * i * KC_ROW]) = stB[i];
+        }
+    };
+
+    v16i num[2][2], den1[2][2], den2[2][2], cnt[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) num[i][j] = den1[i][j] = den2[i][j] = cnt[i][j] = v16i{};
+
+    const int rdA = (wy * 64 + r) * KC_ROW + 16 * h, rdB = (wx * 64 + r) * KC_ROW + 16 * h;
+    const uint64_t n_stage = a.ldu / KC_U;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (uint64_t s = 0; s < n_stage; ++s) {
+        const int buf = (int)(s & 1);
+        if (s + 1 < n_stage) gload((s + 1) * KC_U);
+        const int8_t* LA = lds[buf][0];
+        const int8_t* LB = lds[buf][1];
+#pragma unroll
+        for (int ks = 0; ks < KC_U / 32; ++ks) {
+            v4i Ra[2], Sa[2], Ba[2], Rb[2], Sb[2], Bb[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const v4i ca = *(const v4i*)(LA + rdA + i * 32 * KC_ROW + 32 * ks);
+                const v4i cb = *(const v4i*)(LB + rdB + i * 32 * KC_ROW + 32 * ks);
+                Ra[i] = perm4(a.tR_hi, a.tR_lo, ca);
+                Sa[i] = perm4(a.tS_hi, a.tS_lo, ca);
+                Ba[i] = perm4(a.tB_hi, a.tB_lo, ca);
+                Rb[i] = perm4(a.tR_hi, a.tR_lo, cb);
+                Sb[i] = perm4(a.tS_hi, a.tS_lo, cb);
+                Bb[i] = perm4(a.tB_hi, a.tB_lo, cb);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    num[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ra[i], Rb[j], num[i][j], 0, 0, 0);
+                    den1[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Sa[i], Bb[j], den1[i][j], 0, 0, 0);
+                    den2[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ba[i], Sb[j], den2[i][j], 0, 0, 0);
+                    cnt[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ba[i], Bb[j], cnt[i][j], 0, 0, 0);
+                }
+        }
+        if (s + 1 < n_stage) lstore(buf ^ 1);
+        __syncthreads();
+    }
+    Knn2Args e{};
+    e.n_items = a.n_items;
+    e.w_min = a.w_min;
+    e.cnt_min = a.cnt_min;
+    e.w_out = a.w_out;
+    const bool diag = ta == tb;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            knn2_store(e, ta * KC_T + wy * 64 + 32 * i, tb * KC_T + wx * 64 + 32 * j, diag, num[i][j], den1[i][j],
+                       den2[i][j], cnt[i][j]);
+}
+
+// Which integers in [-11, 11] occur: bit (r + 11) of *mask.
+__global__ void rating_mask_kernel(uint64_t n, const float* rating, unsigned int* mask) {
+    unsigned int m = 0;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (uint64_t)gridDim.x * blockDim.x)
+        m |= 1u << ((int)rating[e] + 11);
+    // wave OR-reduce, one atomic per wave
+    for (int o = 32; o > 0; o >>= 1) m |= __shfl_xor(m, o);
+    if ((threadIdx.x & 63) == 0 && m) atomicOr(mask, m);
+}
+
+struct CodeMap {
+    int8_t code[23];   // code of rating r at [r + 11]
+};
+
+__global__ void plane_code_kernel(uint32_t n_users, const uint64_t* user_off, const uint32_t* item,
+                                  const float* rating, uint64_t ldu, CodeMap map, int8_t* C) {
+    const uint32_t u = blockIdx.x;
+    if (u >= n_users) return;
+    for (uint64_t e = user_off[u] + threadIdx.x; e < user_off[u + 1]; e += blockDim.x)
+        C[(size_t)item[e] * ldu + u] = map.code[(int)rating[e] + 11];
+}
+
 // ---- knn3 ---------------------------------------------------------------------------
 struct Knn3Args {
     uint32_t n_users;
@@ -200,13 +367,7 @@ __global__ __launch_bounds__(256) void knn3_kernel(Knn3Args a) {
 
 }  // namespace
 
-int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64_t* d_user_off,
-                   const uint32_t* d_item, const float* d_rating, int integer_ratings, float w_min,
-                   int cnt_min, float* d_w_out, hipStream_t stream) {
-    const uint64_t ldu = ((uint64_t)n_users + 31) / 32 * 32;
-    const size_t esz = integer_ratings ? 1 : 4;
-    const size_t plane = (size_t)n_items * ldu * esz;
-    const size_t need = 3 * plane;
+static int knn2_alloc(cf_ctx* ctx, size_t need) {
     if (need > ctx->knn_bytes) {
         if (ctx->d_knn) (void)hipFree(ctx->d_knn);
         ctx->d_knn = nullptr;
@@ -215,6 +376,87 @@ int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64
             return cf_set_error(ctx, CF_ENOMEM, "knn2 planes (" + std::to_string(need) + " bytes)");
         ctx->knn_bytes = need;
     }
+    return CF_OK;
+}
+
+// Byte tables of the code path: codes 0..7 -> value, packed as two little-endian dwords.
+static void code_tables(const int* vals, int n, uint32_t& rlo, uint32_t& rhi, uint32_t& slo, uint32_t& shi,
+                        uint32_t& blo, uint32_t& bhi) {
+    uint8_t R[8] = {}, S[8] = {}, B[8] = {};
+    for (int c = 1; c <= n; ++c) {
+        R[c] = (uint8_t)(int8_t)vals[c - 1];
+        S[c] = (uint8_t)(vals[c - 1] * vals[c - 1]);
+        B[c] = 1;
+    }
+    auto pack = [](const uint8_t* b) { return (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24; };
+    rlo = pack(R), rhi = pack(R + 4), slo = pack(S), shi = pack(S + 4), blo = pack(B), bhi = pack(B + 4);
+}
+
+int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64_t* d_user_off,
+                   const uint32_t* d_item, const float* d_rating, int integer_ratings, float w_min,
+                   int cnt_min, float* d_w_out, hipStream_t stream) {
+    if (n_items == 0) return CF_OK;
+    for (hipEvent_t& e : ctx->knn_ev)
+        if (!e) CF_HIP_CHECK(ctx, hipEventCreate(&e));
+    CF_HIP_CHECK(ctx, hipEventRecord(ctx->knn_ev[0], stream));
+    // Integer ratings: which values occur decides between one code plane (<= 7 values)
+    // and the three-plane int8 form.  The scan reads the ratings once (n x 4 B).
+    int vals[23], n_vals = 99;
+    if (integer_ratings) {
+        uint64_t n_rat = 0;
+        CF_HIP_CHECK(ctx, hipMemcpyAsync(&n_rat, d_user_off + n_users, sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+        CF_TRY(knn2_alloc(ctx, 16));
+        unsigned int* d_mask = (unsigned int*)ctx->d_knn;
+        CF_HIP_CHECK(ctx, hipMemsetAsync(d_mask, 0, sizeof(unsigned int), stream));
+        CF_HIP_CHECK(ctx, hipStreamSynchronize(stream));
+        if (n_rat) {
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((n_rat + 255) / 256, 4096);
+            hipLaunchKernelGGL(rating_mask_kernel, dim3(grid), dim3(256), 0, stream, n_rat, d_rating, d_mask);
+            CF_HIP_CHECK(ctx, hipGetLastError());
+        }
+        unsigned int mask = 0;
+        CF_HIP_CHECK(ctx, hipMemcpyAsync(&mask, d_mask, sizeof(mask), hipMemcpyDeviceToHost, stream));
+        CF_HIP_CHECK(ctx, hipStreamSynchronize(stream));
+        n_vals = 0;
+        for (int b = 0; b < 23; ++b)
+            if (mask >> b & 1) vals[n_vals++] = b - 11;
+    }
+    if (integer_ratings && n_vals <= 7) {
+        const uint64_t ldu = ((uint64_t)n_users + KC_U - 1) / KC_U * KC_U;
+        const size_t plane = (size_t)n_items * ldu;
+        CF_TRY(knn2_alloc(ctx, std::max<size_t>(plane, 16)));
+        int8_t* C = (int8_t*)ctx->d_knn;
+        CF_HIP_CHECK(ctx, hipMemsetAsync(C, 0, plane, stream));
+        CodeMap map{};
+        for (int c = 1; c <= n_vals; ++c) map.code[vals[c - 1] + 11] = (int8_t)c;
+        if (n_users) {
+            hipLaunchKernelGGL(plane_code_kernel, dim3(n_users), dim3(64), 0, stream, n_users, d_user_off, d_item,
+                               d_rating, ldu, map, C);
+            CF_HIP_CHECK(ctx, hipGetLastError());
+        }
+        Knn2CodeArgs a{};
+        a.C = C;
+        a.ldu = ldu;
+        a.n_items = n_items;
+        a.n_tiles = (n_items + KC_T - 1) / KC_T;
+        a.n_super = (a.n_tiles + 15) / 16;
+        code_tables(vals, n_vals, a.tR_lo, a.tR_hi, a.tS_lo, a.tS_hi, a.tB_lo, a.tB_hi);
+        a.w_min = w_min;
+        a.cnt_min = cnt_min;
+        a.w_out = d_w_out;
+        const uint32_t grid = a.n_super * (a.n_super + 1) / 2 * 256;
+        ctx->knn_path = 1;
+        CF_HIP_CHECK(ctx, hipEventRecord(ctx->knn_ev[1], stream));
+        hipLaunchKernelGGL(knn2_code_kernel, dim3(grid), dim3(256), 0, stream, a);
+        CF_HIP_CHECK(ctx, hipGetLastError());
+        CF_HIP_CHECK(ctx, hipEventRecord(ctx->knn_ev[2], stream));
+        return CF_OK;
+    }
+    const uint64_t ldu = ((uint64_t)n_users + 31) / 32 * 32;
+    const size_t esz = integer_ratings ? 1 : 4;
+    const size_t plane = (size_t)n_items * ldu * esz;
+    const size_t need = 3 * plane;
+    CF_TRY(knn2_alloc(ctx, need));
     char* base = (char*)ctx->d_knn;
     CF_HIP_CHECK(ctx, hipMemsetAsync(base, 0, need, stream));
     if (n_users) {
@@ -237,6 +479,8 @@ int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64
     a.cnt_min = cnt_min;
     a.w_out = d_w_out;
     const uint32_t ntp = a.n_tiles * (a.n_tiles + 1) / 2;
+    ctx->knn_path = integer_ratings ? 2 : 3;
+    CF_HIP_CHECK(ctx, hipEventRecord(ctx->knn_ev[1], stream));
     if (ntp) {
         if (integer_ratings)
             hipLaunchKernelGGL(knn2_i8_kernel, dim3(ntp), dim3(256), 0, stream, a);
@@ -244,6 +488,7 @@ int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64
             hipLaunchKernelGGL(knn2_f32_kernel, dim3(ntp), dim3(256), 0, stream, a);
         CF_HIP_CHECK(ctx, hipGetLastError());
     }
+    CF_HIP_CHECK(ctx, hipEventRecord(ctx->knn_ev[2], stream));
     return CF_OK;
 }
 

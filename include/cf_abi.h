@@ -156,6 +156,11 @@ int cf_item_cosine_run(cf_ctx* ctx, uint32_t n_users, uint32_t n_items,
                        const uint64_t* d_user_off, const uint32_t* d_item, const float* d_rating,
                        int integer_ratings, float w_min, int cnt_min, float* d_w_out,
                        void* stream);
+/* Durations of the last cf_item_cosine(_run) on its stream (HIP events): plane build
+ * (rating scan, memset, scatter) and the MFMA similarity kernel; path = 1 one code
+ * plane (<= 7 distinct integer ratings), 2 three int8 planes, 3 fp32 planes.
+ * Waits for the launch to finish. */
+int cf_knn2_timing(cf_ctx* ctx, float* plane_ms, float* gemm_ms, int* path);
 /* local_calc vertex_program::apply (local_calc.cpp:262-526) on the uploaded graph (raw
  * out_fin_ weights; edges count iff w > 0.1, graph_loader :113).  Movie unit v lists
  * movie_items[movie_off[v] .. movie_off[v+1]) = [m, the out-neighbours of m with w > 0.1]

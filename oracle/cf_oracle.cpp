@@ -590,35 +590,61 @@ int cfo_local_calc(int n, const double* W, int nu, const double* R, float* mse_o
 // built in ascending user order (the reference iterates a boost::unordered_map, so
 // its order -- and with real-valued ratings the float rounding -- is unpinned).
 //   W_out[a*n_items + b] = w if written, else 0.  cnt_out (optional) = common users.
-int cfo_knn2(int n_users, const int64_t* user_off, const int32_t* item, const double* rating,
-             int n_items, float* W_out, int32_t* cnt_out) {
-    std::vector<std::vector<std::pair<int, double>>> maps(n_items);
+typedef std::vector<std::vector<std::pair<int, double>>> Knn2Maps;
+
+static Knn2Maps knn2_maps(int n_users, const int64_t* user_off, const int32_t* item, const double* rating,
+                          int n_items) {
+    Knn2Maps maps(n_items);
     for (int u = 0; u < n_users; ++u)
         for (int64_t e = user_off[u]; e < user_off[u + 1]; ++e) maps[item[e]].push_back({u, rating[e]});
+    return maps;
+}
+
+// weights_calc for one item pair (knn2.cpp:127-146) plus the writer's w > 0.01 (:157).
+static float knn2_pair(const std::vector<std::pair<int, double>>& ma, const std::vector<std::pair<int, double>>& mb,
+                       int& num_rat) {
+    float num = 0, den1 = 0, den2 = 0;
+    num_rat = 0;
+    size_t j = 0;
+    for (size_t i = 0; i < ma.size(); ++i) {  // (:133-140)
+        while (j < mb.size() && mb[j].first < ma[i].first) ++j;
+        if (j < mb.size() && mb[j].first == ma[i].first) {
+            num_rat++;
+            num += ma[i].second * mb[j].second;
+            den1 += ma[i].second * ma[i].second;
+            den2 += mb[j].second * mb[j].second;
+        }
+    }
+    double obs = 0;
+    if (num_rat > 5) obs = num / (std::sqrt(den1) * std::sqrt(den2));  // (:142-145)
+    return obs > 0.01 ? (float)obs : 0.0f;                              // (:157)
+}
+
+int cfo_knn2(int n_users, const int64_t* user_off, const int32_t* item, const double* rating,
+             int n_items, float* W_out, int32_t* cnt_out) {
+    const Knn2Maps maps = knn2_maps(n_users, user_off, item, rating, n_items);
     for (int a = 0; a < n_items; ++a) {
         for (int b = 0; b < n_items; ++b) {
             float w = 0.0f;
             int num_rat = 0;
-            if (a != b) {
-                const auto& ma = maps[a];
-                const auto& mb = maps[b];
-                float num = 0, den1 = 0, den2 = 0;
-                size_t j = 0;
-                for (size_t i = 0; i < ma.size(); ++i) {  // (:133-140)
-                    while (j < mb.size() && mb[j].first < ma[i].first) ++j;
-                    if (j < mb.size() && mb[j].first == ma[i].first) {
-                        num_rat++;
-                        num += ma[i].second * mb[j].second;
-                        den1 += ma[i].second * ma[i].second;
-                        den2 += mb[j].second * mb[j].second;
-                    }
-                }
-                double obs = 0;
-                if (num_rat > 5) obs = num / (std::sqrt(den1) * std::sqrt(den2));  // (:142-145)
-                if (obs > 0.01) w = (float)obs;                                     // (:157)
-            }
+            if (a != b) w = knn2_pair(maps[a], maps[b], num_rat);
             W_out[(size_t)a * n_items + b] = w;
             if (cnt_out) cnt_out[(size_t)a * n_items + b] = num_rat;
+        }
+    }
+    return 0;
+}
+
+// The same for the rows listed in rows[0..n_rows) only (CPU-baseline sample of bench.py):
+// W_out is n_rows x n_items.
+int cfo_knn2_rows(int n_users, const int64_t* user_off, const int32_t* item, const double* rating,
+                  int n_items, int n_rows, const int32_t* rows, float* W_out) {
+    const Knn2Maps maps = knn2_maps(n_users, user_off, item, rating, n_items);
+    for (int i = 0; i < n_rows; ++i) {
+        const int a = rows[i];
+        for (int b = 0; b < n_items; ++b) {
+            int num_rat = 0;
+            W_out[(size_t)i * n_items + b] = a != b ? knn2_pair(maps[a], maps[b], num_rat) : 0.0f;
         }
     }
     return 0;

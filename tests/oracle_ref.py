@@ -34,6 +34,7 @@ def lib():
         L.cfo_precompute_batch.argtypes = [ci, vp, vp, ctypes.c_int64, vp, vp, ci, ci, vp, vp, vp, vp]
         L.cfo_predict_user.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, ctypes.c_int64, ci, vp, vp, vp, vp]
         L.cfo_knn2.argtypes = [ci, vp, vp, vp, ci, vp, vp]
+        L.cfo_knn2_rows.argtypes = [ci, vp, vp, vp, ci, ci, vp, vp]
         L.cfo_knn3.argtypes = [ci, vp, vp, vp, vp, vp, vp]
         L.cfo_local_graph.argtypes = [ci, ci, vp, vp, ctypes.c_int64, vp]
         L.cfo_local_graph.restype = ci
@@ -122,6 +123,17 @@ def knn2(user_off, item, rating, n_items):
     C = np.zeros((n_items, n_items), dtype=np.int32)
     lib().cfo_knn2(len(user_off) - 1, _p(user_off), _p(item), _p(rating), n_items, _p(W), _p(C))
     return W, C
+
+
+def knn2_rows(user_off, item, rating, n_items, rows):
+    """weights_calc for the listed rows only: float32 (len(rows), n_items)."""
+    user_off = np.ascontiguousarray(user_off, dtype=np.int64)
+    item = np.ascontiguousarray(item, dtype=np.int32)
+    rating = np.ascontiguousarray(rating, dtype=np.float64)
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    W = np.zeros((len(rows), n_items), dtype=np.float32)
+    lib().cfo_knn2_rows(len(user_off) - 1, _p(user_off), _p(item), _p(rating), n_items, len(rows), _p(rows), _p(W))
+    return W
 
 
 def knn3(W, movie_off, user, rating):

@@ -8,15 +8,18 @@ import oracle_ref as orc
 pytestmark = pytest.mark.gpu
 
 
-def synth_train(n_users, n_items, seed, integer=True, zero_frac=0.0, zipf=True):
+def synth_train(n_users, n_items, seed, integer=True, zero_frac=0.0, zipf=True, values=None, kmax=40):
     rng = np.random.default_rng(seed)
     p = 1.0 / np.arange(1, n_items + 1) if zipf else np.ones(n_items)
     p /= p.sum()
     off, items, rats = [0], [], []
     for u in range(n_users):
-        k = int(rng.integers(1, min(40, n_items)))
+        k = int(rng.integers(1, min(kmax, n_items)))
         its = np.sort(rng.choice(n_items, size=k, replace=False, p=p))
-        r = rng.integers(1, 6, size=k).astype(np.float64) if integer else np.round(rng.normal(3, 4, size=k), 4)
+        if values is not None:
+            r = rng.choice(np.asarray(values, np.float64), size=k)
+        else:
+            r = rng.integers(1, 6, size=k).astype(np.float64) if integer else np.round(rng.normal(3, 4, size=k), 4)
         if zero_frac:
             r[rng.random(k) < zero_frac] = 0.0
         items += list(its)
@@ -25,13 +28,27 @@ def synth_train(n_users, n_items, seed, integer=True, zero_frac=0.0, zipf=True):
     return np.array(off, np.uint64), np.array(items, np.uint32), np.array(rats)
 
 
-@pytest.mark.parametrize("n_users,n_items", [(300, 50), (1000, 130), (77, 64)])
+@pytest.mark.parametrize("n_users,n_items", [(300, 50), (1000, 130), (77, 64), (5000, 300), (3000, 2200)])
 def test_knn2_integer_bit_exact(gpu_ctx, n_users, n_items):
     off, items, rats = synth_train(n_users, n_items, seed=n_users, zero_frac=0.03)
     Wg = gpu_ctx.item_cosine(n_items, off, items, rats.astype(np.float32))
     Wo, C = orc.knn2(off.astype(np.int64), items.astype(np.int32), rats, n_items)
     assert (Wo > 0).sum() > n_items  # non-trivial graph
     assert np.array_equal(Wg, Wo)    # weights and thresholded neighbour sets bit-exact
+
+
+@pytest.mark.parametrize("values", [list(range(-3, 4)),            # 7 values: code plane, negative lookups
+                                    list(range(-11, 12)),           # 23 values: three int8 planes
+                                    [0, 11, -11]])
+def test_knn2_integer_value_sets(gpu_ctx, values):
+    """Both int8 paths (one code plane for <= 7 distinct values, three planes otherwise)
+    are bit-exact, including negative ratings and the |r| = 11 extremes."""
+    n_items = 260
+    off, items, rats = synth_train(2500, n_items, seed=len(values), values=values, kmax=60)
+    Wg = gpu_ctx.item_cosine(n_items, off, items, rats.astype(np.float32))
+    Wo, _ = orc.knn2(off.astype(np.int64), items.astype(np.int32), rats, n_items)
+    assert (Wo > 0).sum() > n_items
+    assert np.array_equal(Wg, Wo)
 
 
 def test_knn2_real_valued(gpu_ctx):
