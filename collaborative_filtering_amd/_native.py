@@ -17,6 +17,7 @@ CF_OK = 0
 CF_SIGS_OWN = 0
 CF_SIGS_COMPAT = 1
 CF_MAX_K = 192
+CF_SPILL_MAX_K = 3072
 
 # name -> (restype, argtypes); the list is the ABI contract checked by tests.
 SIGNATURES = {

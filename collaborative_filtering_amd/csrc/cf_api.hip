@@ -78,6 +78,7 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_phase) (void)hipFree(ctx->d_phase);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_knn) (void)hipFree(ctx->d_knn);
+    if (ctx->d_spill) (void)hipFree(ctx->d_spill);
     for (hipEvent_t& e : ctx->knn_ev)
         if (e) (void)hipEventDestroy(e);
     delete ctx;
@@ -223,26 +224,28 @@ int cf_plan_create(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, cf_p
     if (!plan) return cf_set_error(ctx, CF_ENOMEM, "plan allocation");
     plan->n_users = n_users;
     // Bucket by emax = ceil(k/16); within a bucket, largest k first (cost ~ k^3).
+    // by[0]: the spill path (CF_MAX_K < k <= CF_SPILL_MAX_K), launched first.
     std::vector<std::vector<uint32_t>> by(13);
     for (uint32_t u = 0; u < n_users; ++u) {
         const uint64_t k = item_off[u + 1] - item_off[u];
-        if (k > CF_MAX_K) {
+        if (k > CF_SPILL_MAX_K) {
             delete plan;
             return cf_set_error(ctx, CF_ERANGE,
                                 "user " + std::to_string(u) + " has k=" + std::to_string(k) +
-                                    " items; the LDS path supports k <= 192");
+                                    " items; the eigen path supports k <= " + std::to_string(CF_SPILL_MAX_K));
         }
-        by[k == 0 ? 1 : (int)((k + 15) / 16)].push_back(u);
+        by[k == 0 ? 1 : (k > CF_MAX_K ? 0 : (int)((k + 15) / 16))].push_back(u);
         plan->kmax = std::max<uint32_t>(plan->kmax, (uint32_t)k);
     }
-    for (int e = 12; e >= 1; --e) {
+    static const int kOrder[13] = {0, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1};
+    for (const int e : kOrder) {
         auto& v = by[e];
         if (v.empty()) continue;
         std::stable_sort(v.begin(), v.end(), [&](uint32_t x, uint32_t y) {
             return (item_off[x + 1] - item_off[x]) > (item_off[y + 1] - item_off[y]);
         });
         cf_bucket b;
-        b.emax = e;
+        b.emax = e == 0 ? kSpillBucket : e;
         b.first = (uint32_t)plan->h_order.size();
         b.count = (uint32_t)v.size();
         b.kmax = (uint32_t)(item_off[v.front() + 1] - item_off[v.front()]);

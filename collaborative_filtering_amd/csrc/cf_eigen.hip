@@ -498,6 +498,14 @@ int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStre
         if (b.count == 0) continue;
         args.first = b.first;
         int rc;
+        if (b.emax == kSpillBucket) {
+            if (args.mode != kUser)
+                return cf_set_error(ctx, CF_ERANGE, "local_calc units are limited to the LDS path (n <= 192)");
+            rc = cf_launch_eigen_spill(ctx, plan, b, args.item_off, args.items, args.evec_off, args.m_out, args.sigs,
+                                       args.evals, args.evecs, stream);
+            if (rc != CF_OK) return rc;
+            continue;
+        }
         switch (b.emax) {
             case 1: rc = launch_bucket<1>(ctx, args, b.count, stream); break;
             case 2: rc = launch_bucket<2>(ctx, args, b.count, stream); break;

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -28,14 +29,20 @@ struct cf_ctx {
     // knn2 rating planes (R, S, B), grown on demand.
     void* d_knn = nullptr;
     size_t knn_bytes = 0;
+    // eigen spill-path workspace (counter + per-workgroup fp64 k x k), grown on demand.
+    void* d_spill = nullptr;
+    size_t spill_bytes = 0;
     // knn2 stage events (plane build start, GEMM start, GEMM end) of the last launch.
     hipEvent_t knn_ev[3] = {nullptr, nullptr, nullptr};
     int knn_path = 0;   // 1 code plane, 2 three int8 planes, 3 fp32 planes
 };
 
 // One launch of the eigen / predict kernels covers the users of one k-bucket.
+constexpr int kSpillBucket = -1;   // cf_bucket::emax of the CF_MAX_K < k <= CF_SPILL_MAX_K users
+
 struct cf_bucket {
-    int emax = 0;              // elements per lane of a column (k <= 16*emax)
+    int emax = 0;              // elements per lane of a column (k <= 16*emax); kSpillBucket
+
     uint32_t count = 0;        // users in the bucket
     uint32_t first = 0;        // offset into the plan's user order
     uint32_t kmax = 0;         // largest k in the bucket
@@ -98,6 +105,9 @@ int cf_launch_local_sigma(cf_ctx* ctx, const cf_plan* pair_plan, const uint64_t*
                           const uint64_t* d_test_off, const uint32_t* d_test_user,
                           const float* d_test_rating, float* d_wlim, hipStream_t stream);
 
+int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, const uint64_t* d_item_off,
+                          const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs,
+                          float* d_evals, float* d_evecs, hipStream_t stream);
 int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
                     const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m,
                     float* d_sigs, float* d_evals, float* d_evecs, hipStream_t stream);

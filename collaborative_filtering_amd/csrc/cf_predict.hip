@@ -1082,6 +1082,12 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
     int rc = CF_OK;
     for (const cf_bucket& b : plan->buckets) {
         if (b.count == 0) continue;
+        if (b.emax == kSpillBucket) {
+            rc = cf_set_error(ctx, CF_ERANGE, "cf_predict: users with k > " + std::to_string(CF_MAX_K) +
+                                                  " items are eigen-only (spill path); the predictor needs k <= " +
+                                                  std::to_string(CF_MAX_K));
+            break;
+        }
         args.first = b.first;
         const int lmax = std::max<int>(2, 16 * b.emax);
         rc = launch_predict_bucket<T>(ctx, args, b.count, lmax, stream);

@@ -7,7 +7,8 @@
 // Differences (documented in DESIGN.md): the item graph is dense over the compact id
 // space of all ids seen (the reference's 2000x2000 matrix is only defined for ids
 // < 2000); users are written in ascending uid order with their movies ascending (the
-// reference's order is boost::unordered_map order); k is limited to 192 per user.
+// reference's order is boost::unordered_map order); k <= 192 runs on the LDS path,
+// 192 < k <= 3072 on the fp64 spill path.
 #include <cstdio>
 #include <fstream>
 #include <map>
@@ -59,9 +60,9 @@ int main(int argc, char** argv) {
             movies.push_back(mr.first);
         }
         off[++u] = its.size();
-        if (kv.second.size() > CF_MAX_K)
+        if (kv.second.size() > CF_SPILL_MAX_K)
             cfcli::die("user " + std::to_string(kv.first) + " rated " + std::to_string(kv.second.size()) +
-                       " movies; the LDS eigen path supports k <= 192");
+                       " movies; the eigen path supports k <= " + std::to_string(CF_SPILL_MAX_K));
     }
     std::vector<uint64_t> eoff(n_users);
     const uint64_t n_evec = cf_evec_offsets(n_users, off.data(), eoff.data());

@@ -47,6 +47,8 @@ extern "C" {
 #define CF_ESTATE (-5)  /* missing prerequisite (e.g. no item graph uploaded) */
 
 #define CF_MAX_K 192    /* largest per-user item count handled by the LDS eigen path */
+#define CF_SPILL_MAX_K 3072  /* largest k of the eigen spill path (fp64, HBM workspace);
+                                the predictor stays on k <= CF_MAX_K */
 
 typedef struct cf_ctx cf_ctx;
 typedef struct cf_plan cf_plan;

@@ -83,3 +83,48 @@ def test_eigen_closed_form_spectra(gpu_ctx):
     _, ev, _ = res.block(1)
     exp = np.array([0.0] + [1.0] * 48 + [2.0])
     assert np.all(np.abs(ev - exp[: len(ev)]) < 1e-5)
+
+
+def test_eigen_spill_path_mixed(gpu_ctx):
+    """CF_MAX_K < k <= CF_SPILL_MAX_K: fp64 Householder + QL on the HBM workspace, mixed
+    with LDS-path users in one batch (the plan launches the spill bucket first)."""
+    W = cases.item_graph(900, 0.5, seed=41)
+    ks = [193, 5, 200, 256, 100, 300, 192, 513, 700]
+    off, items = cases.user_items(900, ks, seed=42)
+    _check_batch(gpu_ctx, W, off, items, "spill")
+
+
+def test_eigen_spill_path_sparse(gpu_ctx):
+    """Spill users on a sparse graph: lambda = 0 per component, lambda = 1 per isolated item."""
+    W = cases.item_graph(900, 0.01, seed=43, isolated_frac=0.2)
+    off, items = cases.user_items(900, [250, 400, 650], seed=44)
+    _check_batch(gpu_ctx, W, off, items, "spill-sparse")
+
+
+def test_eigen_spill_large_properties(gpu_ctx):
+    """k = 1500 (BASELINE config 5's p95): size-independent checks against an L2 built in
+    numpy from the same formula -- residual ||L2s v - lambda v|| and orthonormality of the
+    kept block, sigs, and m consistent with the returned eigenvalues and the cut."""
+    n_items = 1600
+    W = cases.item_graph(n_items, 0.9, seed=45)
+    off, items = cases.user_items(n_items, [1500], seed=46)
+    gpu_ctx.upload_graph_dense(W)
+    res = gpu_ctx.eigen_batch(off, items)
+    it = items.astype(np.int64)
+    Wu = W[np.ix_(it, it)].astype(np.float64)
+    d = Wu.sum(axis=1)
+    d[d == 0] = 1.0
+    s = np.sqrt(1.0 / d)
+    L2 = (s[:, None] * (np.diag(d) - Wu)) * s[None, :]
+    L2s = np.tril(L2) + np.tril(L2, -1).T
+    sig_g, ev_g, U_g = res.block(0)
+    m = int(res.m[0])
+    sig_ref = np.sqrt(np.sum(L2 * L2, axis=1)) + 0.01
+    assert np.max(np.abs(sig_g - sig_ref) / sig_ref) < 1e-5
+    smm = np.float32(np.float32(np.max(sig_ref - 0.01)) + 0.01)
+    assert np.all(ev_g[:m - 1] <= smm + 1e-6) and np.all(np.diff(ev_g[:m]) >= -1e-7)
+    U = U_g.astype(np.float64)
+    R = L2s @ U - U * ev_g[None, :m]
+    assert np.max(np.linalg.norm(R, axis=0)) < 1e-4
+    assert np.max(np.abs(U.T @ U - np.eye(m))) < 1e-4
+    assert np.all(U.sum(axis=0) >= 0)
