@@ -99,6 +99,18 @@ class Context:
                     "jacobi_cyc_per_step": int(out[5]) / max(int(out[7]), 1)}
         return None
 
+    def debug_spill(self, enable: bool = True, read: bool = False):
+        """Spill-path phase cycles (thread 0 s_memtime sums) when read."""
+        out = np.zeros(8, dtype=np.uint64) if read else None
+        self._chk(self.lib.cf_debug_spill(self.h, int(enable), ptr(out)), "cf_debug_spill")
+        if read:
+            n = max(int(out[0]), 1)
+            names = ["assembly", "tridiag", "accumulate", "ql", "ql_gen"]
+            r = {f"{nm}_cyc_per_user": int(out[i + 1]) / n for i, nm in enumerate(names)}
+            r.update(users=int(out[0]), ql_iters_per_user=int(out[6]) / n, output_cyc_per_user=int(out[7]) / n)
+            return r
+        return None
+
     def debug_phases(self, enable: bool = True, read: bool = False):
         """Predictor phase cycles {setup, basis, fast, block} and rating counts; see cf_abi.h."""
         out = np.zeros(16, dtype=np.uint64) if read else None

@@ -34,6 +34,8 @@ namespace {
 constexpr int SP_T = 512;
 constexpr int SP_W = SP_T / 64;
 constexpr int SP_N = CF_SPILL_MAX_K;
+constexpr int SP_Q = 8;                          // QL iterations applied per pass over Q
+constexpr int SP_TB = 64;                        // positions per staged coefficient block
 
 struct SpillArgs {
     const uint32_t* order;
@@ -51,6 +53,7 @@ struct SpillArgs {
     double* work;
     uint64_t work_stride;    // doubles per workgroup slot (>= kmax^2)
     unsigned int* counter;   // next spill user (zeroed before the launch)
+    unsigned long long* phase;   // 8 counters (cf_debug_spill), summed by thread 0
 };
 
 struct SpillSmem {
@@ -101,6 +104,8 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         const int n = (int)(a.item_off[u + 1] - base);
         float* Wt = a.evecs + a.evec_off[u];   // k x k scratch until the output is written
         auto Mat = [&](int r, int c) -> double& { return M[(size_t)c * n + r]; };
+        unsigned long long t0 = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull, t1 = 0, t2 = 0, t3 = 0, tgen = 0;
+        unsigned long long n_iter = 0;
 
         // ---- 1. W_u, degrees, s, L2, sig_min, A = sym_lower(L2) ------------------------
         for (int i = wave; i < n; i += SP_W) {
@@ -134,6 +139,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         }
         __syncthreads();
 
+        if (tid == 0) t1 = __builtin_amdgcn_s_memtime();
         // ---- 2a. tridiagonalisation (tred2) ---------------------------------------------
         for (int j = tid; j < n; j += SP_T) S.d[j] = Mat(n - 1, j);
         __syncthreads();
@@ -174,11 +180,14 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     Mat(j, i) = S.d[j];
                     double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
                     int q = 0;
-                    for (; q + 4 <= i; q += 4) {
-                        p0 += Mat(j, q) * S.d[q];
-                        p1 += Mat(j, q + 1) * S.d[q + 1];
-                        p2 += Mat(j, q + 2) * S.d[q + 2];
-                        p3 += Mat(j, q + 3) * S.d[q + 3];
+                    for (; q + 8 <= i; q += 8) {
+                        double x[8];
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) x[t] = Mat(j, q + t);
+                        p0 += x[0] * S.d[q] + x[4] * S.d[q + 4];
+                        p1 += x[1] * S.d[q + 1] + x[5] * S.d[q + 5];
+                        p2 += x[2] * S.d[q + 2] + x[6] * S.d[q + 6];
+                        p3 += x[3] * S.d[q + 3] + x[7] * S.d[q + 7];
                     }
                     for (; q < i; ++q) p0 += Mat(j, q) * S.d[q];
                     S.e[j] = ((p0 + p1) + (p2 + p3)) / h;
@@ -193,7 +202,19 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 for (int j = wave; j < i; j += SP_W) {
                     const double dj = S.d[j], ej = S.e[j];
                     double* col = M + (size_t)j * n;
-                    for (int q = lane; q < i; q += 64) col[q] -= dj * S.e[q] + ej * S.d[q];
+                    for (int q0 = 0; q0 < i; q0 += 256) {
+                        double x[4];
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const int q = q0 + 64 * t + lane;
+                            x[t] = q < i ? col[q] : 0.0;
+                        }
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const int q = q0 + 64 * t + lane;
+                            if (q < i) col[q] = x[t] - (dj * S.e[q] + ej * S.d[q]);
+                        }
+                    }
                 }
                 __syncthreads();
                 for (int j = tid; j < i; j += SP_T) {
@@ -205,6 +226,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             if (tid == 0) S.d[i] = h;
             __syncthreads();
         }
+        if (tid == 0) t2 = __builtin_amdgcn_s_memtime();
         // ---- 2b. accumulate Q --------------------------------------------------------------
         for (int i = 0; i < n - 1; ++i) {
             if (tid == 0) {
@@ -215,12 +237,38 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             const double h = S.d[i + 1];
             if (h != 0.0) {
                 const double* uc = M + (size_t)(i + 1) * n;
+                for (int q = tid; q <= i; q += SP_T) S.rc[q] = uc[q];   // u of this step, staged in LDS
+                __syncthreads();
                 for (int j = wave; j <= i; j += SP_W) {
                     double* col = M + (size_t)j * n;
-                    double g = 0.0;
-                    for (int q = lane; q <= i; q += 64) g += uc[q] * col[q];
-                    g = wave_sum(g);
-                    for (int q = lane; q <= i; q += 64) col[q] -= g * (uc[q] / h);
+                    double g0 = 0.0, g1 = 0.0;
+                    for (int q0 = 0; q0 <= i; q0 += 256) {
+                        double x[4];
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const int q = q0 + 64 * t + lane;
+                            x[t] = q <= i ? col[q] : 0.0;
+                        }
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const int q = q0 + 64 * t + lane;
+                            if (q <= i) (t & 1 ? g1 : g0) += S.rc[q] * x[t];
+                        }
+                    }
+                    const double g = wave_sum(g0 + g1);
+                    for (int q0 = 0; q0 <= i; q0 += 256) {
+                        double x[4];
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const int q = q0 + 64 * t + lane;
+                            x[t] = q <= i ? col[q] : 0.0;
+                        }
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const int q = q0 + 64 * t + lane;
+                            if (q <= i) col[q] = x[t] - g * (S.rc[q] / h);
+                        }
+                    }
                 }
             }
             __syncthreads();
@@ -239,86 +287,172 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         }
         __syncthreads();
 
+        if (tid == 0) t3 = __builtin_amdgcn_s_memtime();
         // ---- 3. implicit QL (tql2) -----------------------------------------------------------
-        double f = 0.0, tst1 = 0.0;   // thread 0's state
-        for (int l = 0; l < n; ++l) {
-            if (tid == 0) {
-                tst1 = fmax(tst1, fabs(S.d[l]) + fabs(S.e[l]));
-                int m = l;
-                while (m < n && !(fabs(S.e[m]) <= eps * tst1)) ++m;
-                S.flag[1] = m;
-            }
-            __syncthreads();
-            const int m = S.flag[1];
-            if (m > l) {
-                int iter = 0;
-                for (;;) {
-                    double dl1 = 0.0;
-                    if (tid == 0) {
-                        ++iter;
-                        const double g = S.d[l];
-                        double p = (S.d[l + 1] - g) / (2.0 * S.e[l]);
+        // Thread 0 runs the QL recurrence on (d, e) -- which never reads Q -- and records the
+        // rotation sequences of up to SP_Q consecutive iterations (each on its own [l, m]).
+        // All threads then apply the batch in ONE pass over the touched columns of Q:
+        // sequence t lags sequence t-1 by one position, so a row streams through all SP_Q
+        // sweeps with one load and one store per column (SP_Q carried values per row).
+        {
+            double* Gc = M + (size_t)n * n;      // [SP_Q][n] cosines
+            double* Gs = Gc + (size_t)SP_Q * n;  // [SP_Q][n] sines
+            int* seq_l = S.perm;                 // perm is free until section 4
+            int* seq_m = S.perm + SP_Q;
+            int gl = 0, gm = 0, giter = 0, gphase = 0;   // thread 0's generator state
+            double gf = 0.0, gtst1 = 0.0;
+            for (;;) {
+                if (tid == 0) {
+                    const unsigned long long tg = __builtin_amdgcn_s_memtime();
+                    int nseq = 0;
+                    while (nseq < SP_Q && gl < n) {
+                        if (gphase == 0) {
+                            gtst1 = fmax(gtst1, fabs(S.d[gl]) + fabs(S.e[gl]));
+                            gm = gl;
+                            while (gm < n && !(fabs(S.e[gm]) <= eps * gtst1)) ++gm;
+                            if (gm == gl) {
+                                S.d[gl] += gf;
+                                S.e[gl] = 0.0;
+                                ++gl;
+                                continue;
+                            }
+                            giter = 0;
+                            gphase = 1;
+                        }
+                        const int l = gl, m = gm;
+                        ++giter;
+                        ++n_iter;
+                        const double g0 = S.d[l];
+                        double p = (S.d[l + 1] - g0) / (2.0 * S.e[l]);
                         double r = hypot(p, 1.0);
                         if (p < 0) r = -r;
                         S.d[l] = S.e[l] / (p + r);
                         S.d[l + 1] = S.e[l] * (p + r);
-                        S.red[SP_W + 1] = g - S.d[l];
-                    }
-                    __syncthreads();
-                    const double hsh = S.red[SP_W + 1];
-                    for (int i = l + 2 + tid; i < n; i += SP_T) S.d[i] -= hsh;
-                    __syncthreads();
-                    if (tid == 0) {
-                        dl1 = S.d[l + 1];
-                        f += hsh;
-                        double p = S.d[m];
-                        double c = 1.0, c2 = 1.0, c3 = 1.0;
+                        const double dl1 = S.d[l + 1];
+                        const double hsh = g0 - S.d[l];
+                        for (int i = l + 2; i < n; ++i) S.d[i] -= hsh;
+                        gf += hsh;
+                        p = S.d[m];
+                        double c = 1.0, c2 = 1.0, c3 = 1.0, sn = 0.0, s2 = 0.0;
                         const double el1 = S.e[l + 1];
-                        double s = 0.0, s2 = 0.0;
+                        double* gc = Gc + (size_t)nseq * n;
+                        double* gs = Gs + (size_t)nseq * n;
                         for (int i = m - 1; i >= l; --i) {
                             c3 = c2;
                             c2 = c;
-                            s2 = s;
+                            s2 = sn;
                             const double g = c * S.e[i];
                             const double h = c * p;
-                            const double r = hypot(p, S.e[i]);
-                            S.e[i + 1] = s * r;
-                            s = S.e[i] / r;
+                            r = hypot(p, S.e[i]);
+                            S.e[i + 1] = sn * r;
+                            sn = S.e[i] / r;
                             c = p / r;
-                            p = c * S.d[i] - s * g;
-                            S.d[i + 1] = h + s * (c * g + s * S.d[i]);
-                            S.rc[i] = c;
-                            S.rs[i] = s;
+                            p = c * S.d[i] - sn * g;
+                            S.d[i + 1] = h + sn * (c * g + sn * S.d[i]);
+                            gc[i] = c;
+                            gs[i] = sn;
                         }
-                        p = -s * s2 * c3 * el1 * S.e[l] / dl1;
-                        S.e[l] = s * p;
+                        p = -sn * s2 * c3 * el1 * S.e[l] / dl1;
+                        S.e[l] = sn * p;
                         S.d[l] = c * p;
-                        S.flag[2] = (fabs(S.e[l]) > eps * tst1 && iter < 60) ? 1 : 0;
-                    }
-                    __syncthreads();
-                    // rotations i = m-1 .. l on columns (i, i+1) of Q, one row per thread
-                    for (int r = tid; r < n; r += SP_T) {
-                        double carry = Mat(r, m);
-                        for (int i = m - 1; i >= l; --i) {
-                            const double x = Mat(r, i);
-                            const double c = S.rc[i], s = S.rs[i];
-                            Mat(r, i + 1) = s * x + c * carry;
-                            carry = c * x - s * carry;
+                        seq_l[nseq] = l;
+                        seq_m[nseq] = m;
+                        ++nseq;
+                        if (!(fabs(S.e[l]) > eps * gtst1 && giter < 60)) {
+                            S.d[l] += gf;
+                            S.e[l] = 0.0;
+                            ++gl;
+                            gphase = 0;
                         }
-                        Mat(r, l) = carry;
                     }
-                    const int more = S.flag[2];
-                    __syncthreads();
-                    if (!more) break;
+                    S.flag[1] = nseq;
+                    S.flag[2] = gl >= n;
+                    tgen += __builtin_amdgcn_s_memtime() - tg;
                 }
+                __syncthreads();
+                const int nseq = S.flag[1];
+                const int done = S.flag[2];
+                if (nseq > 0) {
+                    int L = n, Mx = 0;
+                    for (int t = 0; t < nseq; ++t) {
+                        L = min(L, seq_l[t]);
+                        Mx = max(Mx, seq_m[t]);
+                    }
+                    // one row of Q per thread and pass (rows rbase + tid)
+                    for (int rbase = 0; rbase < n; rbase += SP_T) {
+                        const int r = rbase + tid;
+                        const bool act = r < n;
+                        double carry[SP_Q];
+                        carry[0] = act ? Mat(r, Mx) : 0.0;
+#pragma unroll
+                        for (int t = 1; t < SP_Q; ++t) carry[t] = 0.0;
+                        const int tau_hi = Mx - 1, tau_lo = L - nseq;
+                        for (int tb = tau_hi; tb >= tau_lo; tb -= SP_TB) {
+                            // stage the coefficients of this block: [t][j] for tau = tb - j
+                            __syncthreads();
+                            for (int idx = tid; idx < SP_Q * SP_TB; idx += SP_T) {
+                                const int t = idx / SP_TB, j = idx - t * SP_TB;
+                                const int pp = tb - j + t;
+                                double cv = 1.0, sv = 0.0;
+                                if (t < nseq && pp >= seq_l[t] && pp < seq_m[t]) {
+                                    cv = Gc[(size_t)t * n + pp];
+                                    sv = Gs[(size_t)t * n + pp];
+                                }
+                                S.rc[idx] = cv;
+                                S.rs[idx] = sv;
+                            }
+                            __syncthreads();
+                            if (!act) continue;
+                            const int jn = min(SP_TB, tb - tau_lo + 1);
+                            for (int j0 = 0; j0 < jn; j0 += 8) {
+                                double xin[8];
+#pragma unroll
+                                for (int u8 = 0; u8 < 8; ++u8) {
+                                    const int tau = tb - j0 - u8;
+                                    xin[u8] = (j0 + u8 < jn && tau >= L) ? Mat(r, tau) : 0.0;
+                                }
+#pragma unroll
+                                for (int u8 = 0; u8 < 8; ++u8) {
+                                    const int j = j0 + u8;
+                                    if (j < jn) {
+                                        const int tau = tb - j;
+                                        double val = xin[u8];
+                                        bool ok = tau >= L;
+#pragma unroll
+                                        for (int t = 0; t < SP_Q; ++t) {
+                                            const int pp = tau + t;
+                                            if (t >= nseq) {
+                                                // sequences past the batch: pass through
+                                            } else if (pp > Mx) {
+                                                ok = false;
+                                            } else if (pp == Mx) {
+                                                if (ok) carry[t] = val;
+                                                ok = false;
+                                            } else if (pp >= L) {
+                                                const double cv = S.rc[t * SP_TB + j], sv = S.rs[t * SP_TB + j];
+                                                const double out = sv * val + cv * carry[t];
+                                                carry[t] = cv * val - sv * carry[t];
+                                                val = out;
+                                            } else if (pp == L - 1) {
+                                                val = carry[t];
+                                                ok = true;
+                                            } else {
+                                                ok = false;
+                                            }
+                                        }
+                                        if (ok) Mat(r, tau + nseq) = val;
+                                    }
+                                }
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+                if (done) break;
             }
-            if (tid == 0) {
-                S.d[l] += f;
-                S.e[l] = 0.0;
-            }
-            __syncthreads();
         }
 
+        const unsigned long long t4 = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
         // ---- 4. order, sign, lim, output --------------------------------------------------
         for (int j = tid; j < n; j += SP_T) {
             const double lj = S.d[j];
@@ -360,6 +494,17 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             for (int i = lane; i < n; i += 64) Wt[(size_t)i * mm + r] = (float)(col[i] * sg);
         }
         __syncthreads();
+        if (a.phase && tid == 0) {
+            const unsigned long long t5 = __builtin_amdgcn_s_memtime();
+            atomicAdd(&a.phase[0], 1ull);
+            atomicAdd(&a.phase[1], t1 - t0);
+            atomicAdd(&a.phase[2], t2 - t1);
+            atomicAdd(&a.phase[3], t3 - t2);
+            atomicAdd(&a.phase[4], t4 - t3);
+            atomicAdd(&a.phase[5], tgen);
+            atomicAdd(&a.phase[6], n_iter);
+            atomicAdd(&a.phase[7], t5 - t4);
+        }
     }
 }
 
@@ -371,19 +516,23 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     if (b.count == 0) return CF_OK;
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    const uint64_t stride = (uint64_t)b.kmax * b.kmax;
+    const uint64_t stride = (uint64_t)b.kmax * b.kmax + 2ull * SP_Q * b.kmax + 64;
     const uint64_t slot_bytes = stride * sizeof(double);
     const uint64_t budget = 8ull << 30;   // workspace cap; fewer resident users beyond it
     uint32_t grid = std::min<uint32_t>(b.count, (uint32_t)n_cu);
     grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(grid, budget / slot_bytes));
     const size_t need = (size_t)grid * slot_bytes + 256;
     if (need > ctx->spill_bytes) {
+        if (ctx->d_spill && ctx->spill_debug) {   // keep the diagnostic counters across the regrowth
+            CF_HIP_CHECK(ctx, hipStreamSynchronize(stream));
+        }
         if (ctx->d_spill) (void)hipFree(ctx->d_spill);
         ctx->d_spill = nullptr;
         ctx->spill_bytes = 0;
         if (hipMalloc(&ctx->d_spill, need) != hipSuccess)
             return cf_set_error(ctx, CF_ENOMEM, "spill workspace (" + std::to_string(need) + " bytes)");
         ctx->spill_bytes = need;
+        CF_HIP_CHECK(ctx, hipMemsetAsync(ctx->d_spill, 0, 256, stream));
     }
     SpillArgs a{};
     a.order = plan->d_order;
@@ -401,6 +550,7 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     a.counter = reinterpret_cast<unsigned int*>(ctx->d_spill);
     a.work = reinterpret_cast<double*>(static_cast<char*>(ctx->d_spill) + 256);
     a.work_stride = stride;
+    a.phase = ctx->spill_debug ? reinterpret_cast<unsigned long long*>(static_cast<char*>(ctx->d_spill) + 64) : nullptr;
     CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), stream));
     const size_t lds = sizeof(SpillSmem);
     static_assert(sizeof(SpillSmem) <= 163840, "spill LDS");
@@ -408,5 +558,21 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
                                           (int)lds));
     hipLaunchKernelGGL(eigen_spill_kernel, dim3(grid), dim3(SP_T), lds, stream, a);
     CF_HIP_CHECK(ctx, hipGetLastError());
+    return CF_OK;
+}
+
+int cf_debug_spill(cf_ctx* ctx, int enable, uint64_t* out8) {
+    if (!ctx) return CF_EINVAL;
+    CF_TRY(set_device(ctx));
+    ctx->spill_debug = enable != 0;
+    if (out8) {
+        for (int i = 0; i < 8; ++i) out8[i] = 0;
+        if (ctx->d_spill) {
+            CF_HIP_CHECK(ctx, hipDeviceSynchronize());
+            CF_HIP_CHECK(ctx, hipMemcpy(out8, static_cast<char*>(ctx->d_spill) + 64, 8 * sizeof(uint64_t),
+                                        hipMemcpyDeviceToHost));
+            CF_HIP_CHECK(ctx, hipMemset(static_cast<char*>(ctx->d_spill) + 64, 0, 8 * sizeof(uint64_t)));
+        }
+    }
     return CF_OK;
 }

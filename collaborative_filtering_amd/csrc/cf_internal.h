@@ -32,6 +32,7 @@ struct cf_ctx {
     // eigen spill-path workspace (counter + per-workgroup fp64 k x k), grown on demand.
     void* d_spill = nullptr;
     size_t spill_bytes = 0;
+    bool spill_debug = false;   // cf_debug_spill: phase counters in the workspace header
     // knn2 stage events (plane build start, GEMM start, GEMM end) of the last launch.
     hipEvent_t knn_ev[3] = {nullptr, nullptr, nullptr};
     int knn_path = 0;   // 1 code plane, 2 three int8 planes, 3 fp32 planes

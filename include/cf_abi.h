@@ -65,6 +65,11 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
  * hit the sweep cap, assembly cycles, Jacobi cycles, epilogue cycles, tournament
  * steps} (cycles: s_memtime of thread 0).  enable == 0 frees them. */
 int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out8);
+/* Diagnostics of the eigen spill path (k > CF_MAX_K): enable != 0 makes its kernel sum
+ * s_memtime cycles of thread 0 per phase; out8 (optional) receives and resets {users,
+ * assembly, tridiagonalisation, Q accumulation, QL (total), QL rotation generation
+ * (serial part), QL iterations, output} cycles. */
+int cf_debug_spill(cf_ctx* ctx, int enable, uint64_t* out8);
 /* Diagnostics: predictor phase totals in s_memtime cycles.  out16[0..7], thread 0 of
  * each block: {per-user setup, basis, fast-path ratings, block-wide ratings} cycles,
  * the number of ratings taken by the fast path and by the block-wide paths, then the
