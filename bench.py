@@ -51,6 +51,10 @@ def parse():
     p.add_argument("--knn2-users", type=int, default=500_000)
     p.add_argument("--knn2-items", type=int, default=20_000)
     p.add_argument("--knn2-reps", type=int, default=3)
+    p.add_argument("--c5", choices=["auto", "off", "only"], default="auto",
+                   help="BASELINE config 5 sample (N=1, rank 0): power-law k mix through the LDS + spill eigen paths")
+    p.add_argument("--c5-users", type=int, default=1000)
+    p.add_argument("--c5-kmax", type=int, default=1536, help="clip of the config-5 sample (its p95 ~1.5k)")
     return p.parse_args()
 
 
@@ -76,6 +80,11 @@ def main():
     from collaborative_filtering_amd import synth
     from collaborative_filtering_amd.api import CF_SIGS_COMPAT, Context, evec_offsets
 
+    if args.c5 == "only":
+        with Context(dev_index) as cctx:
+            print(json.dumps(c5_leg(args, cctx, dev, torch, synth.graph_model(args.seed, args.items, threads=16))),
+                  flush=True)
+        return
     if args.knn2 == "only":
         with Context(dev_index) as kctx:
             print(json.dumps(knn2_leg(args, kctx, dev, torch)), flush=True)
@@ -294,6 +303,10 @@ def main():
     if rank == 0 and world == 1 and args.knn2 == "auto" and not args.profile_steps_only:
         result["knn2"] = knn2_leg(args, ctx, dev, torch)
 
+    # ---- config 5 sample (rank 0, N=1; not part of `value`) ---------------------------
+    if rank == 0 and world == 1 and args.c5 == "auto" and not args.profile_steps_only:
+        result["config5"] = c5_leg(args, ctx, dev, torch, W)
+
     # ---- CPU baseline (rank 0, N=1): the oracle in precompute_local_threads form ---------
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_steps_only:
         result["cpu_baseline"] = cpu_baseline(args, off, items, ratings, W, k)
@@ -302,6 +315,61 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def c5_leg(args, ctx, dev, torch, W):
+    """BASELINE config 5, bounded sample: a power-law degree mix (lognormal k, median 100,
+    p95 ~1.5k, clipped to [20, --c5-kmax]) through cf_eigen_run -- k <= 192 on the LDS
+    Jacobi path, larger k on the fp64 spill path -- on the config-2 item graph.  Reports
+    users/s of the mix and the per-path split (HIP events around each plan)."""
+    from collaborative_filtering_amd import synth
+    from collaborative_filtering_amd._native import CF_MAX_K, CF_SPILL_MAX_K
+    from collaborative_filtering_amd.api import evec_offsets
+
+    seed = 2026101505
+    sigma = float(np.log(15.0) / 1.6449)            # p95 / median = 15
+    k = synth.degrees(seed, args.c5_users, k_median=100.0, sigma=sigma, kmin=20,
+                      kmax=min(args.c5_kmax, CF_SPILL_MAX_K))
+    off, items, _ = synth.user_items(seed, k, args.items, threads=16)
+    ctx.upload_graph_dense(W)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    out = {"workload": f"BASELINE config 5 sample: {args.c5_users} users, lognormal k (median 100, "
+                       f"sigma {sigma:.3f}, p95 {int(np.percentile(k, 95))}, max {int(k.max())}), "
+                       f"{args.items} items, seed {seed}"}
+    stream = torch.cuda.current_stream(dev)
+    total_ms = 0.0
+    for name, sel in (("lds", k <= CF_MAX_K), ("spill", k > CF_MAX_K)):
+        ks = k[sel]
+        if len(ks) == 0:
+            continue
+        o = np.zeros(len(ks) + 1, dtype=np.uint64)
+        o[1:] = np.cumsum(ks.astype(np.uint64))
+        it = np.concatenate([items[int(off[u]):int(off[u + 1])] for u in np.nonzero(sel)[0]])
+        eo, ne = evec_offsets(o)
+        d_o, d_i, d_e = T(o.view(np.int64)), T(it.view(np.int32)), T(eo.view(np.int64))
+        d_m = torch.zeros(len(ks), dtype=torch.int32, device=dev)
+        d_s = torch.zeros(len(it), dtype=torch.float32, device=dev)
+        d_v = torch.zeros(len(it), dtype=torch.float32, device=dev)
+        d_x = torch.zeros(ne, dtype=torch.float32, device=dev)
+        plan = ctx.plan(o)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        plan.eigen_run(d_o, d_i, d_e, d_m, d_s, d_v, d_x, stream=stream.cuda_stream)
+        e1.record(stream)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        total_ms += ms
+        kf = ks.astype(np.float64)
+        out[name] = {"users": int(len(ks)), "k_mean": float(kf.mean()), "ms": ms,
+                     "users_per_s": len(ks) / ms * 1e3,
+                     "GFLOPs_9k3": float(np.sum(9 * kf ** 3)) / ms / 1e6,
+                     "m_mean": float(d_m.float().mean().item())}
+        plan.close()
+        del d_x
+        torch.cuda.empty_cache()
+    out["users_per_s"] = args.c5_users / total_ms * 1e3
+    out["ms"] = total_ms
+    return out
 
 
 INT8_PEAK_TOPS = 5000.0    # MI355X int8 MFMA dense (2x bf16 2.5 PF), MI355X_MICROARCH.md
