@@ -18,6 +18,8 @@ CF_SIGS_OWN = 0
 CF_SIGS_COMPAT = 1
 CF_MAX_K = 192
 CF_SPILL_MAX_K = 3072
+CF_EIGEN_TRIDIAG = 0
+CF_EIGEN_JACOBI = 1
 
 # name -> (restype, argtypes); the list is the ABI contract checked by tests.
 SIGNATURES = {
@@ -26,6 +28,7 @@ SIGNATURES = {
     "cf_destroy": (None, [c_void_p]),
     "cf_last_error": (c_char_p, [c_void_p]),
     "cf_set_jacobi": (c_int, [c_void_p, c_float, c_int]),
+    "cf_set_eigen_method": (c_int, [c_void_p, c_int]),
     "cf_debug_stats": (c_int, [c_void_p, c_int, c_void_p]),
     "cf_debug_phases": (c_int, [c_void_p, c_int, c_void_p]),
     "cf_debug_spill": (c_int, [c_void_p, c_int, c_void_p]),

@@ -84,6 +84,11 @@ class Context:
     def _chk(self, rc, what):
         _check(self.lib, self.h, rc, what)
 
+    def set_eigen_method(self, method: str = "tridiag"):
+        """'tridiag' (Householder + batched QL, default) or 'jacobi' (one-sided Jacobi in LDS)."""
+        code = {"tridiag": _native.CF_EIGEN_TRIDIAG, "jacobi": _native.CF_EIGEN_JACOBI}[method]
+        self._chk(self.lib.cf_set_eigen_method(self.h, code), "cf_set_eigen_method")
+
     def set_jacobi(self, tol_scale: float = 1.0, max_sweeps: int = 30):
         self._chk(self.lib.cf_set_jacobi(self.h, tol_scale, max_sweeps), "cf_set_jacobi")
 

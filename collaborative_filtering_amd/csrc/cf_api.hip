@@ -79,6 +79,7 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_knn) (void)hipFree(ctx->d_knn);
     if (ctx->d_spill) (void)hipFree(ctx->d_spill);
+    if (ctx->d_tri) (void)hipFree(ctx->d_tri);
     for (hipEvent_t& e : ctx->knn_ev)
         if (e) (void)hipEventDestroy(e);
     delete ctx;
@@ -125,6 +126,13 @@ int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out4) {
 }
 
 const char* cf_last_error(const cf_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+int cf_set_eigen_method(cf_ctx* ctx, int method) {
+    if (!ctx || (method != CF_EIGEN_TRIDIAG && method != CF_EIGEN_JACOBI))
+        return cf_set_error(ctx, CF_EINVAL, "cf_set_eigen_method: unknown method");
+    ctx->eigen_method = method;
+    return CF_OK;
+}
 
 int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps) {
     if (!ctx || !(tol_scale > 0.0f) || max_sweeps <= 0) return cf_set_error(ctx, CF_EINVAL, "bad jacobi options");
@@ -264,6 +272,13 @@ int cf_plan_create(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, cf_p
             return cf_set_error(ctx, CF_EHIP, "plan order copy");
         }
     }
+    {
+        const int rc = cf_tri_prepare(ctx, plan, item_off);
+        if (rc != CF_OK) {
+            cf_plan_destroy(plan);
+            return rc;
+        }
+    }
     *out = plan;
     return CF_OK;
 }
@@ -271,6 +286,8 @@ int cf_plan_create(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, cf_p
 void cf_plan_destroy(cf_plan* plan) {
     if (!plan) return;
     if (plan->d_order) (void)hipFree(plan->d_order);
+    if (plan->d_tri_roff) (void)hipFree(plan->d_tri_roff);
+    if (plan->d_tri_hoff) (void)hipFree(plan->d_tri_hoff);
     delete plan;
 }
 

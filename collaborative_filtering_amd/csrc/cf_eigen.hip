@@ -87,6 +87,7 @@ struct EigenArgs {
     const uint32_t* test_user;
     const float* test_rating;
     float* wlim;                // kSigma output per pair
+    const int* only_flag;       // non-null: run only units j with only_flag[blockIdx.x] != 0
 };
 
 // Test rating of `user` for compact item `movie` (0 if absent): binary search of the
@@ -155,6 +156,7 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     unsigned long long t_phase0 = (a.stats && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
     unsigned long long t_phase1 = 0, t_phase2 = 0;
     const int mode = a.mode;
+    if (a.only_flag && !a.only_flag[blockIdx.x]) return;
     const uint32_t unit = a.order[a.first + blockIdx.x];
     const uint32_t u = (mode == kSigma) ? a.pair_movie[unit] : unit;   // the graph's unit
     const uint64_t base = a.item_off[u];
@@ -572,9 +574,59 @@ int cf_launch_local_sigma(cf_ctx* ctx, const cf_plan* pair_plan, const uint64_t*
     return launch_all_buckets(ctx, pair_plan, args, stream);
 }
 
+static int launch_emax(cf_ctx* ctx, int emax, const EigenArgs& args, uint32_t count, hipStream_t stream) {
+    switch (emax) {
+        case 1: return launch_bucket<1>(ctx, args, count, stream);
+        case 2: return launch_bucket<2>(ctx, args, count, stream);
+        case 3: return launch_bucket<3>(ctx, args, count, stream);
+        case 4: return launch_bucket<4>(ctx, args, count, stream);
+        case 5: return launch_bucket<5>(ctx, args, count, stream);
+        case 6: return launch_bucket<6>(ctx, args, count, stream);
+        case 7: return launch_bucket<7>(ctx, args, count, stream);
+        case 8: return launch_bucket<8>(ctx, args, count, stream);
+        case 9: return launch_bucket<9>(ctx, args, count, stream);
+        case 10: return launch_bucket<10>(ctx, args, count, stream);
+        case 11: return launch_bucket<11>(ctx, args, count, stream);
+        case 12: return launch_bucket<12>(ctx, args, count, stream);
+        default: return cf_set_error(ctx, CF_ERANGE, "eigen bucket out of range (k > 192)");
+    }
+}
+
+int cf_launch_eigen_flagged(cf_ctx* ctx, const cf_plan* plan, int emax, uint32_t first, uint32_t count,
+                            const int* flag, const uint64_t* d_item_off, const uint32_t* d_items,
+                            const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals,
+                            float* d_evecs, hipStream_t stream) {
+    if (count == 0) return CF_OK;
+    EigenArgs args{};
+    args.mode = kUser;
+    args.order = plan->d_order;
+    args.first = first;
+    args.item_off = d_item_off;
+    args.items = d_items;
+    args.graph = ctx->d_graph;
+    args.n_items = ctx->n_items;
+    args.evec_off = d_evec_off;
+    args.m_out = d_m;
+    args.sigs = d_sigs;
+    args.evals = d_evals;
+    args.evecs = d_evecs;
+    args.tol_scale = ctx->tol_scale;
+    args.max_sweeps = ctx->max_sweeps;
+    args.only_flag = flag;
+    return launch_emax(ctx, emax, args, count, stream);
+}
+
 int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
                     const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m,
                     float* d_sigs, float* d_evals, float* d_evecs, hipStream_t stream) {
+    if (ctx->eigen_method == CF_EIGEN_TRIDIAG) {
+        for (const cf_bucket& b : plan->buckets)
+            if (b.emax == kSpillBucket && b.count)
+                CF_TRY(cf_launch_eigen_spill(ctx, plan, b, d_item_off, d_items, d_evec_off, d_m, d_sigs, d_evals,
+                                             d_evecs, stream));
+        return cf_launch_eigen_tri(ctx, plan, d_item_off, d_items, d_evec_off, d_m, d_sigs, d_evals, d_evecs,
+                                   stream);
+    }
     EigenArgs args{};
     args.mode = kUser;
     args.order = plan->d_order;

@@ -33,6 +33,10 @@ struct cf_ctx {
     void* d_spill = nullptr;
     size_t spill_bytes = 0;
     bool spill_debug = false;   // cf_debug_spill: phase counters in the workspace header
+    // tridiagonal eigen path scratch (T, QL records), grown on demand; eigen method
+    void* d_tri = nullptr;
+    size_t tri_bytes = 0;
+    int eigen_method = CF_EIGEN_TRIDIAG;
     // knn2 stage events (plane build start, GEMM start, GEMM end) of the last launch.
     hipEvent_t knn_ev[3] = {nullptr, nullptr, nullptr};
     int knn_path = 0;   // 1 code plane, 2 three int8 planes, 3 fp32 planes
@@ -49,8 +53,22 @@ struct cf_bucket {
     uint32_t kmax = 0;         // largest k in the bucket
 };
 
+struct cf_tri_chunk {
+    int emax;
+    uint32_t first;
+    uint32_t count;
+    uint32_t kmax;
+};
+
 struct cf_plan {
     uint32_t n_users = 0;
+    uint64_t n_entries = 0;
+    // tridiagonal eigen path (cf_eigen_tri.hip): chunks and per-user QL record offsets
+    std::vector<cf_tri_chunk> tri_chunks;
+    uint64_t tri_rot_max = 0, tri_hdr_max = 0;
+    uint32_t tri_users_max = 0;
+    uint64_t* d_tri_roff = nullptr;
+    uint64_t* d_tri_hoff = nullptr;
     std::vector<uint32_t> h_order;   // user ids, grouped by bucket, largest k first
     uint32_t* d_order = nullptr;     // device copy
     std::vector<cf_bucket> buckets;
@@ -109,6 +127,16 @@ int cf_launch_local_sigma(cf_ctx* ctx, const cf_plan* pair_plan, const uint64_t*
 int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, const uint64_t* d_item_off,
                           const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs,
                           float* d_evals, float* d_evecs, hipStream_t stream);
+int cf_tri_prepare(cf_ctx* ctx, cf_plan* plan, const uint64_t* item_off);
+int cf_launch_eigen_tri(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,
+                        const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals, float* d_evecs,
+                        hipStream_t stream);
+// Jacobi kernel over plan order [first, first + count) of LDS bucket emax, only for users
+// with flag[j - first] != 0 (fallback of the tridiagonal path).
+int cf_launch_eigen_flagged(cf_ctx* ctx, const cf_plan* plan, int emax, uint32_t first, uint32_t count,
+                            const int* flag, const uint64_t* d_item_off, const uint32_t* d_items,
+                            const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals,
+                            float* d_evecs, hipStream_t stream);
 int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
                     const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m,
                     float* d_sigs, float* d_evals, float* d_evecs, hipStream_t stream);

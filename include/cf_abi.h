@@ -58,6 +58,11 @@ int cf_version(void);
 int cf_create(int device, cf_ctx** out);
 void cf_destroy(cf_ctx* ctx);
 const char* cf_last_error(const cf_ctx* ctx);
+/* Eigensolver of the k <= CF_MAX_K users: CF_EIGEN_TRIDIAG (default; Householder +
+ * batched QL, cf_eigen_tri.hip) or CF_EIGEN_JACOBI (one-sided Jacobi in LDS). */
+#define CF_EIGEN_TRIDIAG 0
+#define CF_EIGEN_JACOBI 1
+int cf_set_eigen_method(cf_ctx* ctx, int method);
 /* Jacobi off-diagonal tolerance scale (default 1.0) and sweep cap (default 30). */
 int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
 /* Diagnostics: enable != 0 allocates device counters that the eigen kernel fills;

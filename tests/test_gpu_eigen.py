@@ -15,6 +15,15 @@ pytestmark = pytest.mark.gpu
 KS = [1, 2, 3, 5, 8, 15, 16, 17, 31, 32, 33, 47, 64, 65, 100, 127, 128, 129, 150, 180, 191, 192]
 
 
+@pytest.fixture(params=["tridiag", "jacobi"])
+def eig_ctx(gpu_ctx, request):
+    """Both eigensolvers of the k <= 192 path: Householder + batched QL (default) and the
+    one-sided Jacobi kernel."""
+    gpu_ctx.set_eigen_method(request.param)
+    yield gpu_ctx
+    gpu_ctx.set_eigen_method("tridiag")
+
+
 def _check_batch(ctx, W, item_off, items, label):
     ctx.upload_graph_dense(W)
     res = ctx.eigen_batch(item_off, items)
@@ -45,20 +54,23 @@ def _check_batch(ctx, W, item_off, items, label):
     assert not bad, bad
 
 
-def test_eigen_bucket_edges_dense(gpu_ctx):
+def test_eigen_bucket_edges_dense(eig_ctx):
+    gpu_ctx = eig_ctx
     W = cases.item_graph(260, 0.9, seed=11)
     off, items = cases.user_items(260, KS, seed=12)
     _check_batch(gpu_ctx, W, off, items, "dense")
 
 
-def test_eigen_sparse_disconnected(gpu_ctx):
+def test_eigen_sparse_disconnected(eig_ctx):
+    gpu_ctx = eig_ctx
     # sparse graph: many components (lambda = 0 multiplicities) and isolated items (lambda = 1)
     W = cases.item_graph(260, 0.02, seed=21, isolated_frac=0.2)
     off, items = cases.user_items(260, KS, seed=22)
     _check_batch(gpu_ctx, W, off, items, "sparse")
 
 
-def test_eigen_many_users_random_order(gpu_ctx):
+def test_eigen_many_users_random_order(eig_ctx):
+    gpu_ctx = eig_ctx
     rng = np.random.default_rng(31)
     ks = rng.integers(1, 193, size=300)
     W = cases.item_graph(300, 0.3, seed=32)
@@ -66,7 +78,8 @@ def test_eigen_many_users_random_order(gpu_ctx):
     _check_batch(gpu_ctx, W, off, items, "mixed")
 
 
-def test_eigen_closed_form_spectra(gpu_ctx):
+def test_eigen_closed_form_spectra(eig_ctx):
+    gpu_ctx = eig_ctx
     """Complete graph K_n: {0, n/(n-1) x (n-1)}; star S_n: {0, 1 x (n-2), 2}."""
     n_items = 200
     W = np.zeros((n_items, n_items), dtype=np.float32)
