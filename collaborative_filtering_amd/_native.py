@@ -32,6 +32,7 @@ SIGNATURES = {
     "cf_debug_stats": (c_int, [c_void_p, c_int, c_void_p]),
     "cf_debug_phases": (c_int, [c_void_p, c_int, c_void_p]),
     "cf_debug_spill": (c_int, [c_void_p, c_int, c_void_p]),
+    "cf_debug_tri": (c_int, [c_void_p, c_int, c_void_p]),
     "cf_item_graph_upload": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p]),
     "cf_item_graph_upload_dense": (c_int, [c_void_p, c_uint32, c_void_p, c_int]),
     "cf_item_graph_device": (c_void_p, [c_void_p, POINTER(c_uint32)]),

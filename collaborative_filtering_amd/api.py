@@ -84,8 +84,8 @@ class Context:
     def _chk(self, rc, what):
         _check(self.lib, self.h, rc, what)
 
-    def set_eigen_method(self, method: str = "tridiag"):
-        """'tridiag' (Householder + batched QL, default) or 'jacobi' (one-sided Jacobi in LDS)."""
+    def set_eigen_method(self, method: str = "jacobi"):
+        """'jacobi' (one-sided Jacobi in LDS, default) or 'tridiag' (Householder + batched QL)."""
         code = {"tridiag": _native.CF_EIGEN_TRIDIAG, "jacobi": _native.CF_EIGEN_JACOBI}[method]
         self._chk(self.lib.cf_set_eigen_method(self.h, code), "cf_set_eigen_method")
 
@@ -114,6 +114,18 @@ class Context:
             r = {f"{nm}_cyc_per_user": int(out[i + 1]) / n for i, nm in enumerate(names)}
             r.update(users=int(out[0]), ql_iters_per_user=int(out[6]) / n, output_cyc_per_user=int(out[7]) / n)
             return r
+        return None
+
+    def debug_tri(self, enable: bool = True, read: bool = False):
+        """Tridiagonal-path QL counters when read."""
+        out = np.zeros(8, dtype=np.uint64) if read else None
+        self._chk(self.lib.cf_debug_tri(self.h, int(enable), ptr(out)), "cf_debug_tri")
+        if read:
+            n = max(int(out[3]), 1)
+            return {"users": int(out[3]), "rotations_per_user": int(out[0]) / n,
+                    "ql_iters_per_user": int(out[1]) / n, "overflow_users": int(out[2]),
+                    "assembly_cyc_per_user": int(out[4]) / n, "householder_cyc_per_user": int(out[5]) / n,
+                    "q_accum_cyc_per_user": int(out[6]) / n, "k_mean": int(out[7]) / n}
         return None
 
     def debug_phases(self, enable: bool = True, read: bool = False):

@@ -20,7 +20,11 @@
 //        convention sum_i v_ij >= 0, lim (:184-191), k x m row-major block, evals, m.
 //
 // Work: ~4/3 k^3 (reduction) + 4/3 k^3 (Q) + ~6 k^3 (rotations) flops, against ~29 k^3 for
-// the one-sided Jacobi kernel at its measured 9.7 sweeps.  A user whose QL record
+// the one-sided Jacobi kernel at its measured 9.7 sweeps.  Measured (C2 mix, 20k users):
+// 90 ms against the Jacobi kernel's 54 ms -- every phase of a Householder step is a short
+// latency chain (matrix-vector partials, one-wave reflector, rank-2 update) separated by
+// barriers, with one or two workgroups per CU, so the flop saving does not show yet; the
+// Jacobi kernel stays the default (cf_set_eigen_method) and DESIGN.md lists the next steps.  A user whose QL record
 // overflows its budget (never seen: the budget is 3k^2 rotations, tql2 takes ~k^2) is
 // flagged and recomputed by the Jacobi kernel.
 
@@ -55,228 +59,350 @@ struct TriArgs {
     int2* hdr;                 // [l, m] per QL iteration
     const uint64_t* hdr_off;   // per plan index j: [start, end) at 2j, 2j + 1
     int* n_iter;               // per user: QL iterations recorded
+    uint32_t group_first;      // plan index of the group start (smm / flag / n_iter index base)
+    unsigned long long* stats; // cf_debug_tri: {rotations, QL iterations, overflows, users}
 };
 
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
 }
 
-__device__ __forceinline__ double bsum(double v, double* red) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    v = wsum(v);
-    __syncthreads();
-    if (lane == 0) red[wave] = v;
-    __syncthreads();
-    double t = 0.0;
-#pragma unroll
-    for (int w = 0; w < TR_W; ++w) t += red[w];
-    return t;
+// Wave sum in fp64, uniform result: DPP inside each 16-lane row (quad perms, half-row and
+// row mirrors), then the four row sums through readlane.  ~8x shorter latency than the
+// ds_bpermute chain of __shfl_xor on doubles.
+__device__ __forceinline__ double wsum(double v) {
+    v += dpp_d<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_d<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_d<0x141>(v);   // row_half_mirror
+    v += dpp_d<0x140>(v);   // row_mirror
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const double r0 = __hiloint2double(__builtin_amdgcn_readlane(hi, 0), __builtin_amdgcn_readlane(lo, 0));
+    const double r1 = __hiloint2double(__builtin_amdgcn_readlane(hi, 16), __builtin_amdgcn_readlane(lo, 16));
+    const double r2 = __hiloint2double(__builtin_amdgcn_readlane(hi, 32), __builtin_amdgcn_readlane(lo, 32));
+    const double r3 = __hiloint2double(__builtin_amdgcn_readlane(hi, 48), __builtin_amdgcn_readlane(lo, 48));
+    return (r0 + r1) + (r2 + r3);
 }
 
 __host__ __device__ constexpr int tri_ld(int n) { return n | 1; }   // odd row stride: conflict-free columns
 
 // ---- A: assembly + tridiagonalisation + Q ---------------------------------------------------
-__global__ __launch_bounds__(TR_T) void tri_reduce_kernel(TriArgs a) {
+// 1024 threads.  A is row-major with a row stride LD = n rounded up to a multiple of 4 and
+// = 4 (mod 64): float4 rows for the rank-2 updates (lanes over columns), and only 2-way
+// bank conflicts for the thread-per-row passes of the assembly.  Matrix-vector products use
+// the symmetry (A u)_c = sum_q A[q][c] u_q: thread (c, part) sums a quarter of the rows.
+constexpr int TA_T = 1024;
+constexpr int TA_W = TA_T / 64;
+
+__host__ __device__ constexpr int tri_lda(int n) {
+    return ((n + 3) & ~3) + ((4 - (((n + 3) & ~3) & 63)) & 63);
+}
+
+__global__ __launch_bounds__(TA_T) void tri_reduce_kernel(TriArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t jj = blockIdx.x;
     const uint32_t u = a.order[a.first + jj];
     const uint64_t base = a.item_off[u];
     const int n = (int)(a.item_off[u + 1] - base);
+    const uint32_t js = a.first + jj - a.group_first;   // index into the group's per-user arrays
     if (n <= 0) {
-        if (tid == 0) a.m_out[u] = 0;
+        if (tid == 0) {
+            a.m_out[u] = 0;
+            a.smm[js] = 0.0f;
+        }
         return;
     }
-    const int LD = tri_ld(n);
-    float* A = reinterpret_cast<float*>(smem_raw);                 // n x LD, row-major
-    double* vu = reinterpret_cast<double*>(A + ((n * LD + 1) & ~1));  // u of the step
-    double* vp = vu + TR_NMAX;                                     // p / w of the step
-    double* hh = vp + TR_NMAX;                                     // h_i of every step
-    double* red = hh + TR_NMAX;                                    // reductions (8)
-    uint32_t* s_item = reinterpret_cast<uint32_t*>(red + 8);
+    const int LD = tri_lda(n);
+    unsigned long long tA0 = (a.stats && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull, tA1 = 0, tA2 = 0;
+    float* A = reinterpret_cast<float*>(smem_raw);                     // n x LD
+    double* vu = reinterpret_cast<double*>(A + (size_t)n * LD);        // u (fp64); d_i in assembly
+    double* hh = vu + TR_NMAX;                                         // h_i
+    double* part = hh + TR_NMAX;                                       // [4][TR_NMAX] partial sums
+    double* vp = part;                                                 // s_i during the assembly
+    // part + 4N: the second fp64 u buffer.  During the assembly part[0, N) holds s_i,
+    // part + 2N the item ids and part + 3N the per-wave sig maxima.
+    double* red = part + 3 * TR_NMAX;
+    float* uf = reinterpret_cast<float*>(part + 5 * TR_NMAX);          // u (fp32)
+    float* wf = uf + TR_NMAX;                                          // w (fp32)
+    float* s_uf2 = wf + TR_NMAX;                                       // u (fp32), 2nd buffer
+    uint32_t* s_item = reinterpret_cast<uint32_t*>(part + 2 * TR_NMAX);
 
-    for (int i = tid; i < n; i += TR_T) s_item[i] = a.items[base + i];
+    for (int i = tid; i < n; i += TA_T) s_item[i] = a.items[base + i];
     __syncthreads();
-    // W_u: wave per row, lanes over columns
-    for (int i = wave; i < n; i += TR_W) {
+    for (int i = wave; i < n; i += TA_W) {
         const float* grow = a.graph + (size_t)s_item[i] * a.n_items;
         for (int j = lane; j < n; j += 64) A[i * LD + j] = grow[s_item[j]];
     }
     __syncthreads();
-    // degrees and scales, thread per row, sequential j (the oracle's summation order)
-    for (int i = tid; i < n; i += TR_T) {
+    for (int i = tid; i < n; i += TA_T) {
+        const float* row = A + i * LD;
         double d = 0.0;
-        for (int j = 0; j < n; ++j) d += (double)A[i * LD + j];
+        for (int j = 0; j < n; ++j) d += (double)row[j];
         if (d == 0.0) d = 1.0;                       // (:137-140)
         vu[i] = d;
         vp[i] = sqrt(1.0 / d);                       // (:149-153)
     }
     __syncthreads();
-    // sig_min (float accumulation of double squares, :172-176) and L2 rows kept in registers?
-    // No: L2(i,j) is recomputed where needed; each thread owns row i.
     float sig_i = 0.0f;
-    for (int i = tid; i < n; i += TR_T) {
+    for (int i = tid; i < n; i += TA_T) {
+        float* row = A + i * LD;
         const double si = vp[i], di = vu[i];
         float acc = 0.0f;
         for (int j = 0; j < n; ++j) {
-            const double l = (j == i ? di : 0.0) - (double)A[i * LD + j];
+            const double l = (j == i ? di : 0.0) - (double)row[j];
             const double l2 = (si * l) * vp[j];      // (:155)
-            acc = (float)((double)acc + l2 * l2);
+            acc = (float)((double)acc + l2 * l2);    // (:172-176)
         }
         sig_i = sqrtf(acc);
         a.sigs[base + i] = (float)((double)sig_i + 0.01);   // (:177)
+        for (int j = 0; j <= i; ++j) {
+            const double l = (j == i ? di : 0.0) - (double)row[j];
+            row[j] = (float)((si * l) * vp[j]);
+        }
     }
-    // cut smm = float(max sig + 0.01) (:179-182)
-    {
+    {   // cut smm = float(max sig + 0.01) (:179-182)
         float mx = (tid < n) ? sig_i : 0.0f;
         for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-        __syncthreads();
         if (lane == 0) reinterpret_cast<float*>(red)[wave] = mx;
         __syncthreads();
         if (tid == 0) {
             float m = 0.0f;
-            for (int w = 0; w < TR_W; ++w) m = fmaxf(m, reinterpret_cast<float*>(red)[w]);
-            a.smm[jj] = (float)((double)m + 0.01);
-        }
-        __syncthreads();
-    }
-    // A = sym_lower(L2) in place (row i owned by thread i; column writes go to rows j > i
-    // of the upper part, which no thread reads W from any more: W_ij for j < i only)
-    // Two passes so that no W value is overwritten before it is read.
-    for (int i = tid; i < n; i += TR_T) {
-        const double si = vp[i], di = vu[i];
-        for (int j = 0; j <= i; ++j) {
-            const double l = (j == i ? di : 0.0) - (double)A[i * LD + j];
-            A[i * LD + j] = (float)((si * l) * vp[j]);
+            for (int w = 0; w < TA_W; ++w) m = fmaxf(m, reinterpret_cast<float*>(red)[w]);
+            a.smm[js] = (float)((double)m + 0.01);
         }
     }
-    __syncthreads();
-    for (int idx = tid; idx < n * n; idx += TR_T) {
-        const int i = idx / n, j = idx - i * n;
-        if (j > i) A[i * LD + j] = A[j * LD + i];
-    }
+    for (int i = wave; i < n; i += TA_W)
+        for (int j = i + 1 + lane; j < n; j += 64) A[i * LD + j] = A[j * LD + i];
     __syncthreads();
 
     // ---- Householder reduction: step i annihilates A[i][0 .. i-2] --------------------------
+    // Three barriers per step: (1) partial sums of A u, (2) w = p - K u (one wave), (3) the
+    // rank-2 update.  The row of the next step is finished by the wave that owns it in (3),
+    // which then forms the next reflector (scale, h, u) right away into the other buffer.
+    if (a.stats && tid == 0) tA1 = __builtin_amdgcn_s_memtime();
     double* dd = a.dd + base;
     double* ee = a.ee + base;
-    for (int i = n - 1; i > 0; --i) {
-        double part = 0.0;
-        for (int q = tid; q < i; q += TR_T) part += fabs((double)A[i * LD + q]);
-        const double scale = bsum(part, red);
+    const int pc = tid & 255, pq = tid >> 8;   // (column, quarter) of the matrix-vector products
+    double* vub[2] = {vu, part + 4 * TR_NMAX};  // fp64 u, double-buffered by step parity
+    float* ufb[2] = {uf, s_uf2};
+    // reflector of row i by one wave: u into buffer (i & 1), h_i and e_i
+    auto reflector = [&](int i) {
+        double* v = vub[i & 1];
+        float* vf = ufb[i & 1];
+        double x[3];
+        double sa = 0.0, sq = 0.0;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int q = lane + 64 * t;
+            x[t] = q < i ? (double)A[i * LD + q] : 0.0;
+            sa += fabs(x[t]);
+            sq += x[t] * x[t];
+        }
+        const double scale = wsum(sa);
+        const double ssq = wsum(sq);
+        double h = 0.0;
         if (scale == 0.0) {
-            if (tid == 0) {
-                ee[i] = 0.0;
-                hh[i] = 0.0;
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const int q = lane + 64 * t;
+                if (q < ((i + 3) & ~3)) {
+                    v[q] = 0.0;
+                    vf[q] = 0.0f;
+                }
             }
-            for (int q = tid; q < i; q += TR_T) A[i * LD + q] = 0.0f;   // u = 0
+            if (lane == 0) ee[i] = 0.0;
+        } else {
+            h = ssq / (scale * scale);
+            const double f = (double)A[i * LD + i - 1] / scale;
+            const double g = f > 0 ? -sqrt(h) : sqrt(h);
+            h -= f * g;
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const int q = lane + 64 * t;
+                if (q < i) {
+                    const double uq = (q == i - 1) ? f - g : x[t] / scale;
+                    v[q] = uq;
+                    vf[q] = (float)uq;
+                } else if (q < ((i + 3) & ~3)) {
+                    v[q] = 0.0;
+                    vf[q] = 0.0f;
+                }
+            }
+            if (lane == 0) ee[i] = scale * g;
+        }
+        if (lane == 0) hh[i] = h;
+    };
+    if (wave == 0 && n > 1) reflector(n - 1);
+    __syncthreads();
+    for (int i = n - 1; i > 0; --i) {
+        const double h = hh[i];
+        const double* vcur = vub[i & 1];
+        const float* ucur = ufb[i & 1];
+        if (h == 0.0) {   // row i already reduced: no transformation
+            if (i > 1 && wave == ((i - 1) & (TA_W - 1))) reflector(i - 1);
             __syncthreads();
             continue;
         }
-        double hp = 0.0;
-        for (int q = tid; q < i; q += TR_T) {
-            const double v = (double)A[i * LD + q] / scale;
-            vu[q] = v;
-            hp += v * v;
-        }
-        double h = bsum(hp, red);
-        if (tid == 0) {
-            const double f = vu[i - 1];
-            const double g = f > 0 ? -sqrt(h) : sqrt(h);
-            ee[i] = scale * g;
-            h -= f * g;
-            vu[i - 1] = f - g;
-            red[7] = h;
-        }
-        __syncthreads();
-        h = red[7];
-        // p = A[0:i, 0:i] u / h, thread per row
-        for (int j = tid; j < i; j += TR_T) {
-            const float* row = A + j * LD;
-            double p0 = 0.0, p1 = 0.0;
-            int q = 0;
-            for (; q + 2 <= i; q += 2) {
-                p0 += (double)row[q] * vu[q];
-                p1 += (double)row[q + 1] * vu[q + 1];
+        // (1) partial sums of A u: thread (c, quarter) over rows q = quarter (mod 4)
+        if (pc < i) {
+            double s0 = 0.0, s1 = 0.0;
+            int q = pq;
+            for (; q + 4 < i; q += 8) {
+                s0 += (double)A[q * LD + pc] * vcur[q];
+                s1 += (double)A[(q + 4) * LD + pc] * vcur[q + 4];
             }
-            if (q < i) p0 += (double)row[q] * vu[q];
-            vp[j] = (p0 + p1) / h;
+            if (q < i) s0 += (double)A[q * LD + pc] * vcur[q];
+            part[pq * TR_NMAX + pc] = s0 + s1;
         }
         __syncthreads();
-        double kp = 0.0;
-        for (int j = tid; j < i; j += TR_T) kp += vu[j] * vp[j];
-        const double K = bsum(kp, red) / (h + h);
-        for (int j = tid; j < i; j += TR_T) vp[j] -= K * vu[j];
-        __syncthreads();
-        // rank-2 update of the active block; reflector u into row i (dead from now on)
-        for (int idx = tid; idx < i * i; idx += TR_T) {
-            const int r = idx / i, c = idx - r * i;
-            A[r * LD + c] = (float)((double)A[r * LD + c] - (vu[r] * vp[c] + vp[r] * vu[c]));
+        // (2) one wave: p = A u / h, K = u.p / 2h, w = p - K u
+        if (wave == 0) {
+            double pv[3];
+            double kp = 0.0;
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const int c = lane + 64 * t;
+                pv[t] = 0.0;
+                if (c < i) {
+                    pv[t] = ((part[c] + part[TR_NMAX + c]) + (part[2 * TR_NMAX + c] + part[3 * TR_NMAX + c])) / h;
+                    kp += vcur[c] * pv[t];
+                }
+            }
+            const double K = wsum(kp) / (h + h);
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const int c = lane + 64 * t;
+                if (c < i) wf[c] = (float)(pv[t] - K * vcur[c]);
+                else if (c < ((i + 3) & ~3)) wf[c] = 0.0f;   // float4 tail: columns >= i unchanged
+            }
         }
-        for (int q = tid; q < i; q += TR_T) A[i * LD + q] = (float)vu[q];
-        if (tid == 0) hh[i] = h;
+        __syncthreads();
+        // (3) rank-2 update A -= u w^T + w u^T on [0, i)^2 in fp32, float4 per lane; the
+        // reflector u goes into row i (dead from now on); the owner of row i-1 then forms
+        // the next reflector
+        for (int r = wave; r < i; r += TA_W) {
+            const float ur = ucur[r], wr = wf[r];
+            float* row = A + r * LD;
+            for (int c = 4 * lane; c < i; c += 256) {
+                float4 x = *reinterpret_cast<float4*>(row + c);
+                const float4 uc = *reinterpret_cast<const float4*>(ucur + c);
+                const float4 wc = *reinterpret_cast<const float4*>(wf + c);
+                x.x -= ur * wc.x + wr * uc.x;
+                x.y -= ur * wc.y + wr * uc.y;
+                x.z -= ur * wc.z + wr * uc.z;
+                x.w -= ur * wc.w + wr * uc.w;
+                *reinterpret_cast<float4*>(row + c) = x;
+            }
+        }
+        for (int q = tid; q < i; q += TA_T) A[i * LD + q] = ucur[q];
+        if (i > 1 && wave == ((i - 1) & (TA_W - 1))) reflector(i - 1);
         __syncthreads();
     }
-    for (int i = tid; i < n; i += TR_T) dd[i] = (double)A[i * LD + i];
+    for (int i = tid; i < n; i += TA_T) dd[i] = (double)A[i * LD + i];
     if (tid == 0) {
         ee[0] = 0.0;
         hh[0] = 0.0;
     }
-    __syncthreads();
-    // reflectors (strict lower triangle) to the evecs slot, then Q in LDS
     float* slot = a.evecs + a.evec_off[u];
-    for (int idx = tid; idx < n * n; idx += TR_T) {
-        const int i = idx / n, j = idx - i * n;
-        if (j < i) slot[idx] = A[i * LD + j];
+    for (int i = wave; i < n; i += TA_W)
+        for (int j = lane; j < i; j += 64) slot[i * n + j] = A[i * LD + j];
+    __syncthreads();
+    for (int i = wave; i < n; i += TA_W)
+        for (int j = lane; j < LD; j += 64) A[i * LD + j] = (i == j) ? 1.0f : 0.0f;
+    if (a.stats && tid == 0) tA2 = __builtin_amdgcn_s_memtime();
+    // Q = H_{n-1} ... H_1: for i = 1 .. n-1, Q[0:i, 0:i] -= u (u^T Q[0:i, 0:i]) / h_i.
+    // u of the next step is loaded (double buffer) during the update of this one.
+    if (n > 1 && tid < 4) {   // u of step 1 (one element) into buffer 1, zero float4 tail
+        const float v = tid < 1 ? slot[1 * n + tid] : 0.0f;
+        vub[1][tid] = (double)v;
+        ufb[1][tid] = v;
     }
     __syncthreads();
-    for (int idx = tid; idx < n * n; idx += TR_T) {
-        const int i = idx / n, j = idx - i * n;
-        A[i * LD + j] = (i == j) ? 1.0f : 0.0f;
-    }
-    __syncthreads();
-    // Q = H_{n-1} ... H_1: for i = 1 .. n-1, Q[0:i, 0:i] -= u (u^T Q[0:i, 0:i]) / h_i
     for (int i = 1; i < n; ++i) {
         const double h = hh[i];
-        if (h == 0.0) continue;   // uniform
-        for (int q = tid; q < i; q += TR_T) vu[q] = (double)slot[i * n + q];
-        __syncthreads();
-        for (int c = tid; c < i; c += TR_T) {
-            double t0 = 0.0, t1 = 0.0;
-            int r = 0;
-            for (; r + 2 <= i; r += 2) {
-                t0 += vu[r] * (double)A[r * LD + c];
-                t1 += vu[r + 1] * (double)A[(r + 1) * LD + c];
+        const double* vcur = vub[i & 1];
+        const float* ucur = ufb[i & 1];
+        const float unext = (i + 1 < n && tid < i + 1) ? slot[(i + 1) * n + tid] : 0.0f;   // TA_T > k
+        if (h != 0.0) {   // uniform
+            if (pc < i) {
+                double s0 = 0.0, s1 = 0.0;
+                int q = pq;
+                for (; q + 4 < i; q += 8) {
+                    s0 += vcur[q] * (double)A[q * LD + pc];
+                    s1 += vcur[q + 4] * (double)A[(q + 4) * LD + pc];
+                }
+                if (q < i) s0 += vcur[q] * (double)A[q * LD + pc];
+                part[pq * TR_NMAX + pc] = s0 + s1;
             }
-            if (r < i) t0 += vu[r] * (double)A[r * LD + c];
-            vp[c] = (t0 + t1) / h;
+            __syncthreads();
+            if (tid < i)
+                wf[tid] = (float)(((part[tid] + part[TR_NMAX + tid]) + (part[2 * TR_NMAX + tid] + part[3 * TR_NMAX + tid])) / h);
+            else if (tid < ((i + 3) & ~3))
+                wf[tid] = 0.0f;   // float4 tail: Q[r][c >= i] stays 0
+            __syncthreads();
+            for (int r = wave; r < i; r += TA_W) {
+                const float ur = ucur[r];
+                float* row = A + r * LD;
+                for (int c = 4 * lane; c < i; c += 256) {
+                    float4 x = *reinterpret_cast<float4*>(row + c);
+                    const float4 t = *reinterpret_cast<const float4*>(wf + c);
+                    x.x -= ur * t.x;
+                    x.y -= ur * t.y;
+                    x.z -= ur * t.z;
+                    x.w -= ur * t.w;
+                    *reinterpret_cast<float4*>(row + c) = x;
+                }
+            }
         }
-        __syncthreads();
-        for (int idx = tid; idx < i * i; idx += TR_T) {
-            const int r = idx / i, c = idx - r * i;
-            A[r * LD + c] = (float)((double)A[r * LD + c] - vu[r] * vp[c]);
+        // next step's u into the other buffer (loaded at the top of this step)
+        if (i + 1 < n && tid < ((i + 1 + 3) & ~3)) {
+            vub[(i + 1) & 1][tid] = (double)unext;
+            ufb[(i + 1) & 1][tid] = unext;
         }
         __syncthreads();
     }
-    // Q to the slot (row-major n x n)
-    for (int idx = tid; idx < n * n; idx += TR_T) {
-        const int i = idx / n, j = idx - i * n;
-        slot[idx] = A[i * LD + j];
+    for (int i = wave; i < n; i += TA_W)
+        for (int j = lane; j < n; j += 64) slot[i * n + j] = A[i * LD + j];
+    if (a.stats && tid == 0) {
+        const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+        atomicAdd(&a.stats[4], tA1 - tA0);
+        atomicAdd(&a.stats[5], tA2 - tA1);
+        atomicAdd(&a.stats[6], t3 - tA2);
+        atomicAdd(&a.stats[7], (unsigned long long)n);
     }
 }
 
 // ---- B: batched tql2 with rotation recording (one lane per user) ------------------------------
-__global__ __launch_bounds__(64) void tri_ql_kernel(TriArgs a) {
-    const uint32_t jj = blockIdx.x * 64 + threadIdx.x;
-    if (jj >= a.count) return;
+// d and e live in LDS, interleaved by lane ([i][lane]) so the lanes' same-index accesses are
+// conflict-free.  JAMA's per-iteration shift d[i] -= h (i >= l + 2) is kept lazy: those
+// entries are stored as d + f (f = the accumulated shift) and read as stored - f.
+__global__ __launch_bounds__(64) void tri_ql_kernel(TriArgs a, int ub, int kmax) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    double* D = reinterpret_cast<double*>(smem_raw);   // [kmax][ub]
+    double* E = D + (size_t)kmax * ub;
+    const int lane = threadIdx.x;
+    const uint32_t jj = blockIdx.x * ub + lane;   // group launch: first == group_first
+    const bool act = lane < ub && jj < a.count;
+    if (!act) return;
     const uint32_t u = a.order[a.first + jj];
     const uint64_t base = a.item_off[u];
     const int n = (int)(a.item_off[u + 1] - base);
-    if (n <= 0) return;
-    double* d = a.dd + base;
-    double* e = a.ee + base;
+    if (n <= 0) {
+        a.flag[jj] = 0;
+        a.n_iter[jj] = 0;
+        return;
+    }
+    auto dR = [&](int i) -> double& { return D[(size_t)i * ub + lane]; };
+    auto eR = [&](int i) -> double& { return E[(size_t)i * ub + lane]; };
+    const double* gd = a.dd + base;
+    const double* ge = a.ee + base;
+    for (int i = 0; i < n; ++i) {
+        dR(i) = gd[i];
+        eR(i) = (i + 1 < n) ? ge[i + 1] : 0.0;   // tql2 entry shift e[i-1] = e[i]
+    }
     const size_t pj = 2 * (size_t)(a.first + jj);
     float2* rot = a.rot + a.rot_off[pj];
     const uint64_t rot_cap = a.rot_off[pj + 1] - a.rot_off[pj];
@@ -284,14 +410,16 @@ __global__ __launch_bounds__(64) void tri_ql_kernel(TriArgs a) {
     const uint64_t hdr_cap = a.hdr_off[pj + 1] - a.hdr_off[pj];
     uint64_t nrot = 0, nh = 0;
     bool overflow = false;
-    for (int i = 1; i < n; ++i) e[i - 1] = e[i];
-    e[n - 1] = 0.0;
-    double f = 0.0, tst1 = 0.0;
+    double f = 0.0, tst1 = 0.0;   // f: JAMA's accumulated shift; D[i >= l+2] hold d + f
     const double eps = 2.220446049250313e-16;
+    // entries are stored "lazy" (d + f) from the start (f = 0)
     for (int l = 0; l < n && !overflow; ++l) {
-        tst1 = fmax(tst1, fabs(d[l]) + fabs(e[l]));
+        // materialise d[l], d[l+1] (explicit while l is current)
+        dR(l) -= f;
+        if (l + 1 < n) dR(l + 1) -= f;
+        tst1 = fmax(tst1, fabs(dR(l)) + fabs(eR(l)));
         int m = l;
-        while (m < n && !(fabs(e[m]) <= eps * tst1)) ++m;
+        while (m < n && !(fabs(eR(m)) <= eps * tst1)) ++m;
         if (m > l) {
             int iter = 0;
             do {
@@ -300,50 +428,62 @@ __global__ __launch_bounds__(64) void tri_ql_kernel(TriArgs a) {
                     overflow = true;
                     break;
                 }
-                const double g0 = d[l];
-                double p = (d[l + 1] - g0) / (2.0 * e[l]);
+                const double g0 = dR(l);
+                const double el = eR(l);
+                double p = (dR(l + 1) - g0) / (2.0 * el);
                 double r = sqrt(p * p + 1.0);
                 if (p < 0) r = -r;
-                d[l] = e[l] / (p + r);
-                d[l + 1] = e[l] * (p + r);
-                const double dl1 = d[l + 1];
-                const double h0 = g0 - d[l];
-                for (int i = l + 2; i < n; ++i) d[i] -= h0;
-                f += h0;
-                p = d[m];
+                const double dl = el / (p + r);
+                dR(l) = dl;
+                dR(l + 1) = el * (p + r);
+                const double dl1 = dR(l + 1);
+                const double h0 = g0 - dl;
+                f += h0;   // d[i >= l+2] -= h0, lazily
+                // d_at(i): explicit for i <= l+1, stored - f beyond
+                p = (m >= l + 2) ? dR(m) - f : dR(m);
                 double c = 1.0, c2 = 1.0, c3 = 1.0, s = 0.0, s2 = 0.0;
-                const double el1 = e[l + 1];
-                double di = d[m - 1 >= 0 ? m - 1 : 0], ei = e[m - 1 >= 0 ? m - 1 : 0];
+                const double el1 = eR(l + 1);
                 for (int i = m - 1; i >= l; --i) {
-                    const double di_n = i > l ? d[i - 1] : 0.0, ei_n = i > l ? e[i - 1] : 0.0;  // prefetch
+                    const double ei = eR(i);
+                    const double di = (i >= l + 2) ? dR(i) - f : dR(i);
                     c3 = c2;
                     c2 = c;
                     s2 = s;
                     const double g = c * ei;
                     const double h = c * p;
                     r = sqrt(p * p + ei * ei);
-                    e[i + 1] = s * r;
+                    eR(i + 1) = s * r;
                     const double ri = 1.0 / r;
                     s = ei * ri;
                     c = p * ri;
                     p = c * di - s * g;
-                    d[i + 1] = h + s * (c * g + s * di);
+                    const double dn = h + s * (c * g + s * di);
+                    dR(i + 1) = (i + 1 >= l + 2) ? dn + f : dn;
                     rot[nrot + (m - 1 - i)] = make_float2((float)c, (float)s);
-                    di = di_n;
-                    ei = ei_n;
                 }
                 hdr[nh++] = make_int2(l, m);
                 nrot += (uint64_t)(m - l);
-                p = -s * s2 * c3 * el1 * e[l] / dl1;
-                e[l] = s * p;
-                d[l] = c * p;
-            } while (fabs(e[l]) > eps * tst1 && iter < 60);
+                p = -s * s2 * c3 * el1 * eR(l) / dl1;
+                eR(l) = s * p;
+                dR(l) = c * p;
+            } while (fabs(eR(l)) > eps * tst1 && iter < 60);
         }
-        d[l] += f;
-        e[l] = 0.0;
+        dR(l) += f;   // eigenvalue l (JAMA: d[l] += f)
+        eR(l) = 0.0;
+        // d[l+1] goes back to lazy storage for the next l? It becomes the new d[l]
+        // (explicit) -- re-lazify it so the materialisation at the loop head is uniform.
+        if (l + 1 < n) dR(l + 1) += f;
     }
+    double* od = a.dd + base;
+    for (int i = 0; i < n; ++i) od[i] = dR(i);
     a.flag[jj] = overflow ? 1 : 0;
     a.n_iter[jj] = (int)nh;
+    if (a.stats) {
+        atomicAdd(&a.stats[0], (unsigned long long)nrot);
+        atomicAdd(&a.stats[1], (unsigned long long)nh);
+        atomicAdd(&a.stats[2], overflow ? 1ull : 0ull);
+        atomicAdd(&a.stats[3], 1ull);
+    }
 }
 
 // ---- C: rotations applied to Q, ordering, output ---------------------------------------------
@@ -354,21 +494,22 @@ __global__ __launch_bounds__(TR_T) void tri_apply_kernel(TriArgs a) {
     const uint32_t u = a.order[a.first + jj];
     const uint64_t base = a.item_off[u];
     const int n = (int)(a.item_off[u + 1] - base);
-    if (n <= 0 || a.flag[jj]) return;
+    const uint32_t js = a.first + jj - a.group_first;
+    if (n <= 0 || a.flag[js]) return;
     const int LD = tri_ld(n);
     float* V = reinterpret_cast<float*>(smem_raw);                       // n x LD
-    float2* cs = reinterpret_cast<float2*>(V + ((n * LD + 1) & ~1));    // [TR_Q][n]
-    int* perm = reinterpret_cast<int*>(cs + TR_Q * TR_NMAX);
+    float2* cs = reinterpret_cast<float2*>(V + ((n * LD + 1) & ~1));    // [TR_Q][TR_NMAX]
+    double* ev = reinterpret_cast<double*>(cs + TR_Q * TR_NMAX);        // eigenvalues
+    int* perm = reinterpret_cast<int*>(ev + TR_NMAX);
     float* sgn = reinterpret_cast<float*>(perm + TR_NMAX);
     int* sh = reinterpret_cast<int*>(sgn + TR_NMAX);                    // [2 * TR_Q + 4]
     float* slot = a.evecs + a.evec_off[u];
-    for (int idx = tid; idx < n * n; idx += TR_T) {
-        const int i = idx / n, j = idx - i * n;
-        V[i * LD + j] = slot[idx];
-    }
+    for (int i = wave; i < n; i += TR_W)
+        for (int j = lane; j < n; j += 64) V[i * LD + j] = slot[i * n + j];
+    for (int i = tid; i < n; i += TR_T) ev[i] = a.dd[base + i];
     const float2* rot = a.rot + a.rot_off[2 * (size_t)(a.first + jj)];
     const int2* hdr = a.hdr + a.hdr_off[2 * (size_t)(a.first + jj)];
-    const int n_it = a.n_iter[jj];
+    const int n_it = a.n_iter[js];
     uint64_t rpos = 0;
     for (int b0 = 0; b0 < n_it; b0 += TR_Q) {
         const int nseq = min(TR_Q, n_it - b0);
@@ -379,26 +520,34 @@ __global__ __launch_bounds__(TR_T) void tri_apply_kernel(TriArgs a) {
             sh[TR_Q + tid] = lm.y;
         }
         __syncthreads();
-        // stage: sequence t covers positions [l_t, m_t - 1], stored from m_t - 1 down
+        int L = n, Mx = 0;
+        uint64_t offs[TR_Q];
         {
             uint64_t off = rpos;
-            for (int t = 0; t < nseq; ++t) {
-                const int l = sh[t], m = sh[TR_Q + t];
-                for (int p = tid; p < n; p += TR_T) {
-                    float2 v = make_float2(1.0f, 0.0f);
-                    if (p >= l && p < m) v = rot[off + (m - 1 - p)];
-                    cs[t * TR_NMAX + p] = v;
+#pragma unroll
+            for (int t = 0; t < TR_Q; ++t) {
+                offs[t] = off;
+                if (t < nseq) {
+                    L = min(L, sh[t]);
+                    Mx = max(Mx, sh[TR_Q + t]);
+                    off += (uint64_t)(sh[TR_Q + t] - sh[t]);
                 }
-                off += (uint64_t)(m - l);
             }
             rpos = off;
         }
-        __syncthreads();
-        int L = n, Mx = 0;
-        for (int t = 0; t < nseq; ++t) {
-            L = min(L, sh[t]);
-            Mx = max(Mx, sh[TR_Q + t]);
+        // stage [t][pp]: rotation of sequence t at position pp, identity outside [l_t, m_t);
+        // all 8 loads of a thread are issued before the LDS stores
+        for (int pp = tid; pp < n; pp += TR_T) {
+            float2 v[TR_Q];
+#pragma unroll
+            for (int t = 0; t < TR_Q; ++t) {
+                const int l = t < nseq ? sh[t] : 0, m = t < nseq ? sh[TR_Q + t] : 0;
+                v[t] = (pp >= l && pp < m) ? rot[offs[t] + (m - 1 - pp)] : make_float2(1.0f, 0.0f);
+            }
+#pragma unroll
+            for (int t = 0; t < TR_Q; ++t) cs[t * TR_NMAX + pp] = v[t];
         }
+        __syncthreads();
         const int r = tid;
         if (r < n) {
             float* row = V + r * LD;
@@ -406,9 +555,85 @@ __global__ __launch_bounds__(TR_T) void tri_apply_kernel(TriArgs a) {
             carry[0] = row[Mx];
 #pragma unroll
             for (int t = 1; t < TR_Q; ++t) carry[t] = 0.0f;
-            for (int tau = Mx - 1; tau >= L - nseq; --tau) {
-                float val = tau >= L ? row[tau] : 0.0f;
-                bool ok = tau >= L;
+            int tau = Mx - 1;
+            // head: sequences t >= 1 pick up their first carry (pp == Mx)
+            for (; tau >= L && tau > Mx - nseq; --tau) {
+                float val = row[tau];
+                bool ok = true;
+#pragma unroll
+                for (int t = 0; t < TR_Q; ++t) {
+                    if (t < nseq) {
+                        const int pp = tau + t;
+                        if (pp > Mx) {
+                            ok = false;
+                        } else if (pp == Mx) {
+                            if (ok) carry[t] = val;
+                            ok = false;
+                        } else {
+                            const float2 q = cs[t * TR_NMAX + pp];
+                            const float out = q.y * val + q.x * carry[t];
+                            carry[t] = q.x * val - q.y * carry[t];
+                            val = out;
+                        }
+                    }
+                }
+                if (ok) row[tau + nseq] = val;
+            }
+            // interior: every sequence rotates (L <= tau, tau + nseq - 1 < Mx)
+            if (nseq == TR_Q) {
+                // 4 positions per iteration: rotation (tau, t) depends on (tau, t-1) and
+                // (tau+1, t) only, so the unrolled block runs as a wavefront
+                for (; tau - 3 >= L; tau -= 4) {
+                    float2 q[4][TR_Q];
+                    float x[4];
+#pragma unroll
+                    for (int s4 = 0; s4 < 4; ++s4) {
+                        x[s4] = row[tau - s4];
+#pragma unroll
+                        for (int t = 0; t < TR_Q; ++t) q[s4][t] = cs[t * TR_NMAX + tau - s4 + t];
+                    }
+#pragma unroll
+                    for (int s4 = 0; s4 < 4; ++s4) {
+                        float val = x[s4];
+#pragma unroll
+                        for (int t = 0; t < TR_Q; ++t) {
+                            const float out = q[s4][t].y * val + q[s4][t].x * carry[t];
+                            carry[t] = q[s4][t].x * val - q[s4][t].y * carry[t];
+                            val = out;
+                        }
+                        row[tau - s4 + TR_Q] = val;
+                    }
+                }
+                for (; tau >= L; --tau) {
+                    float val = row[tau];
+#pragma unroll
+                    for (int t = 0; t < TR_Q; ++t) {
+                        const float2 q = cs[t * TR_NMAX + tau + t];
+                        const float out = q.y * val + q.x * carry[t];
+                        carry[t] = q.x * val - q.y * carry[t];
+                        val = out;
+                    }
+                    row[tau + TR_Q] = val;
+                }
+            } else {
+                for (; tau >= L; --tau) {
+                    float val = row[tau];
+#pragma unroll
+                    for (int t = 0; t < TR_Q; ++t) {
+                        if (t < nseq) {
+                            const float2 q = cs[t * TR_NMAX + tau + t];
+                            const float out = q.y * val + q.x * carry[t];
+                            carry[t] = q.x * val - q.y * carry[t];
+                            val = out;
+                        }
+                    }
+                    row[tau + nseq] = val;
+                }
+            }
+            // tail: flush (pp == L - 1 emits the carry), tau = L-1 .. L-nseq
+            for (; tau >= L - nseq; --tau) {
+                float val = 0.0f;
+                bool ok = false;
 #pragma unroll
                 for (int t = 0; t < TR_Q; ++t) {
                     if (t < nseq) {
@@ -437,22 +662,21 @@ __global__ __launch_bounds__(TR_T) void tri_apply_kernel(TriArgs a) {
     }
     __syncthreads();
     // ascending order of the eigenvalues (ties by index), signs, lim, output
-    const double* ev = a.dd + base;
     for (int j = tid; j < n; j += TR_T) {
         const double lj = ev[j];
         int rank = 0;
+        double s = 0.0;
         for (int i = 0; i < n; ++i) {
             const double li = ev[i];
             rank += (li < lj) || (li == lj && i < j);
+            s += (double)V[i * LD + j];
         }
         perm[rank] = j;
-        double s = 0.0;
-        for (int i = 0; i < n; ++i) s += (double)V[i * LD + j];
         sgn[j] = s < 0.0 ? -1.0f : 1.0f;
     }
     __syncthreads();
     if (tid == 0) {
-        const float smm = a.smm[jj];
+        const float smm = a.smm[js];
         int lim;
         for (lim = 0; lim < n; ++lim)
             if (ev[perm[lim]] > (double)smm) break;   // (:186-188)
@@ -463,56 +687,65 @@ __global__ __launch_bounds__(TR_T) void tri_apply_kernel(TriArgs a) {
     __syncthreads();
     const int m = sh[2 * TR_Q];
     for (int r = tid; r < m && r < n; r += TR_T) a.evals[base + r] = (float)ev[perm[r]];
-    for (int idx = tid; idx < n * m; idx += TR_T) {
-        const int i = idx / m, r = idx - i * m;
-        float v = 0.0f;
-        if (r < n) {
-            const int j = perm[r];
-            v = V[i * LD + j] * sgn[j];
+    for (int i = wave; i < n; i += TR_W)
+        for (int r = lane; r < m; r += 64) {
+            float v = 0.0f;
+            if (r < n) {
+                const int j = perm[r];
+                v = V[i * LD + j] * sgn[j];
+            }
+            slot[i * m + r] = v;
         }
-        slot[idx] = v;
-    }
-    (void)lane;
-    (void)wave;
 }
 
 size_t tri_lds_a(int kmax) {
-    return sizeof(float) * (size_t)((kmax * tri_ld(kmax) + 1) & ~1) + sizeof(double) * (3 * TR_NMAX + 8) +
-           sizeof(uint32_t) * TR_NMAX;
+    return sizeof(float) * (size_t)kmax * tri_lda(kmax) + sizeof(double) * 7 * TR_NMAX + sizeof(float) * 3 * TR_NMAX;
 }
 size_t tri_lds_c(int kmax) {
     return sizeof(float) * (size_t)((kmax * tri_ld(kmax) + 1) & ~1) + sizeof(float2) * TR_Q * TR_NMAX +
-           sizeof(int) * TR_NMAX + sizeof(float) * TR_NMAX + sizeof(int) * (2 * TR_Q + 4);
+           sizeof(double) * TR_NMAX + sizeof(int) * TR_NMAX + sizeof(float) * TR_NMAX + sizeof(int) * (2 * TR_Q + 4);
 }
+// kernel B: users per 64-lane block so that D and E ([kmax][ub] fp64 each) fit 150 KB
+int tri_ql_ub(int kmax) { return std::max(1, std::min(64, (int)(150 * 1024 / (16 * std::max(kmax, 1))))); }
 
 }  // namespace
 
 // Rotation-record budget per user (float2 units) and header budget (QL iterations).
-static inline uint64_t tri_rot_cap(uint64_t k) { return 3 * k * k + 64; }
-static inline uint64_t tri_hdr_cap(uint64_t k) { return 4 * k + 16; }
+static inline uint64_t tri_rot_cap(uint64_t k) { return (3 * k * k) / 2 + 64; }
+static inline uint64_t tri_hdr_cap(uint64_t k) { return 3 * k + 16; }
 
 int cf_tri_prepare(cf_ctx* ctx, cf_plan* plan, const uint64_t* item_off) {
-    // Chunks: plan-order ranges inside one LDS bucket whose QL records fit the budget.
-    // Per plan index j: [start, end) of its rotation / header records, chunk-relative,
-    // stored at 2j and 2j + 1.
-    const uint64_t budget = (uint64_t)1536 << 20;   // bytes of rotation records per chunk
+    // Groups: plan-order ranges (across LDS buckets) whose QL records fit the budget; kernel
+    // B runs once per group.  Parts: a group's sub-range inside one bucket (kernels A, C and
+    // the Jacobi fallback are per bucket).  Per plan index j: [start, end) of its records,
+    // group-relative, at 2j and 2j + 1.
+    const uint64_t budget = (uint64_t)8 << 30;   // bytes of rotation records per group
     plan->tri_chunks.clear();
+    plan->tri_groups.clear();
     plan->n_entries = plan->n_users ? item_off[plan->n_users] : 0;
     std::vector<uint64_t> r2(2 * (size_t)plan->n_users + 2, 0), h2(2 * (size_t)plan->n_users + 2, 0);
+    uint64_t acc = 0, acch = 0;
+    bool open = false;
     for (const cf_bucket& b : plan->buckets) {
         if (b.emax == kSpillBucket || b.count == 0) continue;
         uint32_t start = b.first;
-        uint64_t acc = 0, acch = 0;
         for (uint32_t j = b.first; j < b.first + b.count; ++j) {
             const uint32_t u = plan->h_order[j];
             const uint64_t k = item_off[u + 1] - item_off[u];
             const uint64_t rc = tri_rot_cap(k), hc = tri_hdr_cap(k);
-            if (j > start && (acc + rc) * sizeof(float2) > budget) {
-                plan->tri_chunks.push_back({b.emax, start, j - start, b.kmax});
-                start = j;
+            if (!open || (acc + rc) * sizeof(float2) > budget) {
+                if (open && j > start) {
+                    plan->tri_chunks.push_back({b.emax, start, j - start, b.kmax, (uint32_t)plan->tri_groups.size() - 1});
+                    start = j;
+                }
+                plan->tri_groups.push_back({j, 0, 0});
                 acc = 0;
                 acch = 0;
+                open = true;
             }
+            cf_tri_group& g = plan->tri_groups.back();
+            g.count = j + 1 - g.first;
+            g.kmax = std::max<uint32_t>(g.kmax, (uint32_t)k);
             r2[2 * (size_t)j] = acc;
             h2[2 * (size_t)j] = acch;
             acc += rc;
@@ -522,9 +755,10 @@ int cf_tri_prepare(cf_ctx* ctx, cf_plan* plan, const uint64_t* item_off) {
             plan->tri_rot_max = std::max(plan->tri_rot_max, acc);
             plan->tri_hdr_max = std::max(plan->tri_hdr_max, acch);
         }
-        plan->tri_chunks.push_back({b.emax, start, b.first + b.count - start, b.kmax});
+        plan->tri_chunks.push_back({b.emax, start, b.first + b.count - start, b.kmax,
+                                    (uint32_t)plan->tri_groups.size() - 1});
     }
-    for (const auto& c : plan->tri_chunks) plan->tri_users_max = std::max(plan->tri_users_max, c.count);
+    for (const auto& g : plan->tri_groups) plan->tri_users_max = std::max(plan->tri_users_max, g.count);
     if (plan->n_users) {
         CF_HIP_CHECK(ctx, hipMalloc(&plan->d_tri_roff, sizeof(uint64_t) * r2.size()));
         CF_HIP_CHECK(ctx, hipMalloc(&plan->d_tri_hoff, sizeof(uint64_t) * h2.size()));
@@ -537,7 +771,8 @@ int cf_tri_prepare(cf_ctx* ctx, cf_plan* plan, const uint64_t* item_off) {
 static int tri_scratch(cf_ctx* ctx, const cf_plan* plan, TriArgs& a) {
     const size_t ne = std::max<uint64_t>(plan->n_entries, 1), nu = std::max<uint32_t>(plan->tri_users_max, 1);
     const size_t need = 2 * ne * sizeof(double) + nu * (sizeof(float) + 2 * sizeof(int)) + 256 +
-                        (plan->tri_rot_max + 1) * sizeof(float2) + (plan->tri_hdr_max + 1) * sizeof(int2);
+                        (plan->tri_rot_max + 1) * sizeof(float2) + (plan->tri_hdr_max + 1) * sizeof(int2) +
+                        8 * sizeof(unsigned long long);
     if (need > ctx->tri_bytes) {
         if (ctx->d_tri) (void)hipFree(ctx->d_tri);
         ctx->d_tri = nullptr;
@@ -545,8 +780,11 @@ static int tri_scratch(cf_ctx* ctx, const cf_plan* plan, TriArgs& a) {
         if (hipMalloc(&ctx->d_tri, need) != hipSuccess)
             return cf_set_error(ctx, CF_ENOMEM, "tridiagonal eigen scratch (" + std::to_string(need) + " bytes)");
         ctx->tri_bytes = need;
+        CF_HIP_CHECK(ctx, hipMemset(ctx->d_tri, 0, 8 * sizeof(unsigned long long)));
     }
     char* p = static_cast<char*>(ctx->d_tri);
+    a.stats = ctx->tri_debug ? reinterpret_cast<unsigned long long*>(p) : nullptr;
+    p += 8 * sizeof(unsigned long long);
     a.dd = reinterpret_cast<double*>(p);
     p += ne * sizeof(double);
     a.ee = reinterpret_cast<double*>(p);
@@ -566,7 +804,7 @@ static int tri_scratch(cf_ctx* ctx, const cf_plan* plan, TriArgs& a) {
 int cf_launch_eigen_tri(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,
                         const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals, float* d_evecs,
                         hipStream_t stream) {
-    if (plan->tri_chunks.empty()) return CF_OK;
+    if (plan->tri_groups.empty()) return CF_OK;
     TriArgs a{};
     CF_TRY(tri_scratch(ctx, plan, a));
     a.order = plan->d_order;
@@ -587,21 +825,54 @@ int cf_launch_eigen_tri(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)tri_lds_a(TR_NMAX)));
         CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)tri_apply_kernel,
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)tri_lds_c(TR_NMAX)));
+        CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)tri_ql_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              150 * 1024));
         configured = true;
     }
-    for (const cf_tri_chunk& c : plan->tri_chunks) {
-        a.first = c.first;
-        a.count = c.count;
-        const int kmax = std::max<int>(1, (int)c.kmax);
-        hipLaunchKernelGGL(tri_reduce_kernel, dim3(c.count), dim3(TR_T), tri_lds_a(kmax), stream, a);
+    for (uint32_t gi = 0; gi < plan->tri_groups.size(); ++gi) {
+        const cf_tri_group& g = plan->tri_groups[gi];
+        a.group_first = g.first;
+        for (const cf_tri_chunk& c : plan->tri_chunks) {
+            if (c.group != gi) continue;
+            a.first = c.first;
+            a.count = c.count;
+            hipLaunchKernelGGL(tri_reduce_kernel, dim3(c.count), dim3(TA_T), tri_lds_a(std::max<int>(1, c.kmax)),
+                               stream, a);
+            CF_HIP_CHECK(ctx, hipGetLastError());
+        }
+        a.first = g.first;
+        a.count = g.count;
+        const int kmax = std::max<int>(1, (int)g.kmax);
+        const int ub = tri_ql_ub(kmax);
+        hipLaunchKernelGGL(tri_ql_kernel, dim3((g.count + ub - 1) / ub), dim3(64), (size_t)16 * kmax * ub, stream, a,
+                           ub, kmax);
         CF_HIP_CHECK(ctx, hipGetLastError());
-        hipLaunchKernelGGL(tri_ql_kernel, dim3((c.count + 63) / 64), dim3(64), 0, stream, a);
-        CF_HIP_CHECK(ctx, hipGetLastError());
-        hipLaunchKernelGGL(tri_apply_kernel, dim3(c.count), dim3(TR_T), tri_lds_c(kmax), stream, a);
-        CF_HIP_CHECK(ctx, hipGetLastError());
-        // users whose QL record overflowed: recomputed by the Jacobi kernel
-        CF_TRY(cf_launch_eigen_flagged(ctx, plan, c.emax, c.first, c.count, a.flag, d_item_off, d_items, d_evec_off,
-                                       d_m, d_sigs, d_evals, d_evecs, stream));
+        for (const cf_tri_chunk& c : plan->tri_chunks) {
+            if (c.group != gi) continue;
+            a.first = c.first;
+            a.count = c.count;
+            hipLaunchKernelGGL(tri_apply_kernel, dim3(c.count), dim3(TR_T), tri_lds_c(std::max<int>(1, c.kmax)),
+                               stream, a);
+            CF_HIP_CHECK(ctx, hipGetLastError());
+            // users whose QL record overflowed: recomputed by the Jacobi kernel
+            CF_TRY(cf_launch_eigen_flagged(ctx, plan, c.emax, c.first, c.count, a.flag + (c.first - g.first),
+                                           d_item_off, d_items, d_evec_off, d_m, d_sigs, d_evals, d_evecs, stream));
+        }
+    }
+    return CF_OK;
+}
+
+int cf_debug_tri(cf_ctx* ctx, int enable, uint64_t* out4) {   // out4: 8 slots
+    if (!ctx) return CF_EINVAL;
+    CF_TRY(set_device(ctx));
+    ctx->tri_debug = enable != 0;
+    if (out4) {
+        for (int i = 0; i < 8; ++i) out4[i] = 0;
+        if (ctx->d_tri) {
+            CF_HIP_CHECK(ctx, hipDeviceSynchronize());
+            CF_HIP_CHECK(ctx, hipMemcpy(out4, ctx->d_tri, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+            CF_HIP_CHECK(ctx, hipMemset(ctx->d_tri, 0, 8 * sizeof(uint64_t)));
+        }
     }
     return CF_OK;
 }

@@ -36,7 +36,8 @@ struct cf_ctx {
     // tridiagonal eigen path scratch (T, QL records), grown on demand; eigen method
     void* d_tri = nullptr;
     size_t tri_bytes = 0;
-    int eigen_method = CF_EIGEN_TRIDIAG;
+    int eigen_method = CF_EIGEN_JACOBI;
+    bool tri_debug = false;
     // knn2 stage events (plane build start, GEMM start, GEMM end) of the last launch.
     hipEvent_t knn_ev[3] = {nullptr, nullptr, nullptr};
     int knn_path = 0;   // 1 code plane, 2 three int8 planes, 3 fp32 planes
@@ -53,8 +54,14 @@ struct cf_bucket {
     uint32_t kmax = 0;         // largest k in the bucket
 };
 
-struct cf_tri_chunk {
+struct cf_tri_chunk {   // a group's sub-range inside one LDS bucket
     int emax;
+    uint32_t first;
+    uint32_t count;
+    uint32_t kmax;
+    uint32_t group;
+};
+struct cf_tri_group {   // plan-order range sharing one QL-record buffer and one kernel-B launch
     uint32_t first;
     uint32_t count;
     uint32_t kmax;
@@ -65,6 +72,7 @@ struct cf_plan {
     uint64_t n_entries = 0;
     // tridiagonal eigen path (cf_eigen_tri.hip): chunks and per-user QL record offsets
     std::vector<cf_tri_chunk> tri_chunks;
+    std::vector<cf_tri_group> tri_groups;
     uint64_t tri_rot_max = 0, tri_hdr_max = 0;
     uint32_t tri_users_max = 0;
     uint64_t* d_tri_roff = nullptr;

@@ -58,8 +58,8 @@ int cf_version(void);
 int cf_create(int device, cf_ctx** out);
 void cf_destroy(cf_ctx* ctx);
 const char* cf_last_error(const cf_ctx* ctx);
-/* Eigensolver of the k <= CF_MAX_K users: CF_EIGEN_TRIDIAG (default; Householder +
- * batched QL, cf_eigen_tri.hip) or CF_EIGEN_JACOBI (one-sided Jacobi in LDS). */
+/* Eigensolver of the k <= CF_MAX_K users: CF_EIGEN_JACOBI (default; one-sided Jacobi in
+ * LDS, cf_eigen.hip) or CF_EIGEN_TRIDIAG (Householder + batched QL, cf_eigen_tri.hip). */
 #define CF_EIGEN_TRIDIAG 0
 #define CF_EIGEN_JACOBI 1
 int cf_set_eigen_method(cf_ctx* ctx, int method);
@@ -75,6 +75,11 @@ int cf_debug_stats(cf_ctx* ctx, int enable, uint64_t* out8);
  * assembly, tridiagonalisation, Q accumulation, QL (total), QL rotation generation
  * (serial part), QL iterations, output} cycles. */
 int cf_debug_spill(cf_ctx* ctx, int enable, uint64_t* out8);
+/* Diagnostics of the tridiagonal eigen path: enable != 0 makes its kernels count;
+ * out8 (optional) receives and resets {rotations, QL iterations, record overflows (users
+ * recomputed by Jacobi), users, then thread-0 s_memtime cycles of the reduction kernel:
+ * assembly, Householder steps, Q accumulation, and the sum of k}. */
+int cf_debug_tri(cf_ctx* ctx, int enable, uint64_t* out8);
 /* Diagnostics: predictor phase totals in s_memtime cycles.  out16[0..7], thread 0 of
  * each block: {per-user setup, basis, fast-path ratings, block-wide ratings} cycles,
  * the number of ratings taken by the fast path and by the block-wide paths, then the

@@ -17,11 +17,11 @@ KS = [1, 2, 3, 5, 8, 15, 16, 17, 31, 32, 33, 47, 64, 65, 100, 127, 128, 129, 150
 
 @pytest.fixture(params=["tridiag", "jacobi"])
 def eig_ctx(gpu_ctx, request):
-    """Both eigensolvers of the k <= 192 path: Householder + batched QL (default) and the
-    one-sided Jacobi kernel."""
+    """Both eigensolvers of the k <= 192 path: the one-sided Jacobi kernel (default) and
+    Householder + batched QL."""
     gpu_ctx.set_eigen_method(request.param)
     yield gpu_ctx
-    gpu_ctx.set_eigen_method("tridiag")
+    gpu_ctx.set_eigen_method("jacobi")
 
 
 def _check_batch(ctx, W, item_off, items, label):
