@@ -95,6 +95,7 @@ __host__ __device__ constexpr int tri_ld(int n) { return n | 1; }   // odd row s
 // the symmetry (A u)_c = sum_q A[q][c] u_q: thread (c, part) sums a quarter of the rows.
 constexpr int TA_T = 1024;
 constexpr int TA_W = TA_T / 64;
+constexpr int TR_SLOTS = (TR_NMAX + TA_W - 1) / TA_W;   // matrix rows per wave (12)
 
 __host__ __device__ constexpr int tri_lda(int n) {
     return ((n + 3) & ~3) + ((4 - (((n + 3) & ~3) & 63)) & 63);
@@ -125,9 +126,6 @@ __global__ __launch_bounds__(TA_T) void tri_reduce_kernel(TriArgs a) {
     // part + 4N: the second fp64 u buffer.  During the assembly part[0, N) holds s_i,
     // part + 2N the item ids and part + 3N the per-wave sig maxima.
     double* red = part + 3 * TR_NMAX;
-    float* uf = reinterpret_cast<float*>(part + 5 * TR_NMAX);          // u (fp32)
-    float* wf = uf + TR_NMAX;                                          // w (fp32)
-    float* s_uf2 = wf + TR_NMAX;                                       // u (fp32), 2nd buffer
     uint32_t* s_item = reinterpret_cast<uint32_t*>(part + 2 * TR_NMAX);
 
     for (int i = tid; i < n; i += TA_T) s_item[i] = a.items[base + i];
@@ -178,194 +176,206 @@ __global__ __launch_bounds__(TA_T) void tri_reduce_kernel(TriArgs a) {
         for (int j = i + 1 + lane; j < n; j += 64) A[i * LD + j] = A[j * LD + i];
     __syncthreads();
 
-    // ---- Householder reduction: step i annihilates A[i][0 .. i-2] --------------------------
-    // Three barriers per step: (1) partial sums of A u, (2) w = p - K u (one wave), (3) the
-    // rank-2 update.  The row of the next step is finished by the wave that owns it in (3),
-    // which then forms the next reflector (scale, h, u) right away into the other buffer.
-    if (a.stats && tid == 0) tA1 = __builtin_amdgcn_s_memtime();
+    // ---- Householder reduction with the matrix in registers -------------------------------
+    // Row r lives in wave r % 16, slot r / 16; lane holds columns lane, lane + 64, lane + 128:
+    // ra[j][t] = A[16 j + wave][lane + 64 t] (36 registers; 16 waves x 12 slots x 192 columns
+    // cover k <= 192).  A step is then: per-wave partials of A u from registers (LDS 16 x 192),
+    // one wave reduces them to w = p - K u, every wave applies the rank-2 update to its own
+    // registers, and the owner wave of the next row forms the next reflector straight from its
+    // registers.  Three barriers per step and no LDS round trip of the matrix.
+    float ra[TR_SLOTS][3];
+#pragma unroll
+    for (int j = 0; j < TR_SLOTS; ++j)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int r = 16 * j + wave, c = lane + 64 * t;
+            ra[j][t] = (r < n && c < n) ? A[r * LD + c] : 0.0f;
+        }
+    __syncthreads();   // A (LDS) is dead from here: the region is reused below
+    float* P = reinterpret_cast<float*>(smem_raw);        // [16][TR_NMAX] partial sums
+    float* Ub = P + TA_W * TR_NMAX;                        // [2][TR_NMAX] reflectors (fp32)
+    float* Wv = Ub + 2 * TR_NMAX;                          // [TR_NMAX] w / t
+    double* hh2 = reinterpret_cast<double*>(Wv + TR_NMAX); // [TR_NMAX] h_i
+    double* Kw = hh2 + TR_NMAX;                            // [TA_W] per-wave u^T A u
+    double* e2 = Kw + TA_W;                                // [TR_NMAX] off-diagonal of T
+    // The reflector rows go to the evecs slot (global) and are read back for Q.  (Keeping them
+    // packed in LDS failed the k = 15/16 parity cases and was not faster; not pursued.)
     double* dd = a.dd + base;
     double* ee = a.ee + base;
-    const int pc = tid & 255, pq = tid >> 8;   // (column, quarter) of the matrix-vector products
-    double* vub[2] = {vu, part + 4 * TR_NMAX};  // fp64 u, double-buffered by step parity
-    float* ufb[2] = {uf, s_uf2};
-    // reflector of row i by one wave: u into buffer (i & 1), h_i and e_i
+    float* slot = a.evecs + a.evec_off[u];
+    if (a.stats && tid == 0) tA1 = __builtin_amdgcn_s_memtime();
+    // reflector of row i by its owner wave: u (fp32, zero beyond i) into Ub[i & 1], the
+    // reflector row into the evecs slot (for Q), h_i = |u|^2 / 2 of the rounded u, e_i
     auto reflector = [&](int i) {
-        double* v = vub[i & 1];
-        float* vf = ufb[i & 1];
+        const int ji = i >> 4;
         double x[3];
         double sa = 0.0, sq = 0.0;
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
-            const int q = lane + 64 * t;
-            x[t] = q < i ? (double)A[i * LD + q] : 0.0;
+            float v = 0.0f;
+#pragma unroll
+            for (int j = 0; j < TR_SLOTS; ++j) v = (j == ji) ? ra[j][t] : v;
+            const int c = lane + 64 * t;
+            x[t] = c < i ? (double)v : 0.0;
             sa += fabs(x[t]);
             sq += x[t] * x[t];
         }
         const double scale = wsum(sa);
         const double ssq = wsum(sq);
-        double h = 0.0;
+        float* ub = Ub + (i & 1) * TR_NMAX;
         if (scale == 0.0) {
 #pragma unroll
-            for (int t = 0; t < 3; ++t) {
-                const int q = lane + 64 * t;
-                if (q < ((i + 3) & ~3)) {
-                    v[q] = 0.0;
-                    vf[q] = 0.0f;
-                }
+            for (int t = 0; t < 3; ++t) ub[lane + 64 * t] = 0.0f;
+            if (lane == 0) {
+                e2[i] = 0.0;
+                hh2[i] = 0.0;
             }
-            if (lane == 0) ee[i] = 0.0;
-        } else {
-            h = ssq / (scale * scale);
-            const double f = (double)A[i * LD + i - 1] / scale;
-            const double g = f > 0 ? -sqrt(h) : sqrt(h);
-            h -= f * g;
-#pragma unroll
-            for (int t = 0; t < 3; ++t) {
-                const int q = lane + 64 * t;
-                if (q < i) {
-                    const double uq = (q == i - 1) ? f - g : x[t] / scale;
-                    v[q] = uq;
-                    vf[q] = (float)uq;
-                } else if (q < ((i + 3) & ~3)) {
-                    v[q] = 0.0;
-                    vf[q] = 0.0f;
-                }
-            }
-            if (lane == 0) ee[i] = scale * g;
+            return;
         }
-        if (lane == 0) hh[i] = h;
+        const double inv = 1.0 / scale;
+        const double hn = ssq * inv * inv;
+        double xf = x[0];
+        if (((i - 1) >> 6) == 1) xf = x[1];
+        if (((i - 1) >> 6) == 2) xf = x[2];
+        const double f = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(xf), (i - 1) & 63),
+                                          __builtin_amdgcn_readlane(__double2loint(xf), (i - 1) & 63)) * inv;
+        const double g = f > 0 ? -sqrt(hn) : sqrt(hn);
+        double uu = 0.0;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int c = lane + 64 * t;
+            float uf_ = 0.0f;
+            if (c < i) uf_ = (float)(c == i - 1 ? f - g : x[t] * inv);
+            ub[c] = uf_;
+            uu += (double)uf_ * (double)uf_;
+            if (c < i) slot[i * n + c] = uf_;
+        }
+        const double h = 0.5 * wsum(uu);
+        if (lane == 0) {
+            e2[i] = scale * g;
+            hh2[i] = h;
+        }
     };
-    if (wave == 0 && n > 1) reflector(n - 1);
+    if (n > 1 && wave == ((n - 1) & (TA_W - 1))) reflector(n - 1);
     __syncthreads();
     for (int i = n - 1; i > 0; --i) {
-        const double h = hh[i];
-        const double* vcur = vub[i & 1];
-        const float* ucur = ufb[i & 1];
-        if (h == 0.0) {   // row i already reduced: no transformation
-            if (i > 1 && wave == ((i - 1) & (TA_W - 1))) reflector(i - 1);
+        const double h = hh2[i];
+        const float* ub = Ub + (i & 1) * TR_NMAX;
+        if (h != 0.0) {
+            // (1) per-wave partials of (A u)_c over this wave's rows, and the wave's share of
+            // u^T A u (so that K needs no second reduction)
+            float acc[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int j = 0; j < TR_SLOTS; ++j) {
+                const float ur = ub[16 * j + wave];
+#pragma unroll
+                for (int t = 0; t < 3; ++t) acc[t] = fmaf(ra[j][t], ur, acc[t]);
+            }
+            double kw = 0.0;
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                P[wave * TR_NMAX + lane + 64 * t] = acc[t];
+                kw += (double)acc[t] * (double)ub[lane + 64 * t];
+            }
+            kw = wsum(kw);
+            if (lane == 0) Kw[wave] = kw;
             __syncthreads();
-            continue;
-        }
-        // (1) partial sums of A u: thread (c, quarter) over rows q = quarter (mod 4)
-        if (pc < i) {
-            double s0 = 0.0, s1 = 0.0;
-            int q = pq;
-            for (; q + 4 < i; q += 8) {
-                s0 += (double)A[q * LD + pc] * vcur[q];
-                s1 += (double)A[(q + 4) * LD + pc] * vcur[q + 4];
-            }
-            if (q < i) s0 += (double)A[q * LD + pc] * vcur[q];
-            part[pq * TR_NMAX + pc] = s0 + s1;
-        }
-        __syncthreads();
-        // (2) one wave: p = A u / h, K = u.p / 2h, w = p - K u
-        if (wave == 0) {
-            double pv[3];
-            double kp = 0.0;
+            // (2) p = (A u) / h, K = u^T A u / 2h^2, w = p - K u (zero beyond i)
+            if (tid < TR_NMAX) {
+                double sum = 0.0, ks = 0.0;
 #pragma unroll
-            for (int t = 0; t < 3; ++t) {
-                const int c = lane + 64 * t;
-                pv[t] = 0.0;
-                if (c < i) {
-                    pv[t] = ((part[c] + part[TR_NMAX + c]) + (part[2 * TR_NMAX + c] + part[3 * TR_NMAX + c])) / h;
-                    kp += vcur[c] * pv[t];
+                for (int w = 0; w < TA_W; ++w) {
+                    sum += (double)P[w * TR_NMAX + tid];
+                    ks += Kw[w];
                 }
+                const double K = ks / (2.0 * h * h);
+                Wv[tid] = tid < i ? (float)(sum / h - K * (double)ub[tid]) : 0.0f;
             }
-            const double K = wsum(kp) / (h + h);
+            __syncthreads();
+            // (3) rank-2 update of this wave's rows
+            float uc[3], wc[3];
 #pragma unroll
             for (int t = 0; t < 3; ++t) {
-                const int c = lane + 64 * t;
-                if (c < i) wf[c] = (float)(pv[t] - K * vcur[c]);
-                else if (c < ((i + 3) & ~3)) wf[c] = 0.0f;   // float4 tail: columns >= i unchanged
+                uc[t] = ub[lane + 64 * t];
+                wc[t] = Wv[lane + 64 * t];
+            }
+#pragma unroll
+            for (int j = 0; j < TR_SLOTS; ++j) {
+                const float ur = ub[16 * j + wave], wr = Wv[16 * j + wave];
+#pragma unroll
+                for (int t = 0; t < 3; ++t) ra[j][t] -= ur * wc[t] + wr * uc[t];
             }
         }
-        __syncthreads();
-        // (3) rank-2 update A -= u w^T + w u^T on [0, i)^2 in fp32, float4 per lane; the
-        // reflector u goes into row i (dead from now on); the owner of row i-1 then forms
-        // the next reflector
-        for (int r = wave; r < i; r += TA_W) {
-            const float ur = ucur[r], wr = wf[r];
-            float* row = A + r * LD;
-            for (int c = 4 * lane; c < i; c += 256) {
-                float4 x = *reinterpret_cast<float4*>(row + c);
-                const float4 uc = *reinterpret_cast<const float4*>(ucur + c);
-                const float4 wc = *reinterpret_cast<const float4*>(wf + c);
-                x.x -= ur * wc.x + wr * uc.x;
-                x.y -= ur * wc.y + wr * uc.y;
-                x.z -= ur * wc.z + wr * uc.z;
-                x.w -= ur * wc.w + wr * uc.w;
-                *reinterpret_cast<float4*>(row + c) = x;
-            }
-        }
-        for (int q = tid; q < i; q += TA_T) A[i * LD + q] = ucur[q];
         if (i > 1 && wave == ((i - 1) & (TA_W - 1))) reflector(i - 1);
         __syncthreads();
     }
-    for (int i = tid; i < n; i += TA_T) dd[i] = (double)A[i * LD + i];
+    // diagonal of T from the owners' registers
+#pragma unroll
+    for (int j = 0; j < TR_SLOTS; ++j)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int r = 16 * j + wave, c = lane + 64 * t;
+            if (r == c && r < n) dd[r] = (double)ra[j][t];
+        }
     if (tid == 0) {
-        ee[0] = 0.0;
-        hh[0] = 0.0;
+        e2[0] = 0.0;
+        hh2[0] = 0.0;
     }
-    float* slot = a.evecs + a.evec_off[u];
-    for (int i = wave; i < n; i += TA_W)
-        for (int j = lane; j < i; j += 64) slot[i * n + j] = A[i * LD + j];
-    __syncthreads();
-    for (int i = wave; i < n; i += TA_W)
-        for (int j = lane; j < LD; j += 64) A[i * LD + j] = (i == j) ? 1.0f : 0.0f;
     if (a.stats && tid == 0) tA2 = __builtin_amdgcn_s_memtime();
-    // Q = H_{n-1} ... H_1: for i = 1 .. n-1, Q[0:i, 0:i] -= u (u^T Q[0:i, 0:i]) / h_i.
-    // u of the next step is loaded (double buffer) during the update of this one.
-    if (n > 1 && tid < 4) {   // u of step 1 (one element) into buffer 1, zero float4 tail
-        const float v = tid < 1 ? slot[1 * n + tid] : 0.0f;
-        vub[1][tid] = (double)v;
-        ufb[1][tid] = v;
-    }
+    // ---- Q = H_{n-1} ... H_1 in registers (same distribution) ---------------------------------
+#pragma unroll
+    for (int j = 0; j < TR_SLOTS; ++j)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int r = 16 * j + wave, c = lane + 64 * t;
+            ra[j][t] = (r == c && r < n) ? 1.0f : 0.0f;
+        }
+    __syncthreads();   // e2, hh2 and the reflector rows visible
+    for (int q = tid; q < n; q += TA_T) ee[q] = e2[q];
+    if (n > 1 && tid < TR_NMAX) Ub[TR_NMAX + tid] = tid < 1 ? slot[1 * n + tid] : 0.0f;
     __syncthreads();
     for (int i = 1; i < n; ++i) {
-        const double h = hh[i];
-        const double* vcur = vub[i & 1];
-        const float* ucur = ufb[i & 1];
-        const float unext = (i + 1 < n && tid < i + 1) ? slot[(i + 1) * n + tid] : 0.0f;   // TA_T > k
-        if (h != 0.0) {   // uniform
-            if (pc < i) {
-                double s0 = 0.0, s1 = 0.0;
-                int q = pq;
-                for (; q + 4 < i; q += 8) {
-                    s0 += vcur[q] * (double)A[q * LD + pc];
-                    s1 += vcur[q + 4] * (double)A[(q + 4) * LD + pc];
-                }
-                if (q < i) s0 += vcur[q] * (double)A[q * LD + pc];
-                part[pq * TR_NMAX + pc] = s0 + s1;
+        const double h = hh2[i];
+        const float* ub = Ub + (i & 1) * TR_NMAX;
+        const float unext = (i + 1 < n && tid < i + 1) ? slot[(i + 1) * n + tid] : 0.0f;
+        if (h != 0.0) {
+            float acc[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int j = 0; j < TR_SLOTS; ++j) {
+                const float ur = ub[16 * j + wave];
+#pragma unroll
+                for (int t = 0; t < 3; ++t) acc[t] = fmaf(ur, ra[j][t], acc[t]);
+            }
+#pragma unroll
+            for (int t = 0; t < 3; ++t) P[wave * TR_NMAX + lane + 64 * t] = acc[t];
+            __syncthreads();
+            if (tid < TR_NMAX) {
+                double sum = 0.0;
+#pragma unroll
+                for (int w = 0; w < TA_W; ++w) sum += (double)P[w * TR_NMAX + tid];
+                Wv[tid] = (float)(sum / h);
             }
             __syncthreads();
-            if (tid < i)
-                wf[tid] = (float)(((part[tid] + part[TR_NMAX + tid]) + (part[2 * TR_NMAX + tid] + part[3 * TR_NMAX + tid])) / h);
-            else if (tid < ((i + 3) & ~3))
-                wf[tid] = 0.0f;   // float4 tail: Q[r][c >= i] stays 0
-            __syncthreads();
-            for (int r = wave; r < i; r += TA_W) {
-                const float ur = ucur[r];
-                float* row = A + r * LD;
-                for (int c = 4 * lane; c < i; c += 256) {
-                    float4 x = *reinterpret_cast<float4*>(row + c);
-                    const float4 t = *reinterpret_cast<const float4*>(wf + c);
-                    x.x -= ur * t.x;
-                    x.y -= ur * t.y;
-                    x.z -= ur * t.z;
-                    x.w -= ur * t.w;
-                    *reinterpret_cast<float4*>(row + c) = x;
-                }
+            float tc[3];
+#pragma unroll
+            for (int t = 0; t < 3; ++t) tc[t] = Wv[lane + 64 * t];
+#pragma unroll
+            for (int j = 0; j < TR_SLOTS; ++j) {
+                const float ur = ub[16 * j + wave];
+#pragma unroll
+                for (int t = 0; t < 3; ++t) ra[j][t] -= ur * tc[t];
             }
         }
-        // next step's u into the other buffer (loaded at the top of this step)
-        if (i + 1 < n && tid < ((i + 1 + 3) & ~3)) {
-            vub[(i + 1) & 1][tid] = (double)unext;
-            ufb[(i + 1) & 1][tid] = unext;
-        }
+        if (i + 1 < n && tid < TR_NMAX) Ub[((i + 1) & 1) * TR_NMAX + tid] = unext;
         __syncthreads();
     }
-    for (int i = wave; i < n; i += TA_W)
-        for (int j = lane; j < n; j += 64) slot[i * n + j] = A[i * LD + j];
+#pragma unroll
+    for (int j = 0; j < TR_SLOTS; ++j)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int r = 16 * j + wave, c = lane + 64 * t;
+            if (r < n && c < n) slot[r * n + c] = ra[j][t];
+        }
     if (a.stats && tid == 0) {
         const unsigned long long t3 = __builtin_amdgcn_s_memtime();
         atomicAdd(&a.stats[4], tA1 - tA0);
@@ -699,7 +709,10 @@ __global__ __launch_bounds__(TR_T) void tri_apply_kernel(TriArgs a) {
 }
 
 size_t tri_lds_a(int kmax) {
-    return sizeof(float) * (size_t)kmax * tri_lda(kmax) + sizeof(double) * 7 * TR_NMAX + sizeof(float) * 3 * TR_NMAX;
+    const size_t assembly = sizeof(float) * (size_t)kmax * tri_lda(kmax) + sizeof(double) * 7 * TR_NMAX +
+                            sizeof(float) * 3 * TR_NMAX;
+    const size_t reduction = sizeof(float) * (TA_W + 3) * TR_NMAX + sizeof(double) * TR_NMAX;
+    return std::max(assembly, reduction);
 }
 size_t tri_lds_c(int kmax) {
     return sizeof(float) * (size_t)((kmax * tri_ld(kmax) + 1) & ~1) + sizeof(float2) * TR_Q * TR_NMAX +
