@@ -168,12 +168,12 @@ __global__ __launch_bounds__(256) void knn2_f32_kernel(Knn2Args a) {
 //     R = tR[code], S = tS[code] = tR[code]^2, B = tB[code] (presence).
 // That is a third of the HBM / L2 bytes of the three-plane form.
 //
-// Tiling: one 256-thread workgroup (4 waves, one per SIMD) per 128 x 128 item tile of
-// the upper triangle; wave (wy, wx) owns 64 x 64 = 2 x 2 blocks of 32 x 32, i.e. 16
-// int32 accumulators (4 products x 4 blocks, 256 registers).  Users are staged 128 at
+// Tiling: one 512-thread workgroup (8 waves, two per SIMD) per 128 x 128 item tile of
+// the upper triangle; wave (wy, wx) owns 64 x 32 = 2 x 1 blocks of 32 x 32, i.e. 8
+// int32 accumulators (4 products x 2 blocks, 128 AGPRs).  Users are staged 128 at
 // a time through double-buffered LDS (rows padded to 144 B: conflict-free
-// ds_read_b128 / ds_write_b128), one barrier per stage.  Per stage a wave issues 64
-// MFMAs (2048 SIMD cycles) against 8 KB of staged codes per operand.
+// ds_read_b128 / ds_write_b128), one barrier per stage.  Per stage a wave issues 32
+// MFMAs (1024 SIMD cycles) against 8 KB of staged codes per operand.
 //
 // Tile order is XCD-aware: 256 consecutive workgroup ids cover a 16 x 16 super-block
 // of tiles, and the 32 ids of one XCD (id % 8) a 4 x 8 sub-block, so the tiles that
@@ -212,47 +212,50 @@ __device__ __forceinline__ v4i perm4(uint32_t hi, uint32_t lo, v4i c) {
     return o;
 }
 
-__global__ __launch_bounds__(256, 1) void knn2_code_kernel(Knn2CodeArgs a) {
+// 512 threads = 8 waves, two per SIMD: wave (wy, wx) owns 64 x 32 items of the 128 x 128
+// tile (2 x 1 blocks of 32 x 32, 8 accumulators = 128 AGPRs), so each SIMD interleaves two
+// waves' MFMA streams across LDS-read and barrier latencies.
+__global__ __launch_bounds__(512, 1) void knn2_code_kernel(Knn2CodeArgs a) {
     __shared__ __attribute__((aligned(16))) int8_t lds[2][2][KC_T * KC_ROW];   // [buf][A|B], 73,728 B
     uint32_t ta, tb;
     if (!code_tile(blockIdx.x, a.n_tiles, a.n_super, ta, tb)) return;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wy = wave >> 1, wx = wave & 1, r = lane & 31, h = lane >> 5;
+    const int wy = wave >> 2, wx = wave & 3, r = lane & 31, h = lane >> 5;
 
-    // staging: piece q = t + 256 i (i < 4) of each operand is row q >> 3, 16-byte segment q & 7
-    const int8_t* srcA[4];
-    const int8_t* srcB[4];
+    // staging: piece q = t + 512 i (i < KC_P) of each operand is row q / (KC_U / 16), 16-byte
+    // segment q % (KC_U / 16)
+    constexpr int SEG = KC_U / 16, KC_P = KC_T * SEG / 512, ROWS_PER = 512 / SEG;
+    const int8_t* srcA[KC_P];
+    const int8_t* srcB[KC_P];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t row = (t >> 3) + 32 * i;
+    for (int i = 0; i < KC_P; ++i) {
+        const uint32_t row = t / SEG + ROWS_PER * i;
         const uint32_t ra = min(ta * KC_T + row, a.n_items - 1), rb = min(tb * KC_T + row, a.n_items - 1);
-        srcA[i] = a.C + (size_t)ra * a.ldu + 16 * (t & 7);
-        srcB[i] = a.C + (size_t)rb * a.ldu + 16 * (t & 7);
+        srcA[i] = a.C + (size_t)ra * a.ldu + 16 * (t % SEG);
+        srcB[i] = a.C + (size_t)rb * a.ldu + 16 * (t % SEG);
     }
-    const int st_off = (t >> 3) * KC_ROW + 16 * (t & 7);     // + 32 rows per piece
-    v4i stA[4], stB[4];
+    const int st_off = (t / SEG) * KC_ROW + 16 * (t % SEG);   // + ROWS_PER rows per piece
+    v4i stA[KC_P], stB[KC_P];
     auto gload = [&](uint64_t k0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < KC_P; ++i) {
             stA[i] = *(const v4i*)(srcA[i] + k0);
             stB[i] = *(const v4i*)(srcB[i] + k0);
         }
     };
     auto lstore = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            *(v4i*)(&lds[buf][0][st_off + 32 * i * KC_ROW]) = stA[i];
-            *(v4i*)(&lds[buf][1][st_off + 32 * i * KC_ROW]) = stB[i];
+        for (int i = 0; i < KC_P; ++i) {
+            *(v4i*)(&lds[buf][0][st_off + ROWS_PER * i * KC_ROW]) = stA[i];
+            *(v4i*)(&lds[buf][1][st_off + ROWS_PER * i * KC_ROW]) = stB[i];
         }
     };
 
-    v16i num[2][2], den1[2][2], den2[2][2], cnt[2][2];
+    v16i num[2], den1[2], den2[2], cnt[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) num[i][j] = den1[i][j] = den2[i][j] = cnt[i][j] = v16i{};
+    for (int i = 0; i < 2; ++i) num[i] = den1[i] = den2[i] = cnt[i] = v16i{};
 
-    const int rdA = (wy * 64 + r) * KC_ROW + 16 * h, rdB = (wx * 64 + r) * KC_ROW + 16 * h;
+    const int rdA = (wy * 64 + r) * KC_ROW + 16 * h, rdB = (wx * 32 + r) * KC_ROW + 16 * h;
     const uint64_t n_stage = a.ldu / KC_U;
     gload(0);
     lstore(0);
@@ -262,29 +265,32 @@ __global__ __launch_bounds__(256, 1) void knn2_code_kernel(Knn2CodeArgs a) {
         if (s + 1 < n_stage) gload((s + 1) * KC_U);
         const int8_t* LA = lds[buf][0];
         const int8_t* LB = lds[buf][1];
+        // codes of k-step ks + 1 are read while the MFMAs of k-step ks issue
+        v4i cbn = *(const v4i*)(LB + rdB);
+        v4i can[2] = {*(const v4i*)(LA + rdA), *(const v4i*)(LA + rdA + 32 * KC_ROW)};
 #pragma unroll
         for (int ks = 0; ks < KC_U / 32; ++ks) {
-            v4i Ra[2], Sa[2], Ba[2], Rb[2], Sb[2], Bb[2];
+            const v4i cb = cbn;
+            const v4i cac[2] = {can[0], can[1]};
+            if (ks + 1 < KC_U / 32) {
+                cbn = *(const v4i*)(LB + rdB + 32 * (ks + 1));
+                can[0] = *(const v4i*)(LA + rdA + 32 * (ks + 1));
+                can[1] = *(const v4i*)(LA + rdA + 32 * KC_ROW + 32 * (ks + 1));
+            }
+            const v4i Rb = perm4(a.tR_hi, a.tR_lo, cb);
+            const v4i Sb = perm4(a.tS_hi, a.tS_lo, cb);
+            const v4i Bb = perm4(a.tB_hi, a.tB_lo, cb);
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const v4i ca = *(const v4i*)(LA + rdA + i * 32 * KC_ROW + 32 * ks);
-                const v4i cb = *(const v4i*)(LB + rdB + i * 32 * KC_ROW + 32 * ks);
-                Ra[i] = perm4(a.tR_hi, a.tR_lo, ca);
-                Sa[i] = perm4(a.tS_hi, a.tS_lo, ca);
-                Ba[i] = perm4(a.tB_hi, a.tB_lo, ca);
-                Rb[i] = perm4(a.tR_hi, a.tR_lo, cb);
-                Sb[i] = perm4(a.tS_hi, a.tS_lo, cb);
-                Bb[i] = perm4(a.tB_hi, a.tB_lo, cb);
+                const v4i ca = cac[i];
+                const v4i Ra = perm4(a.tR_hi, a.tR_lo, ca);
+                const v4i Sa = perm4(a.tS_hi, a.tS_lo, ca);
+                const v4i Ba = perm4(a.tB_hi, a.tB_lo, ca);
+                num[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ra, Rb, num[i], 0, 0, 0);
+                den1[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Sa, Bb, den1[i], 0, 0, 0);
+                den2[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ba, Sb, den2[i], 0, 0, 0);
+                cnt[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ba, Bb, cnt[i], 0, 0, 0);
             }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    num[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ra[i], Rb[j], num[i][j], 0, 0, 0);
-                    den1[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Sa[i], Bb[j], den1[i][j], 0, 0, 0);
-                    den2[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ba[i], Sb[j], den2[i][j], 0, 0, 0);
-                    cnt[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ba[i], Bb[j], cnt[i][j], 0, 0, 0);
-                }
         }
         if (s + 1 < n_stage) lstore(buf ^ 1);
         __syncthreads();
@@ -297,10 +303,7 @@ __global__ __launch_bounds__(256, 1) void knn2_code_kernel(Knn2CodeArgs a) {
     const bool diag = ta == tb;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            knn2_store(e, ta * KC_T + wy * 64 + 32 * i, tb * KC_T + wx * 64 + 32 * j, diag, num[i][j], den1[i][j],
-                       den2[i][j], cnt[i][j]);
+        knn2_store(e, ta * KC_T + wy * 64 + 32 * i, tb * KC_T + wx * 32, diag, num[i], den1[i], den2[i], cnt[i]);
 }
 
 // Which integers in [-11, 11] occur: bit (r + 11) of *mask.
@@ -447,7 +450,7 @@ int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64
         const uint32_t grid = a.n_super * (a.n_super + 1) / 2 * 256;
         ctx->knn_path = 1;
         CF_HIP_CHECK(ctx, hipEventRecord(ctx->knn_ev[1], stream));
-        hipLaunchKernelGGL(knn2_code_kernel, dim3(grid), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL(knn2_code_kernel, dim3(grid), dim3(512), 0, stream, a);
         CF_HIP_CHECK(ctx, hipGetLastError());
         CF_HIP_CHECK(ctx, hipEventRecord(ctx->knn_ev[2], stream));
         return CF_OK;
