@@ -27,7 +27,9 @@ int main(int argc, char** argv) {
     const int nshards = std::stoi(cfcli::opt(argc, argv, "nshards", "4"));
     const std::string eig_path = cfcli::opt(argc, argv, "eigen", "out_eigen_");
 
-    std::vector<cfio::EigenRecord> recs = cfio::load_eigen_file(eig_path);
+    // text (parsed on --threads threads, default all) or the binary form, detected by its magic
+    std::vector<cfio::EigenRecord> recs =
+        cfio::load_eigen_file(eig_path, std::stoi(cfcli::opt(argc, argv, "threads", "0")));
     std::printf("Loaded %zu test users\n", recs.size());
     auto edges = cfio::load_edges(".", "out_fin_");
     for (auto& e : edges) e.w = (double)(float)e.w;   // parsed as float (:129)

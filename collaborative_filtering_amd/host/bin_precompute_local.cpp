@@ -9,7 +9,9 @@
 // < 2000); users are written in ascending uid order with their movies ascending (the
 // reference's order is boost::unordered_map order); k <= 192 runs on the LDS path,
 // 192 < k <= 3072 on the fp64 spill path.
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <map>
 
@@ -74,19 +76,12 @@ int main(int argc, char** argv) {
                                      evals.data(), evecs.data()),
                  "cf_eigen_batch");
     cf_destroy(ctx);
-    std::string out;
-    out.reserve(1 << 20);
-    std::ofstream f(out_path, std::ofstream::out | std::ofstream::app | std::ofstream::binary);
-    for (uint32_t i = 0; i < n_users; ++i) {
-        const uint32_t k = (uint32_t)(off[i + 1] - off[i]);
-        cfio::append_eigen_record(out, uid[i], k, (uint32_t)m[i], movies.data() + off[i], sigs.data() + off[i],
-                                  evals.data() + off[i], evecs.data() + eoff[i]);
-        if (out.size() > (64u << 20)) {
-            f.write(out.data(), (std::streamsize)out.size());
-            out.clear();
-        }
-    }
-    f.write(out.data(), (std::streamsize)out.size());
+    // out_eigen_: text records formatted on the reference's n_threads (its first argument,
+    // :217-222), or the binary form with --format binary
+    const int n_threads = std::max(1, std::atoi(argv[1]));
+    const bool binary = cfcli::opt(argc, argv, "format", "text") == "binary";
+    cfio::write_eigen_file(out_path, false, n_threads, binary, n_users, uid.data(), off.data(), m.data(),
+                           movies.data(), sigs.data(), evals.data(), eoff.data(), evecs.data());
     std::printf("Wrote %u eigen records to %s\n", n_users, out_path.c_str());
     return 0;
 }

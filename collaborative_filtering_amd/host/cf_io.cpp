@@ -1,6 +1,12 @@
 // cf_io.cpp -- text-file contract of the reference (see cf_io.hpp).
 #include "cf_io.hpp"
 
+#include <algorithm>
+#include <cstring>
+#include <fstream>
+#include <stdexcept>
+#include <thread>
+
 #include <dirent.h>
 #include <sys/stat.h>
 
@@ -245,49 +251,205 @@ void append_eigen_record(std::string& out, uint32_t user, uint32_t k, uint32_t m
     out += '\n';
 }
 
-std::vector<EigenRecord> load_eigen_file(const std::string& path) {
-    std::vector<EigenRecord> out;
-    const std::string text = read_file(path);
-    int state = 0;
-    EigenRecord cur;
+namespace {
+
+constexpr char kEigenMagic[8] = {'C', 'F', 'E', 'I', 'G', 'E', 'N', '1'};
+
+// One 3-line text record (load_precomputed_data's state machine, local_calc_precomp.cpp:
+// 426-476) from its three line spans; false on a malformed line (the reference asserts).
+bool parse_eigen_record(const char* const* lb, const char* const* le, EigenRecord& cur) {
     uint32_t kk = 0, mm = 0;
-    bool bad = false;
-    for_each_line(text, [&](const char* b, const char* e) {
-        Tok t{b, e};
-        switch (state) {
-            case 0: {  // (:426-442)
-                cur = EigenRecord();
-                if (!t.u32(cur.user) || !t.u32(kk) || !t.u32(mm)) {
-                    bad = true;
-                    return;
-                }
-                cur.movies.resize(kk);
-                cur.sigs.resize(kk);
-                for (uint32_t i = 0; i < kk; ++i)
-                    if (!t.u32(cur.movies[i]) || !t.f64(cur.sigs[i])) bad = true;  // assert (:434)
-                state = 1;
-                break;
-            }
-            case 1:  // (:444-452)
-                cur.evals.resize(mm);
-                for (uint32_t i = 0; i < mm; ++i)
-                    if (!t.f64(cur.evals[i])) bad = true;  // assert (:447)
-                state = 2;
-                break;
-            case 2:  // (:454-476)
-                cur.evecs.resize((size_t)kk * mm);
-                for (size_t i = 0; i < (size_t)kk * mm; ++i)
-                    if (!t.f64(cur.evecs[i])) bad = true;  // assert (:462)
-                out.push_back(std::move(cur));
-                state = 0;
-                break;
-        }
-    });
-    if (bad) throw std::runtime_error("malformed out_eigen_ record in " + path);
+    bool ok = true;
+    {   // "uid k m" + "movie sig" x k (:426-442)
+        Tok t{lb[0], le[0]};
+        if (!t.u32(cur.user) || !t.u32(kk) || !t.u32(mm)) return false;
+        cur.movies.resize(kk);
+        cur.sigs.resize(kk);
+        for (uint32_t i = 0; i < kk; ++i)
+            if (!t.u32(cur.movies[i]) || !t.f64(cur.sigs[i])) ok = false;   // assert (:434)
+    }
+    {   // m eigenvalues (:444-452)
+        Tok t{lb[1], le[1]};
+        cur.evals.resize(mm);
+        for (uint32_t i = 0; i < mm; ++i)
+            if (!t.f64(cur.evals[i])) ok = false;   // assert (:447)
+    }
+    {   // k x m eigenvectors (:454-476)
+        Tok t{lb[2], le[2]};
+        cur.evecs.resize((size_t)kk * mm);
+        for (size_t i = 0; i < (size_t)kk * mm; ++i)
+            if (!t.f64(cur.evecs[i])) ok = false;   // assert (:462)
+    }
+    return ok;
+}
+
+int resolve_threads(int n_threads) {
+    if (n_threads > 0) return n_threads;
+    const unsigned h = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(h, 64u));
+}
+
+// Run f(t) for t in [0, n) on n threads (inline when n == 1).
+template <class F>
+void parallel_for(int n, F&& f) {
+    if (n <= 1) {
+        f(0);
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (int t = 0; t < n; ++t) pool.emplace_back([&, t] { f(t); });
+    for (auto& th : pool) th.join();
+}
+
+std::vector<EigenRecord> load_eigen_binary(const std::string& text, const std::string& path) {
+    std::vector<EigenRecord> out;
+    size_t pos = sizeof(kEigenMagic);
+    auto take = [&](void* dst, size_t bytes) {
+        if (pos + bytes > text.size()) throw std::runtime_error("truncated binary out_eigen_ " + path);
+        std::memcpy(dst, text.data() + pos, bytes);
+        pos += bytes;
+    };
+    uint64_t n = 0;
+    take(&n, sizeof(n));
+    out.resize(n);
+    std::vector<float> buf;
+    for (auto& r : out) {
+        uint32_t hdr[3];
+        take(hdr, sizeof(hdr));
+        const uint32_t k = hdr[1], m = hdr[2];
+        r.user = hdr[0];
+        r.movies.resize(k);
+        take(r.movies.data(), sizeof(uint32_t) * k);
+        auto floats = [&](std::vector<double>& dst, size_t cnt) {
+            buf.resize(cnt);
+            take(buf.data(), sizeof(float) * cnt);
+            dst.assign(buf.begin(), buf.end());
+        };
+        floats(r.sigs, k);
+        floats(r.evals, m);
+        floats(r.evecs, (size_t)k * m);
+    }
     return out;
 }
 
+}  // namespace
+
+std::vector<EigenRecord> load_eigen_file(const std::string& path, int n_threads) {
+    const std::string text = read_file(path);
+    if (text.size() >= sizeof(kEigenMagic) && std::memcmp(text.data(), kEigenMagic, sizeof(kEigenMagic)) == 0)
+        return load_eigen_binary(text, path);
+    // non-empty line spans, then records of 3 lines parsed in parallel over record ranges
+    std::vector<const char*> lb, le;
+    {
+        const char* p = text.data();
+        const char* end = p + text.size();
+        while (p < end) {
+            const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(end - p)));
+            if (!nl) nl = end;
+            if (nl > p) {
+                lb.push_back(p);
+                le.push_back(nl);
+            }
+            p = nl + 1;
+        }
+    }
+    const size_t n_rec = lb.size() / 3;   // a trailing partial record is dropped (state machine)
+    std::vector<EigenRecord> out(n_rec);
+    const int T = (int)std::min<size_t>((size_t)resolve_threads(n_threads), std::max<size_t>(n_rec, 1));
+    std::vector<char> bad(T, 0);
+    parallel_for(T, [&](int t) {
+        const size_t r0 = n_rec * t / T, r1 = n_rec * (t + 1) / T;
+        for (size_t r = r0; r < r1; ++r)
+            if (!parse_eigen_record(&lb[3 * r], &le[3 * r], out[r])) bad[t] = 1;
+    });
+    for (char b : bad)
+        if (b) throw std::runtime_error("malformed out_eigen_ record in " + path);
+    return out;
+}
+
+void write_eigen_file(const std::string& path, bool append, int n_threads, bool binary, uint32_t n_users,
+                      const uint32_t* uid, const uint64_t* off, const int32_t* m, const uint32_t* movies,
+                      const float* sigs, const float* evals, const uint64_t* eoff, const float* evecs) {
+    std::ofstream f(path, std::ofstream::binary | (append ? std::ofstream::app : std::ofstream::trunc));
+    if (!f) throw std::runtime_error("cannot open " + path);
+    if (binary) {   // "CFEIGEN1", n, then per record uid k m movies[k] sigs[k] evals[m] evecs[k*m]
+        const uint64_t n = n_users;
+        f.write(kEigenMagic, sizeof(kEigenMagic));
+        f.write(reinterpret_cast<const char*>(&n), sizeof(n));
+        std::vector<float> ev;
+        for (uint32_t u = 0; u < n_users; ++u) {
+            const uint32_t k = (uint32_t)(off[u + 1] - off[u]), mm = (uint32_t)m[u];
+            const uint32_t hdr[3] = {uid[u], k, mm};
+            f.write(reinterpret_cast<const char*>(hdr), sizeof(hdr));
+            f.write(reinterpret_cast<const char*>(movies + off[u]), sizeof(uint32_t) * k);
+            f.write(reinterpret_cast<const char*>(sigs + off[u]), sizeof(float) * k);
+            ev.assign(mm, 0.0f);   // entries past k (k == 1 padding) are 0, as in the text form
+            for (uint32_t j = 0; j < mm && j < k; ++j) ev[j] = evals[off[u] + j];
+            f.write(reinterpret_cast<const char*>(ev.data()), sizeof(float) * mm);
+            f.write(reinterpret_cast<const char*>(evecs + eoff[u]), sizeof(float) * (size_t)k * mm);
+        }
+        return;
+    }
+    // text: contiguous user ranges formatted in parallel, written in order
+    const int T = (int)std::min<uint32_t>((uint32_t)resolve_threads(n_threads), std::max<uint32_t>(n_users, 1));
+    const uint32_t chunk = 4096;   // users per formatting task
+    const uint32_t n_chunks = (n_users + chunk - 1) / chunk;
+    for (uint32_t c0 = 0; c0 < n_chunks; c0 += (uint32_t)T) {
+        const int nt = (int)std::min<uint32_t>((uint32_t)T, n_chunks - c0);
+        std::vector<std::string> part(nt);
+        parallel_for(nt, [&](int t) {
+            const uint32_t u0 = (c0 + t) * chunk, u1 = std::min(n_users, u0 + chunk);
+            for (uint32_t u = u0; u < u1; ++u) {
+                const uint32_t k = (uint32_t)(off[u + 1] - off[u]);
+                append_eigen_record(part[t], uid[u], k, (uint32_t)m[u], movies + off[u], sigs + off[u],
+                                    evals + off[u], evecs + eoff[u]);
+            }
+        });
+        for (auto& p : part) f.write(p.data(), (std::streamsize)p.size());
+    }
+}
+
 }  // namespace cfio
+
+// C entry points used by the Python side (tests compare the formatting with printf, and the
+// parallel / binary out_eigen_ writers and readers with the serial text form).
+extern "C" int cfh_write_eigen(const char* path, int append, int n_threads, int binary, uint32_t n_users,
+                               const uint32_t* uid, const uint64_t* off, const int32_t* m, const uint32_t* movies,
+                               const float* sigs, const float* evals, const uint64_t* eoff, const float* evecs) {
+    try {
+        cfio::write_eigen_file(path, append != 0, n_threads, binary != 0, n_users, uid, off, m, movies, sigs, evals,
+                               eoff, evecs);
+    } catch (const std::exception&) {
+        return -1;
+    }
+    return 0;
+}
+
+// Loads out_eigen_ (text or binary) and returns the record count; when `flat` is non-null it
+// receives, per record, uid, k, m, then movies, sigs, evals, evecs as doubles (cap doubles).
+extern "C" int64_t cfh_load_eigen(const char* path, int n_threads, double* flat, int64_t cap) {
+    try {
+        const auto recs = cfio::load_eigen_file(path, n_threads);
+        int64_t pos = 0;
+        auto put = [&](double v) {
+            if (flat && pos < cap) flat[pos] = v;
+            ++pos;
+        };
+        for (const auto& r : recs) {
+            put(r.user);
+            put((double)r.movies.size());
+            put((double)r.evals.size());
+            for (auto v : r.movies) put(v);
+            for (auto v : r.sigs) put(v);
+            for (auto v : r.evals) put(v);
+            for (auto v : r.evecs) put(v);
+        }
+        if (flat && pos > cap) return -2;
+        return (int64_t)recs.size();
+    } catch (const std::exception&) {
+        return -1;
+    }
+}
 
 // C entry points used by the Python side (tests compare the formatting with printf).
 extern "C" int cfh_format_g(double v, char* buf, int cap) {

@@ -85,7 +85,15 @@ struct EigenRecord {
 void append_eigen_record(std::string& out, uint32_t user, uint32_t k, uint32_t m,
                          const uint32_t* movies, const float* sigs, const float* evals,
                          const float* evecs);
-// load_precomputed_data (local_calc_precomp.cpp:406-482): the 3-line state machine.
-std::vector<EigenRecord> load_eigen_file(const std::string& path);
+// load_precomputed_data (local_calc_precomp.cpp:406-482): the 3-line state machine, with the
+// records parsed on n_threads threads (0 = hardware concurrency).  A file that starts with
+// "CFEIGEN1" is the binary form written by write_eigen_file(binary = true).
+std::vector<EigenRecord> load_eigen_file(const std::string& path, int n_threads = 0);
+// out_eigen_ writer (precompute_local_threads.cpp:196-211): text records formatted on
+// n_threads threads (contiguous user ranges, written in user order), or the binary form
+// (the reference's own TODO, README.md:29).
+void write_eigen_file(const std::string& path, bool append, int n_threads, bool binary, uint32_t n_users,
+                      const uint32_t* uid, const uint64_t* off, const int32_t* m, const uint32_t* movies,
+                      const float* sigs, const float* evals, const uint64_t* eoff, const float* evecs);
 
 }  // namespace cfio

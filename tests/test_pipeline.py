@@ -211,3 +211,43 @@ def test_stage_local_calc(work):
             n_rows += 1
     assert len(res) == n_rows and n_rows > 100
     assert good >= 0.5 * n_rows, (good, n_rows)
+
+
+def test_binary_out_eigen(work):
+    """precompute_local --format binary writes the exact float record
+    (magic CFEIGEN1); it carries the text file's records, and local_calc_precomp reads either
+    form (detected by the magic) with the same kk and, up to the text's 6-digit rounding, the
+    same mse."""
+    import ctypes
+    from collaborative_filtering_amd import _native
+
+    run(work, "precompute_local", "4", "--format", "binary", "--output", "out_eigen_bin")
+    run(work, "precompute_local", "4", "--output", "out_eigen_txt")
+    lib = ctypes.CDLL(_native.HOST_LIB_PATH)
+    lib.cfh_load_eigen.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64]
+    lib.cfh_load_eigen.restype = ctypes.c_int64
+
+    def load(name):
+        path = os.path.join(work, name).encode()
+        flat = np.zeros(5_000_000)
+        n = lib.cfh_load_eigen(path, 4, ctypes.c_void_p(flat.ctypes.data), len(flat))
+        assert n > 0
+        return n, flat
+
+    nb, fb = load("out_eigen_bin")
+    nt, ft = load("out_eigen_txt")
+    assert nb == nt
+    assert np.allclose(fb, ft, rtol=1e-5, atol=1e-6)
+    assert open(os.path.join(work, "out_eigen_bin"), "rb").read(8) == b"CFEIGEN1"
+    run(work, "local_calc_precomp", "--pct", "100", "--seed", "1", "--eigen", "out_eigen_txt")
+    res_t = pu.parse_res(pu.read_shards(work, "out_res_"))
+    run(work, "local_calc_precomp", "--pct", "100", "--seed", "1", "--eigen", "out_eigen_bin")
+    res_b = pu.parse_res(pu.read_shards(work, "out_res_"))
+    assert res_t.keys() == res_b.keys()
+    close = 0
+    for key, (mt, kt) in res_t.items():
+        mb, kb = res_b[key]
+        assert kt == kb
+        assert np.isnan(mt) == np.isnan(mb)
+        close += bool(np.isnan(mt) or abs(mt - mb) <= 1e-3 * max(1.0, mt))
+    assert close >= 0.9 * len(res_t), (close, len(res_t))
