@@ -7,9 +7,10 @@ from collaborative_filtering_amd import synth
 from collaborative_filtering_amd.api import CF_SIGS_COMPAT, Context, evec_offsets
 
 users = int(sys.argv[1]) if len(sys.argv) > 1 else 4000
+n_items = int(os.environ.get("ITEMS", "10000"))
 k = synth.degrees(2026101502, users)
-off, items, rat = synth.user_items(2026101502, k, 10000, threads=16)
-W = synth.graph_model(2026101502, 10000, threads=16)
+off, items, rat = synth.user_items(2026101502, k, n_items, threads=16)
+W = synth.graph_model(2026101502, n_items, threads=16)
 ctx = Context(0); ctx.upload_graph_dense(W); plan = ctx.plan(off)
 dev = torch.device("cuda")
 T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
@@ -25,6 +26,7 @@ def pred():
                      CF_SIGS_COMPAT, d["mse"], d["kk"])
 pred(); torch.cuda.synchronize()
 t = time.perf_counter(); pred(); torch.cuda.synchronize(); dt = time.perf_counter() - t
+
 print(f"predict {n} ratings in {dt*1e3:.1f} ms -> {n/dt:.0f}/s", flush=True)
 ctx.debug_phases(True); pred(); torch.cuda.synchronize()
 ph = ctx.debug_phases(True, read=True)
