@@ -34,8 +34,10 @@ namespace {
 constexpr int SP_T = 512;
 constexpr int SP_W = SP_T / 64;
 constexpr int SP_N = CF_SPILL_MAX_K;
-constexpr int SP_Q = 8;                          // QL iterations applied per pass over Q
-constexpr int SP_TB = 64;                        // positions per staged coefficient block
+constexpr int SP_QB = 16;                        // QL iterations applied per pass over Z
+constexpr int SP_NB = 32;                        // Householder panel width (dlatrd block)
+constexpr int SP_CC = 32;                        // columns staged per trailing-update step
+constexpr int SP_RC = 64;                        // rows of V staged per back-transform step
 
 struct SpillArgs {
     const uint32_t* order;
@@ -61,6 +63,9 @@ struct SpillSmem {
     double e[SP_N];
     double rc[SP_N];
     double rs[SP_N];
+    double tau[SP_N];
+    double vj[SP_NB], wj[SP_NB], xv[SP_NB], xw[SP_NB];
+    double part[8 * 64];
     float sig[SP_N];
     int perm[SP_N];
     double red[SP_W + 4];
@@ -71,6 +76,14 @@ __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
+}
+
+// Lane l's double as a wave-uniform value (two v_readlane_b32 into SGPRs).
+__device__ __forceinline__ double bcast_lane(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 // Sum over the workgroup, returned to every thread (two barriers).
@@ -104,6 +117,9 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         const int n = (int)(a.item_off[u + 1] - base);
         float* Wt = a.evecs + a.evec_off[u];   // k x k scratch until the output is written
         auto Mat = [&](int r, int c) -> double& { return M[(size_t)c * n + r]; };
+        double* Zb = M + (size_t)n * n;          // tridiagonal eigenvectors Z (column-major, then rows)
+        double* Wp = Zb + (size_t)n * n;         // [SP_NB][n] panel W of the tridiagonalisation
+        auto Zm = [&](int r, int c) -> double& { return Zb[(size_t)c * n + r]; };
         unsigned long long t0 = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull, t1 = 0, t2 = 0, t3 = 0, tgen = 0;
         unsigned long long n_iter = 0;
 
@@ -140,320 +156,569 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         __syncthreads();
 
         if (tid == 0) t1 = __builtin_amdgcn_s_memtime();
-        // ---- 2a. tridiagonalisation (tred2) ---------------------------------------------
-        for (int j = tid; j < n; j += SP_T) S.d[j] = Mat(n - 1, j);
-        __syncthreads();
-        for (int i = n - 1; i > 0; --i) {
-            double part = 0.0;
-            for (int q = tid; q < i; q += SP_T) part += fabs(S.d[q]);
-            const double scale = block_sum(part, S.red);
-            double h = 0.0;
-            if (scale == 0.0) {
-                if (tid == 0) S.e[i] = S.d[i - 1];
-                __syncthreads();
-                for (int j = tid; j < i; j += SP_T) {
-                    S.d[j] = Mat(i - 1, j);
-                    Mat(i, j) = 0.0;
-                    Mat(j, i) = 0.0;
+        // ---- 2. blocked Householder tridiagonalisation (LAPACK dsytrd/dlatrd, lower) ---------
+        // Panels of SP_NB columns.  Inside a panel, column j is brought up to date with the
+        // panel's earlier reflectors (A -= V W^T + W V^T restricted to column j), its
+        // reflector H_j = I - tau_j v v^T (v[j+1] = 1) annihilates A(j+2:n, j), and
+        //   w = tau (A v - V (W^T v) - W (V^T v)),  w += -tau/2 (w.v) v
+        // uses the trailing matrix as of the panel start.  After the panel one rank-2*SP_NB
+        // update A -= V W^T + W V^T refreshes the trailing square.  The symmetric
+        // matrix-vector product is the only per-column pass over the trailing matrix, so the
+        // workspace traffic is ~8 B per element-step instead of tred2's ~24 B.
+        // v_j is stored in M(j+1:n, j); A = Q T Q^T with Q = H_0 H_1 ... H_{n-2},
+        // T = tridiag(d, e) with e[j] = T(j+1, j).
+        for (int p = 0; p < n - 1; p += SP_NB) {
+            const int jb = min(SP_NB, n - 1 - p);
+            for (int jj = 0; jj < jb; ++jj) {
+                const int j = p + jj;
+                double* colj = M + (size_t)j * n;
+                if (jj > 0) {
+                    if (tid < jj) {
+                        S.vj[tid] = M[(size_t)(p + tid) * n + j];
+                        S.wj[tid] = Wp[(size_t)tid * n + j];
+                    }
+                    __syncthreads();
+                    for (int r = j + tid; r < n; r += SP_T) {
+                        double acc = colj[r];
+                        for (int t = 0; t < jj; ++t)
+                            acc -= M[(size_t)(p + t) * n + r] * S.wj[t] + Wp[(size_t)t * n + r] * S.vj[t];
+                        colj[r] = acc;
+                    }
+                    __syncthreads();
                 }
-            } else {
-                double hp = 0.0;
-                for (int q = tid; q < i; q += SP_T) {
-                    const double v = S.d[q] / scale;
-                    S.d[q] = v;
-                    hp += v * v;
+                // reflector of x = A(j+1:n, j) (dlarfg without the rescaling loop)
+                const double alpha = colj[j + 1];
+                const double ajj = colj[j];
+                double part = 0.0;
+                for (int r = j + 2 + tid; r < n; r += SP_T) {
+                    const double x = colj[r];
+                    part += x * x;
                 }
-                h = block_sum(hp, S.red);
+                const double sigma = block_sum(part, S.red);   // barriers: alpha read before v is stored
+                double tj = 0.0, beta = alpha, scal = 0.0;
+                if (sigma != 0.0) {
+                    beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+                    tj = (beta - alpha) / beta;
+                    scal = 1.0 / (alpha - beta);
+                }
                 if (tid == 0) {
-                    const double f = S.d[i - 1];
-                    double g = sqrt(h);
-                    if (f > 0) g = -g;
-                    S.e[i] = scale * g;
-                    h -= f * g;
-                    S.d[i - 1] = f - g;
-                    S.red[SP_W] = h;
+                    S.d[j] = ajj;
+                    S.e[j] = beta;
+                    S.tau[j] = tj;
+                }
+                for (int r = j + 1 + tid; r < n; r += SP_T) {
+                    const double vr = (r == j + 1) ? 1.0 : colj[r] * scal;
+                    S.rc[r] = vr;
+                    colj[r] = vr;
                 }
                 __syncthreads();
-                h = S.red[SP_W];
-                // u into column i; p = A[0:i, 0:i] u, thread per row (column reads coalesce)
-                for (int j = tid; j < i; j += SP_T) {
-                    Mat(j, i) = S.d[j];
+                const int r0 = j + 1;
+                if (tj == 0.0) {   // H_j = I: w = 0
+                    for (int r = tid; r < n; r += SP_T) Wp[(size_t)jj * n + r] = 0.0;
+                    __syncthreads();
+                    continue;
+                }
+                // x_v[t] = W(:,t).v and x_w[t] = V(:,t).v over rows r0..n-1, one wave per dot
+                for (int q = wave; q < 2 * jj; q += SP_W) {
+                    const int t = q >> 1;
+                    const double* src = (q & 1) ? M + (size_t)(p + t) * n : Wp + (size_t)t * n;
+                    double s = 0.0;
+                    for (int r = r0 + lane; r < n; r += 64) s += src[r] * S.rc[r];
+                    s = wave_sum(s);
+                    if (lane == 0) {
+                        if (q & 1)
+                            S.xw[t] = s;
+                        else
+                            S.xv[t] = s;
+                    }
+                }
+                // y = A(r0:n, r0:n) v: a wave per (64-row block, column segment), lane per row
+                // (column-major reads coalesce); segments split the columns when there are
+                // fewer row blocks than waves, partial sums combined in LDS in a fixed order.
+                const int rows = n - r0;
+                const int nrb = (rows + 63) >> 6;
+                const int segs = nrb >= SP_W ? 1 : SP_W / nrb;
+                const int seglen = (rows + segs - 1) / segs;
+                for (int unit = wave; unit < nrb * segs; unit += SP_W) {
+                    const int rb = unit % nrb, sg = unit / nrb;
+                    const int r = r0 + rb * 64 + lane;
+                    const int c_lo = r0 + sg * seglen, c_hi = min(n, c_lo + seglen);
                     double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-                    int q = 0;
-                    for (; q + 8 <= i; q += 8) {
-                        double x[8];
+                    if (r < n) {
+                        const double* mr = M + r;
+                        int c = c_lo;
+                        for (; c + 8 <= c_hi; c += 8) {
+                            double x[8];
 #pragma unroll
-                        for (int t = 0; t < 8; ++t) x[t] = Mat(j, q + t);
-                        p0 += x[0] * S.d[q] + x[4] * S.d[q + 4];
-                        p1 += x[1] * S.d[q + 1] + x[5] * S.d[q + 5];
-                        p2 += x[2] * S.d[q + 2] + x[6] * S.d[q + 6];
-                        p3 += x[3] * S.d[q + 3] + x[7] * S.d[q + 7];
+                            for (int t = 0; t < 8; ++t) x[t] = mr[(size_t)(c + t) * n];
+                            p0 += x[0] * S.rc[c] + x[4] * S.rc[c + 4];
+                            p1 += x[1] * S.rc[c + 1] + x[5] * S.rc[c + 5];
+                            p2 += x[2] * S.rc[c + 2] + x[6] * S.rc[c + 6];
+                            p3 += x[3] * S.rc[c + 3] + x[7] * S.rc[c + 7];
+                        }
+                        for (; c < c_hi; ++c) p0 += mr[(size_t)c * n] * S.rc[c];
                     }
-                    for (; q < i; ++q) p0 += Mat(j, q) * S.d[q];
-                    S.e[j] = ((p0 + p1) + (p2 + p3)) / h;
-                }
-                __syncthreads();
-                double fp = 0.0;
-                for (int j = tid; j < i; j += SP_T) fp += S.e[j] * S.d[j];
-                const double hh = block_sum(fp, S.red) / (h + h);
-                for (int j = tid; j < i; j += SP_T) S.e[j] -= hh * S.d[j];
-                __syncthreads();
-                // rank-2 update of the active block, wave per column
-                for (int j = wave; j < i; j += SP_W) {
-                    const double dj = S.d[j], ej = S.e[j];
-                    double* col = M + (size_t)j * n;
-                    for (int q0 = 0; q0 < i; q0 += 256) {
-                        double x[4];
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const int q = q0 + 64 * t + lane;
-                            x[t] = q < i ? col[q] : 0.0;
-                        }
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const int q = q0 + 64 * t + lane;
-                            if (q < i) col[q] = x[t] - (dj * S.e[q] + ej * S.d[q]);
-                        }
+                    const double ps = (p0 + p1) + (p2 + p3);
+                    if (segs == 1) {
+                        if (r < n) S.rs[r] = ps;
+                    } else {
+                        S.part[sg * (nrb * 64) + rb * 64 + lane] = ps;
                     }
                 }
                 __syncthreads();
-                for (int j = tid; j < i; j += SP_T) {
-                    S.d[j] = Mat(i - 1, j);
-                    Mat(i, j) = 0.0;
+                double yv = 0.0;
+                for (int r = r0 + tid; r < n; r += SP_T) {
+                    double y;
+                    if (segs == 1) {
+                        y = S.rs[r];
+                    } else {
+                        y = 0.0;
+                        for (int sg = 0; sg < segs; ++sg) y += S.part[sg * (nrb * 64) + (r - r0)];
+                    }
+                    for (int t = 0; t < jj; ++t)
+                        y -= M[(size_t)(p + t) * n + r] * S.xv[t] + Wp[(size_t)t * n + r] * S.xw[t];
+                    y *= tj;
+                    S.rs[r] = y;
+                    yv += y * S.rc[r];
                 }
+                const double a2 = -0.5 * tj * block_sum(yv, S.red);
+                for (int r = tid; r < n; r += SP_T) Wp[(size_t)jj * n + r] = r >= r0 ? S.rs[r] + a2 * S.rc[r] : 0.0;
+                __syncthreads();
             }
-            __syncthreads();
-            if (tid == 0) S.d[i] = h;
-            __syncthreads();
-        }
-        if (tid == 0) t2 = __builtin_amdgcn_s_memtime();
-        // ---- 2b. accumulate Q --------------------------------------------------------------
-        for (int i = 0; i < n - 1; ++i) {
-            if (tid == 0) {
-                Mat(n - 1, i) = Mat(i, i);
-                Mat(i, i) = 1.0;
-            }
-            __syncthreads();
-            const double h = S.d[i + 1];
-            if (h != 0.0) {
-                const double* uc = M + (size_t)(i + 1) * n;
-                for (int q = tid; q <= i; q += SP_T) S.rc[q] = uc[q];   // u of this step, staged in LDS
-                __syncthreads();
-                for (int j = wave; j <= i; j += SP_W) {
-                    double* col = M + (size_t)j * n;
-                    double g0 = 0.0, g1 = 0.0;
-                    for (int q0 = 0; q0 <= i; q0 += 256) {
-                        double x[4];
+            // trailing update A(q:n, q:n) -= V W^T + W V^T (q = p + jb), full square so the
+            // next panels' column-major symv stays coalesced.  Lane per row with that row's
+            // V and W entries in registers; each column's V and W entries are broadcast from
+            // LDS (SP_CC columns staged at a time).
+            const int q = p + jb;
+            const int mq = n - q;
+            if (mq > 0) {
+                const int nrb = (mq + 63) >> 6;
+                double* stg = S.rc;   // [SP_CC][2 * SP_NB]: V(c, t) then W(c, t)
+                for (int pass = 0; pass < nrb; pass += SP_W) {
+                    const int rb = pass + wave;
+                    const int r = q + rb * 64 + lane;
+                    const bool act = rb < nrb && r < n;
+                    double vr[SP_NB], wr[SP_NB];
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const int q = q0 + 64 * t + lane;
-                            x[t] = q <= i ? col[q] : 0.0;
-                        }
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const int q = q0 + 64 * t + lane;
-                            if (q <= i) (t & 1 ? g1 : g0) += S.rc[q] * x[t];
-                        }
+                    for (int t = 0; t < SP_NB; ++t) {
+                        vr[t] = (act && t < jb) ? M[(size_t)(p + t) * n + r] : 0.0;
+                        wr[t] = (act && t < jb) ? Wp[(size_t)t * n + r] : 0.0;
                     }
-                    const double g = wave_sum(g0 + g1);
-                    for (int q0 = 0; q0 <= i; q0 += 256) {
-                        double x[4];
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const int q = q0 + 64 * t + lane;
-                            x[t] = q <= i ? col[q] : 0.0;
+                    for (int c0 = q; c0 < n; c0 += SP_CC) {
+                        const int cn = min(SP_CC, n - c0);
+                        __syncthreads();
+                        for (int idx = tid; idx < SP_CC * 2 * SP_NB; idx += SP_T) {
+                            const int cc = idx / (2 * SP_NB), t2 = idx - cc * (2 * SP_NB);
+                            const int t = t2 & (SP_NB - 1);
+                            double v = 0.0;
+                            if (cc < cn && t < jb)
+                                v = t2 < SP_NB ? M[(size_t)(p + t) * n + c0 + cc] : Wp[(size_t)t * n + c0 + cc];
+                            stg[idx] = v;
                         }
+                        __syncthreads();
+                        if (!act) continue;
+                        // software-pipelined: the next 8 columns' loads are in flight while
+                        // the current 8 are updated; sched_barrier keeps the scheduler from
+                        // hoisting every column's 64 LDS operands at once (VGPR spills)
+                        double* mp = M + (size_t)c0 * n + r;
+                        double cur[8];
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const int q = q0 + 64 * t + lane;
-                            if (q <= i) col[q] = x[t] - g * (S.rc[q] / h);
+                        for (int u8 = 0; u8 < 8; ++u8) cur[u8] = u8 < cn ? mp[(size_t)u8 * n] : 0.0;
+                        for (int cc = 0; cc < cn; cc += 8) {
+                            double nxt[8];
+#pragma unroll
+                            for (int u8 = 0; u8 < 8; ++u8)
+                                nxt[u8] = cc + 8 + u8 < cn ? mp[(size_t)(cc + 8 + u8) * n] : 0.0;
+#pragma unroll
+                            for (int u8 = 0; u8 < 8; ++u8) {
+                                __builtin_amdgcn_sched_barrier(0);
+                                const double* sv = stg + (cc + u8) * 2 * SP_NB;
+                                double acc0 = cur[u8], acc1 = 0.0;
+#pragma unroll
+                                for (int t = 0; t < SP_NB; t += 2) {
+                                    if ((t & 7) == 0) __builtin_amdgcn_sched_barrier(0);
+                                    acc0 -= vr[t] * sv[SP_NB + t] + wr[t] * sv[t];
+                                    acc1 -= vr[t + 1] * sv[SP_NB + t + 1] + wr[t + 1] * sv[t + 1];
+                                }
+                                if (cc + u8 < cn) mp[(size_t)(cc + u8) * n] = acc0 + acc1;
+                            }
+#pragma unroll
+                            for (int u8 = 0; u8 < 8; ++u8) cur[u8] = nxt[u8];
                         }
                     }
                 }
+                __syncthreads();
             }
-            __syncthreads();
-            for (int q = tid; q <= i; q += SP_T) Mat(q, i + 1) = 0.0;
-            __syncthreads();
         }
-        for (int j = tid; j < n; j += SP_T) {
-            S.d[j] = Mat(n - 1, j);
-            Mat(n - 1, j) = 0.0;
-        }
-        __syncthreads();
         if (tid == 0) {
-            Mat(n - 1, n - 1) = 1.0;
-            for (int i = 1; i < n; ++i) S.e[i - 1] = S.e[i];   // tql2 entry shift
+            S.d[n - 1] = M[(size_t)(n - 1) * n + (n - 1)];
             S.e[n - 1] = 0.0;
         }
+        // Z = I: tql2 accumulates the tridiagonal eigenvectors, Q is applied afterwards
+        for (size_t idx = tid; idx < (size_t)n * n; idx += SP_T) Zb[idx] = 0.0;
         __syncthreads();
+        for (int i = tid; i < n; i += SP_T) Zb[(size_t)i * n + i] = 1.0;
+        __syncthreads();
+        if (tid == 0) t2 = __builtin_amdgcn_s_memtime();
 
         if (tid == 0) t3 = __builtin_amdgcn_s_memtime();
-        // ---- 3. implicit QL (tql2) -----------------------------------------------------------
-        // Thread 0 runs the QL recurrence on (d, e) -- which never reads Q -- and records the
-        // rotation sequences of up to SP_Q consecutive iterations (each on its own [l, m]).
-        // All threads then apply the batch in ONE pass over the touched columns of Q:
-        // sequence t lags sequence t-1 by one position, so a row streams through all SP_Q
-        // sweeps with one load and one store per column (SP_Q carried values per row).
+        // ---- 3. implicit QL (tql2) on Z: one generator wave, seven applier waves ------------
+        // Wave 0 runs the QL recurrence on (d, e) -- which never reads Z -- and writes the
+        // rotation sequences of up to SP_QB consecutive iterations (each on its own [l, m])
+        // into one of two coefficient buffers; lane 0 carries the serial rotation chain, the
+        // whole wave does the per-iteration shift of d and the buffer resets.  Meanwhile
+        // waves 1..7 apply the previous batch in ONE pass over the touched columns of Z:
+        // sequence t lags sequence t-1 by one position, so a row streams through all SP_QB
+        // sweeps with one load and one store per column.  Positions outside a sequence's
+        // range hold the identity rotation (c = 1, s = 0), which turns the carry into a plain
+        // one-column delay, so the pass is branch-free.
         {
-            double* Gc = M + (size_t)n * n;      // [SP_Q][n] cosines
-            double* Gs = Gc + (size_t)SP_Q * n;  // [SP_Q][n] sines
-            int* seq_l = S.perm;                 // perm is free until section 4
-            int* seq_m = S.perm + SP_Q;
-            int gl = 0, gm = 0, giter = 0, gphase = 0;   // thread 0's generator state
+            constexpr int QB = SP_QB;
+            // coefficient buffers, diagonal layout: row rw holds stage t's rotation at position
+            // rw + t in column t, so the QB pairs one applier step needs are contiguous
+            constexpr int OFF = QB + 4;
+            static_assert(QB == 16, "applier: 64 lanes = 4 steps x 16 stages");
+            const int gld = n + 2 * QB + 4;                 // rows -OFF .. n+QB-1
+            double2* Gbuf = reinterpret_cast<double2*>(Wp + (size_t)SP_NB * n);   // [2][gld][QB]
+            int* seq_l = S.perm;                            // [2][QB]  (perm is free until 4c)
+            int* seq_m = S.perm + 2 * QB;                   // [2][QB]
+            int* bflag = S.perm + 4 * QB;                   // [2] nseq, [2] generator done
+            for (size_t idx = tid; idx < (size_t)2 * QB * gld; idx += SP_T) Gbuf[idx] = make_double2(1.0, 0.0);
+            if (tid < 2 * QB) {
+                seq_l[tid] = 0;
+                seq_m[tid] = 0;
+            }
+            if (tid < 4) bflag[tid] = 0;
+            __syncthreads();
+            // generator state (wave 0, uniform across its lanes)
+            int gl = 0, gm = 0, giter = 0, gphase = 0;
             double gf = 0.0, gtst1 = 0.0;
-            for (;;) {
-                if (tid == 0) {
-                    const unsigned long long tg = __builtin_amdgcn_s_memtime();
-                    int nseq = 0;
-                    while (nseq < SP_Q && gl < n) {
-                        if (gphase == 0) {
-                            gtst1 = fmax(gtst1, fabs(S.d[gl]) + fabs(S.e[gl]));
-                            gm = gl;
-                            while (gm < n && !(fabs(S.e[gm]) <= eps * gtst1)) ++gm;
-                            if (gm == gl) {
+            auto gen_batch = [&](int buf) {
+                const unsigned long long tg = lane == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
+                double2* G = Gbuf + (size_t)buf * QB * gld;
+                // identity back into the ranges this buffer held two batches ago
+                for (int t = 0; t < bflag[buf]; ++t) {
+                    const int lo = seq_l[buf * QB + t], hi = seq_m[buf * QB + t];
+                    for (int pp = lo + lane; pp < hi; pp += 64) G[(size_t)(pp - t + OFF) * QB + t] = make_double2(1.0, 0.0);
+                }
+                __threadfence_block();
+                int nseq = 0;
+                while (nseq < QB && gl < n) {
+                    if (gphase == 0) {
+                        gtst1 = fmax(gtst1, fabs(S.d[gl]) + fabs(S.e[gl]));
+                        // m = first index >= l with a negligible e[m] (n if none): 64 at a time
+                        int mfound = n;
+                        for (int m0 = gl; m0 < n; m0 += 64) {
+                            const int mi = m0 + lane;
+                            const bool neg = mi < n && fabs(S.e[mi]) <= eps * gtst1;
+                            const unsigned long long bal = __ballot(neg);
+                            if (bal) {
+                                mfound = m0 + __builtin_ctzll(bal);
+                                break;
+                            }
+                        }
+                        gm = mfound;
+                        if (gm == gl) {
+                            if (lane == 0) {
                                 S.d[gl] += gf;
                                 S.e[gl] = 0.0;
-                                ++gl;
-                                continue;
                             }
-                            giter = 0;
-                            gphase = 1;
+                            ++gl;
+                            continue;
                         }
-                        const int l = gl, m = gm;
-                        ++giter;
-                        ++n_iter;
+                        giter = 0;
+                        gphase = 1;
+                    }
+                    const int l = gl, m = gm;
+                    ++giter;
+                    if (lane == 0) ++n_iter;
+                    double hsh = 0.0;
+                    if (lane == 0) {
                         const double g0 = S.d[l];
                         double p = (S.d[l + 1] - g0) / (2.0 * S.e[l]);
                         double r = hypot(p, 1.0);
                         if (p < 0) r = -r;
                         S.d[l] = S.e[l] / (p + r);
                         S.d[l + 1] = S.e[l] * (p + r);
+                        hsh = g0 - S.d[l];
+                    }
+                    hsh = __shfl(hsh, 0);
+                    for (int i = l + 2 + lane; i < n; i += 64) S.d[i] -= hsh;
+                    gf += hsh;
+                    int conv = 0;
+                    if (lane == 0) {
                         const double dl1 = S.d[l + 1];
-                        const double hsh = g0 - S.d[l];
-                        for (int i = l + 2; i < n; ++i) S.d[i] -= hsh;
-                        gf += hsh;
-                        p = S.d[m];
+                        double p = S.d[m];
                         double c = 1.0, c2 = 1.0, c3 = 1.0, sn = 0.0, s2 = 0.0;
                         const double el1 = S.e[l + 1];
-                        double* gc = Gc + (size_t)nseq * n;
-                        double* gs = Gs + (size_t)nseq * n;
+                        double2* gt = G + (ptrdiff_t)(OFF - nseq) * QB + nseq;
+                        double ei = S.e[m - 1], di = S.d[m - 1];
                         for (int i = m - 1; i >= l; --i) {
+                            // prefetch the next position's (e, d), unconditionally (index
+                            // clamped) so the loop body has no branch and the LDS wait lands
+                            // at the end of the chain instead of its start
+                            const int ip = max(i - 1, 0);
+                            const double ein = S.e[ip];
+                            const double din = S.d[ip];
                             c3 = c2;
                             c2 = c;
                             s2 = sn;
-                            const double g = c * S.e[i];
+                            const double g = c * ei;
                             const double h = c * p;
-                            r = hypot(p, S.e[i]);
+                            // r = hypot(p, e_i); |p|, |e_i| <= ||T|| here, so the plain form
+                            // neither overflows nor underflows.  1/r = rsq(x2) refined by two
+                            // Newton steps (the serial chain is ~11 dependent operations; r
+                            // itself is off the chain)
+                            const double x2 = fma(p, p, ei * ei);
+                            double inv = __builtin_amdgcn_rsq(x2);
+                            const double hx = 0.5 * x2;
+                            inv = inv * fma(-hx, inv * inv, 1.5);
+                            inv = inv * fma(-hx, inv * inv, 1.5);
+                            const double r = x2 * inv;
                             S.e[i + 1] = sn * r;
-                            sn = S.e[i] / r;
-                            c = p / r;
-                            p = c * S.d[i] - sn * g;
-                            S.d[i + 1] = h + sn * (c * g + sn * S.d[i]);
-                            gc[i] = c;
-                            gs[i] = sn;
+                            sn = ei * inv;
+                            c = p * inv;
+                            p = c * di - sn * g;
+                            S.d[i + 1] = h + sn * (c * g + sn * di);
+                            gt[(size_t)i * QB] = make_double2(c, sn);
+                            ei = ein;
+                            di = din;
                         }
                         p = -sn * s2 * c3 * el1 * S.e[l] / dl1;
                         S.e[l] = sn * p;
                         S.d[l] = c * p;
-                        seq_l[nseq] = l;
-                        seq_m[nseq] = m;
-                        ++nseq;
-                        if (!(fabs(S.e[l]) > eps * gtst1 && giter < 60)) {
+                        seq_l[buf * QB + nseq] = l;
+                        seq_m[buf * QB + nseq] = m;
+                        conv = !(fabs(S.e[l]) > eps * gtst1 && giter < 60);
+                        if (conv) {
                             S.d[l] += gf;
                             S.e[l] = 0.0;
-                            ++gl;
-                            gphase = 0;
                         }
                     }
-                    S.flag[1] = nseq;
-                    S.flag[2] = gl >= n;
+                    conv = __shfl(conv, 0);
+                    ++nseq;
+                    if (conv) {
+                        ++gl;
+                        gphase = 0;
+                    }
+                }
+                if (lane == 0) {
+                    bflag[buf] = nseq;
+                    bflag[2 + buf] = gl >= n;
                     tgen += __builtin_amdgcn_s_memtime() - tg;
                 }
-                __syncthreads();
-                const int nseq = S.flag[1];
-                const int done = S.flag[2];
-                if (nseq > 0) {
+            };
+            if (wave == 0) gen_batch(0);
+            __syncthreads();
+            // appliers: waves 1..7, two rows per thread (rows r0 and r0 + NA share each
+            // coefficient load)
+            const bool applier = wave != 0;
+            const int ta = tid - 64;
+            constexpr int NA = SP_T - 64;
+            for (int b = 0;; ++b) {
+                const int buf = b & 1;
+                const int nseq = bflag[buf];
+                if (nseq == 0) break;                       // uniform
+                const int gen_done = bflag[2 + buf];
+                if (wave == 0) {
+                    if (!gen_done) {
+                        gen_batch(buf ^ 1);
+                    } else if (lane == 0) {
+                        bflag[buf ^ 1] = 0;
+                    }
+                } else if (applier) {
                     int L = n, Mx = 0;
                     for (int t = 0; t < nseq; ++t) {
-                        L = min(L, seq_l[t]);
-                        Mx = max(Mx, seq_m[t]);
+                        L = min(L, seq_l[buf * QB + t]);
+                        Mx = max(Mx, seq_m[buf * QB + t]);
                     }
-                    // one row of Q per thread and pass (rows rbase + tid)
-                    for (int rbase = 0; rbase < n; rbase += SP_T) {
-                        const int r = rbase + tid;
-                        const bool act = r < n;
-                        double carry[SP_Q];
-                        carry[0] = act ? Mat(r, Mx) : 0.0;
+                    const double2* G = Gbuf + (size_t)buf * QB * gld;
+                    for (int rbase = 0; rbase < n; rbase += 2 * NA) {
+                        // every lane stays active (the coefficient pairs are read from all
+                        // 64 lanes); rows past n alias row 0 and do not store
+                        const int r0 = rbase + ta, r1 = r0 + NA;
+                        if (rbase + (wave - 1) * 64 >= n) continue;   // the whole wave is past n
+                        const bool a0 = r0 < n, a1 = r1 < n;
+                        double c0[QB], c1[QB];
 #pragma unroll
-                        for (int t = 1; t < SP_Q; ++t) carry[t] = 0.0;
-                        const int tau_hi = Mx - 1, tau_lo = L - nseq;
-                        for (int tb = tau_hi; tb >= tau_lo; tb -= SP_TB) {
-                            // stage the coefficients of this block: [t][j] for tau = tb - j
-                            __syncthreads();
-                            for (int idx = tid; idx < SP_Q * SP_TB; idx += SP_T) {
-                                const int t = idx / SP_TB, j = idx - t * SP_TB;
-                                const int pp = tb - j + t;
-                                double cv = 1.0, sv = 0.0;
-                                if (t < nseq && pp >= seq_l[t] && pp < seq_m[t]) {
-                                    cv = Gc[(size_t)t * n + pp];
-                                    sv = Gs[(size_t)t * n + pp];
-                                }
-                                S.rc[idx] = cv;
-                                S.rs[idx] = sv;
+                        for (int t = 0; t < QB; ++t) {
+                            c0[t] = 0.0;
+                            c1[t] = 0.0;
+                        }
+                        double* z0 = Zb + (a0 ? r0 : 0);
+                        double* z1 = Zb + (a1 ? r1 : 0);
+                        // four steps per iteration: one coalesced load brings the 4 x 16
+                        // coefficient pairs (lane 16u + t: step u, stage t), v_readlane puts
+                        // each pair in SGPRs for the FMAs; the next four columns of both rows
+                        // are loaded one iteration ahead
+                        double n0[4], n1[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            n0[u] = Mx - u >= L ? z0[(size_t)(Mx - u) * n] : 0.0;
+                            n1[u] = Mx - u >= L ? z1[(size_t)(Mx - u) * n] : 0.0;
+                        }
+                        for (int tau = Mx; tau >= L - QB; tau -= 4) {
+                            const double2 csl = G[(size_t)(tau - (lane >> 4) + OFF) * QB + (lane & 15)];
+                            double v0[4], v1[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                v0[u] = n0[u];
+                                v1[u] = n1[u];
+                                const int tn = tau - 4 - u;
+                                n0[u] = tn >= L ? z0[(size_t)tn * n] : 0.0;
+                                n1[u] = tn >= L ? z1[(size_t)tn * n] : 0.0;
                             }
-                            __syncthreads();
-                            if (!act) continue;
-                            const int jn = min(SP_TB, tb - tau_lo + 1);
-                            for (int j0 = 0; j0 < jn; j0 += 8) {
-                                double xin[8];
 #pragma unroll
-                                for (int u8 = 0; u8 < 8; ++u8) {
-                                    const int tau = tb - j0 - u8;
-                                    xin[u8] = (j0 + u8 < jn && tau >= L) ? Mat(r, tau) : 0.0;
+                            for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                                for (int t = 0; t < QB; ++t) {
+                                    const double cx = bcast_lane(csl.x, 16 * u + t);
+                                    const double sy = bcast_lane(csl.y, 16 * u + t);
+                                    const double o0 = sy * v0[u] + cx * c0[t];
+                                    c0[t] = cx * v0[u] - sy * c0[t];
+                                    v0[u] = o0;
+                                    const double o1 = sy * v1[u] + cx * c1[t];
+                                    c1[t] = cx * v1[u] - sy * c1[t];
+                                    v1[u] = o1;
                                 }
-#pragma unroll
-                                for (int u8 = 0; u8 < 8; ++u8) {
-                                    const int j = j0 + u8;
-                                    if (j < jn) {
-                                        const int tau = tb - j;
-                                        double val = xin[u8];
-                                        bool ok = tau >= L;
-#pragma unroll
-                                        for (int t = 0; t < SP_Q; ++t) {
-                                            const int pp = tau + t;
-                                            if (t >= nseq) {
-                                                // sequences past the batch: pass through
-                                            } else if (pp > Mx) {
-                                                ok = false;
-                                            } else if (pp == Mx) {
-                                                if (ok) carry[t] = val;
-                                                ok = false;
-                                            } else if (pp >= L) {
-                                                const double cv = S.rc[t * SP_TB + j], sv = S.rs[t * SP_TB + j];
-                                                const double out = sv * val + cv * carry[t];
-                                                carry[t] = cv * val - sv * carry[t];
-                                                val = out;
-                                            } else if (pp == L - 1) {
-                                                val = carry[t];
-                                                ok = true;
-                                            } else {
-                                                ok = false;
-                                            }
-                                        }
-                                        if (ok) Mat(r, tau + nseq) = val;
-                                    }
+                                const int tc = tau - u + QB;
+                                if (tc <= Mx && tc >= L) {
+                                    if (a0) z0[(size_t)tc * n] = v0[u];
+                                    if (a1) z1[(size_t)tc * n] = v1[u];
                                 }
                             }
                         }
                     }
                 }
                 __syncthreads();
-                if (done) break;
             }
         }
-
         const unsigned long long t4 = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
-        // ---- 4. order, sign, lim, output --------------------------------------------------
+        // ---- 4a. Z to row-major (in place, 32 x 32 tile pairs through LDS) ------------------
+        {
+            double* buf = S.rc;   // two 32 x 33 tiles
+            const int nt = (n + 31) >> 5;
+            for (int I = 0; I < nt; ++I) {
+                for (int J = I; J < nt; ++J) {
+                    for (int idx = tid; idx < 2048; idx += SP_T) {
+                        const int which = idx >> 10, el = idx & 1023, cc = el >> 5, rr = el & 31;
+                        const int r = (which ? J : I) * 32 + rr, c = (which ? I : J) * 32 + cc;
+                        buf[which * 1056 + cc * 33 + rr] = (r < n && c < n) ? Zb[(size_t)c * n + r] : 0.0;
+                    }
+                    __syncthreads();
+                    for (int idx = tid; idx < 2048; idx += SP_T) {
+                        const int which = idx >> 10, el = idx & 1023, cc = el >> 5, rr = el & 31;
+                        // which 0: block (rows I, cols J) <- tile B transposed; 1: (rows J, cols I) <- A^T
+                        const int r = (which ? J : I) * 32 + rr, c = (which ? I : J) * 32 + cc;
+                        if (r < n && c < n) Zb[(size_t)c * n + r] = buf[(which ? 0 : 1056) + rr * 33 + cc];
+                    }
+                    __syncthreads();
+                }
+            }
+        }
+        // ---- 4b. eigenvectors of A = Q Z: compact-WY panels applied last to first --------------
+        // P_b = H_p ... H_{p+jb-1} = I - V T V^T (dlarft forward/columnwise), Z(p+1:n, :) -=
+        // V (T (V^T Z)).  Lane per column of the row-major Z; V rows staged in LDS and read as
+        // wave-uniform broadcasts, the jb-vectors V^T z and T (V^T z) live in registers.
+        {
+            double* Tm = S.rc;              // [SP_NB][SP_NB]
+            double* Gm = S.rc + SP_NB * SP_NB;
+            double* Vs = S.e;               // [SP_RC][SP_NB + 1]
+            constexpr int VLD = SP_NB + 1;
+            for (int p = ((n - 2) / SP_NB) * SP_NB; p >= 0; p -= SP_NB) {
+                const int jb = min(SP_NB, n - 1 - p);
+                for (int q = wave; q < SP_NB * SP_NB; q += SP_W) {
+                    const int t = q / SP_NB, i = q - t * SP_NB;
+                    if (t < i && i < jb) {
+                        const double* vt = M + (size_t)(p + t) * n;
+                        const double* vi = M + (size_t)(p + i) * n;
+                        double s = 0.0;
+                        for (int r = p + i + 1 + lane; r < n; r += 64) s += vt[r] * vi[r];
+                        s = wave_sum(s);
+                        if (lane == 0) Gm[q] = s;
+                    }
+                }
+                for (int idx = tid; idx < SP_NB * SP_NB; idx += SP_T) Tm[idx] = 0.0;
+                __syncthreads();
+                for (int i = 0; i < jb; ++i) {
+                    const double ti = S.tau[p + i];
+                    if (tid < i) {
+                        double s = 0.0;
+                        for (int s_ = tid; s_ < i; ++s_) s += Tm[tid * SP_NB + s_] * Gm[s_ * SP_NB + i];
+                        Tm[tid * SP_NB + i] = -ti * s;
+                    } else if (tid == i) {
+                        Tm[i * SP_NB + i] = ti;
+                    }
+                    __syncthreads();
+                }
+                const int r_lo = p + 1;
+                for (int cbase = 0; cbase < n; cbase += SP_W * 64) {
+                    const int c = cbase + wave * 64 + lane;
+                    const bool cact = c < n;
+                    double x[SP_NB];
+#pragma unroll
+                    for (int t = 0; t < SP_NB; ++t) x[t] = 0.0;
+                    for (int half = 0; half < 2; ++half) {
+                        for (int rc0 = r_lo; rc0 < n; rc0 += SP_RC) {
+                            const int rn = min(SP_RC, n - rc0);
+                            __syncthreads();
+                            for (int idx = tid; idx < SP_RC * SP_NB; idx += SP_T) {
+                                const int t = idx / SP_RC, rr = idx - t * SP_RC;
+                                const int r = rc0 + rr;
+                                Vs[rr * VLD + t] = (rr < rn && t < jb && r >= p + t + 1) ? M[(size_t)(p + t) * n + r] : 0.0;
+                            }
+                            __syncthreads();
+                            if (!cact) continue;
+                            double* zc = Zb + (size_t)rc0 * n + c;
+                            // software-pipelined rows: the next 8 rows' loads are in flight
+                            // while the current 8 are used (the row loop is latency-bound
+                            // otherwise); rows past rn read row rc0 and meet zero V entries
+                            double cur[8];
+#pragma unroll
+                            for (int u8 = 0; u8 < 8; ++u8) cur[u8] = zc[(size_t)(u8 < rn ? u8 : 0) * n];
+                            for (int rr = 0; rr < rn; rr += 8) {
+                                double nxt[8];
+#pragma unroll
+                                for (int u8 = 0; u8 < 8; ++u8) {
+                                    const int rq = rr + 8 + u8;
+                                    nxt[u8] = zc[(size_t)(rq < rn ? rq : 0) * n];
+                                }
+#pragma unroll
+                                for (int u8 = 0; u8 < 8; ++u8) {
+                                    __builtin_amdgcn_sched_barrier(0);
+                                    const double* vr = Vs + (rr + u8) * VLD;
+                                    if (half == 0) {
+#pragma unroll
+                                        for (int t = 0; t < SP_NB; ++t) x[t] += vr[t] * cur[u8];
+                                    } else {
+                                        double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+                                        for (int t = 0; t < SP_NB; t += 2) {
+                                            s0 += vr[t] * x[t];
+                                            s1 += vr[t + 1] * x[t + 1];
+                                        }
+                                        if (rr + u8 < rn) zc[(size_t)(rr + u8) * n] = cur[u8] - (s0 + s1);
+                                    }
+                                }
+#pragma unroll
+                                for (int u8 = 0; u8 < 8; ++u8) cur[u8] = nxt[u8];
+                            }
+                        }
+                        if (half == 0) {   // x <- T x (T upper triangular)
+#pragma unroll
+                            for (int s_ = 0; s_ < SP_NB; ++s_) {
+                                double acc = 0.0;
+#pragma unroll
+                                for (int t = s_; t < SP_NB; ++t) acc += Tm[s_ * SP_NB + t] * x[t];
+                                x[s_] = acc;
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        // ---- 4c. order, sign, lim, output --------------------------------------------------
         for (int j = tid; j < n; j += SP_T) {
             const double lj = S.d[j];
             int rank = 0;
@@ -463,12 +728,18 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             }
             S.perm[rank] = j;
         }
-        for (int j = wave; j < n; j += SP_W) {
-            const double* col = M + (size_t)j * n;
-            double sum = 0.0;
-            for (int q = lane; q < n; q += 64) sum += col[q];
-            sum = wave_sum(sum);
-            if (lane == 0) S.rs[j] = sum < 0.0 ? -1.0 : 1.0;
+        for (int cb = wave * 64; cb < n; cb += SP_W * 64) {
+            const int c = cb + lane;
+            if (c < n) {
+                double s0 = 0.0, s1 = 0.0;
+                int r = 0;
+                for (; r + 2 <= n; r += 2) {
+                    s0 += Zb[(size_t)r * n + c];
+                    s1 += Zb[(size_t)(r + 1) * n + c];
+                }
+                if (r < n) s0 += Zb[(size_t)r * n + c];
+                S.rs[c] = (s0 + s1) < 0.0 ? -1.0 : 1.0;
+            }
         }
         __syncthreads();
         if (tid == 0) {
@@ -487,11 +758,10 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         const int mm = S.flag[3];
         for (int i = tid; i < n; i += SP_T) a.sigs[base + i] = (float)((double)S.sig[i] + 0.01);
         for (int r = tid; r < mm; r += SP_T) a.evals[base + r] = (float)S.d[S.perm[r]];
-        for (int r = wave; r < mm; r += SP_W) {
+        for (size_t idx = tid; idx < (size_t)n * mm; idx += SP_T) {
+            const int i = (int)(idx / mm), r = (int)(idx - (size_t)i * mm);
             const int j = S.perm[r];
-            const double sg = S.rs[j];
-            const double* col = M + (size_t)j * n;
-            for (int i = lane; i < n; i += 64) Wt[(size_t)i * mm + r] = (float)(col[i] * sg);
+            Wt[idx] = (float)(Zb[(size_t)i * n + j] * S.rs[j]);
         }
         __syncthreads();
         if (a.phase && tid == 0) {
@@ -516,9 +786,9 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     if (b.count == 0) return CF_OK;
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    const uint64_t stride = (uint64_t)b.kmax * b.kmax + 2ull * SP_Q * b.kmax + 64;
+    const uint64_t stride = 2ull * b.kmax * b.kmax + (uint64_t)SP_NB * b.kmax + 4ull * SP_QB * (b.kmax + 2 * SP_QB + 4) + 64;
     const uint64_t slot_bytes = stride * sizeof(double);
-    const uint64_t budget = 8ull << 30;   // workspace cap; fewer resident users beyond it
+    const uint64_t budget = 24ull << 30;   // workspace cap; fewer resident users beyond it
     uint32_t grid = std::min<uint32_t>(b.count, (uint32_t)n_cu);
     grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(grid, budget / slot_bytes));
     const size_t need = (size_t)grid * slot_bytes + 256;
