@@ -247,14 +247,19 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     if (r < n) {
                         const double* mr = M + r;
                         int c = c_lo;
-                        for (; c + 8 <= c_hi; c += 8) {
-                            double x[8];
+                        // 16 column loads in flight per lane: the pass is bound by memory
+                        // latency x bytes in flight as much as by HBM bandwidth
+                        for (; c + 16 <= c_hi; c += 16) {
+                            double x[16];
 #pragma unroll
-                            for (int t = 0; t < 8; ++t) x[t] = mr[(size_t)(c + t) * n];
-                            p0 += x[0] * S.rc[c] + x[4] * S.rc[c + 4];
-                            p1 += x[1] * S.rc[c + 1] + x[5] * S.rc[c + 5];
-                            p2 += x[2] * S.rc[c + 2] + x[6] * S.rc[c + 6];
-                            p3 += x[3] * S.rc[c + 3] + x[7] * S.rc[c + 7];
+                            for (int t = 0; t < 16; ++t) x[t] = mr[(size_t)(c + t) * n];
+#pragma unroll
+                            for (int t = 0; t < 16; t += 4) {
+                                p0 += x[t] * S.rc[c + t];
+                                p1 += x[t + 1] * S.rc[c + t + 1];
+                                p2 += x[t + 2] * S.rc[c + t + 2];
+                                p3 += x[t + 3] * S.rc[c + t + 3];
+                            }
                         }
                         for (; c < c_hi; ++c) p0 += mr[(size_t)c * n] * S.rc[c];
                     }
