@@ -320,8 +320,11 @@ def main():
 def c5_leg(args, ctx, dev, torch, W):
     """BASELINE config 5, bounded sample: a power-law degree mix (lognormal k, median 100,
     p95 ~1.5k, clipped to [20, --c5-kmax]) through cf_eigen_run -- k <= 192 on the LDS
-    Jacobi path, larger k on the fp64 spill path -- on the config-2 item graph.  Reports
-    users/s of the mix and the per-path split (HIP events around each plan)."""
+    Jacobi path, larger k on the fp64 spill path -- on the config-2 item graph, then the
+    predictor (cf_predict_run_f32, own sigs) over every rating of those users: k <= 192 on
+    predict_kernel, larger k on the spill predictor.  Reports users/s and ratings/s of the
+    mix and the per-path split (HIP events around each plan)."""
+    from collaborative_filtering_amd.api import CF_SIGS_OWN
     from collaborative_filtering_amd import synth
     from collaborative_filtering_amd._native import CF_MAX_K, CF_SPILL_MAX_K
     from collaborative_filtering_amd.api import evec_offsets
@@ -330,14 +333,14 @@ def c5_leg(args, ctx, dev, torch, W):
     sigma = float(np.log(15.0) / 1.6449)            # p95 / median = 15
     k = synth.degrees(seed, args.c5_users, k_median=100.0, sigma=sigma, kmin=20,
                       kmax=min(args.c5_kmax, CF_SPILL_MAX_K))
-    off, items, _ = synth.user_items(seed, k, args.items, threads=16)
+    off, items, ratings = synth.user_items(seed, k, args.items, threads=16)
     ctx.upload_graph_dense(W)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     out = {"workload": f"BASELINE config 5 sample: {args.c5_users} users, lognormal k (median 100, "
                        f"sigma {sigma:.3f}, p95 {int(np.percentile(k, 95))}, max {int(k.max())}), "
                        f"{args.items} items, seed {seed}"}
     stream = torch.cuda.current_stream(dev)
-    total_ms = 0.0
+    total_ms = total_pms = 0.0
     for name, sel in (("lds", k <= CF_MAX_K), ("spill", k > CF_MAX_K)):
         ks = k[sel]
         if len(ks) == 0:
@@ -345,6 +348,7 @@ def c5_leg(args, ctx, dev, torch, W):
         o = np.zeros(len(ks) + 1, dtype=np.uint64)
         o[1:] = np.cumsum(ks.astype(np.uint64))
         it = np.concatenate([items[int(off[u]):int(off[u + 1])] for u in np.nonzero(sel)[0]])
+        rt = np.concatenate([ratings[int(off[u]):int(off[u + 1])] for u in np.nonzero(sel)[0]])
         eo, ne = evec_offsets(o)
         d_o, d_i, d_e = T(o.view(np.int64)), T(it.view(np.int32)), T(eo.view(np.int64))
         d_m = torch.zeros(len(ks), dtype=torch.int32, device=dev)
@@ -359,16 +363,31 @@ def c5_leg(args, ctx, dev, torch, W):
         e1.synchronize()
         ms = e0.elapsed_time(e1)
         total_ms += ms
+        d_mse = torch.zeros(len(it), dtype=torch.float32, device=dev)
+        d_kk = torch.zeros(len(it), dtype=torch.int32, device=dev)
+        p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        p0.record(stream)
+        plan.predict_run(d_o, d_i, T(rt), d_m, d_v, d_e, d_x, d_s, CF_SIGS_OWN, d_mse, d_kk,
+                         stream=stream.cuda_stream)
+        p1.record(stream)
+        p1.synchronize()
+        pms = p0.elapsed_time(p1)
+        total_pms += pms
         kf = ks.astype(np.float64)
         out[name] = {"users": int(len(ks)), "k_mean": float(kf.mean()), "ms": ms,
                      "users_per_s": len(ks) / ms * 1e3,
                      "GFLOPs_9k3": float(np.sum(9 * kf ** 3)) / ms / 1e6,
-                     "m_mean": float(d_m.float().mean().item())}
+                     "m_mean": float(d_m.float().mean().item()),
+                     "predict_ms": pms, "ratings": int(len(it)), "ratings_per_s": len(it) / pms * 1e3,
+                     "kk_mean": float(d_kk.float().mean().item()),
+                     "nan_predictions": int(torch.isnan(d_mse).sum().item())}
         plan.close()
         del d_x
         torch.cuda.empty_cache()
     out["users_per_s"] = args.c5_users / total_ms * 1e3
     out["ms"] = total_ms
+    out["predict_ms"] = total_pms
+    out["ratings_per_s"] = int(k.sum()) / total_pms * 1e3
     return out
 
 

@@ -79,6 +79,7 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_knn) (void)hipFree(ctx->d_knn);
     if (ctx->d_spill) (void)hipFree(ctx->d_spill);
+    if (ctx->d_pspill) (void)hipFree(ctx->d_pspill);
     if (ctx->d_tri) (void)hipFree(ctx->d_tri);
     for (hipEvent_t& e : ctx->knn_ev)
         if (e) (void)hipEventDestroy(e);

@@ -33,6 +33,9 @@ struct cf_ctx {
     void* d_spill = nullptr;
     size_t spill_bytes = 0;
     bool spill_debug = false;   // cf_debug_spill: phase counters in the workspace header
+    // predictor spill-path workspace (per-user Q / Gbar slots, per-workgroup LDL^T), grown on demand.
+    void* d_pspill = nullptr;
+    size_t pspill_bytes = 0;
     // tridiagonal eigen path scratch (T, QL records), grown on demand; eigen method
     void* d_tri = nullptr;
     size_t tri_bytes = 0;
@@ -155,6 +158,13 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
                       const T* d_evals, const uint64_t* d_evec_off, const T* d_evecs,
                       const T* d_sigtab, int sig_mode, float* d_mse, int32_t* d_kk,
                       double* d_pred, hipStream_t stream);
+
+// Predictor for the spill bucket (CF_MAX_K < k <= CF_SPILL_MAX_K), cf_predict_spill.hip.
+template <typename T>
+int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, const uint64_t* d_item_off,
+                            const uint32_t* d_items, const float* d_ratings, const int32_t* d_m,
+                            const T* d_evals, const uint64_t* d_evec_off, const T* d_evecs, const T* d_sigtab,
+                            int sig_mode, float* d_mse, int32_t* d_kk, double* d_pred, hipStream_t stream);
 
 int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64_t* d_user_off,
                    const uint32_t* d_item, const float* d_rating, int integer_ratings, float w_min,

@@ -1082,11 +1082,11 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
     int rc = CF_OK;
     for (const cf_bucket& b : plan->buckets) {
         if (b.count == 0) continue;
-        if (b.emax == kSpillBucket) {
-            rc = cf_set_error(ctx, CF_ERANGE, "cf_predict: users with k > " + std::to_string(CF_MAX_K) +
-                                                  " items are eigen-only (spill path); the predictor needs k <= " +
-                                                  std::to_string(CF_MAX_K));
-            break;
+        if (b.emax == kSpillBucket) {   // k > CF_MAX_K: HBM-workspace predictor
+            rc = cf_launch_predict_spill<T>(ctx, plan, b, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off,
+                                            d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, stream);
+            if (rc != CF_OK) break;
+            continue;
         }
         args.first = b.first;
         const int lmax = std::max<int>(2, 16 * b.emax);

@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
     for (uint32_t u = 0; u < n_users; ++u) {
         const auto& r = recs[u];
         const uint32_t k = (uint32_t)r.movies.size();
-        if (k > CF_MAX_K) cfcli::die("record with k > 192 is outside the supported buckets");
+        if (k > CF_SPILL_MAX_K) cfcli::die("record with k > 3072 is outside the supported buckets");
         rec_of_user[r.user] = u;   // a later record of the same user replaces it (:472)
         m[u] = (int32_t)r.evals.size();
         auto& ur = urat[r.user];

@@ -33,8 +33,7 @@ def gram_cond(items, evals, U, sigtab_row, W, r):
     return np.linalg.cond(G.T @ G)
 
 
-def build_case(density, ks, seed):
-    n_items = 220
+def build_case(density, ks, seed, n_items=220):
     W = cases.item_graph(n_items, density, seed=seed, isolated_frac=0.02)
     off, items = cases.user_items(n_items, ks, seed=seed + 1)
     rat = cases.ratings_for(len(items), seed + 2)
@@ -165,3 +164,62 @@ def test_predict_wide_complement_full_rank(gpu_ctx):
                 bad.append((u, r, float(mse_g[g]), float(mse_o[r])))
     assert not bad, bad[:10]
     assert n_wide > 20, n_wide
+
+
+def _compare_users(off, items, rat, m, blocks, sigs, sigtab, mode, W, mse_g, kk_g, users):
+    """kk exact; c = 0 NaN on both sides; |d mse| <= 1e-6 max(1, mse) where cond <= 1e8."""
+    n_good = n_ill = 0
+    bad = []
+    for u in users:
+        b, e = int(off[u]), int(off[u + 1])
+        it = items[b:e].astype(np.int64)
+        ev, U = blocks[u]
+        ev_full = np.zeros(m[u])
+        ev_full[: min(m[u], e - b)] = ev[: min(m[u], e - b)]
+        tab = sigtab[: e - b] if mode == CF_SIGS_COMPAT else sigtab[b:e]
+        mse_o, kk_o, _ = orc.predict_user(it, rat[b:e], ev_full, U, tab, W)
+        for r in range(e - b):
+            g = b + r
+            if kk_g[g] != kk_o[r]:
+                bad.append((u, r, "kk", kk_g[g], kk_o[r]))
+                continue
+            if kk_o[r] == 0:
+                if not (np.isnan(mse_g[g]) and np.isnan(mse_o[r])):
+                    bad.append((u, r, "c=0 not NaN", mse_g[g], mse_o[r]))
+                continue
+            cond = gram_cond(it, ev_full, U, tab[r], W, r)
+            if cond <= 1e8:
+                if np.isnan(mse_g[g]) or np.isnan(mse_o[r]):
+                    bad.append((u, r, "nan", mse_g[g], mse_o[r], cond))
+                    continue
+                n_good += 1
+                if abs(float(mse_g[g]) - float(mse_o[r])) > 1e-6 * max(1.0, float(mse_o[r])):
+                    bad.append((u, r, "mse", float(mse_g[g]), float(mse_o[r]), cond))
+            else:
+                n_ill += 1
+    return n_good, n_ill, bad
+
+
+@pytest.mark.parametrize("density,mode,wlim,min_good", [(0.6, CF_SIGS_COMPAT, None, 200),
+                                                        (0.05, CF_SIGS_OWN, None, 0),
+                                                        (0.05, CF_SIGS_OWN, 0.3, 200),
+                                                        (0.1, CF_SIGS_OWN, 0.2, 200),
+                                                        (0.5, CF_SIGS_OWN, 0.3, 200)])
+def test_predict_spill_users_match_oracle(gpu_ctx, density, mode, wlim, min_good):
+    """Users above CF_MAX_K (the eigen spill bucket) take the HBM-workspace predictor
+    (cf_predict_spill.hip) in the same call as LDS-path users.  Dense graphs exercise its
+    Woodbury form (small complements, tiled P for large ones), the sparse graph its
+    dense path (columns dropped by the zero-column filter, rank-deficient Gram
+    matrices: almost all rank-deficient at the reference's own w_lim, hence min_good = 0;
+    a low w_lim keeps them full rank), w_lim = 0.3 on a dense graph wide complements."""
+    ks = [300, 193, 150, 257, 64, 210]
+    W, off, items, rat, m, sigs, evals, evec_off, evecs, blocks = build_case(density, ks, seed=80, n_items=400)
+    sigtab = sigs.copy() if wlim is None else np.full_like(sigs, wlim)
+    gpu_ctx.upload_graph_dense(W)
+    mse_g, kk_g, _ = gpu_ctx.predict_precomp(off, items, rat, m, evals, evec_off, evecs, sigtab,
+                                             sig_mode=mode, want_pred=True)
+    n_good, n_ill, bad = _compare_users(off, items, rat, m, blocks, sigs, sigtab, mode, W, mse_g, kk_g,
+                                        range(len(ks)))
+    assert not bad, bad[:10]
+    assert n_good >= min_good, (n_good, n_ill)
+    print(f"spill density={density} mode={mode} wlim={wlim} well-conditioned={n_good} ill-conditioned={n_ill}")
