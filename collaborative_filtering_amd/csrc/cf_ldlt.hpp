@@ -23,13 +23,17 @@ constexpr int kNB = 16;   // LDL^T panel width
 // block has cancelled to exact zeros gives finite, clamped garbage like the
 // reference's, not inf - inf = NaN.  Called by the whole block; starts and ends
 // synchronised.
+//
+// ldlt_bordered_range factors only the columns [k0, k1) (all rows below them, trailing
+// updates confined to columns < k1): a caller blocking the factorisation in wider panels
+// applies the update of columns >= k1 itself.  ldlt_bordered = the full range.
 template <int kThreads>
-__device__ void ldlt_bordered(double* A, int L, int nrows) {
+__device__ void ldlt_bordered_range(double* A, int L, int nrows, int k0, int k1) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    for (int kb = 0; kb < L; kb += kNB) {
-        const int b = min(kNB, L - kb);
+    for (int kb = k0; kb < k1; kb += kNB) {
+        const int b = min(kNB, k1 - kb);
         // (1) diagonal block, unblocked LDL^T, in wave 0's registers: lane i < b holds
         //     row kb + i; column j is broadcast by shuffles.
         if (wave == 0) {
@@ -82,7 +86,7 @@ __device__ void ldlt_bordered(double* A, int L, int nrows) {
         {
             const int r0 = kb + b;
             const int nr = nrows - r0;
-            const int nc = L - r0;
+            const int nc = k1 - r0;
             if (nc > 0) {
                 const int tr = (nr + 3) >> 2, tcn = (nc + 3) >> 2;
                 for (int tix = tid; tix < tr * tcn; tix += kThreads) {
@@ -98,7 +102,7 @@ __device__ void ldlt_bordered(double* A, int L, int nrows) {
 #pragma unroll
                     for (int x = 0; x < 4; ++x) {
                         Ar[x] = A + tri(min(r0 + 4 * ti + x, nrows - 1), 0);
-                        Aq[x] = A + tri(min(r0 + 4 * tq + x, L - 1), 0);
+                        Aq[x] = A + tri(min(r0 + 4 * tq + x, k1 - 1), 0);
                     }
                     for (int j = kb; j < kb + b; ++j) {
                         double vr[4], vq[4];
@@ -118,7 +122,7 @@ __device__ void ldlt_bordered(double* A, int L, int nrows) {
 #pragma unroll
                         for (int y = 0; y < 4; ++y) {
                             const int gi = r0 + 4 * ti + x, gq = r0 + 4 * tq + y;
-                            if (gi < nrows && gq < L && gq <= gi) A[tri(gi, gq)] -= acc[x][y];
+                            if (gi < nrows && gq < k1 && gq <= gi) A[tri(gi, gq)] -= acc[x][y];
                         }
                 }
             }
@@ -127,3 +131,7 @@ __device__ void ldlt_bordered(double* A, int L, int nrows) {
     }
 }
 
+template <int kThreads>
+__device__ void ldlt_bordered(double* A, int L, int nrows) {
+    ldlt_bordered_range<kThreads>(A, L, nrows, 0, L);
+}

@@ -13,7 +13,8 @@
 //                        Q = U T1 T2 ... of U's leading Lu columns, T = I - su(G - I) -
 //                        diag(G - I)/2 (upper triangular: Q's leading lim columns span
 //                        U's for every row; each step squares the orthogonality error);
-//                        g = Q^T r, h = Q^T 1.  Products are 64 x 64-tiled fp64 GEMMs.
+//                        g = Q^T r, h = Q^T 1, P = Q Q^T (k x k), Q g and Q h.  Products
+//                        are 64 x 64-tiled fp64 GEMMs.
 //   spill_predict_kernel persistent workgroups claim (user, test movie) items, heaviest
 //                        users first.  C = the user's items that are out-neighbours of
 //                        the movie with w > 0.1 (:132,254-265), Cbar = the rest (it holds
@@ -22,7 +23,8 @@
 //                          pred - mean = a_r + P_{r,Cbar} K^-1 b,   K = I - P_{Cbar,Cbar},
 //                          a_r = (P y)_r - P_{r,Cbar} y_Cbar,  b = (P y)_Cbar - P_{Cbar,Cbar} y_Cbar
 //                        (Woodbury on U_CS^T U_CS = I - Q_CbarS^T Q_CbarS in the Q basis),
-//                        (P y)_a = Q_aS (g - mean h)_S.  Ratings this form does not take --
+//                        (P y)_a = Q_aS (g - mean h)_S; every entry is a gather from the
+//                        per-user tables (columns [lim, Lu) subtracted when lim < Lu).  Ratings this form does not take --
 //                        a column dropped by the filter, no basis, c = 0, or a pivot of K
 //                        below kPivMin while c >= lim -- solve the rating's own bordered
 //                        Gram matrix M = U_CS^T U_CS (complement form Gbar_SS -
@@ -43,7 +45,6 @@ constexpr float kOrthoMax = 1e-2f;   // as cf_predict.hip
 constexpr float kOrthoDone = 1e-8f;  // as cf_predict.hip
 constexpr int kMaxSteps = 4;
 constexpr int kLdsA = 1920;          // doubles of the LDS factorisation region
-constexpr int kSmallNp = 16;         // Woodbury rows up to which P entries are wave dots
 
 template <typename T>
 struct SpArgs {
@@ -65,13 +66,14 @@ struct SpArgs {
     float* mse;
     int32_t* kk;
     double* pred;
-    double* ws;              // per slot: Q0, Q1, Gbar, Gt (kmax^2 each), g, h, diag (kmax each)
+    double* ws;              // per slot: Q0, Q1 (Q and P = Q Q^T), Gbar, Gt (kmax^2 each), g, h, PG, PH
     size_t slot_d;
     int* wsi;                // per slot: lim[kmax], cpos[kmax], hdr[4] = {Lu, basis, qsel, -}
     size_t slot_i;
     double* fa;              // per workgroup factorisation region
     size_t fa_d;
     unsigned int* counter;   // work-item counter of the predict kernel
+    unsigned long long* phase;   // diagnostics (cf_debug_phases) or null: see spill_predict_kernel
 };
 
 __device__ __forceinline__ double wsum(double v) {
@@ -81,59 +83,82 @@ __device__ __forceinline__ double wsum(double v) {
 }
 
 // out(i, j, C(i, j)) over the 64 x 64 output tiles (i0, j0) of an M x N product with
-// want(i0, j0), depth kend(j0) (triangular operands end early), operands staged in LDS
-// 16 deep; thread (ty, tx) owns rows 4ty + x, columns 4tx + y of the tile.  A_LFAST: the
-// depth index is A's contiguous one (staging walks it fastest so loads coalesce).
-// Called by the whole block; ends synchronised.
-template <bool A_LFAST, class FA, class FB, class FK, class FW, class FO>
+// want(i0, j0), depth kend(j0) (triangular operands end early).  Operands are staged in
+// LDS 16 deep (row stride kSt == 16 mod 32: the four 16-lane groups of a fragment read
+// hit disjoint banks) with the next chunk's loads in flight while the current one is
+// consumed; unconditional loads from clamped indices (a guarded load would become a
+// branch with its own wait).  The products run on the fp64 matrix cores: wave w owns the
+// 32 x 32 quadrant (w >> 1, w & 1) as 2 x 2 v_mfma_f64_16x16x4_f64 tiles (A lane l =
+// A[l & 15][l >> 4], B lane l = B[l >> 4][l & 15], result q of lane l = C[(l >> 4) + 4q]
+// [l & 15]; tools/mfma_f64_probe.hip).  A_LFAST / B_LFAST: the depth index is the
+// operand's contiguous one (staging walks it fastest so loads coalesce).  Called by the
+// whole block; ends synchronised.
+using f64x4 = __attribute__((ext_vector_type(4))) double;
+constexpr int kSt = 80;
+template <bool A_LFAST, bool B_LFAST, class FA, class FB, class FK, class FW, class FO>
 __device__ void tile_gemm(int M, int N, FA ldA, FB ldB, FK kend, FW want, FO out, double* sA, double* sB) {
-    const int tid = threadIdx.x;
-    const int ty = tid >> 4, tx = tid & 15;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wr = (tid >> 6) >> 1, wc = (tid >> 6) & 1;
     const int ti = (M + 63) >> 6, tj = (N + 63) >> 6;
     for (int t = 0; t < ti * tj; ++t) {
         const int i0 = (t / tj) << 6, j0 = (t % tj) << 6;
         if (!want(i0, j0)) continue;
         const int K = kend(j0);
-        double acc[4][4];
+        f64x4 acc[2][2];
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
+        for (int x = 0; x < 2; ++x)
 #pragma unroll
-            for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+            for (int y = 0; y < 2; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
+        double ra[4], rb[4];
+        auto fetch = [&](int l0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int e = tid + q * kT;
+                const int ii = A_LFAST ? (e >> 4) : (e & 63), la = A_LFAST ? (e & 15) : (e >> 6);
+                const int jj = B_LFAST ? (e >> 4) : (e & 63), lb = B_LFAST ? (e & 15) : (e >> 6);
+                ra[q] = ldA(min(i0 + ii, M - 1), min(l0 + la, K - 1));
+                rb[q] = ldB(min(l0 + lb, K - 1), min(j0 + jj, N - 1));
+            }
+        };
+        if (K > 0) fetch(0);
         for (int l0 = 0; l0 < K; l0 += 16) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int e = tid + q * kT;
-                const int ii = A_LFAST ? (e >> 4) : (e & 63);
-                const int ll = A_LFAST ? (e & 15) : (e >> 6);
-                const int gi = i0 + ii, gl = l0 + ll;
-                sA[ll * 64 + ii] = (gi < M && gl < K) ? ldA(gi, gl) : 0.0;
-                const int jj = e & 63, lb = e >> 6;
-                const int gj = j0 + jj, glb = l0 + lb;
-                sB[lb * 64 + jj] = (gj < N && glb < K) ? ldB(glb, gj) : 0.0;
+                const int ii = A_LFAST ? (e >> 4) : (e & 63), la = A_LFAST ? (e & 15) : (e >> 6);
+                const int jj = B_LFAST ? (e >> 4) : (e & 63), lb = B_LFAST ? (e & 15) : (e >> 6);
+                sA[la * kSt + ii] = (i0 + ii < M && l0 + la < K) ? ra[q] : 0.0;
+                sB[lb * kSt + jj] = (j0 + jj < N && l0 + lb < K) ? rb[q] : 0.0;
             }
             __syncthreads();
-#pragma unroll 4
-            for (int ll = 0; ll < 16; ++ll) {
-                double va[4], vb[4];
+            if (l0 + 16 < K) fetch(l0 + 16);
 #pragma unroll
-                for (int x = 0; x < 4; ++x) {
-                    va[x] = sA[ll * 64 + 4 * ty + x];
-                    vb[x] = sB[ll * 64 + 4 * tx + x];
+            for (int ks = 0; ks < 4; ++ks) {
+                const int row = (4 * ks + (lane >> 4)) * kSt + (lane & 15);
+                double av[2], bv[2];
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {
+                    av[x] = sA[row + 32 * wr + 16 * x];
+                    bv[x] = sB[row + 32 * wc + 16 * x];
                 }
 #pragma unroll
-                for (int x = 0; x < 4; ++x)
+                for (int x = 0; x < 2; ++x)
 #pragma unroll
-                    for (int y = 0; y < 4; ++y) acc[x][y] = fma(va[x], vb[y], acc[x][y]);
+                    for (int y = 0; y < 2; ++y)
+                        acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
             }
-            __syncthreads();
+            __syncthreads();   // the chunk is consumed before the next one is staged
         }
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
+        for (int x = 0; x < 2; ++x)
 #pragma unroll
-            for (int y = 0; y < 4; ++y) {
-                const int gi = i0 + 4 * ty + x, gj = j0 + 4 * tx + y;
-                if (gi < M && gj < N) out(gi, gj, acc[x][y]);
-            }
+            for (int y = 0; y < 2; ++y)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int gi = i0 + 32 * wr + 16 * x + (lane >> 4) + 4 * q;
+                    const int gj = j0 + 32 * wc + 16 * y + (lane & 15);
+                    if (gi < M && gj < N) out(gi, gj, acc[x][y][q]);
+                }
     }
     __syncthreads();
 }
@@ -162,10 +187,32 @@ __device__ int compact(int n, F f, int* out, int* s_tmp) {
     return total;
 }
 
+// LDL^T of the packed bordered matrix (as ldlt_bordered) in panels of 64 columns: each
+// panel is factored by ldlt_bordered_range (rank-16 updates inside it), then the columns
+// right of it take one rank-64 update A22 -= L21 D1 L21^T as LDS-tiled products -- the
+// trailing matrix (L2/HBM-resident for large systems) is read and written once per 64
+// columns instead of once per 16.
+__device__ void ldlt_bordered_wide(double* A, int L, int nrows, double* sA, double* sB) {
+    for (int k0 = 0; k0 < L; k0 += 64) {
+        const int k1 = min(L, k0 + 64);
+        ldlt_bordered_range<kT>(A, L, nrows, k0, k1);
+        if (k1 < L)
+            tile_gemm<true, true>(
+                nrows - k1, L - k1,
+                [=](int i, int l) { return A[tri(k1 + i, k0 + l)] * A[tri(k0 + l, k0 + l)]; },
+                [=](int l, int j) { return A[tri(k1 + j, k0 + l)]; }, [=](int) { return k1 - k0; },
+                [](int i0, int j0) { return j0 <= i0; },
+                [=](int i, int j, double v) {
+                    if (j <= i) A[tri(k1 + i, k1 + j)] -= v;
+                },
+                sA, sB);
+    }
+}
+
 // ---- per-user tables ---------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
-    __shared__ double sA[16 * 64], sB[16 * 64];
+    __shared__ double sA[16 * kSt], sB[16 * kSt];
     __shared__ double s_ev[CF_SPILL_MAX_K];
     __shared__ int s_hdr[4];
     __shared__ float s_dev[kW];
@@ -181,7 +228,7 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
     double* Qb[2] = {slot, slot + kk2};
     double* Gb = slot + 2 * kk2;   // Gbar = U^T U over [0, Lu), full, ld Lu
     double* Gt = slot + 3 * kk2;   // Gram of the current Q (steps > 0)
-    double* gh = slot + 4 * kk2;   // g[Lu], h[Lu], diag[Lu]
+    double* gh = slot + 4 * kk2;   // g[Lu], h[Lu], PG[k], PH[k]
     int* lim = a.wsi + s * a.slot_i;
     int* cpos = lim + a.kmax;
     int* hdr = cpos + a.kmax;
@@ -220,7 +267,7 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
         const double* Q = Qb[cur];
         double* G = step == 0 ? Gb : Gt;
         float dev = 0.0f;
-        tile_gemm<false>(
+        tile_gemm<false, false>(
             Lu, Lu, [=](int i, int l) { return Q[(size_t)l * Lu + i]; },
             [=](int l, int j) { return Q[(size_t)l * Lu + j]; }, [=](int) { return k; },
             [](int, int) { return true; },
@@ -241,7 +288,7 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
         // Q' = Q T,  T(l, j) = -G(l, j) (l < j), 1.5 - G(j, j)/2 (l = j), 0 (l > j)
         const double* Gr = G;
         double* Qn = Qb[cur ^ 1];
-        tile_gemm<true>(
+        tile_gemm<true, false>(
             k, Lu, [=](int i, int l) { return Q[(size_t)i * Lu + l]; },
             [=](int l, int j) {
                 const double gv = Gr[(size_t)l * Lu + j];
@@ -265,6 +312,35 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
             gh[j] = g;
             gh[Lu + j] = h;
         }
+        __syncthreads();
+        // P = Q Q^T over [0, Lu) (k x k, ld k) into the spare Q buffer; PG = Q g, PH = Q h
+        double* P = Qb[cur ^ 1];
+        tile_gemm<true, true>(
+            k, k, [=](int i, int l) { return Q[(size_t)i * Lu + l]; },
+            [=](int l, int j) { return Q[(size_t)j * Lu + l]; }, [=](int) { return Lu; },
+            [](int i0, int j0) { return j0 <= i0; },
+            [=](int i, int j, double v) {
+                if (j <= i) {
+                    P[(size_t)i * k + j] = v;
+                    P[(size_t)j * k + i] = v;
+                }
+            },
+            sA, sB);
+        double* pg = gh + 2 * Lu;
+        for (int i = wave; i < k; i += kW) {
+            const double* qi = Q + (size_t)i * Lu;
+            double x = 0.0, y = 0.0;
+            for (int j = lane; j < Lu; j += 64) {
+                x = fma(qi[j], gh[j], x);
+                y = fma(qi[j], gh[Lu + j], y);
+            }
+            x = wsum(x);
+            y = wsum(y);
+            if (lane == 0) {
+                pg[i] = x;
+                pg[k + i] = y;
+            }
+        }
     }
     if (tid == 0) {
         hdr[0] = Lu;
@@ -276,7 +352,7 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
 // ---- per-rating predictions --------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
-    __shared__ double sA[16 * 64], sB[16 * 64];   // GEMM staging
+    __shared__ double sA[16 * kSt], sB[16 * kSt];   // GEMM staging
     __shared__ double s_la[kLdsA];
     __shared__ float s_rat[CF_SPILL_MAX_K];
     __shared__ int s_conn[CF_SPILL_MAX_K];
@@ -288,6 +364,18 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     double* fa = a.fa + (size_t)blockIdx.x * a.fa_d;
     const uint32_t total = a.nu * (uint32_t)a.kmax;
+    // Diagnostic counters (thread 0, s_memtime; no effect on outputs): cycles of
+    // {0 sets + mean, 1 column filter, 2 P entries, 3 b and K, 4 Woodbury LDL^T, 5 dense
+    // path}, counts {6 Woodbury, 7 dense, 8 sum nc (Woodbury), 9 np > 64,
+    // 10 dense by dropped column, 11 dense by pivot}.
+    unsigned long long pc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long pt = 0;
+#define SP_STAMP(ph)                                                        \
+    if (a.phase && tid == 0) {                                              \
+        const unsigned long long now = __builtin_amdgcn_s_memtime();        \
+        if ((ph) >= 0) pc[(ph) < 0 ? 0 : (ph)] += now - pt;                 \
+        pt = now;                                                           \
+    }
     for (;;) {
         if (tid == 0) s_item = atomicAdd(a.counter, 1u);
         __syncthreads();
@@ -310,10 +398,13 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
         const int Lu = hdr[0];
         const bool basis = hdr[1] != 0;
         const double* Q = slot + (hdr[2] ? kk2 : 0);
+        const double* Pm = slot + (hdr[2] ? 0 : kk2);   // P = Q Q^T over [0, Lu), k x k
         const double* Gb = slot + 2 * kk2;
         const double* gvec = slot + 4 * kk2;
         const double* hvec = gvec + Lu;
+        const double* pgv = gvec + 2 * Lu;   // (Q g)_a, then (Q h)_a at + k
         const int lim = lim_t[r];
+        SP_STAMP(-1);
 
         // connected set C (:254-265); Cbar = the rest, the movie's own row r included
         const float* nrow = a.graph + (size_t)a.items[base + r] * a.n_items;
@@ -329,6 +420,7 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
         }
         __syncthreads();
         const double mu = s_misc[0];
+        SP_STAMP(0);
         bool fast = basis && c > 0;
         if (fast) {
             // zero-column filter from the complement: column j < lim is dropped iff every
@@ -341,44 +433,39 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
                     drop |= hit == cpos[j];
                 }
             fast = !__syncthreads_or(drop);
+            if (!fast && a.phase && tid == 0) pc[10] += 1;
         }
+        SP_STAMP(1);
         if (fast) {
             const int np = nc + 1;   // rows Cbar..., then r
             const size_t need = (size_t)(nc + 2) * (nc + 3) / 2;
             double* A = need <= (size_t)kLdsA ? s_la : fa;
             const auto rowid = [&](int q) { return q < np - 1 ? s_ncon[q] : r; };
-            // E = P_S over rows [Cbar, r] into packed rows 0..nc; (P y)_a into row nc + 1
+            // E = P_S over rows [Cbar, r] into packed rows 0..nc, (P y)_a into row nc + 1:
+            // gathers from P and PG/PH, less the (usually empty) tail of columns [lim, Lu)
             const int ne = np * (np + 1) / 2;
-            const int nd = np <= kSmallNp ? ne + np : np;   // wave dots
-            for (int e = wave; e < nd; e += kW) {
-                const bool isE = np <= kSmallNp && e < ne;
-                const int pa = isE ? 0 : (np <= kSmallNp ? e - ne : e);
-                int ra = pa, rb = 0;
-                if (isE) {
-                    ra = 0;
+            for (int e = tid; e < ne + np; e += kT) {
+                double v;
+                if (e < ne) {
+                    int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+                    while (ra * (ra + 1) / 2 > e) --ra;
                     while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
-                    rb = e - ra * (ra + 1) / 2;
+                    const int ia = rowid(ra), ib = rowid(e - ra * (ra + 1) / 2);
+                    v = Pm[(size_t)ia * k + ib];
+                    const double* xa = Q + (size_t)ia * Lu;
+                    const double* xb = Q + (size_t)ib * Lu;
+                    for (int j = lim; j < Lu; ++j) v = fma(-xa[j], xb[j], v);
+                    A[e] = v;
+                } else {
+                    const int ia = rowid(e - ne);
+                    v = pgv[ia] - mu * pgv[k + ia];
+                    const double* xa = Q + (size_t)ia * Lu;
+                    for (int j = lim; j < Lu; ++j) v = fma(-xa[j], gvec[j] - mu * hvec[j], v);
+                    A[tri(np, e - ne)] = v;
                 }
-                const double* xa = Q + (size_t)rowid(ra) * Lu;
-                const double* xb = Q + (size_t)rowid(rb) * Lu;
-                double acc = 0.0;
-                if (isE)
-                    for (int j = lane; j < lim; j += 64) acc = fma(xa[j], xb[j], acc);
-                else
-                    for (int j = lane; j < lim; j += 64) acc = fma(xa[j], gvec[j] - mu * hvec[j], acc);
-                acc = wsum(acc);
-                if (lane == 0) A[isE ? e : tri(np, pa)] = acc;
             }
-            if (np > kSmallNp)
-                tile_gemm<true>(
-                    np, np, [&](int i, int l) { return Q[(size_t)rowid(i) * Lu + l]; },
-                    [&](int l, int j) { return Q[(size_t)rowid(j) * Lu + l]; }, [=](int) { return lim; },
-                    [](int i0, int j0) { return j0 <= i0; },
-                    [&](int i, int j, double v) {
-                        if (j <= i) A[tri(i, j)] = v;
-                    },
-                    sA, sB);
             __syncthreads();
+            SP_STAMP(2);
             // b_a = (P y)_a - sum_q E_aq y_q (in place of (P y)_a), a_r likewise
             for (int pa = tid; pa < np; pa += kT) {
                 double v = A[tri(np, pa)];
@@ -400,7 +487,8 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
                 A[e] = (e == tri(ra, ra) ? 1.0 : 0.0) - A[e];
             }
             __syncthreads();
-            ldlt_bordered<kT>(A, nc, nc + 2);
+            SP_STAMP(3);
+            ldlt_bordered_wide(A, nc, nc + 2, sA, sB);
             if (wave == 0) {
                 double minpiv = 1.0, dot = 0.0;
                 for (int j = lane; j < nc; j += 64) {
@@ -428,6 +516,16 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
                 if (a.pred) a.pred[base + r] = pred;
             }
             __syncthreads();
+            SP_STAMP(4);
+            if (a.phase && tid == 0) {
+                if (fast) {
+                    pc[6] += 1;
+                    pc[8] += nc;
+                    pc[9] += np > 64;
+                } else {
+                    pc[11] += 1;
+                }
+            }
             if (fast) continue;
         }
 
@@ -449,7 +547,7 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
         const int nrows = use_complement ? nc : c;
         const int* rows = use_complement ? s_ncon : s_conn;
         // A(i, j) = (U_CS^T U_CS)_ij (j <= i < L), A(L, j) = t_j, A(L + 1, j) = v_j
-        tile_gemm<false>(
+        tile_gemm<false, false>(
             L, L, [&](int i, int l) { return (double)U[(size_t)rows[l] * m + s_keep[i]]; },
             [&](int l, int j) { return (double)U[(size_t)rows[l] * m + s_keep[j]]; },
             [=](int) { return nrows; }, [](int i0, int j0) { return j0 <= i0; },
@@ -465,7 +563,7 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
             A[tri(L + 1, j)] = (double)U[(size_t)r * m + cj];
         }
         __syncthreads();
-        ldlt_bordered<kT>(A, L, L + 2);
+        ldlt_bordered_wide(A, L, L + 2, sA, sB);
         // pred = v^T M^-1 t + mean = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean (:314-327)
         if (wave == 0) {
             double dot = 0.0;
@@ -482,7 +580,12 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
             }
         }
         __syncthreads();
+        SP_STAMP(5);
+        if (a.phase && tid == 0) pc[7] += 1;
     }
+    if (a.phase && tid == 0)
+        for (int x = 0; x < 12; ++x) atomicAdd(&a.phase[x], pc[x]);
+#undef SP_STAMP
 }
 
 }  // namespace
@@ -512,12 +615,19 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
     a.mse = d_mse;
     a.kk = d_kk;
     a.pred = d_pred;
+    a.phase = ctx->d_phase;
     // workspace: counter | factorisation regions | user slots (doubles) | slot ints
     const size_t kk2 = (size_t)kmax * kmax;
-    a.slot_d = 4 * kk2 + 3 * (size_t)kmax;
+    a.slot_d = 4 * kk2 + 4 * (size_t)kmax;
     a.slot_i = 2 * (size_t)kmax + 4;
     a.fa_d = (size_t)(kmax + 2) * (kmax + 3) / 2;
-    const size_t kSlotBudget = (size_t)8 << 30, kFaBudget = (size_t)4 << 30;
+    // Slots: as many users per chunk as a third of the free HBM holds (288 GB per GPU: all
+    // of a config-5 shard's spill users at once, so the basis launch fills the chip),
+    // at least 8 GB.
+    size_t free_b = 0, total_b = 0;
+    CF_HIP_CHECK(ctx, hipMemGetInfo(&free_b, &total_b));
+    const size_t kSlotBudget = std::max<size_t>((size_t)8 << 30, (free_b + ctx->pspill_bytes) / 3);
+    const size_t kFaBudget = (size_t)4 << 30;
     const uint32_t slots = (uint32_t)std::max<size_t>(1, std::min<size_t>(b.count, kSlotBudget / (a.slot_d * 8)));
     const int blocks = (int)std::max<size_t>(32, std::min<size_t>(512, kFaBudget / (a.fa_d * 8)));
     const size_t fa_bytes = (size_t)blocks * a.fa_d * sizeof(double);
