@@ -12,20 +12,25 @@
 //      identical to the oracle's L2 -- sig_min_i from the full row (:169-177), and
 //      A = sym_lower(L2) (:164, Eigen reads the lower triangle) as a full symmetric
 //      fp64 matrix, column-major, in the workspace;
-//   2. Householder tridiagonalisation and accumulation of Q (the EISPACK tred2 order
-//      that the oracle restates, oracle/cf_oracle.cpp tridiag_householder), with the
-//      symmetric matrix-vector product thread-per-row (coalesced column reads) and the
-//      rank-2 update wave-per-column;
-//   3. implicit-shift QL (tql2, oracle tridiag_ql): one lane generates the rotation
-//      sequence of an iteration into LDS, then every thread applies it to its own rows
-//      of Q, carrying one value across the sequence (one read + one write per element);
-//   4. rank sort, sign convention sum_i v_ij >= 0 (as cf_eigen.hip), lim (:184-191),
+//   2. blocked Householder tridiagonalisation (LAPACK dsytrd/dlatrd, lower): panels of
+//      SP_NB = 32 reflectors, each panel's W built with symmetric matrix-vector products
+//      against the not-yet-updated trailing matrix, then one rank-2*SP_NB update of the
+//      trailing matrix (A -= V W^T + W V^T) with SP_CC columns staged per step;
+//   3. implicit-shift QL (tql2, oracle tridiag_ql) on Z = I: a generator wave runs the
+//      serial recurrence and publishes each iteration's rotation sequence (coefficients
+//      broadcast with v_readlane) while seven applier waves apply the previous batch of
+//      SP_QB = 16 iterations to Z in one lagged, branch-free pass (identity-padded
+//      sequences), one read + one write per element per batch;
+//   4a. eigenvectors of A = Q Z: the Householder panels applied to Z last to first in
+//      compact-WY form (I - V T V^T, SP_RC rows of V staged per step);
+//   4b. rank sort, sign convention sum_i v_ij >= 0 (as cf_eigen.hip), lim (:184-191),
 //      and the k x m row-major block, sigs, evals, m -- the same record as the LDS path.
 //
 // Everything is fp64: the matrices are too large for the fp32 Jacobi tolerance argument
 // of the LDS path, and the FP64 vector rate of MI355X equals its unpacked FP32 rate.
-// The path is bound by workspace traffic (tridiagonalisation ~k^3/3 elements read and
-// 2k^3/3 read+written, QL ~ (#rotations) x k x 16 B), see DESIGN.md.
+// Cost: tridiagonalisation 4k^3/3 flops (half in matrix-vector products), QL
+// ~ (#rotations) x 6k flops over one Z pass per 16 iterations, back-transform 2k^3; see
+// DESIGN.md 3.6.
 
 #include "cf_internal.h"
 
