@@ -501,10 +501,19 @@ int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStre
         args.first = b.first;
         int rc;
         if (b.emax == kSpillBucket) {
-            if (args.mode != kUser)
-                return cf_set_error(ctx, CF_ERANGE, "local_calc units are limited to the LDS path (n <= 192)");
+            // n > 192: the fp64 HBM-workspace solver; a8 units in its local-graph / w_lim modes
+            cf_spill_local loc{};
+            loc.mode = args.mode == kLocal ? 1 : (args.mode == kSigma ? 2 : 0);
+            loc.l2 = args.l2;
+            loc.l2_off = args.l2_off;
+            loc.pair_movie = args.pair_movie;
+            loc.pair_user = args.pair_user;
+            loc.test_off = args.test_off;
+            loc.test_user = args.test_user;
+            loc.test_rating = args.test_rating;
+            loc.wlim = args.wlim;
             rc = cf_launch_eigen_spill(ctx, plan, b, args.item_off, args.items, args.evec_off, args.m_out, args.sigs,
-                                       args.evals, args.evecs, stream);
+                                       args.evals, args.evecs, stream, &loc);
             if (rc != CF_OK) return rc;
             continue;
         }

@@ -61,6 +61,7 @@ struct SpillArgs {
     uint64_t work_stride;    // doubles per workgroup slot (>= kmax^2)
     unsigned int* counter;   // next spill user (zeroed before the launch)
     unsigned long long* phase;   // 8 counters (cf_debug_spill), summed by thread 0
+    cf_spill_local loc;      // a8 modes (loc.mode = 0: compute_eigens of a user)
 };
 
 struct SpillSmem {
@@ -117,32 +118,103 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         const int idx = S.flag[0];
         __syncthreads();
         if (idx >= (int)a.count) break;   // uniform: every wave leaves together
-        const uint32_t u = a.order[a.first + idx];
+        const int mode = a.loc.mode;
+        const uint32_t unit = a.order[a.first + idx];
+        const uint32_t u = mode == 2 ? a.loc.pair_movie[unit] : unit;   // the unit whose items index the graph
         const uint64_t base = a.item_off[u];
-        const int n = (int)(a.item_off[u + 1] - base);
-        float* Wt = a.evecs + a.evec_off[u];   // k x k scratch until the output is written
+        const int nrows = (int)(a.item_off[u + 1] - base);
+        int n = nrows;
+        if (mode == 2) {
+            // w_lim pass (local_calc.cpp:402-436): the unrated rows h of the movie's L2 (row 0,
+            // the movie itself, counts as unrated, :405-413), in row order, into S.perm
+            const uint32_t user = a.loc.pair_user[unit];
+            int h = 0;
+            for (int b0 = 0; b0 < nrows; b0 += SP_T) {
+                const int i = b0 + tid;
+                bool unr = false;
+                if (i < nrows) {
+                    if (i == 0) {
+                        unr = true;
+                    } else {
+                        const uint32_t mv = a.items[base + i];
+                        uint64_t lo = a.loc.test_off[mv];
+                        const uint64_t end = a.loc.test_off[mv + 1];
+                        uint64_t hi = end;
+                        while (lo < hi) {
+                            const uint64_t mid = (lo + hi) >> 1;
+                            if (a.loc.test_user[mid] < user) lo = mid + 1;
+                            else hi = mid;
+                        }
+                        unr = !(lo < end && a.loc.test_user[lo] == user) || a.loc.test_rating[lo] == 0.0f;
+                    }
+                }
+                const unsigned long long bal = __ballot(unr);
+                if (lane == 0) S.red[wave] = (double)__popcll(bal);
+                __syncthreads();
+                int off = h, all = 0;
+                for (int w = 0; w < SP_W; ++w) {
+                    const int cw = (int)S.red[w];
+                    if (w < wave) off += cw;
+                    all += cw;
+                }
+                if (unr) S.perm[off + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+                h += all;
+                __syncthreads();
+            }
+            n = h;
+        }
+        float* Wt = mode == 2 ? nullptr : a.evecs + a.evec_off[u];   // k x k scratch until the output is written
         auto Mat = [&](int r, int c) -> double& { return M[(size_t)c * n + r]; };
         double* Zb = M + (size_t)n * n;          // tridiagonal eigenvectors Z (column-major, then rows)
         double* Wp = Zb + (size_t)n * n;         // [SP_NB][n] panel W of the tridiagonalisation
-        auto Zm = [&](int r, int c) -> double& { return Zb[(size_t)c * n + r]; };
         unsigned long long t0 = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull, t1 = 0, t2 = 0, t3 = 0, tgen = 0;
         unsigned long long n_iter = 0;
 
+        if (mode == 2) {
+            // ---- 1s. A = L2_h L2_h^T (h x h, fp64 sums of the stored fp32 L2 rows, :425-435)
+            const float* L2m = a.loc.l2 + a.loc.l2_off[u];
+            const int npk = n * (n + 1) / 2;
+            for (int e = wave; e < npk; e += SP_W) {
+                int p = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+                while (p * (p + 1) / 2 > e) --p;
+                while ((p + 1) * (p + 2) / 2 <= e) ++p;
+                const int q = e - p * (p + 1) / 2;
+                const float* rp = L2m + (size_t)S.perm[p] * nrows;
+                const float* rq = L2m + (size_t)S.perm[q] * nrows;
+                double acc = 0.0;
+                for (int j = lane; j < nrows; j += 64) acc = fma((double)rp[j], (double)rq[j], acc);
+                acc = wave_sum(acc);
+                if (lane == 0) {
+                    Mat(p, q) = acc;
+                    Mat(q, p) = acc;
+                }
+            }
+            __syncthreads();
+        } else {
         // ---- 1. W_u, degrees, s, L2, sig_min, A = sym_lower(L2) ------------------------
+        // mode 1 (local graph, local_calc.cpp:326-360): W(i, j) = w(item_i -> item_j) if
+        // > 0.1, column 0 mirrors row 0 (W(i, 0) = w(movie -> item_i), W(0, 0) = 0), and no
+        // 0 -> 1 degree rule.
         for (int i = wave; i < n; i += SP_W) {
             const float* grow = a.graph + (size_t)a.items[base + i] * a.n_items;
+            const float* grow0 = a.graph + (size_t)a.items[base] * a.n_items;
             double ds = 0.0;
             for (int j = lane; j < n; j += 64) {
-                const float w = grow[a.items[base + j]];
+                float w = grow[a.items[base + j]];
+                if (mode == 1) {
+                    if (j == 0) w = (i == 0) ? 0.0f : grow0[a.items[base + i]];
+                    if (!((double)w > 0.1)) w = 0.0f;
+                }
                 Wt[(size_t)i * n + j] = w;
                 ds += (double)w;
             }
             ds = wave_sum(ds);
-            if (lane == 0) S.rs[i] = (ds == 0.0) ? 1.0 : ds;   // (:137-140)
+            if (lane == 0) S.rs[i] = (ds == 0.0 && mode == 0) ? 1.0 : ds;   // (:137-140)
         }
         __syncthreads();
         for (int i = tid; i < n; i += SP_T) S.rc[i] = sqrt(1.0 / S.rs[i]);   // (:149-153)
         __syncthreads();
+        float* L2out = mode == 1 ? a.loc.l2 + a.loc.l2_off[u] : nullptr;
         for (int i = wave; i < n; i += SP_W) {
             const double si = S.rc[i], di = S.rs[i];
             double sq = 0.0;
@@ -150,6 +222,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 const double l = (j == i ? di : 0.0) - (double)Wt[(size_t)i * n + j];
                 const double l2 = (si * l) * S.rc[j];   // (:155)
                 sq += l2 * l2;
+                if (L2out) L2out[(size_t)i * n + j] = (float)l2;   // unsymmetrised, for the w_lim pass
                 if (j <= i) {
                     Mat(i, j) = l2;
                     Mat(j, i) = l2;
@@ -159,6 +232,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             if (lane == 0) S.sig[i] = sqrtf((float)sq);   // (:172-176)
         }
         __syncthreads();
+        }   // mode != 2
 
         if (tid == 0) t1 = __builtin_amdgcn_s_memtime();
         // ---- 2. blocked Householder tridiagonalisation (LAPACK dsytrd/dlatrd, lower) ---------
@@ -363,6 +437,46 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         if (tid == 0) {
             S.d[n - 1] = M[(size_t)(n - 1) * n + (n - 1)];
             S.e[n - 1] = 0.0;
+        }
+        if (mode == 2) {
+            // w_lim = sqrt(lambda_min(L2_h L2_h^T)) (:435-436): the smallest eigenvalue of
+            // tridiag(d, e) by Sturm-count multisection, 65 sub-intervals per round over the
+            // lanes of wave 0 (12 rounds shrink the Gershgorin interval by 65^12 ~ 5e21)
+            __syncthreads();
+            if (wave == 0) {
+                double lo = 1e300, hi = -1e300;
+                for (int i = lane; i < n; i += 64) {
+                    const double rad = (i > 0 ? fabs(S.e[i - 1]) : 0.0) + (i < n - 1 ? fabs(S.e[i]) : 0.0);
+                    lo = fmin(lo, S.d[i] - rad);
+                    hi = fmax(hi, S.d[i] + rad);
+                }
+                for (int off = 32; off >= 1; off >>= 1) {
+                    lo = fmin(lo, __shfl_xor(lo, off));
+                    hi = fmax(hi, __shfl_xor(hi, off));
+                }
+                for (int it = 0; it < 12 && hi - lo > 4.0 * eps * fmax(fabs(lo), fabs(hi)); ++it) {
+                    const double x = lo + (hi - lo) * (double)(lane + 1) / 65.0;
+                    int cnt = 0;
+                    double q = 1.0;
+                    for (int i = 0; i < n; ++i) {
+                        const double ei = i > 0 ? S.e[i - 1] : 0.0;
+                        q = (S.d[i] - x) - (i > 0 ? ei * ei / q : 0.0);
+                        if (q == 0.0) q = -1e-300;   // x is an eigenvalue of the leading block
+                        cnt += q < 0.0;
+                    }
+                    const unsigned long long hit = __ballot(cnt >= 1);   // lambda_min < x_lane
+                    const int f = hit ? __ffsll((long long)hit) - 1 : 64;
+                    const double xf = __shfl(x, f < 64 ? f : 63);
+                    const double xp = __shfl(x, f > 0 ? f - 1 : 0);
+                    const double nlo = f > 0 ? xp : lo;
+                    const double nhi = f < 64 ? xf : hi;
+                    lo = nlo;
+                    hi = nhi;
+                }
+                if (lane == 0) a.loc.wlim[unit] = (float)sqrt(fmax(0.5 * (lo + hi), 0.0));
+            }
+            __syncthreads();
+            continue;
         }
         // Z = I: tql2 accumulates the tridiagonal eigenvectors, Q is applied afterwards
         for (size_t idx = tid; idx < (size_t)n * n; idx += SP_T) Zb[idx] = 0.0;
@@ -761,12 +875,14 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             for (lim = 0; lim < n; ++lim)
                 if (S.d[S.perm[lim]] > (double)smm) break;   // (:186-188)
             if (lim < 2) lim = 2;                             // (:190-191)
+            if (mode == 1) lim = n;   // local_calc keeps every eigenpair (es(ll2), local_calc.cpp:378)
             S.flag[3] = lim;
             a.m_out[u] = lim;
         }
         __syncthreads();
         const int mm = S.flag[3];
-        for (int i = tid; i < n; i += SP_T) a.sigs[base + i] = (float)((double)S.sig[i] + 0.01);
+        if (mode == 0)
+            for (int i = tid; i < n; i += SP_T) a.sigs[base + i] = (float)((double)S.sig[i] + 0.01);
         for (int r = tid; r < mm; r += SP_T) a.evals[base + r] = (float)S.d[S.perm[r]];
         for (size_t idx = tid; idx < (size_t)n * mm; idx += SP_T) {
             const int i = (int)(idx / mm), r = (int)(idx - (size_t)i * mm);
@@ -792,7 +908,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
 
 int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, const uint64_t* d_item_off,
                           const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs,
-                          float* d_evals, float* d_evecs, hipStream_t stream) {
+                          float* d_evals, float* d_evecs, hipStream_t stream, const cf_spill_local* loc) {
     if (b.count == 0) return CF_OK;
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
@@ -830,6 +946,7 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     a.counter = reinterpret_cast<unsigned int*>(ctx->d_spill);
     a.work = reinterpret_cast<double*>(static_cast<char*>(ctx->d_spill) + 256);
     a.work_stride = stride;
+    if (loc) a.loc = *loc;
     a.phase = ctx->spill_debug ? reinterpret_cast<unsigned long long*>(static_cast<char*>(ctx->d_spill) + 64) : nullptr;
     CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), stream));
     const size_t lds = sizeof(SpillSmem);

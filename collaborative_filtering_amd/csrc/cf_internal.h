@@ -135,9 +135,29 @@ int cf_launch_local_sigma(cf_ctx* ctx, const cf_plan* pair_plan, const uint64_t*
                           const uint64_t* d_test_off, const uint32_t* d_test_user,
                           const float* d_test_rating, float* d_wlim, hipStream_t stream);
 
+// a8 (local_calc) modes of the spill eigen kernel for units with n > CF_MAX_K.
+struct cf_spill_local {
+    int mode;                      // 1: the movie's local graph (all n eigenpairs, L2 kept);
+                                   // 2: w_lim of a (movie, test user) pair (eigenvalue only)
+    float* l2;                     // per movie n x n row-major L2 (mode 1 writes, mode 2 reads)
+    const uint64_t* l2_off;
+    const uint32_t* pair_movie;    // mode 2: unit -> movie unit, test user
+    const uint32_t* pair_user;
+    const uint64_t* test_off;      // mode 2: test ratings, CSR over compact item ids
+    const uint32_t* test_user;
+    const float* test_rating;
+    float* wlim;                   // mode 2 output per pair
+};
 int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, const uint64_t* d_item_off,
                           const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs,
-                          float* d_evals, float* d_evecs, hipStream_t stream);
+                          float* d_evals, float* d_evecs, hipStream_t stream, const cf_spill_local* loc = nullptr);
+// a8 predictor for (movie, test user) pairs of units with n > CF_MAX_K (cf_predict_spill.hip).
+int cf_launch_local_predict_spill(cf_ctx* ctx, uint32_t n_pairs, int nmax, const uint32_t* d_pair_movie,
+                                  const uint32_t* d_pair_user, const uint64_t* d_pair_out, const uint64_t* d_item_off,
+                                  const uint32_t* d_items, const float* d_evals, const uint64_t* d_evec_off,
+                                  const float* d_evecs, const float* d_wlim, const uint64_t* d_test_off,
+                                  const uint32_t* d_test_user, const float* d_test_rating, float* d_mse,
+                                  int32_t* d_kk, double* d_pred, int32_t* d_lim, hipStream_t stream);
 int cf_tri_prepare(cf_ctx* ctx, cf_plan* plan, const uint64_t* item_off);
 int cf_launch_eigen_tri(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,
                         const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals, float* d_evecs,

@@ -177,10 +177,10 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
     std::vector<uint64_t> pair_out, pair_k;
     for (uint32_t v = 0; v < n_movies; ++v) {
         const uint64_t n = movie_off[v + 1] - movie_off[v];
-        if (n > CF_MAX_K)
+        if (n > CF_SPILL_MAX_K)
             return cf_set_error(ctx, CF_ERANGE, "cf_local_calc: movie unit " + std::to_string(v) + " has " +
-                                                    std::to_string(n - 1) +
-                                                    " out-neighbours; the LDS path supports n <= 192");
+                                                    std::to_string(n - 1) + " out-neighbours; at most " +
+                                                    std::to_string(CF_SPILL_MAX_K - 1) + " are supported");
         sq_off[v + 1] = sq_off[v] + n * n;
         if (n < 3) continue;
         const uint32_t m = movie_items[movie_off[v]];
@@ -192,7 +192,27 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
             pair_k.push_back(n);
         }
     }
+    // pairs of units with n <= CF_MAX_K first (LDS predictor), then the rest (spill predictor)
+    {
+        std::vector<uint32_t> idx(pair_movie.size());
+        for (uint32_t i = 0; i < idx.size(); ++i) idx[i] = i;
+        std::stable_partition(idx.begin(), idx.end(), [&](uint32_t i) { return pair_k[i] <= CF_MAX_K; });
+        std::vector<uint32_t> pm(idx.size()), pu(idx.size());
+        std::vector<uint64_t> po(idx.size()), pk(idx.size());
+        for (size_t i = 0; i < idx.size(); ++i) {
+            pm[i] = pair_movie[idx[i]];
+            pu[i] = pair_user[idx[i]];
+            po[i] = pair_out[idx[i]];
+            pk[i] = pair_k[idx[i]];
+        }
+        pair_movie.swap(pm);
+        pair_user.swap(pu);
+        pair_out.swap(po);
+        pair_k.swap(pk);
+    }
     const uint32_t n_pairs = (uint32_t)pair_movie.size();
+    uint32_t n_small = 0;
+    while (n_small < n_pairs && pair_k[n_small] <= CF_MAX_K) ++n_small;
     // movie plan (units with n < 3 are excluded by giving them k = 0)
     std::vector<uint64_t> plan_off(n_movies + 1, 0);
     for (uint32_t v = 0; v < n_movies; ++v) {
@@ -254,7 +274,21 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
                                         static_cast<const uint32_t*>(d_tuser.p),
                                         static_cast<const float*>(d_trat.p), static_cast<float*>(d_wlim.p), 0)))
             break;
-        if (n_pairs) {
+        if (n_pairs > n_small) {
+            int nbig = 3;
+            for (uint32_t p = n_small; p < n_pairs; ++p) nbig = std::max<int>(nbig, (int)pair_k[p]);
+            if ((rc = cf_launch_local_predict_spill(
+                     ctx, n_pairs - n_small, nbig, static_cast<const uint32_t*>(d_pm.p) + n_small,
+                     static_cast<const uint32_t*>(d_pu.p) + n_small, static_cast<const uint64_t*>(d_po.p) + n_small,
+                     moff, mit, static_cast<const float*>(d_evals.p), sqo, static_cast<const float*>(d_evecs.p),
+                     static_cast<const float*>(d_wlim.p) + n_small, static_cast<const uint64_t*>(d_toff.p),
+                     static_cast<const uint32_t*>(d_tuser.p), static_cast<const float*>(d_trat.p),
+                     static_cast<float*>(d_mse.p), static_cast<int32_t*>(d_kk.p),
+                     pred ? static_cast<double*>(d_pred.p) : nullptr, lim ? static_cast<int32_t*>(d_lim.p) : nullptr,
+                     0)))
+                break;
+        }
+        if (n_small) {
             LocalPredArgs la{};
             la.pair_movie = static_cast<const uint32_t*>(d_pm.p);
             la.pair_user = static_cast<const uint32_t*>(d_pu.p);
@@ -273,7 +307,7 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
             la.pred = pred ? static_cast<double*>(d_pred.p) : nullptr;
             la.lim_out = lim ? static_cast<int32_t*>(d_lim.p) : nullptr;
             uint64_t nmax = 3;
-            for (uint64_t k : pair_k) nmax = std::max(nmax, k);
+            for (uint32_t p = 0; p < n_small; ++p) nmax = std::max(nmax, pair_k[p]);
             la.lmax = (int)nmax;
             const size_t lds = sizeof(double) * ((size_t)(nmax + 2) * (nmax + 3) / 2 + 4) +
                                CF_MAX_K * (sizeof(float) + sizeof(int)) + 8 * sizeof(int);
@@ -286,8 +320,8 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
                 rc = cf_set_error(ctx, CF_EHIP, "local predict LDS attribute");
                 break;
             }
-            const uint32_t blocks = std::min<uint32_t>(n_pairs, 4096u);
-            hipLaunchKernelGGL(local_predict_kernel, dim3(blocks), dim3(kThreads), lds, 0, la, n_pairs);
+            const uint32_t blocks = std::min<uint32_t>(n_small, 4096u);
+            hipLaunchKernelGGL(local_predict_kernel, dim3(blocks), dim3(kThreads), lds, 0, la, n_small);
             if (hipGetLastError() != hipSuccess) {
                 rc = cf_set_error(ctx, CF_EHIP, "local_predict_kernel launch");
                 break;

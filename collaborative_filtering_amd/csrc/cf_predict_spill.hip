@@ -588,6 +588,132 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
 #undef SP_STAMP
 }
 
+// ---- a8: local_calc's predictor for units with n > CF_MAX_K ----------------------------
+// local_predict_kernel (cf_local.hip) with the bordered Gram matrix in HBM: per (movie,
+// test user) pair, the rated rows C of the movie's n x n eigenvector block (row 0 = the
+// movie, its rating unknown, :400-405), lim = first eigenvalue > w_lim (>= 2, :444-451),
+// M = U_CS^T U_CS over S = [0, lim) with no zero-column filter (:455-485), pred = v^T
+// M^-1 U_CS^T (r - mean) + mean with v = U(0, S), clamp, mse (float), kk = |C| (:487-521).
+struct LocSpArgs {
+    const uint32_t* pair_movie;
+    const uint32_t* pair_user;
+    const uint64_t* pair_out;
+    const uint64_t* item_off;
+    const uint32_t* items;
+    const float* evals;
+    const uint64_t* evec_off;
+    const float* evecs;
+    const float* wlim;
+    const uint64_t* test_off;
+    const uint32_t* test_user;
+    const float* test_rating;
+    float* mse;
+    int32_t* kk;
+    double* pred;
+    int32_t* lim_out;
+    uint32_t n_pairs;
+    double* fa;
+    size_t fa_d;
+    unsigned int* counter;
+};
+
+__global__ __launch_bounds__(kT) void local_predict_spill_kernel(LocSpArgs a) {
+    __shared__ double sA[16 * kSt], sB[16 * kSt];
+    __shared__ double s_la[kLdsA];
+    __shared__ float s_rat[CF_SPILL_MAX_K];
+    __shared__ int s_c[CF_SPILL_MAX_K];
+    __shared__ double s_misc[4];
+    __shared__ int s_tmp[kW];
+    __shared__ int s_lim;
+    __shared__ unsigned int s_item;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double* fa = a.fa + (size_t)blockIdx.x * a.fa_d;
+    for (;;) {
+        if (tid == 0) s_item = atomicAdd(a.counter, 1u);
+        __syncthreads();
+        const uint32_t p = s_item;
+        __syncthreads();
+        if (p >= a.n_pairs) break;   // every wave of every block reaches this exit
+        const uint32_t mv = a.pair_movie[p];
+        const uint32_t user = a.pair_user[p];
+        const uint64_t base = a.item_off[mv];
+        const int n = (int)(a.item_off[mv + 1] - base);
+        const float* U = a.evecs + a.evec_off[mv];
+        // ratings of the local graph's rows by this user; row 0 is the unknown (:400-405)
+        for (int i = tid; i < n; i += kT) {
+            const uint32_t it = a.items[base + i];
+            uint64_t lo = a.test_off[it];
+            const uint64_t end = a.test_off[it + 1];
+            uint64_t hi = end;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (a.test_user[mid] < user) lo = mid + 1;
+                else hi = mid;
+            }
+            const float v = (lo < end && a.test_user[lo] == user) ? a.test_rating[lo] : 0.0f;
+            if (i == 0) s_misc[1] = (double)v;
+            s_rat[i] = i == 0 ? 0.0f : v;
+        }
+        if (tid == 0) {
+            const double wl = (double)a.wlim[p];
+            int lim = 0;
+            for (; lim < n; ++lim)
+                if ((double)a.evals[base + lim] > wl) break;
+            s_lim = lim < 2 ? 2 : lim;
+        }
+        __syncthreads();
+        const int c = compact(n, [&](int i) { return s_rat[i] != 0.0f; }, s_c, s_tmp);   // (:470-479)
+        const int L = s_lim;
+        if (wave == 0) {
+            double sum = 0.0;
+            for (int i = lane; i < c; i += 64) sum += (double)s_rat[s_c[i]];
+            sum = wsum(sum);
+            if (lane == 0) s_misc[0] = sum / (double)c;   // 0/0 = NaN when nothing is rated (:487)
+        }
+        __syncthreads();
+        const double mean = s_misc[0];
+        const size_t need = (size_t)(L + 2) * (L + 3) / 2;
+        double* A = need <= (size_t)kLdsA ? s_la : fa;
+        // bordered Gram: A[i][j] = (U_C^T U_C)_ij (j <= i < L), A[L][j] = t_j, A[L+1][j] = v_j
+        tile_gemm<false, false>(
+            L, L, [&](int i, int l) { return (double)U[(size_t)s_c[l] * n + i]; },
+            [&](int l, int j) { return (double)U[(size_t)s_c[l] * n + j]; }, [=](int) { return c; },
+            [](int i0, int j0) { return j0 <= i0; },
+            [&](int i, int j, double v) {
+                if (j <= i) A[tri(i, j)] = v;
+            },
+            sA, sB);
+        for (int b = tid; b < L; b += kT) {
+            double t = 0.0;
+            for (int q = 0; q < c; ++q) {
+                const int ri = s_c[q];
+                t = fma((double)U[(size_t)ri * n + b], (double)s_rat[ri] - mean, t);
+            }
+            A[tri(L, b)] = t;
+            A[tri(L + 1, b)] = (double)U[b];   // vv = row 0 (:465-466)
+        }
+        __syncthreads();
+        ldlt_bordered_wide(A, L, L + 2, sA, sB);
+        if (wave == 0) {
+            double dot = 0.0;
+            for (int j = lane; j < L; j += 64) dot = fma(A[tri(L, j)] * A[tri(L + 1, j)], A[tri(j, j)], dot);
+            dot = wsum(dot);
+            if (lane == 0) {
+                double pred = dot + mean;
+                if (pred > 5) pred = 5;   // (:494-497)
+                if (pred < 1) pred = 1;
+                const double d = s_misc[1] - pred;
+                const uint64_t o = a.pair_out[p];
+                a.mse[o] = (float)(d * d);
+                a.kk[o] = c;
+                if (a.pred) a.pred[o] = pred;
+                if (a.lim_out) a.lim_out[o] = L;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 template <typename T>
@@ -667,3 +793,48 @@ template int cf_launch_predict_spill<double>(cf_ctx*, const cf_plan*, const cf_b
                                              const uint32_t*, const float*, const int32_t*, const double*,
                                              const uint64_t*, const double*, const double*, int, float*,
                                              int32_t*, double*, hipStream_t);
+
+int cf_launch_local_predict_spill(cf_ctx* ctx, uint32_t n_pairs, int nmax, const uint32_t* d_pair_movie,
+                                  const uint32_t* d_pair_user, const uint64_t* d_pair_out, const uint64_t* d_item_off,
+                                  const uint32_t* d_items, const float* d_evals, const uint64_t* d_evec_off,
+                                  const float* d_evecs, const float* d_wlim, const uint64_t* d_test_off,
+                                  const uint32_t* d_test_user, const float* d_test_rating, float* d_mse,
+                                  int32_t* d_kk, double* d_pred, int32_t* d_lim, hipStream_t stream) {
+    if (n_pairs == 0) return CF_OK;
+    if (nmax > CF_SPILL_MAX_K) return cf_set_error(ctx, CF_ERANGE, "local predict spill: n above CF_SPILL_MAX_K");
+    LocSpArgs a{};
+    a.pair_movie = d_pair_movie;
+    a.pair_user = d_pair_user;
+    a.pair_out = d_pair_out;
+    a.item_off = d_item_off;
+    a.items = d_items;
+    a.evals = d_evals;
+    a.evec_off = d_evec_off;
+    a.evecs = d_evecs;
+    a.wlim = d_wlim;
+    a.test_off = d_test_off;
+    a.test_user = d_test_user;
+    a.test_rating = d_test_rating;
+    a.mse = d_mse;
+    a.kk = d_kk;
+    a.pred = d_pred;
+    a.lim_out = d_lim;
+    a.n_pairs = n_pairs;
+    a.fa_d = (size_t)(nmax + 2) * (nmax + 3) / 2;
+    const int blocks = (int)std::min<size_t>(
+        n_pairs, std::max<size_t>(32, std::min<size_t>(512, ((size_t)4 << 30) / (a.fa_d * 8))));
+    const size_t need = 256 + (size_t)blocks * a.fa_d * sizeof(double);
+    if (need > ctx->pspill_bytes) {
+        if (ctx->d_pspill) (void)hipFree(ctx->d_pspill);
+        ctx->d_pspill = nullptr;
+        ctx->pspill_bytes = 0;
+        CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_pspill, need));
+        ctx->pspill_bytes = need;
+    }
+    a.counter = reinterpret_cast<unsigned int*>(ctx->d_pspill);
+    a.fa = reinterpret_cast<double*>(static_cast<char*>(ctx->d_pspill) + 256);
+    CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), stream));
+    hipLaunchKernelGGL(local_predict_spill_kernel, dim3(blocks), dim3(kT), 0, stream, a);
+    CF_HIP_CHECK(ctx, hipGetLastError());
+    return CF_OK;
+}

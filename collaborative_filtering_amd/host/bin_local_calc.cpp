@@ -7,8 +7,8 @@
 //   :548-558  writer "movie user mse kk" -> out_res_<i>_of_<N>
 // Options: --pct P / positional P (percent of vertices, sampled like rand()%100 < P,
 // :266; default 100), --seed S (default: time, as the reference :566), --verbosity
-// (accepted, ignored), --nshards N.  A movie with more than 191 out-neighbours is an
-// error: the LDS path covers n <= 192 and the spill path is not built yet.
+// (accepted, ignored), --nshards N.  Movies with up to 191 out-neighbours run on the LDS
+// kernels, up to 3071 on the fp64 spill kernels; more is an error.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -72,9 +72,9 @@ int main(int argc, char** argv) {
     for (uint32_t v : order) {
         if ((unsigned)(rng() % 100) >= (unsigned)pct) continue;
         if (nb[v].size() + 1 < 3 || toff[v + 1] == toff[v]) continue;   // no rows written (:271, :394)
-        if (nb[v].size() + 1 > CF_MAX_K)
+        if (nb[v].size() + 1 > CF_SPILL_MAX_K)
             cfcli::die("movie " + std::to_string(items.ids[v]) + " has " + std::to_string(nb[v].size()) +
-                       " out-neighbours; the LDS path supports at most 191 (spill path not built)");
+                       " out-neighbours; at most 3071 are supported");
         units.push_back(v);
         mitems.push_back(v);
         for (auto& kv : nb[v]) mitems.push_back(kv.first);

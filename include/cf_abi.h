@@ -182,7 +182,8 @@ int cf_knn2_timing(cf_ctx* ctx, float* plane_ms, float* gemm_ms, int* path);
  * out_fin_ weights; edges count iff w > 0.1, graph_loader :113).  Movie unit v lists
  * movie_items[movie_off[v] .. movie_off[v+1]) = [m, the out-neighbours of m with w > 0.1]
  * (compact ids, any order: results are permutation-equivariant).  Units with fewer than 2
- * out-neighbours are skipped (:271-272); more than 191 is CF_ERANGE (LDS path).
+ * out-neighbours are skipped (:271-272); up to 191 run on the LDS kernels, up to
+ * CF_SPILL_MAX_K - 1 on the fp64 spill kernels (HBM workspace), more is CF_ERANGE.
  * Test ratings: CSR over all n_items compact ids, test_off[n_items + 1], users ascending
  * within an item.  For every test entry t of a processed movie m (test_off[m] <= t <
  * test_off[m+1]): mse[t] (float, :499), kk[t] (rated rows of the local graph), and when
