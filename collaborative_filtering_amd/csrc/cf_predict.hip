@@ -95,6 +95,9 @@ struct PredArgs {
     double* qs;            // per-block scratch: Q ((lmax + 2) x lmax rows: Q, g, h), fp64
     double* q1;            // per-block scratch: U T1, then P = Q Q^T (lmax x lmax), fp64
     double* pgh;           // per-block scratch: {PG, PH}(i, l), lmax x (lmax + 1) pairs, fp64
+    double* abig;          // per-block HBM region of the block-wide systems (when !big_lds)
+    size_t abig_elems;     // (lmax + 2)(lmax + 3) / 2
+    int big_lds;           // 1: the block-wide systems use the LDS region A
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -774,6 +777,9 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
         }
         PHASE_STAMP(2);
 
+        // The block-wide systems live in LDS when the bucket's full triangle fits beside two
+        // resident blocks per CU, else in this block's HBM region (L2-resident while used).
+        double* AW = a.big_lds ? A : a.abig + (size_t)blockIdx.x * a.abig_elems;
         // ---- block-wide paths: the K system of the fast path for large complements, and
         // the rating's own bordered Gram matrix (dense) for everything else ---------------
         for (int si = 0; si < nslow; ++si) {
@@ -798,7 +804,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                 wide = !__syncthreads_or(drop);
             }
             if (wide) {
-                // E = P_S over the rows [Cbar..., r] into A (packed), then the bordered K
+                // E = P_S over the rows [Cbar..., r] into AW (packed), then the bordered K
                 // system exactly as in the fast path, factored by the blocked LDL^T.
                 const int np = nc + 1;
                 for (int e = tid; e < np * (np + 1) / 2; e += kThreads) {
@@ -812,7 +818,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                     const double* xa = Qs + (size_t)ia * Lq;
                     const double* xb = Qs + (size_t)ib * Lq;
                     for (int j = lim; j < Lq; ++j) v = fma(-xa[j], xb[j], v);
-                    A[e] = v;
+                    AW[e] = v;
                 }
                 if (wave == 0) {
                     double sc = 0.0;
@@ -828,32 +834,32 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                     const double2 py = pgh_lim[(size_t)s_nconn[tid] * (Lq + 1)];
                     bl = py.x - mu * py.y;
                     for (int q = 0; q < nc; ++q) {
-                        const double eq = q <= tid ? A[tri(tid, q)] : A[tri(q, tid)];
+                        const double eq = q <= tid ? AW[tri(tid, q)] : AW[tri(q, tid)];
                         bl = fma(-eq, (double)s_rat[s_nconn[q]] - mu, bl);
                     }
                 }
                 if (tid == kThreads - 1) {   // a_r (k <= 192 < 255: never a row thread)
                     const double2 py = pgh_lim[(size_t)r * (Lq + 1)];
                     double ar = py.x - mu * py.y;
-                    for (int q = 0; q < nc; ++q) ar = fma(-A[tri(nc, q)], (double)s_rat[s_nconn[q]] - mu, ar);
+                    for (int q = 0; q < nc; ++q) ar = fma(-AW[tri(nc, q)], (double)s_rat[s_nconn[q]] - mu, ar);
                     s_misc[2] = ar;
                 }
                 __syncthreads();
-                if (tid < nc) A[tri(nc + 1, tid)] = bl;
+                if (tid < nc) AW[tri(nc + 1, tid)] = bl;
                 for (int e = tid; e < nc * (nc + 1) / 2; e += kThreads) {
                     int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
                     while (ra * (ra + 1) / 2 > e) --ra;
                     while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
-                    A[e] = (e == tri(ra, ra) ? 1.0 : 0.0) - A[e];   // K = I - P_CbarCbar
+                    AW[e] = (e == tri(ra, ra) ? 1.0 : 0.0) - AW[e];   // K = I - P_CbarCbar
                 }
                 __syncthreads();
-                ldlt_bordered<kThreads>(A, nc, nc + 2);
+                ldlt_bordered<kThreads>(AW, nc, nc + 2);
                 if (wave == 0) {
                     double minpiv = 1.0, dot = 0.0;
                     for (int j = lane; j < nc; j += 64) {
-                        const double dj = A[tri(j, j)];
+                        const double dj = AW[tri(j, j)];
                         minpiv = fmin(minpiv, dj);
-                        dot = fma(A[tri(nc, j)] * A[tri(nc + 1, j)], dj, dot);
+                        dot = fma(AW[tri(nc, j)] * AW[tri(nc + 1, j)], dj, dot);
                     }
                     dot = wave_sum(dot);
                     for (int off = 32; off >= 1; off >>= 1) minpiv = fmin(minpiv, __shfl_xor(minpiv, off));
@@ -899,7 +905,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
             __syncthreads();
             const double mean = s_misc[0];
 
-            // bordered Gram: A[i][j] = (G^T G)_ij (j <= i < L), A[L][j] = t_j, A[L+1][j] = v_j
+            // bordered Gram: AW[i][j] = (G^T G)_ij (j <= i < L), AW[L][j] = t_j, AW[L+1][j] = v_j
             {
                 const int nt4 = (L + 3) >> 2;
                 const int ntile = nt4 * (nt4 + 1) / 2;
@@ -961,7 +967,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                         for (int y = 0; y < 4; ++y) {
                             const int ia = 4 * ta + x, ib = 4 * tb + y;
                             if (ia < L && ib <= ia)
-                                A[tri(ia, ib)] = use_complement
+                                AW[tri(ia, ib)] = use_complement
                                                      ? Gb[(size_t)ca[x] * lmax + cb[y]] - acc[x][y]
                                                      : acc[x][y];
                         }
@@ -986,21 +992,21 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                     acc += __shfl_xor(acc, 1);
                     acc += __shfl_xor(acc, 2);
                     if (part == 0) {
-                        A[tri(L, j)] = acc;
-                        A[tri(L + 1, j)] = (double)U[(size_t)r * m + cj];
+                        AW[tri(L, j)] = acc;
+                        AW[tri(L + 1, j)] = (double)U[(size_t)r * m + cj];
                     }
                 }
             }
             __syncthreads();
 
-            ldlt_bordered<kThreads>(A, L, L + 2);
+            ldlt_bordered<kThreads>(AW, L, L + 2);
 
             // pred = v^T M^-1 t + mean = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean (:314-327)
             if (wave == 0) {
                 double dot = 0.0;
-                const double* y = A + tri(L, 0);
-                const double* z = A + tri(L + 1, 0);
-                for (int j = lane; j < L; j += 64) dot = fma(y[j] * z[j], A[tri(j, j)], dot);
+                const double* y = AW + tri(L, 0);
+                const double* z = AW + tri(L + 1, 0);
+                for (int j = lane; j < L; j += 64) dot = fma(y[j] * z[j], AW[tri(j, j)], dot);
                 dot = wave_sum(dot);
                 if (lane == 0) {
                     double pred = dot + mean;
@@ -1025,16 +1031,26 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
 template <typename T>
 int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lmax, hipStream_t stream) {
     args.lmax = lmax;
+    const size_t lds_fixed = sizeof(double) * 4 + CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 6 * sizeof(int)) +
+                             12 * sizeof(int) + CF_MAX_K * (3 * sizeof(uint64_t) + sizeof(int));   // s_cmask, s_order
+    const int big = (lmax + 2) * (lmax + 3) / 2;
+    // The full (lmax + 2)-row triangle of the block-wide systems in LDS would leave one
+    // 4-wave block per CU for k > 128; there it moves to HBM and the LDS keeps only the
+    // basis GEMM staging and the per-wave fast-path systems (nc <= 60), two blocks per CU.
     args.ncw = std::min(kNcMax, lmax);
     args.ew = (args.ncw + 2) * (args.ncw + 3) / 2 + 64;   // + y of the complement rows
-    args.a_elems = std::max({(lmax + 2) * (lmax + 3) / 2, kWaves * args.ew, kStageElems});
-    const size_t lds = sizeof(double) * ((size_t)args.a_elems + 4) +
-                       CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 6 * sizeof(int)) + 12 * sizeof(int) +
-                       CF_MAX_K * (3 * sizeof(uint64_t) + sizeof(int));   // s_cmask, s_order
+    args.big_lds = sizeof(double) * (size_t)std::max({big, kWaves * args.ew, kStageElems}) + lds_fixed <= 81920;
+    if (!args.big_lds) {
+        args.ncw = std::min(60, lmax);
+        args.ew = (args.ncw + 2) * (args.ncw + 3) / 2 + 64;
+    }
+    args.a_elems = std::max({args.big_lds ? big : 0, kWaves * args.ew, kStageElems, 2 * lmax});
+    args.abig_elems = (size_t)big;
+    const size_t lds = sizeof(double) * (size_t)args.a_elems + lds_fixed;
     if (lds > 163840) return cf_set_error(ctx, CF_ERANGE, "predict bucket exceeds LDS");
     int blocks = (int)std::min<uint32_t>(count, 2048u);
     const size_t per_block = (size_t)lmax * lmax + (size_t)(lmax + 2) * lmax + (size_t)lmax * (lmax + 1) * 2 +
-                             (size_t)lmax * lmax;
+                             (size_t)lmax * lmax + (args.big_lds ? 0 : (size_t)big);
     const size_t need = (size_t)blocks * per_block * sizeof(double);
     if (need > ctx->scratch_bytes) {
         if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
@@ -1047,6 +1063,7 @@ int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lma
     args.qs = args.gbar + (size_t)blocks * lmax * lmax;
     args.pgh = args.qs + (size_t)blocks * (lmax + 2) * lmax;
     args.q1 = args.pgh + (size_t)blocks * lmax * (lmax + 1) * 2;
+    args.abig = args.q1 + (size_t)blocks * lmax * lmax;
     CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)predict_kernel<T>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(predict_kernel<T>, dim3(blocks), dim3(kThreads), lds, stream, args, count);
