@@ -20,6 +20,8 @@ CF_MAX_K = 192
 CF_SPILL_MAX_K = 3072
 CF_EIGEN_TRIDIAG = 0
 CF_EIGEN_JACOBI = 1
+CF_FILTER_CHEBY = 0
+CF_FILTER_BINOMIAL = 1
 
 # name -> (restype, argtypes); the list is the ABI contract checked by tests.
 SIGNATURES = {
@@ -59,6 +61,9 @@ SIGNATURES = {
                                    c_int, c_void_p, c_void_p]),
     "cf_knn2_timing": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "cf_knn_predict": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "cf_graph_filter": (c_int, [c_void_p, c_int, c_uint32, ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_uint32, c_void_p]),
+    "cf_graph_filter_timing": (c_int, [c_void_p, c_void_p, c_void_p]),
     "cf_local_calc": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p]),
 }

@@ -12,7 +12,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _native
-from ._native import CF_SIGS_COMPAT, CF_SIGS_OWN, NativeError, ptr
+from ._native import CF_FILTER_BINOMIAL, CF_FILTER_CHEBY, CF_SIGS_COMPAT, CF_SIGS_OWN, NativeError, ptr
 
 
 def _check(lib, ctx, rc, what):
@@ -261,6 +261,23 @@ class Context:
                                          ptr(lim)), "cf_local_calc")
         return mse, kk, pred, wlim, lim
 
+    def graph_filter(self, kind, n_vertices, va, vb, w, signal, coeff):
+        """cheby (CF_FILTER_CHEBY) / binomials (CF_FILTER_BINOMIAL) graph-signal filter
+        (cheby.cpp:152-274, binomials.cpp:145-253) over topology lines (va, vb, w) on compact
+        vertex ids.  Returns (filtered signal fp64, device ms of the supersteps, directed edges)."""
+        va = np.ascontiguousarray(va, dtype=np.uint32)
+        vb = np.ascontiguousarray(vb, dtype=np.uint32)
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        signal = np.ascontiguousarray(signal, dtype=np.float64)
+        coeff = np.ascontiguousarray(coeff, dtype=np.float64)
+        out = np.zeros(int(n_vertices), dtype=np.float64)
+        self._chk(self.lib.cf_graph_filter(self.h, int(kind), int(n_vertices), len(w), ptr(va), ptr(vb), ptr(w),
+                                           ptr(signal), ptr(coeff), len(coeff), ptr(out)), "cf_graph_filter")
+        ms = np.zeros(1, dtype=np.float32)
+        ne = np.zeros(1, dtype=np.uint64)
+        self._chk(self.lib.cf_graph_filter_timing(self.h, ptr(ms), ptr(ne)), "cf_graph_filter_timing")
+        return out, float(ms[0]), int(ne[0])
+
     # -- device-resident paths (torch CUDA tensors) -------------------------------
     def plan(self, item_off_host) -> "Plan":
         return Plan(self, item_off_host)
@@ -303,4 +320,5 @@ class Plan:
                   ptr(d_pred), c_void_p(stream or 0)), "cf_predict_run")
 
 
-__all__ = ["Context", "Plan", "EigenResult", "evec_offsets", "CF_SIGS_OWN", "CF_SIGS_COMPAT"]
+__all__ = ["Context", "Plan", "EigenResult", "evec_offsets", "CF_SIGS_OWN", "CF_SIGS_COMPAT", "CF_FILTER_CHEBY",
+           "CF_FILTER_BINOMIAL"]

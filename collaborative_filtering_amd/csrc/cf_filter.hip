@@ -1,0 +1,247 @@
+// cf_filter.hip -- graph-signal polynomial filters on gfx950:
+// cheby.cpp:152-274 (Chebyshev recurrence) and binomials.cpp:145-253 (quadratic factors).
+//
+// Both reference programs are GraphLab sync engines over the same graph: every line
+// "va vb w" of graph_topology with w > 0.1 adds the edges va -> vb and vb -> va (parallel
+// edges kept, self-edges dropped as GraphLab's add_edge does), vertex values come from
+// graph_signal.  Per superstep every vertex gathers over its OUT edges
+//     sum_i = sum_{e = i -> j} w_e / sqrt(d_j d_i) * x_j        (cheby.cpp:188-191)
+// with d = out-degree weight sums (degree_program, :152-170), then applies a per-vertex
+// update.  With S = D^-1/2 W D^-1/2 and L = I - S:
+//   cheby (a1 = 1, a2 = 1 for arange [0, 2], :17-19):
+//     init (:175-206):  t_old = x, t_cur = (x - Sx - a2 x)/a1, y = c0/2 t_old + c1 t_cur
+//     step k = 2.. (:210-245): t_new = 2/a1 (t_cur - S t_cur - a2 t_cur) - t_old,
+//                              y += c_k t_new, (t_old, t_cur) = (t_cur, t_new)
+//   binomials, round i while 3i < n_coeff (:318-357; ind = i: the coefficient windows
+//   overlap, as the reference's ind++ makes them):
+//     a (:179-213): p_a = (c_i + c_{i+1}) x - c_{i+1} Sx,  t = x - Sx
+//     b (:218-250): x = p_a + c_{i+2} (t - S t)
+//
+// Layout in HBM: CSR by source (u64 row_ptr, u32 col) with the normalised weight
+// w_e / sqrt(d_j d_i) precomputed once per call in fp64 (12 B per edge per superstep);
+// vertex vectors fp64.  Each superstep is ONE kernel: the row gather by a G-lane group
+// (G = 4 / 16 / 64 from the mean degree; lanes stride the row, coalesced col / weight
+// reads, shuffle reduction) fused with the vertex update -- HBM-bound, ~12 B per edge.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "cf_internal.h"
+
+namespace {
+
+constexpr int kFT = 256;
+
+enum FStep : int { kDeg = 0, kNorm = 1, kChebInit = 2, kChebStep = 3, kBinA = 4, kBinB = 5 };
+
+struct FArgs {
+    uint32_t n;
+    const uint64_t* row;
+    const uint32_t* col;
+    const double* w;      // raw weights (kDeg, kNorm)
+    double* wn;           // normalised weights
+    double* deg;
+    const double* x;      // gathered vector
+    double* v0;           // per-step vectors, see filter_step
+    double* v1;
+    double* v2;
+    double* y;
+    double c0, c1, c2;
+};
+
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+    for (int off = G / 2; off >= 1; off >>= 1) v += __shfl_xor(v, off, G);
+    return v;
+}
+
+// One G-lane group per vertex row.
+template <int G, int STEP>
+__global__ __launch_bounds__(kFT) void filter_step(FArgs a) {
+    const uint32_t gid = (blockIdx.x * (uint32_t)kFT + threadIdx.x) / G;
+    const int sl = threadIdx.x & (G - 1);
+    if (gid >= a.n) return;   // whole groups leave together
+    const uint64_t b = a.row[gid], e = a.row[gid + 1];
+    double s = 0.0;
+    if (STEP == kDeg) {
+        for (uint64_t p = b + sl; p < e; p += G) s += a.w[p];
+        s = group_sum<G>(s);
+        if (sl == 0) a.deg[gid] = s;   // degree_program::apply (cheby.cpp:163-165)
+        return;
+    }
+    if (STEP == kNorm) {
+        const double di = a.deg[gid];
+        for (uint64_t p = b + sl; p < e; p += G) a.wn[p] = a.w[p] / std::sqrt(a.deg[a.col[p]] * di);
+        return;
+    }
+    for (uint64_t p = b + sl; p < e; p += G) s = fma(a.wn[p], a.x[a.col[p]], s);
+    s = group_sum<G>(s);
+    if (sl != 0) return;
+    const uint32_t i = gid;
+    if (STEP == kChebInit) {   // v0 = t_old, v1 = t_cur, y = val (x = val)
+        const double val = a.x[i];
+        const double tc = (val - s - 1.0 * val) / 1.0;
+        a.v0[i] = val;
+        a.v1[i] = tc;
+        a.y[i] = 0.5 * a.c0 * val + a.c1 * tc;
+    } else if (STEP == kChebStep) {   // x = t_cur (v1), v0 = t_old, v2 = t_new
+        const double tc = a.x[i];
+        const double tn = (2.0 / 1.0) * (tc - s - 1.0 * tc) - a.v0[i];
+        a.v2[i] = tn;
+        a.y[i] = a.y[i] + a.c0 * tn;
+    } else if (STEP == kBinA) {   // x = val; v0 = part_a, v1 = tmp
+        const double val = a.x[i];
+        a.v0[i] = (a.c0 + a.c1) * val - a.c1 * s;
+        a.v1[i] = val - s;
+    } else {   // kBinB: x = tmp; v0 = part_a; y = val
+        a.y[i] = a.v0[i] + a.c2 * (a.x[i] - s);
+    }
+}
+
+template <int STEP>
+void launch_step(int G, const FArgs& a, hipStream_t st) {
+    const uint64_t threads = (uint64_t)a.n * G;
+    const dim3 grid((unsigned)((threads + kFT - 1) / kFT));
+    switch (G) {
+        case 4: hipLaunchKernelGGL((filter_step<4, STEP>), grid, dim3(kFT), 0, st, a); break;
+        case 16: hipLaunchKernelGGL((filter_step<16, STEP>), grid, dim3(kFT), 0, st, a); break;
+        default: hipLaunchKernelGGL((filter_step<64, STEP>), grid, dim3(kFT), 0, st, a); break;
+    }
+}
+
+}  // namespace
+
+extern "C" int cf_graph_filter(cf_ctx* ctx, int kind, uint32_t n_vertices, uint64_t n_lines, const uint32_t* va,
+                               const uint32_t* vb, const double* w, const double* signal, const double* coeff,
+                               uint32_t n_coeff, double* out) {
+    if (!ctx || (n_lines && (!va || !vb || !w)) || (n_vertices && (!signal || !out)) || !coeff)
+        return cf_set_error(ctx, CF_EINVAL, "cf_graph_filter: null argument");
+    if (kind != CF_FILTER_CHEBY && kind != CF_FILTER_BINOMIAL)
+        return cf_set_error(ctx, CF_EINVAL, "cf_graph_filter: unknown filter kind");
+    if (n_coeff < 3)   // both reference programs read coeff[2] (cheby :230, binomials :241)
+        return cf_set_error(ctx, CF_EINVAL, "cf_graph_filter: at least 3 coefficients are required");
+    CF_TRY(set_device(ctx));
+    // CSR by source: each line with w > 0.1 gives va -> vb and vb -> va (graph_loader,
+    // cheby.cpp:88-92); self-edges are dropped, parallel edges kept.
+    std::vector<uint64_t> row(n_vertices + 1, 0);
+    for (uint64_t l = 0; l < n_lines; ++l) {
+        if (!(w[l] > 0.1) || va[l] == vb[l]) continue;
+        if (va[l] >= n_vertices || vb[l] >= n_vertices)
+            return cf_set_error(ctx, CF_EINVAL, "cf_graph_filter: vertex index out of range");
+        row[va[l] + 1]++;
+        row[vb[l] + 1]++;
+    }
+    for (uint32_t i = 0; i < n_vertices; ++i) row[i + 1] += row[i];
+    const uint64_t nnz = row[n_vertices];
+    std::vector<uint32_t> col(nnz);
+    std::vector<double> wv(nnz);
+    {
+        std::vector<uint64_t> fill(row.begin(), row.end() - 1);
+        for (uint64_t l = 0; l < n_lines; ++l) {
+            if (!(w[l] > 0.1) || va[l] == vb[l]) continue;
+            uint64_t p = fill[va[l]]++;
+            col[p] = vb[l];
+            wv[p] = w[l];
+            p = fill[vb[l]]++;
+            col[p] = va[l];
+            wv[p] = w[l];
+        }
+    }
+    const double mean_deg = n_vertices ? (double)nnz / n_vertices : 0.0;
+    const int G = mean_deg >= 48.0 ? 64 : (mean_deg >= 8.0 ? 16 : 4);
+    DevBuf d_row, d_col, d_w, d_wn, d_deg, d_x, d_v0, d_v1, d_v2, d_y;
+    const size_t vb8 = sizeof(double) * std::max<uint32_t>(n_vertices, 1);
+    CF_TRY(dev_alloc(ctx, d_row, sizeof(uint64_t) * (n_vertices + 1)));
+    CF_TRY(dev_alloc(ctx, d_col, sizeof(uint32_t) * std::max<uint64_t>(nnz, 1)));
+    CF_TRY(dev_alloc(ctx, d_w, sizeof(double) * std::max<uint64_t>(nnz, 1)));
+    CF_TRY(dev_alloc(ctx, d_wn, sizeof(double) * std::max<uint64_t>(nnz, 1)));
+    for (DevBuf* b : {&d_deg, &d_x, &d_v0, &d_v1, &d_v2, &d_y}) CF_TRY(dev_alloc(ctx, *b, vb8));
+    CF_HIP_CHECK(ctx, hipMemcpy(d_row.p, row.data(), sizeof(uint64_t) * (n_vertices + 1), hipMemcpyHostToDevice));
+    if (nnz) {
+        CF_HIP_CHECK(ctx, hipMemcpy(d_col.p, col.data(), sizeof(uint32_t) * nnz, hipMemcpyHostToDevice));
+        CF_HIP_CHECK(ctx, hipMemcpy(d_w.p, wv.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
+    }
+    if (n_vertices) CF_HIP_CHECK(ctx, hipMemcpy(d_x.p, signal, vb8, hipMemcpyHostToDevice));
+    if (n_vertices == 0) return CF_OK;
+
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    CF_HIP_CHECK(ctx, hipEventCreate(&ev0));
+    CF_HIP_CHECK(ctx, hipEventCreate(&ev1));
+    hipStream_t st = nullptr;
+    FArgs a{};
+    a.n = n_vertices;
+    a.row = static_cast<const uint64_t*>(d_row.p);
+    a.col = static_cast<const uint32_t*>(d_col.p);
+    a.w = static_cast<const double*>(d_w.p);
+    a.wn = static_cast<double*>(d_wn.p);
+    a.deg = static_cast<double*>(d_deg.p);
+    double* X = static_cast<double*>(d_x.p);
+    double* V0 = static_cast<double*>(d_v0.p);
+    double* V1 = static_cast<double*>(d_v1.p);
+    double* V2 = static_cast<double*>(d_v2.p);
+    double* Y = static_cast<double*>(d_y.p);
+    CF_HIP_CHECK(ctx, hipEventRecord(ev0, st));
+    launch_step<kDeg>(G, a, st);
+    launch_step<kNorm>(G, a, st);
+    double* result = Y;
+    if (kind == CF_FILTER_CHEBY) {
+        a.x = X;
+        a.v0 = V0;
+        a.v1 = V1;
+        a.y = Y;
+        a.c0 = coeff[0];
+        a.c1 = coeff[1];
+        launch_step<kChebInit>(G, a, st);
+        double *t_old = V0, *t_cur = V1, *t_new = V2;
+        for (uint32_t kc = 2; kc < n_coeff; ++kc) {   // counter 2 .. n_coeff - 1 (:236-241)
+            a.x = t_cur;
+            a.v0 = t_old;
+            a.v2 = t_new;
+            a.y = Y;
+            a.c0 = coeff[kc];
+            launch_step<kChebStep>(G, a, st);
+            double* t = t_old;
+            t_old = t_cur;
+            t_cur = t_new;
+            t_new = t;
+        }
+    } else {
+        double *val = X, *nxt = Y;
+        for (uint32_t i = 0; 3 * i < n_coeff; ++i) {   // ind = i (:357)
+            a.c0 = coeff[i];
+            a.c1 = coeff[i + 1];
+            a.c2 = coeff[i + 2];
+            a.x = val;
+            a.v0 = V0;
+            a.v1 = V1;
+            launch_step<kBinA>(G, a, st);
+            a.x = V1;
+            a.y = nxt;
+            launch_step<kBinB>(G, a, st);
+            std::swap(val, nxt);
+        }
+        result = val;
+    }
+    CF_HIP_CHECK(ctx, hipGetLastError());
+    CF_HIP_CHECK(ctx, hipEventRecord(ev1, st));
+    CF_HIP_CHECK(ctx, hipEventSynchronize(ev1));
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, ev0, ev1);
+    ctx->filter_ms = ms;
+    ctx->filter_nnz = nnz;
+    (void)hipEventDestroy(ev0);
+    (void)hipEventDestroy(ev1);
+    CF_HIP_CHECK(ctx, hipMemcpy(out, result, vb8, hipMemcpyDeviceToHost));
+    return CF_OK;
+}
+
+extern "C" int cf_graph_filter_timing(cf_ctx* ctx, float* device_ms, uint64_t* n_edges) {
+    if (!ctx) return CF_EINVAL;
+    if (device_ms) *device_ms = ctx->filter_ms;
+    if (n_edges) *n_edges = ctx->filter_nnz;
+    return CF_OK;
+}

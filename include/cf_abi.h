@@ -203,6 +203,23 @@ int cf_knn_predict(cf_ctx* ctx, uint32_t n_users, const uint64_t* user_off,
                    const uint32_t* items, const float* ratings, double* pred,
                    float* movie_mse, uint32_t* movie_count);
 
+/* ---- graph-signal polynomial filters ------------------------ */
+#define CF_FILTER_CHEBY 0     /* cheby.cpp:152-274 (Chebyshev recurrence on [0, 2]) */
+#define CF_FILTER_BINOMIAL 1  /* binomials.cpp:145-253 (quadratic factors, overlapping windows) */
+/* Replaces the degree / init_values / cheby programs (cheby.cpp:152-245) and the degree /
+ * binomial_a / binomial_b programs (binomials.cpp:145-250) with their sync-engine loops
+ * (cheby.cpp:296-366, binomials.cpp:296-358).  Vertices are compact indices 0..n_vertices-1;
+ * topology line l is (va[l], vb[l], w[l]): when w > 0.1 it adds va -> vb and vb -> va
+ * (graph_loader, cheby.cpp:88-92), parallel edges kept, self-edges dropped.  signal[i] is
+ * the graph_signal value of vertex i (0 where the file has none).  coeff holds n_coeff >= 3
+ * values (both programs read coeff[2]).  out[i] = the filtered signal (fp64).  Synchronous:
+ * returns after the copy-out. */
+int cf_graph_filter(cf_ctx* ctx, int kind, uint32_t n_vertices, uint64_t n_lines, const uint32_t* va,
+                    const uint32_t* vb, const double* w, const double* signal, const double* coeff,
+                    uint32_t n_coeff, double* out);
+/* Device time of the last cf_graph_filter's supersteps (HIP events) and its directed edges. */
+int cf_graph_filter_timing(cf_ctx* ctx, float* device_ms, uint64_t* n_edges);
+
 #ifdef __cplusplus
 }
 #endif

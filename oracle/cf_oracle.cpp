@@ -699,4 +699,68 @@ int cfo_knn3(int n_items, const float* W, const int64_t* movie_off, const int32_
     return 0;
 }
 
+// Graph-signal polynomial filters, restated superstep by superstep as
+// the reference's GraphLab sync engines run them, over an explicit directed edge list.
+//   graph_loader (cheby.cpp:88-92 / binomials.cpp:77-93): a line with w > 0.1 adds
+//     va -> vb and vb -> va (self-edges dropped, as GraphLab's add_edge does);
+//   degree_program (cheby.cpp:152-170): d_i = sum of OUT-edge weights;
+//   gather (cheby.cpp:188-191, :222-225; binomials.cpp:192-196, :231-235):
+//     sum_i = sum_{e = i -> j} w_e / sqrt(d_j * d_i) * x_j;
+//   cheby init / step (cheby.cpp:195-206, :228-244), binomials a / b (binomials.cpp:199-205,
+//   :238-243) with ind = round index (:357).  kind 0 = cheby, 1 = binomials.
+int cfo_graph_filter(int kind, int n, int64_t n_lines, const int32_t* va, const int32_t* vb,
+                     const double* w, const double* signal, const double* coeff, int n_coeff,
+                     double* out) {
+    if (n_coeff < 3) return -1;
+    std::vector<int32_t> es, ed;
+    std::vector<double> ew;
+    for (int64_t l = 0; l < n_lines; ++l) {
+        if (!(w[l] > 0.1) || va[l] == vb[l]) continue;
+        es.push_back(va[l]); ed.push_back(vb[l]); ew.push_back(w[l]);
+        es.push_back(vb[l]); ed.push_back(va[l]); ew.push_back(w[l]);
+    }
+    const size_t E = es.size();
+    std::vector<double> deg(n, 0.0);
+    for (size_t e = 0; e < E; ++e) deg[es[e]] += ew[e];
+    auto gather = [&](const std::vector<double>& x) {
+        std::vector<double> sum(n, 0.0);
+        for (size_t e = 0; e < E; ++e)
+            sum[es[e]] += ew[e] / std::sqrt(deg[ed[e]] * deg[es[e]]) * x[ed[e]];
+        return sum;
+    };
+    const double a1 = 1.0, a2 = 1.0;   // arange {0, 2} (cheby.cpp:17-19)
+    std::vector<double> val(signal, signal + n);
+    if (kind == 0) {
+        std::vector<double> t_old(n), t_cur(n), t_new(n);
+        std::vector<double> sum = gather(val);
+        for (int i = 0; i < n; ++i) {
+            t_old[i] = val[i];
+            t_cur[i] = (val[i] - sum[i] - a2 * val[i]) / a1;
+            val[i] = 0.5 * coeff[0] * t_old[i] + coeff[1] * t_cur[i];
+        }
+        for (int counter = 2; counter < n_coeff; ++counter) {
+            sum = gather(t_cur);
+            for (int i = 0; i < n; ++i) {
+                t_new[i] = (2 / a1) * (t_cur[i] - sum[i] - a2 * t_cur[i]) - t_old[i];
+                val[i] = val[i] + coeff[counter] * t_new[i];
+                t_old[i] = t_cur[i];
+                t_cur[i] = t_new[i];
+            }
+        }
+    } else {
+        std::vector<double> part_a(n), tmp(n);
+        for (int ind = 0; 3 * ind < n_coeff; ++ind) {
+            std::vector<double> sum = gather(val);
+            for (int i = 0; i < n; ++i) {
+                part_a[i] = (coeff[ind] + coeff[ind + 1]) * val[i] - coeff[ind + 1] * sum[i];
+                tmp[i] = val[i] - sum[i];
+            }
+            sum = gather(tmp);
+            for (int i = 0; i < n; ++i) val[i] = part_a[i] + coeff[ind + 2] * (tmp[i] - sum[i]);
+        }
+    }
+    for (int i = 0; i < n; ++i) out[i] = val[i];
+    return 0;
+}
+
 }  // extern "C"

@@ -39,6 +39,8 @@ def lib():
         L.cfo_local_graph.argtypes = [ci, ci, vp, vp, ctypes.c_int64, vp]
         L.cfo_local_graph.restype = ci
         L.cfo_local_calc.argtypes = [ci, vp, ci, vp, vp, vp, vp, vp, vp]
+        L.cfo_graph_filter.argtypes = [ci, ci, ctypes.c_int64, vp, vp, vp, vp, vp, ci, vp]
+        L.cfo_graph_filter.restype = ci
         _lib = L
     return _lib
 
@@ -245,3 +247,18 @@ def compare_eigen_block(L2, m_ref, ev_full_ref, U_ref, m_gpu, ev_gpu, U_gpu, ev_
         if d > proj_tol:
             fails.append(f"projector cluster {g[0]}..{g[-1]} err {d:.3g}")
     return fails
+
+
+def graph_filter(kind, n, va, vb, w, signal, coeff):
+    """cheby (kind 0) / binomials (kind 1) filtered signal of n vertices (cheby.cpp, binomials.cpp)."""
+    va = np.ascontiguousarray(va, np.int32)
+    vb = np.ascontiguousarray(vb, np.int32)
+    w = np.ascontiguousarray(w, np.float64)
+    signal = np.ascontiguousarray(signal, np.float64)
+    coeff = np.ascontiguousarray(coeff, np.float64)
+    out = np.zeros(n, np.float64)
+    rc = lib().cfo_graph_filter(int(kind), int(n), len(w), _p(va), _p(vb), _p(w), _p(signal), _p(coeff),
+                                len(coeff), _p(out))
+    assert rc == 0, rc
+    return out
+
