@@ -78,8 +78,26 @@ __global__ __launch_bounds__(kFT) void filter_step(FArgs a) {
         for (uint64_t p = b + sl; p < e; p += G) a.wn[p] = a.w[p] / std::sqrt(a.deg[a.col[p]] * di);
         return;
     }
-    for (uint64_t p = b + sl; p < e; p += G) s = fma(a.wn[p], a.x[a.col[p]], s);
-    s = group_sum<G>(s);
+    // four edges per lane in flight: the col -> x gather is a dependent load pair
+    double s1 = 0.0;
+    uint64_t p = b + sl;
+    for (; p + 3 * G < e; p += 4 * G) {
+        uint32_t cc[4];
+        double ww[4], xx[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            cc[t] = a.col[p + t * G];
+            ww[t] = a.wn[p + t * G];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) xx[t] = a.x[cc[t]];
+        s = fma(ww[0], xx[0], s);
+        s1 = fma(ww[1], xx[1], s1);
+        s = fma(ww[2], xx[2], s);
+        s1 = fma(ww[3], xx[3], s1);
+    }
+    for (; p < e; p += G) s = fma(a.wn[p], a.x[a.col[p]], s);
+    s = group_sum<G>(s + s1);
     if (sl != 0) return;
     const uint32_t i = gid;
     if (STEP == kChebInit) {   // v0 = t_old, v1 = t_cur, y = val (x = val)
