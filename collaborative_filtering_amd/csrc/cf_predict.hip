@@ -779,7 +779,9 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
 
         // The block-wide systems live in LDS when the bucket's full triangle fits beside two
         // resident blocks per CU, else in this block's HBM region (L2-resident while used).
-        double* AW = a.big_lds ? A : a.abig + (size_t)blockIdx.x * a.abig_elems;
+        // (The per-wave fast-path scratch in A is dead by now: a system that fits in A --
+        // (n + 2)(n + 3)/2 doubles for n rows -- uses it whatever big_lds says.)
+        double* const Ahbm = a.abig + (size_t)blockIdx.x * a.abig_elems;
         // ---- block-wide paths: the K system of the fast path for large complements, and
         // the rating's own bordered Gram matrix (dense) for everything else ---------------
         for (int si = 0; si < nslow; ++si) {
@@ -791,6 +793,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
             const int nc = block_compact(tid < k && !conn, tid, s_nconn, s_cnt);
             const bool use_complement = nc < c;
             const int lim = s_lim[r];
+            double* AW = (a.big_lds || (size_t)(nc + 2) * (nc + 3) / 2 <= (size_t)a.a_elems) ? A : Ahbm;
 
             bool wide = (s_slow[si] >> 16) != 0;
             const unsigned long long tw0 = (a.phase_cycles && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -894,6 +897,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                     }
             }
             const int L = block_compact(keep, tid, s_keep, s_cnt);
+            AW = (a.big_lds || (size_t)(L + 2) * (L + 3) / 2 <= (size_t)a.a_elems) ? A : Ahbm;
 
             // mean of the connected ratings (:311)
             if (wave == 0) {

@@ -8,7 +8,7 @@ from collaborative_filtering_amd.api import CF_SIGS_COMPAT, Context, evec_offset
 
 users = int(sys.argv[1]) if len(sys.argv) > 1 else 4000
 n_items = int(os.environ.get("ITEMS", "10000"))
-k = synth.degrees(2026101502, users)
+k = synth.degrees(2026101502, users) if not os.environ.get("KFIX") else np.full(users, int(os.environ["KFIX"]), dtype=np.uint32)
 off, items, rat = synth.user_items(2026101502, k, n_items, threads=16)
 W = synth.graph_model(2026101502, n_items, threads=16)
 ctx = Context(0); ctx.upload_graph_dense(W); plan = ctx.plan(off)
