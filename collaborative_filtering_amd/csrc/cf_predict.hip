@@ -832,23 +832,30 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                 __syncthreads();
                 const double mu = s_misc[0];
                 const double2* pgh_lim = reinterpret_cast<const double2*>(PGH) + lim;
-                double bl = 0.0;
-                if (tid < nc) {
-                    const double2 py = pgh_lim[(size_t)s_nconn[tid] * (Lq + 1)];
-                    bl = py.x - mu * py.y;
-                    for (int q = 0; q < nc; ++q) {
-                        const double eq = q <= tid ? AW[tri(tid, q)] : AW[tri(q, tid)];
-                        bl = fma(-eq, (double)s_rat[s_nconn[q]] - mu, bl);
+                // b_a = (Py)_a - sum_q E_aq y_q for the rows a of Cbar, a_r likewise as row nc:
+                // g lanes per row (g = 4 / 2 / 1 as (nc + 1) g fits the block), shuffle-reduced
+                {
+                    const int nrw = nc + 1;
+                    const int g = nrw * 4 <= kThreads ? 4 : (nrw * 2 <= kThreads ? 2 : 1);
+                    const int ra = tid / g, part = tid - ra * g;
+                    double v = 0.0;
+                    if (ra < nrw)
+                        for (int q = part; q < nc; q += g) {
+                            const double eq = q <= ra ? AW[tri(ra, q)] : AW[tri(q, ra)];
+                            v = fma(-eq, (double)s_rat[s_nconn[q]] - mu, v);
+                        }
+                    if (g >= 4) v += __shfl_xor(v, 2);
+                    if (g >= 2) v += __shfl_xor(v, 1);
+                    if (ra < nrw && part == 0) {
+                        const double2 py = pgh_lim[(size_t)(ra < nc ? s_nconn[ra] : r) * (Lq + 1)];
+                        v += py.x - mu * py.y;
+                        if (ra < nc)
+                            AW[tri(nc + 1, ra)] = v;   // row nc + 1 is read by nobody before the sync
+                        else
+                            s_misc[2] = v;
                     }
                 }
-                if (tid == kThreads - 1) {   // a_r (k <= 192 < 255: never a row thread)
-                    const double2 py = pgh_lim[(size_t)r * (Lq + 1)];
-                    double ar = py.x - mu * py.y;
-                    for (int q = 0; q < nc; ++q) ar = fma(-AW[tri(nc, q)], (double)s_rat[s_nconn[q]] - mu, ar);
-                    s_misc[2] = ar;
-                }
                 __syncthreads();
-                if (tid < nc) AW[tri(nc + 1, tid)] = bl;
                 for (int e = tid; e < nc * (nc + 1) / 2; e += kThreads) {
                     int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
                     while (ra * (ra + 1) / 2 > e) --ra;
