@@ -23,7 +23,7 @@ HOST_LIB := $(PKG)/libcf_host.so
 
 all: $(LIB) $(HOST_LIB) $(HOST_BINS) oracle
 
-$(BUILD)/%.o: $(CSRC)/%.hip $(wildcard $(CSRC)/*.h) include/cf_abi.h
+$(BUILD)/%.o: $(CSRC)/%.hip $(wildcard $(CSRC)/*.h) $(wildcard $(CSRC)/*.hpp) include/cf_abi.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

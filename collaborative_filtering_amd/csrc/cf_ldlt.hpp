@@ -13,7 +13,7 @@ inline __device__ int tri(int i, int j) { return (i * (i + 1)) / 2 + j; }
         __builtin_amdgcn_wave_barrier();                         \
     } while (0)
 
-constexpr int kNB = 16;   // LDL^T panel width
+constexpr int kNB = 16;   // default LDL^T panel width
 
 // Blocked right-looking LDL^T of the leading L x L block of the packed lower triangle
 // A (rows [0, nrows), nrows >= L), carrying rows [L, nrows) as border rows: on return
@@ -27,29 +27,29 @@ constexpr int kNB = 16;   // LDL^T panel width
 // ldlt_bordered_range factors only the columns [k0, k1) (all rows below them, trailing
 // updates confined to columns < k1): a caller blocking the factorisation in wider panels
 // applies the update of columns >= k1 itself.  ldlt_bordered = the full range.
-template <int kThreads>
+template <int kThreads, int NB = kNB>
 __device__ void ldlt_bordered_range(double* A, int L, int nrows, int k0, int k1) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    for (int kb = k0; kb < k1; kb += kNB) {
-        const int b = min(kNB, k1 - kb);
+    for (int kb = k0; kb < k1; kb += NB) {
+        const int b = min(NB, k1 - kb);
         // (1) diagonal block, unblocked LDL^T, in wave 0's registers: lane i < b holds
         //     row kb + i; column j is broadcast by shuffles.
         if (wave == 0) {
-            double rowv[kNB];
+            double rowv[NB];
             const int i = lane;
             const bool live = i < b;
 #pragma unroll
-            for (int q = 0; q < kNB; ++q) rowv[q] = (live && q <= i) ? A[tri(kb + i, kb + q)] : 0.0;
+            for (int q = 0; q < NB; ++q) rowv[q] = (live && q <= i) ? A[tri(kb + i, kb + q)] : 0.0;
 #pragma unroll
-            for (int j = 0; j < kNB; ++j) {
+            for (int j = 0; j < NB; ++j) {
                 if (j < b) {
                     const double dj = __shfl(rowv[j], j);
                     const double w = (i > j) ? rowv[j] : 0.0;   // unscaled a_ij
                     const double lij = dj != 0.0 ? w / dj : 0.0;   // exact-zero pivot: skipped
 #pragma unroll
-                    for (int q = j + 1; q < kNB; ++q) {
+                    for (int q = j + 1; q < NB; ++q) {
                         const double wq = __shfl(w, q);
                         if (q <= i) rowv[q] = fma(-lij, wq, rowv[q]);
                     }
@@ -57,18 +57,18 @@ __device__ void ldlt_bordered_range(double* A, int L, int nrows, int k0, int k1)
                 }
             }
 #pragma unroll
-            for (int q = 0; q < kNB; ++q)
+            for (int q = 0; q < NB; ++q)
                 if (live && q <= i) A[tri(kb + i, kb + q)] = rowv[q];
         }
         __syncthreads();
         // (2) panel: rows below the block (incl. the border rows) solve against L11^T
         for (int i = kb + b + tid; i < nrows; i += kThreads) {
             double* Ai = A + tri(i, kb);
-            double x[kNB];
+            double x[NB];
 #pragma unroll
-            for (int jj = 0; jj < kNB; ++jj) x[jj] = jj < b ? Ai[jj] : 0.0;
+            for (int jj = 0; jj < NB; ++jj) x[jj] = jj < b ? Ai[jj] : 0.0;
 #pragma unroll
-            for (int jj = 0; jj < kNB; ++jj) {
+            for (int jj = 0; jj < NB; ++jj) {
                 if (jj < b) {
                     const double* Aj = A + tri(kb + jj, kb);
                     double sacc = x[jj];
@@ -78,7 +78,7 @@ __device__ void ldlt_bordered_range(double* A, int L, int nrows, int k0, int k1)
                 }
             }
 #pragma unroll
-            for (int jj = 0; jj < kNB; ++jj)
+            for (int jj = 0; jj < NB; ++jj)
                 if (jj < b) Ai[jj] = x[jj];
         }
         __syncthreads();
@@ -131,7 +131,7 @@ __device__ void ldlt_bordered_range(double* A, int L, int nrows, int k0, int k1)
     }
 }
 
-template <int kThreads>
+template <int kThreads, int NB = kNB>
 __device__ void ldlt_bordered(double* A, int L, int nrows) {
-    ldlt_bordered_range<kThreads>(A, L, nrows, 0, L);
+    ldlt_bordered_range<kThreads, NB>(A, L, nrows, 0, L);
 }
