@@ -11,7 +11,7 @@ from collaborative_filtering_amd.api import Context, evec_offsets  # noqa: E402
 
 users = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 methods = sys.argv[2].split(",") if len(sys.argv) > 2 else ["tridiag", "jacobi"]
-k = synth.degrees(2026101502, users)
+k = synth.degrees(2026101502, users) if not os.environ.get("KFIX") else np.full(users, int(os.environ["KFIX"]), dtype=np.uint32)
 off, items, _ = synth.user_items(2026101502, k, 10000, threads=16)
 W = synth.graph_model(2026101502, 10000, threads=16)
 ctx = Context(0)
