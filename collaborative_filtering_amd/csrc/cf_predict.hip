@@ -1060,7 +1060,11 @@ int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lma
     args.abig_elems = (size_t)big;
     const size_t lds = sizeof(double) * (size_t)args.a_elems + lds_fixed;
     if (lds > 163840) return cf_set_error(ctx, CF_ERANGE, "predict bucket exceeds LDS");
-    int blocks = (int)std::min<uint32_t>(count, 2048u);
+    // Up to 8192 workgroups (~one user each for most buckets): the hardware dispatcher then
+    // balances the per-user cost (~k^3) dynamically.  Measured at C2: 2048 -> 160.2 ms,
+    // 4096 -> 155.7, 8192 -> 152.3, 16384 / all users -> 152.5.  Scratch: ~1.6 MB per
+    // workgroup at k <= 192 (13 GB of the 288 GB).
+    int blocks = (int)std::min<uint32_t>(count, 8192u);
     const size_t per_block = (size_t)lmax * lmax + (size_t)(lmax + 2) * lmax + (size_t)lmax * (lmax + 1) * 2 +
                              (size_t)lmax * lmax + (args.big_lds ? 0 : (size_t)big);
     const size_t need = (size_t)blocks * per_block * sizeof(double);
