@@ -83,6 +83,10 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_tri) (void)hipFree(ctx->d_tri);
     for (hipEvent_t& e : ctx->knn_ev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t& e : ctx->aux_event)
+        if (e) (void)hipEventDestroy(e);
+    for (hipStream_t& st : ctx->aux_stream)
+        if (st) (void)hipStreamDestroy(st);
     delete ctx;
 }
 

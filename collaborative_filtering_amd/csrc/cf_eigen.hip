@@ -495,10 +495,46 @@ int launch_bucket(cf_ctx* ctx, const EigenArgs& args, uint32_t count, hipStream_
 }  // namespace
 
 namespace {
-int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStream_t stream) {
+// Bucket launches alternate between two context-owned non-blocking streams, forked from and
+// joined back to the caller's stream by events: the tail of one bucket (its last users on a
+// few CUs) overlaps the start of the next.  Buckets write disjoint users and the kernel keeps
+// no global scratch (the spill solver's workspace is per launch and it runs first, alone).
+int eigen_fork(cf_ctx* ctx, hipStream_t stream) {
+    if (!ctx->aux_stream[0]) {
+        for (int i = 0; i < 2; ++i) {
+            CF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->aux_stream[i], hipStreamNonBlocking));
+            CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->aux_event[i], hipEventDisableTiming));
+        }
+        CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->aux_event[2], hipEventDisableTiming));
+    }
+    CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[2], stream));
+    for (int i = 0; i < 2; ++i) CF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux_stream[i], ctx->aux_event[2], 0));
+    return CF_OK;
+}
+int eigen_join(cf_ctx* ctx, hipStream_t stream) {
+    for (int i = 0; i < 2; ++i) {
+        CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[i], ctx->aux_stream[i]));
+        CF_HIP_CHECK(ctx, hipStreamWaitEvent(stream, ctx->aux_event[i], 0));
+    }
+    return CF_OK;
+}
+
+int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStream_t caller) {
+    hipStream_t stream = caller;
+    int nb = 0;
+    const bool overlap = args.mode == kUser && !args.stats;   // diagnostics keep one stream
+    if (overlap) CF_TRY(eigen_fork(ctx, caller));
     for (const cf_bucket& b : plan->buckets) {
         if (b.count == 0) continue;
         args.first = b.first;
+        if (overlap) {
+            // the spill bucket (first) runs alone on stream 0; LDS buckets alternate after it
+            if (b.emax == kSpillBucket) {
+                stream = ctx->aux_stream[0];
+            } else {
+                stream = ctx->aux_stream[nb++ & 1];
+            }
+        }
         int rc;
         if (b.emax == kSpillBucket) {
             // n > 192: the fp64 HBM-workspace solver; a8 units in its local-graph / w_lim modes
@@ -515,6 +551,10 @@ int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStre
             rc = cf_launch_eigen_spill(ctx, plan, b, args.item_off, args.items, args.evec_off, args.m_out, args.sigs,
                                        args.evals, args.evecs, stream, &loc);
             if (rc != CF_OK) return rc;
+            if (overlap) {   // LDS buckets start after the spill solver (it fills every CU)
+                CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[0], stream));
+                CF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux_stream[1], ctx->aux_event[0], 0));
+            }
             continue;
         }
         switch (b.emax) {
@@ -534,6 +574,7 @@ int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStre
         }
         if (rc != CF_OK) return rc;
     }
+    if (overlap) CF_TRY(eigen_join(ctx, caller));
     return CF_OK;
 }
 }  // namespace
