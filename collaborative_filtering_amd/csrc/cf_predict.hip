@@ -1040,8 +1040,17 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
         for (int ph = 0; ph < 8; ++ph) atomicAdd(&a.phase_cycles[ph], ph_acc[ph]);
 }
 
+// Scratch doubles per workgroup and workgroups of a bucket launch (see launch_predict_bucket).
+inline int predict_blocks(uint32_t count) { return (int)std::min<uint32_t>(count, 8192u); }
+inline size_t predict_per_block(int lmax) {
+    const size_t big = (size_t)(lmax + 2) * (lmax + 3) / 2;
+    return (size_t)lmax * lmax + (size_t)(lmax + 2) * lmax + (size_t)lmax * (lmax + 1) * 2 +
+           (size_t)lmax * lmax + big;
+}
+
 template <typename T>
-int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lmax, hipStream_t stream) {
+int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lmax, double* scratch,
+                          size_t scratch_bytes, hipStream_t stream) {
     args.lmax = lmax;
     const size_t lds_fixed = sizeof(double) * 4 + CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 6 * sizeof(int)) +
                              12 * sizeof(int) + CF_MAX_K * (3 * sizeof(uint64_t) + sizeof(int));   // s_cmask, s_order
@@ -1067,15 +1076,9 @@ int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lma
     int blocks = (int)std::min<uint32_t>(count, 8192u);
     const size_t per_block = (size_t)lmax * lmax + (size_t)(lmax + 2) * lmax + (size_t)lmax * (lmax + 1) * 2 +
                              (size_t)lmax * lmax + (args.big_lds ? 0 : (size_t)big);
-    const size_t need = (size_t)blocks * per_block * sizeof(double);
-    if (need > ctx->scratch_bytes) {
-        if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
-        ctx->d_scratch = nullptr;
-        ctx->scratch_bytes = 0;
-        CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_scratch, need));
-        ctx->scratch_bytes = need;
-    }
-    args.gbar = reinterpret_cast<double*>(ctx->d_scratch);
+    if ((size_t)blocks * per_block * sizeof(double) > scratch_bytes)
+        return cf_set_error(ctx, CF_EINVAL, "predict scratch undersized");
+    args.gbar = scratch;
     args.qs = args.gbar + (size_t)blocks * lmax * lmax;
     args.pgh = args.qs + (size_t)blocks * (lmax + 2) * lmax;
     args.q1 = args.pgh + (size_t)blocks * lmax * (lmax + 1) * 2;
@@ -1113,19 +1116,62 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
     args.pred = d_pred;
     args.phase_cycles = ctx->d_phase;
     int rc = CF_OK;
+    // Scratch for every LDS bucket, sized once (largest bucket) per stream; the bucket launches
+    // alternate between two context-owned streams (fork/join by events with the caller's
+    // stream) so one bucket's tail overlaps the next -- each stream has its own scratch copy.
+    // Diagnostics (phase counters) keep one stream.
+    size_t need = 0;
+    for (const cf_bucket& b : plan->buckets)
+        if (b.count && b.emax != kSpillBucket)
+            need = std::max(need, (size_t)predict_blocks(b.count) *
+                                      predict_per_block(std::max<int>(2, 16 * b.emax)) * sizeof(double));
+    const bool overlap = !ctx->d_phase;
+    const size_t copies = overlap ? 2 : 1;
+    if (need * copies > ctx->scratch_bytes) {
+        if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+        ctx->d_scratch = nullptr;
+        ctx->scratch_bytes = 0;
+        CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_scratch, need * copies));
+        ctx->scratch_bytes = need * copies;
+    }
+    if (overlap) {
+        if (!ctx->aux_stream[0]) {
+            for (int i = 0; i < 2; ++i) {
+                CF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->aux_stream[i], hipStreamNonBlocking));
+                CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->aux_event[i], hipEventDisableTiming));
+            }
+            CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->aux_event[2], hipEventDisableTiming));
+        }
+        CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[2], stream));
+        for (int i = 0; i < 2; ++i) CF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux_stream[i], ctx->aux_event[2], 0));
+    }
+    int nb = 0;
     for (const cf_bucket& b : plan->buckets) {
         if (b.count == 0) continue;
-        if (b.emax == kSpillBucket) {   // k > CF_MAX_K: HBM-workspace predictor
+        if (b.emax == kSpillBucket) {   // k > CF_MAX_K: HBM-workspace predictor, alone, first
+            hipStream_t st = overlap ? ctx->aux_stream[0] : stream;
             rc = cf_launch_predict_spill<T>(ctx, plan, b, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off,
-                                            d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, stream);
+                                            d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, st);
             if (rc != CF_OK) break;
+            if (overlap) {
+                CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[0], st));
+                CF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux_stream[1], ctx->aux_event[0], 0));
+            }
             continue;
         }
         args.first = b.first;
         const int lmax = std::max<int>(2, 16 * b.emax);
-        rc = launch_predict_bucket<T>(ctx, args, b.count, lmax, stream);
+        const int si = overlap ? (nb++ & 1) : 0;
+        rc = launch_predict_bucket<T>(ctx, args, b.count, lmax,
+                                      reinterpret_cast<double*>(static_cast<char*>(ctx->d_scratch) + si * need), need,
+                                      overlap ? ctx->aux_stream[si] : stream);
         if (rc != CF_OK) break;
     }
+    if (overlap)
+        for (int i = 0; i < 2; ++i) {
+            CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[i], ctx->aux_stream[i]));
+            CF_HIP_CHECK(ctx, hipStreamWaitEvent(stream, ctx->aux_event[i], 0));
+        }
     return rc;
 }
 
