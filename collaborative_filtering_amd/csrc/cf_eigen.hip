@@ -501,18 +501,18 @@ namespace {
 // no global scratch (the spill solver's workspace is per launch and it runs first, alone).
 int eigen_fork(cf_ctx* ctx, hipStream_t stream) {
     if (!ctx->aux_stream[0]) {
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < cf_ctx::kAuxStreams; ++i) {
             CF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->aux_stream[i], hipStreamNonBlocking));
             CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->aux_event[i], hipEventDisableTiming));
         }
-        CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->aux_event[2], hipEventDisableTiming));
+        CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->aux_event[cf_ctx::kAuxStreams], hipEventDisableTiming));
     }
-    CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[2], stream));
-    for (int i = 0; i < 2; ++i) CF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux_stream[i], ctx->aux_event[2], 0));
+    CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[cf_ctx::kAuxStreams], stream));
+    for (int i = 0; i < cf_ctx::kAuxStreams; ++i) CF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux_stream[i], ctx->aux_event[cf_ctx::kAuxStreams], 0));
     return CF_OK;
 }
 int eigen_join(cf_ctx* ctx, hipStream_t stream) {
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < cf_ctx::kAuxStreams; ++i) {
         CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[i], ctx->aux_stream[i]));
         CF_HIP_CHECK(ctx, hipStreamWaitEvent(stream, ctx->aux_event[i], 0));
     }
@@ -532,7 +532,7 @@ int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStre
             if (b.emax == kSpillBucket) {
                 stream = ctx->aux_stream[0];
             } else {
-                stream = ctx->aux_stream[nb++ & 1];
+                stream = ctx->aux_stream[nb++ % cf_ctx::kAuxStreams];
             }
         }
         int rc;
@@ -553,7 +553,7 @@ int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStre
             if (rc != CF_OK) return rc;
             if (overlap) {   // LDS buckets start after the spill solver (it fills every CU)
                 CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[0], stream));
-                CF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux_stream[1], ctx->aux_event[0], 0));
+                for (int i = 1; i < cf_ctx::kAuxStreams; ++i) CF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux_stream[i], ctx->aux_event[0], 0));
             }
             continue;
         }

@@ -44,9 +44,11 @@ struct cf_ctx {
     // knn2 stage events (plane build start, GEMM start, GEMM end) of the last launch.
     hipEvent_t knn_ev[3] = {nullptr, nullptr, nullptr};
     int knn_path = 0;   // 1 code plane, 2 three int8 planes, 3 fp32 planes
-    // eigen bucket overlap: two non-blocking streams and fork/join events (cf_eigen.hip)
-    hipStream_t aux_stream[2] = {nullptr, nullptr};
-    hipEvent_t aux_event[3] = {nullptr, nullptr, nullptr};
+    // bucket overlap (eigen, predict): kAuxStreams non-blocking streams, a join event per
+    // stream and one fork event (cf_eigen.hip, cf_predict.hip)
+    static constexpr int kAuxStreams = 2;   // measured: 3 streams no faster at C2
+    hipStream_t aux_stream[kAuxStreams] = {};
+    hipEvent_t aux_event[kAuxStreams + 1] = {};
     // graph filter (cf_graph_filter): device time of the last call's supersteps, its edges
     float filter_ms = 0.0f;
     uint64_t filter_nnz = 0;

@@ -1126,7 +1126,7 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
             need = std::max(need, (size_t)predict_blocks(b.count) *
                                       predict_per_block(std::max<int>(2, 16 * b.emax)) * sizeof(double));
     const bool overlap = !ctx->d_phase;
-    const size_t copies = overlap ? 2 : 1;
+    const size_t copies = overlap ? cf_ctx::kAuxStreams : 1;
     if (need * copies > ctx->scratch_bytes) {
         if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
         ctx->d_scratch = nullptr;
@@ -1136,14 +1136,14 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
     }
     if (overlap) {
         if (!ctx->aux_stream[0]) {
-            for (int i = 0; i < 2; ++i) {
+            for (int i = 0; i < cf_ctx::kAuxStreams; ++i) {
                 CF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->aux_stream[i], hipStreamNonBlocking));
                 CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->aux_event[i], hipEventDisableTiming));
             }
-            CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->aux_event[2], hipEventDisableTiming));
+            CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->aux_event[cf_ctx::kAuxStreams], hipEventDisableTiming));
         }
-        CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[2], stream));
-        for (int i = 0; i < 2; ++i) CF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux_stream[i], ctx->aux_event[2], 0));
+        CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[cf_ctx::kAuxStreams], stream));
+        for (int i = 0; i < cf_ctx::kAuxStreams; ++i) CF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux_stream[i], ctx->aux_event[cf_ctx::kAuxStreams], 0));
     }
     int nb = 0;
     for (const cf_bucket& b : plan->buckets) {
@@ -1155,20 +1155,20 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
             if (rc != CF_OK) break;
             if (overlap) {
                 CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[0], st));
-                CF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux_stream[1], ctx->aux_event[0], 0));
+                for (int i = 1; i < cf_ctx::kAuxStreams; ++i) CF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux_stream[i], ctx->aux_event[0], 0));
             }
             continue;
         }
         args.first = b.first;
         const int lmax = std::max<int>(2, 16 * b.emax);
-        const int si = overlap ? (nb++ & 1) : 0;
+        const int si = overlap ? (nb++ % cf_ctx::kAuxStreams) : 0;
         rc = launch_predict_bucket<T>(ctx, args, b.count, lmax,
                                       reinterpret_cast<double*>(static_cast<char*>(ctx->d_scratch) + si * need), need,
                                       overlap ? ctx->aux_stream[si] : stream);
         if (rc != CF_OK) break;
     }
     if (overlap)
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < cf_ctx::kAuxStreams; ++i) {
             CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[i], ctx->aux_stream[i]));
             CF_HIP_CHECK(ctx, hipStreamWaitEvent(stream, ctx->aux_event[i], 0));
         }
