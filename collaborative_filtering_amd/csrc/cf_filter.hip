@@ -186,9 +186,16 @@ extern "C" int cf_graph_filter(cf_ctx* ctx, int kind, uint32_t n_vertices, uint6
     if (n_vertices) CF_HIP_CHECK(ctx, hipMemcpy(d_x.p, signal, vb8, hipMemcpyHostToDevice));
     if (n_vertices == 0) return CF_OK;
 
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    CF_HIP_CHECK(ctx, hipEventCreate(&ev0));
-    CF_HIP_CHECK(ctx, hipEventCreate(&ev1));
+    struct Events {   // destroyed on every return path
+        hipEvent_t e[2] = {nullptr, nullptr};
+        ~Events() {
+            for (hipEvent_t x : e)
+                if (x) (void)hipEventDestroy(x);
+        }
+    } evs;
+    CF_HIP_CHECK(ctx, hipEventCreate(&evs.e[0]));
+    CF_HIP_CHECK(ctx, hipEventCreate(&evs.e[1]));
+    hipEvent_t ev0 = evs.e[0], ev1 = evs.e[1];
     hipStream_t st = nullptr;
     FArgs a{};
     a.n = n_vertices;
@@ -251,8 +258,6 @@ extern "C" int cf_graph_filter(cf_ctx* ctx, int kind, uint32_t n_vertices, uint6
     (void)hipEventElapsedTime(&ms, ev0, ev1);
     ctx->filter_ms = ms;
     ctx->filter_nnz = nnz;
-    (void)hipEventDestroy(ev0);
-    (void)hipEventDestroy(ev1);
     CF_HIP_CHECK(ctx, hipMemcpy(out, result, vb8, hipMemcpyDeviceToHost));
     return CF_OK;
 }
