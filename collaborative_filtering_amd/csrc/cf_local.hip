@@ -320,7 +320,7 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
                 rc = cf_set_error(ctx, CF_EHIP, "local predict LDS attribute");
                 break;
             }
-            const uint32_t blocks = std::min<uint32_t>(n_small, 4096u);
+            const uint32_t blocks = std::min<uint32_t>(n_small, 65536u);   // ~one pair each: dispatcher-balanced
             hipLaunchKernelGGL(local_predict_kernel, dim3(blocks), dim3(kThreads), lds, 0, la, n_small);
             if (hipGetLastError() != hipSuccess) {
                 rc = cf_set_error(ctx, CF_EHIP, "local_predict_kernel launch");
