@@ -3,15 +3,23 @@
 (precompute_local_threads) fused with the graph-signal predictor
 (local_calc_precomp), on device-resident synthetic MovieLens-shaped data.
 
-One step = one pass of the hot path over the rank's user shard:
-    cf_eigen_run   (compute_eigens for every user, fp32 one-sided Jacobi in LDS)
- -> cf_predict_run (neigh_program::apply for every test rating of those users, fp64)
-with inputs already resident in HBM.  Users are range-split across ranks (weak
-scaling: every rank owns --users users); there is no collective on the data path.
+Workload (default): BASELINE config 4, the one the metric is quoted on -- ONE global set of
+1,000,000 test users x 50,000 items, k lognormal (median 100, sigma 0.5) clipped to
+[20, 180], Zipf(1) items, ratings 1..5, seed 2026101504.  The item graph is knn2's output
+(cf_item_cosine_run, the int8 MFMA path) over a 500,000-user train population from the same
+generator (seed + 1), built in untimed setup.
 
-Prints ONE JSON line (rank 0).  `value` = user-subgraph eigendecomps/sec of the
-whole job through the fused step; predicted ratings/sec and per-stage rates are
-extra fields.  See DESIGN.md for the roofline accounting.
+One step = one pass of the hot path over the rank's users with inputs resident in HBM:
+    cf_eigen_run       compute_eigens for every user (precompute_local_threads.cpp:100-213)
+ -> cf_pack_eigen_run  the records packed contiguously (the binary out_eigen_ payload)
+ -> cf_predict_run_f32 neigh_program::apply for every test rating (local_calc_precomp.cpp:217-380)
+ -> (N > 1) gather of the packed records to rank 0 over RCCL p2p
+Users are range-split across ranks by cumulative k^3 (multi.cost_split) out of the ONE
+global set: total work is fixed as N grows ("scaling": "strong").
+
+Prints ONE JSON line (rank 0).  `value` = user-subgraph eigendecomps/sec of the whole job
+through the step; predicted ratings/sec and per-stage rates are extra fields.  See DESIGN.md
+sec. 6 for the roofline accounting.
 """
 from __future__ import annotations
 
@@ -26,9 +34,18 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 (vector = f32 MFMA dense) peak, MI355X_MICROARCH.md
-FP64_PEAK_TFLOPS = 78.6
+FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 vector peak (packed FMA), MI355X_MICROARCH.md
+FP64_PEAK_TFLOPS = 78.6    # fp64 vector peak
 HBM_PEAK_GBS = 8000.0
+INT8_PEAK_TOPS = 5000.0    # int8 MFMA dense (2x bf16 2.5 PF), MI355X_MICROARCH.md
+
+CONFIGS = {
+    "c4": {"name": "BASELINE config 4", "users": 1_000_000, "items": 50_000, "seed": 2026101504,
+           "train_users": 500_000},
+    "c2": {"name": "BASELINE config 2", "users": 100_000, "items": 10_000, "seed": 2026101502,
+           "train_users": 400_000},
+}
+K_MEDIAN, K_SIGMA, K_MIN, K_MAX = 100.0, 0.5, 20, 180
 
 
 def parse():
@@ -36,26 +53,145 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--users", type=int, default=100_000, help="users per rank (BASELINE config 2: 100k)")
-    p.add_argument("--items", type=int, default=10_000)
-    p.add_argument("--k-median", type=float, default=100.0)
-    p.add_argument("--seed", type=int, default=2026101502)
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    p.add_argument("--config", choices=sorted(CONFIGS), default="c4")
+    p.add_argument("--users", type=int, default=0, help="global test users (default: the config's)")
+    p.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--profile-steps-only", action="store_true", help="skip CPU baseline (for rocprof runs)")
+    p.add_argument("--profile-steps-only", action="store_true", help="no legs, no PMC, no CPU baseline")
     p.add_argument("--pmc", choices=["auto", "off"], default="auto",
-                   help="N=1: measure HBM traffic with two rocprofv3 --pmc child passes (FETCH_SIZE, WRITE_SIZE)")
+                   help="N=1: HBM traffic from two rocprofv3 --pmc child passes (FETCH_SIZE, WRITE_SIZE)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)   # one pass, no output
+    p.add_argument("--c2", choices=["auto", "off"], default="auto",
+                   help="N=1 secondary leg: BASELINE config 2 (100k x 10k) steps and the out_eigen_ text phases")
     p.add_argument("--knn2", choices=["auto", "off", "only"], default="auto",
                    help="BASELINE config 3 knn2 leg (N=1, rank 0): int8 MFMA item cosine, 20k items x 500k users")
     p.add_argument("--knn2-users", type=int, default=500_000)
     p.add_argument("--knn2-items", type=int, default=20_000)
     p.add_argument("--knn2-reps", type=int, default=3)
     p.add_argument("--c5", choices=["auto", "off", "only"], default="auto",
-                   help="BASELINE config 5 sample (N=1, rank 0): power-law k mix through the LDS + spill eigen paths")
+                   help="BASELINE config 5 sample (N=1, rank 0): power-law k mix through the LDS + spill paths")
     p.add_argument("--c5-users", type=int, default=1000)
     p.add_argument("--c5-kmax", type=int, default=1536, help="clip of the config-5 sample (its p95 ~1.5k)")
     return p.parse_args()
+
+
+def host_threads():
+    """Host threads this process can use: the affinity mask, capped by the cgroup CPU quota
+    (on the GPU box the mask lists all 256 CPUs of the machine but the quota is 16), plus the
+    machine's counts for the record."""
+    import shutil
+    import subprocess
+
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:   # cgroup v2 CPU quota, if any ("max 100000" = none)
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    nproc = None
+    if shutil.which("nproc"):
+        try:
+            nproc = int(subprocess.run(["nproc"], capture_output=True, text=True, timeout=10).stdout.strip())
+        except (subprocess.SubprocessError, ValueError):
+            pass
+    threads = max(1, min(aff, int(np.ceil(quota)))) if quota else aff
+    return threads, {"nproc": nproc, "affinity_cpus": aff, "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota}
+
+
+def train_graph(ctx_cls, dev_index, dev, torch, seed, n_train, n_items, keep_host=False):
+    """The item graph of a config: knn2 (cf_item_cosine_run, int8 MFMA, cnt > 5, w > 0.01)
+    over a train population from the same generator (seed + 1).  Runs on its own context
+    (closed afterwards, releasing the code plane).  Returns (device dense W, host copy or
+    None, knn2 stats)."""
+    from collaborative_filtering_amd import synth
+
+    tseed = seed + 1
+    tk = synth.degrees(tseed, n_train, k_median=K_MEDIAN, sigma=K_SIGMA, kmin=K_MIN, kmax=K_MAX)
+    toff, titems, trat = synth.user_items(tseed, tk, n_items, threads=16)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    d_W = torch.empty(n_items * n_items, dtype=torch.float32, device=dev)
+    with ctx_cls(dev_index) as kctx:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        stream = torch.cuda.current_stream(dev)
+        e0.record(stream)
+        kctx.item_cosine_run(n_train, n_items, T(toff.view(np.int64)), T(titems.view(np.int32)), T(trat), 1, d_W,
+                             stream=stream.cuda_stream)
+        e1.record(stream)
+        e1.synchronize()
+        _, gemm_ms, path = kctx.knn2_timing()
+    W2 = d_W.view(n_items, n_items)
+    stats = {"train_users": n_train, "train_seed": tseed, "knn2_ms": e0.elapsed_time(e1), "knn2_kernel_ms": gemm_ms,
+             "knn2_path": path, "edges_w_gt_0.01": int((W2 > 0).sum().item()),
+             "edges_w_gt_0.1": int((W2 > 0.1).sum().item())}
+    W_host = d_W.cpu().numpy().reshape(n_items, n_items) if keep_host else None
+    return d_W, W_host, stats
+
+
+class Workload:
+    """One rank's share of a config: its users (range of the global set), device buffers."""
+
+    def __init__(self, args, cfg, rank, world, dev, torch, ctx, W_dev):
+        from collaborative_filtering_amd import synth
+        from collaborative_filtering_amd.api import evec_offsets
+        from collaborative_filtering_amd.multi import cost_split
+
+        self.torch = torch
+        self.U = args.users or cfg["users"]
+        self.seed = cfg["seed"]
+        self.n_items = cfg["items"]
+        k_all = synth.degrees(self.seed, self.U, k_median=K_MEDIAN, sigma=K_SIGMA, kmin=K_MIN, kmax=K_MAX)
+        self.split = cost_split(k_all, world)
+        lo, hi = int(self.split[rank]), int(self.split[rank + 1])
+        self.lo, self.hi = lo, hi
+        self.k = k_all[lo:hi]
+        self.k_all = k_all
+        self.off, self.items, self.ratings = synth.user_items(self.seed, self.k, self.n_items, threads=16, u_base=lo)
+        self.evec_off, n_evec = evec_offsets(self.off)
+        self.n_users = hi - lo
+        self.n_entries = int(self.off[-1])
+        ctx.upload_graph_dense(W_dev)
+        self.plan = ctx.plan(self.off)
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        self.d_off = T(self.off.view(np.int64))
+        self.d_items = T(self.items.view(np.int32))
+        self.d_rat = T(self.ratings)
+        self.d_eoff = T(self.evec_off.view(np.int64))
+        nu = max(self.n_users, 1)
+        self.d_m = torch.zeros(nu, dtype=torch.int32, device=dev)
+        self.d_sigs = torch.zeros(max(self.n_entries, 1), dtype=torch.float32, device=dev)
+        self.d_evals = torch.zeros(max(self.n_entries, 1), dtype=torch.float32, device=dev)
+        self.d_evecs = torch.zeros(max(n_evec, 1), dtype=torch.float32, device=dev)
+        self.d_mse = torch.zeros(max(self.n_entries, 1), dtype=torch.float32, device=dev)
+        self.d_kk = torch.zeros(max(self.n_entries, 1), dtype=torch.int32, device=dev)
+        self.d_poff = torch.zeros(self.n_users + 1, dtype=torch.int64, device=dev)
+        self.d_packed = None
+        self.ctx = ctx
+
+    def eigen(self, sp):
+        self.plan.eigen_run(self.d_off, self.d_items, self.d_eoff, self.d_m, self.d_sigs, self.d_evals, self.d_evecs,
+                            stream=sp)
+
+    def pack(self, sp):
+        """The records packed contiguously (cf_pack_eigen_run); the buffer is sized once."""
+        if self.d_packed is None:
+            self.ctx.pack_eigen_run(self.n_users, self.d_off, self.d_m, None, None, self.d_poff, None, stream=sp)
+            self.torch.cuda.synchronize()
+            self.d_packed = self.torch.empty(max(int(self.d_poff[-1].item()), 1), dtype=self.torch.float32,
+                                             device=self.d_m.device)
+        self.ctx.pack_eigen_run(self.n_users, self.d_off, self.d_m, self.d_eoff, self.d_evecs, self.d_poff,
+                                self.d_packed, stream=sp)
+
+    def predict(self, sp):
+        from collaborative_filtering_amd.api import CF_SIGS_COMPAT
+
+        # compat w_lim: the concatenated sigs table of the records in user order (d_sigs)
+        self.plan.predict_run(self.d_off, self.d_items, self.d_rat, self.d_m, self.d_evals, self.d_eoff, self.d_evecs,
+                              self.d_sigs, CF_SIGS_COMPAT, self.d_mse, self.d_kk, stream=sp)
 
 
 def main():
@@ -67,7 +203,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("CF_DIST_BACKEND", "nccl")   # "gloo" only to rehearse N>1 on one GPU
-    dev_index = local_rank % max(1, torch.cuda.device_count())
+    n_vis = max(1, torch.cuda.device_count())
+    dev_index = local_rank % n_vis
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(dev_index)
@@ -78,64 +215,73 @@ def main():
     dev = torch.device("cuda", dev_index)
 
     from collaborative_filtering_amd import synth
-    from collaborative_filtering_amd.api import CF_SIGS_COMPAT, Context, evec_offsets
+    from collaborative_filtering_amd.api import Context
 
     if args.c5 == "only":
         with Context(dev_index) as cctx:
-            print(json.dumps(c5_leg(args, cctx, dev, torch, synth.graph_model(args.seed, args.items, threads=16))),
-                  flush=True)
+            W, _, _ = train_graph(Context, dev_index, dev, torch, CONFIGS["c2"]["seed"], CONFIGS["c2"]["train_users"],
+                                  CONFIGS["c2"]["items"])
+            print(json.dumps(c5_leg(args, cctx, dev, torch, W.view(CONFIGS["c2"]["items"], -1))), flush=True)
         return
     if args.knn2 == "only":
         with Context(dev_index) as kctx:
             print(json.dumps(knn2_leg(args, kctx, dev, torch)), flush=True)
         return
 
+    cfg = CONFIGS[args.config]
+    solo = rank == 0 and world == 1 and not args.profile_steps_only and not args.pmc_child
+    want_cpu = solo and not args.no_cpu_baseline
+
     # ---- workload (untimed setup) -------------------------------------------------
     t_setup = time.time()
-    shard_seed = args.seed + 7919 * rank
-    k = synth.degrees(shard_seed, args.users, k_median=args.k_median, sigma=0.5, kmin=20, kmax=180)
-    off, items, ratings = synth.user_items(shard_seed, k, args.items, threads=16)
-    W = synth.graph_model(args.seed, args.items, threads=16)  # same item graph on every rank
-    evec_off, n_evec = evec_offsets(off)
-    n_entries = int(off[-1])
-
+    d_W, W_host, gstats = train_graph(Context, dev_index, dev, torch, cfg["seed"], cfg["train_users"], cfg["items"],
+                                      keep_host=want_cpu)
     ctx = Context(dev_index)
-    ctx.upload_graph_dense(W)
-    plan = ctx.plan(off)
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-    d_off = T(off.view(np.int64))
-    d_items = T(items.view(np.int32))
-    d_rat = T(ratings)
-    d_eoff = T(evec_off.view(np.int64))
-    d_m = torch.zeros(args.users, dtype=torch.int32, device=dev)
-    d_sigs = torch.zeros(n_entries, dtype=torch.float32, device=dev)
-    d_evals = torch.zeros(n_entries, dtype=torch.float32, device=dev)
-    d_evecs = torch.zeros(n_evec, dtype=torch.float32, device=dev)
-    d_mse = torch.zeros(n_entries, dtype=torch.float32, device=dev)
-    d_kk = torch.zeros(n_entries, dtype=torch.int32, device=dev)
+    wl = Workload(args, cfg, rank, world, dev, torch, ctx, d_W.view(cfg["items"], cfg["items"]))
+    del d_W
+    torch.cuda.empty_cache()
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     setup_s = time.time() - t_setup
 
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    eig_ms, pred_ms = [], []
+    gather_state = {}
+
+    def gather():
+        """Packed records of every rank to rank 0 (per-peer RCCL p2p, one group)."""
+        from collaborative_filtering_amd.multi import exchange_counts, gather_to_rank0
+
+        if "counts" not in gather_state:   # sizes are fixed for the workload: exchanged once
+            coll_dev = dev if backend == "nccl" else torch.device("cpu")
+            gather_state["n_packed"] = int(wl.d_poff[-1].item())
+            gather_state["counts"] = exchange_counts([wl.n_users, wl.n_entries, wl.n_entries,
+                                                      gather_state["n_packed"]], device=coll_dev)
+        parts = [wl.d_m[:wl.n_users], wl.d_sigs[:wl.n_entries], wl.d_evals[:wl.n_entries],
+                 wl.d_packed[:gather_state["n_packed"]]]
+        if backend != "nccl":
+            parts = [p_.cpu() for p_ in parts]
+        return gather_to_rank0(parts, gather_state["counts"])
+
+    n_ev = 4
+    evs = []
 
     def step(record):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)] if record else None
         if record:
-            ev[0].record(stream)
-        plan.eigen_run(d_off, d_items, d_eoff, d_m, d_sigs, d_evals, d_evecs, stream=sp)
+            e[0].record(stream)
+        wl.eigen(sp)
+        wl.pack(sp)
         if record:
-            ev[1].record(stream)
-        # compat w_lim: the concatenated sigs table of the records in user order (d_sigs)
-        plan.predict_run(d_off, d_items, d_rat, d_m, d_evals, d_eoff, d_evecs, d_sigs, CF_SIGS_COMPAT,
-                         d_mse, d_kk, stream=sp)
+            e[1].record(stream)
+        wl.predict(sp)
         if record:
-            ev[2].record(stream)
-            ev[2].synchronize()
-            eig_ms.append(ev[0].elapsed_time(ev[1]))
-            pred_ms.append(ev[1].elapsed_time(ev[2]))
+            e[2].record(stream)
+        if world > 1:
+            gather()
+        if record:
+            e[3].record(stream)
+            evs.append(e)
 
-    if args.pmc_child:   # one eigen + one predict pass for the PMC collector, then exit
+    if args.pmc_child:   # one step for the PMC collector, then exit
         step(False)
         torch.cuda.synchronize(dev)
         return
@@ -150,7 +296,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(False)
+        step(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -161,138 +307,99 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # Final gather of the eigen blocks (out_eigen_ content) to rank 0 over RCCL p2p,
-    # once, outside the timed steps (the only exchange step of the path).
-    gather = None
-    if world > 1:
-        from collaborative_filtering_amd.multi import exchange_counts, gather_to_rank0
-
-        coll_dev = dev if backend == "nccl" else torch.device("cpu")
-        parts = [d_m, d_sigs, d_evals, d_evecs]
-        parts = [p_ if backend == "nccl" else p_.cpu() for p_ in parts]
-        counts = exchange_counts([p_.numel() for p_ in parts], device=coll_dev)
-        dist.barrier()
-        torch.cuda.synchronize(dev)
-        tg = time.perf_counter()
-        got = gather_to_rank0(parts, counts)
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        gsec = time.perf_counter() - tg
-        gbytes = float(sum(counts[r][i] * parts[i].element_size() for r in range(1, world) for i in range(len(parts))))
-        gather = {"gather_eigen_ms": gsec * 1e3, "bytes_to_rank0": gbytes, "GBps": gbytes / gsec / 1e9,
-                  "users_gathered": int(got[0].numel()) if got is not None else None}
-
-    # Per-stage durations (separate, event-bracketed passes; outside the timed region).
-    for _ in range(max(2, args.steps)):
-        step(True)
+    # per-stage durations: HIP events on the launch stream, recorded inside the timed steps
+    eig_ms = [e[0].elapsed_time(e[1]) for e in evs]
+    pred_ms = [e[1].elapsed_time(e[2]) for e in evs]
+    gat_ms = [e[2].elapsed_time(e[3]) for e in evs]
     eig_s = float(np.median(eig_ms)) / 1e3
     pred_s = float(np.median(pred_ms)) / 1e3
+    gat_s = float(np.median(gat_ms)) / 1e3
     # Jacobi sweep counts of one more (untimed) eigen pass, for the executed-flop estimate
     ctx.debug_stats(True)
-    plan.eigen_run(d_off, d_items, d_eoff, d_m, d_sigs, d_evals, d_evecs, stream=sp)
+    wl.eigen(sp)
     torch.cuda.synchronize(dev)
     jstats = ctx.debug_stats(False, read=True)
 
     # ---- accounting -------------------------------------------------------------------
-    m_h = d_m.cpu().numpy()
-    kk_h = d_kk.cpu().numpy()
-    mse_h = d_mse.cpu().numpy()
-    kf = k.astype(np.float64)
-    flops_eig = float(np.sum(9.0 * kf ** 3 + 4.0 * kf ** 2))
-    # algorithmic bytes: item ids in, W_u entries (index+weight), sigs/evals/evecs out
-    nnz_wu = float(np.sum(kf * kf))
-    bytes_eig = float(np.sum(4 * kf) + 8 * nnz_wu + np.sum(4 * (2 * kf + m_h + kf * m_h)))
-    n_pred = n_entries
-    users_total = args.users * world
+    m_h = wl.d_m.cpu().numpy()[:wl.n_users]
+    kk_h = wl.d_kk.cpu().numpy()[:wl.n_entries]
+    mse_h = wl.d_mse.cpu().numpy()[:wl.n_entries]
+    evals_h = wl.d_evals.cpu().numpy()
+    sigs_h = wl.d_sigs.cpu().numpy()
     step_s = elapsed / args.steps
-    value = users_total / step_s
-    achieved_tf = flops_eig / eig_s / 1e12
-    pred_acc = predictor_flops(off, k, m_h, kk_h, d_evals.cpu().numpy(), d_sigs.cpu().numpy())
-    roof_eigen = {
-        "bound": "mfma",
-        "roof_note": "fp32 compute roof: 157.3 TF/s = fp32 MFMA dense peak = fp32 VALU peak; "
-                     "the Jacobi kernel is VALU (no MFMA); algorithmic flops = 9k^3+4k^2 per user",
-        "kernel": "eigen_kernel<EMAX> (all k-bucket launches of one eigen stage)",
-        "achieved": achieved_tf,
-        "peak": FP32_PEAK_TFLOPS,
-        "unit": "TFLOP/s",
-        "frac": achieved_tf / FP32_PEAK_TFLOPS,
-        "traffic": None,
-        "algorithmic_bytes_per_stage": bytes_eig,
-        "algorithmic_GBps": bytes_eig / eig_s / 1e9,
-        # one-sided Jacobi executes ~3k^3 FMA (6k^3 flops) per sweep: a dot and a two-column
-        # rotation per pair (DESIGN 3.1); sweeps from cf_debug_stats, mean over users
-        "sweeps_mean": jstats["sweeps_mean"],
-        "executed_flops_per_stage": float(np.sum(6.0 * kf ** 3)) * jstats["sweeps_mean"],
-        "executed_TFLOPs": float(np.sum(6.0 * kf ** 3)) * jstats["sweeps_mean"] / eig_s / 1e12,
-        "executed_frac": float(np.sum(6.0 * kf ** 3)) * jstats["sweeps_mean"] / eig_s / 1e12 / FP32_PEAK_TFLOPS,
-    }
-    pred_tf = pred_acc["algorithmic_flops"] / pred_s / 1e12
-    exec_tf = pred_acc["executed_flops"] / pred_s / 1e12
-    roof_pred = {
-        "bound": "mfma",
-        "roof_note": "fp64 compute roof: 78.6 TF/s = fp64 VALU peak = fp64 MFMA dense peak; the "
-                     "predictor is fp64 VALU. achieved/frac use SURVEY 8d's algorithmic count of the "
-                     "reference's per-pair work (2cL^2 + 2L^3 + 2cL + 2L^2 + 2L, L = lim); this kernel "
-                     "does far less (per-user basis + per-rating projector/Woodbury solve), so frac can "
-                     "exceed 1 and executed_frac is the hardware-efficiency figure",
-        "kernel": "predict_kernel<float> (all k-bucket launches of one predict stage)",
-        "achieved": pred_tf,
-        "peak": FP64_PEAK_TFLOPS,
-        "unit": "TFLOP/s",
-        "frac": pred_tf / FP64_PEAK_TFLOPS,
-        "traffic": None,
-        "executed_flops_per_stage": pred_acc["executed_flops"],
-        "executed_TFLOPs": exec_tf,
-        "executed_frac": exec_tf / FP64_PEAK_TFLOPS,
-        "algorithmic_bytes_per_stage": pred_acc["algorithmic_bytes"],
-        "algorithmic_GBps": pred_acc["algorithmic_bytes"] / pred_s / 1e9,
-        "lim_mean": pred_acc["lim_mean"],
-    }
+    n_pred_local = wl.n_entries
+    if world > 1:
+        coll_dev = dev if backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([float(n_pred_local)], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t)
+        n_pred_total = int(t.item())
+    else:
+        n_pred_total = n_pred_local
+    value = wl.U / step_s
+    roof_eigen = eigen_roofline(wl.k, m_h, eig_s, jstats)
+    pred_acc = predictor_flops(wl.off, wl.k, m_h, kk_h, evals_h, sigs_h)
+    roof_pred = predict_roofline(pred_acc, pred_s)
     dominant_is_pred = pred_s >= eig_s
+    devices = None
+    if world > 1:
+        coll_dev = dev if backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([dev_index], dtype=torch.int64, device=coll_dev)
+        allv = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allv, t)
+        devices = sorted(set(int(x.item()) for x in allv))
+    n_gpus = len(devices) if devices else 1
 
+    kf_all = wl.k_all.astype(np.float64)
     result = {
         "metric": "user-subgraph eigendecomps/sec + predicted ratings/sec, 1M users avg deg 100",
         "value": value,
         "unit": "user-subgraph eigendecomps/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": step_s * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32 (eigen) / f64 (predict)",
-        "data": "synthetic (splitmix64 MovieLens-shaped: Zipf(1) items, lognormal k, ratings 1..5; "
-                "item graph = expected knn2 output model)",
+        "data": "synthetic (splitmix64 MovieLens-shaped: Zipf(1) items, lognormal k, ratings 1..5); item graph = "
+                "this repo's knn2 (int8 MFMA) over a train population of the same generator",
         "config": {
-            "workload": "BASELINE config 2: batched per-user Laplacian+Jacobi eig fused with the "
-                        "local_calc_precomp predictor",
-            "users_per_gpu": args.users,
-            "items": args.items,
-            "k_mean": float(kf.mean()),
-            "k_range": [int(k.min()), int(k.max())],
-            "predictions_per_gpu": n_pred,
-            "parallelism": f"user range split x{world}",
+            "workload": f"{cfg['name']}: {wl.U} users x {wl.n_items} items, one global set range-split by k^3; "
+                        "batched per-user Laplacian + eigensolve fused with the local_calc_precomp predictor",
+            "users_global": wl.U,
+            "users_per_gpu": wl.U // max(world, 1),
+            "items": wl.n_items,
+            "seed": wl.seed,
+            "k_mean": float(kf_all.mean()),
+            "k_range": [int(wl.k_all.min()), int(wl.k_all.max())],
+            "predictions": n_pred_total,
+            "parallelism": f"user range split x{world} (cost_split on sum k^3)" + (
+                f", ranks on devices {devices}" if devices else ""),
+            "graph": gstats,
         },
-        "predicted_ratings_per_s": n_pred * world / step_s,
+        "predicted_ratings_per_s": n_pred_total / step_s,
         "stages": {
             "eigen_ms": eig_s * 1e3,
             "predict_ms": pred_s * 1e3,
-            "eigen_users_per_s": users_total / eig_s,
-            "predict_ratings_per_s": n_pred * world / pred_s,
+            "gather_ms": gat_s * 1e3 if world > 1 else 0.0,
+            "eigen_users_per_s": wl.n_users / eig_s,
+            "predict_ratings_per_s": n_pred_local / pred_s,
+            "rank0_users": wl.n_users,
+            "note": "per-stage times are rank 0's (HIP events on the launch stream, median over the timed steps); "
+                    "eigen_ms includes the record pack",
         },
         "roofline": roof_pred if dominant_is_pred else roof_eigen,
         "roofline_other": roof_eigen if dominant_is_pred else roof_pred,
-        "gather": gather,
         "setup_s": setup_s,
         "m_mean": float(m_h.mean()),
         "kk_mean": float(kk_h.mean()),
         "nan_predictions": int(np.isnan(mse_h).sum()),
+        "nc_gt_62_frac": float(np.mean((np.repeat(wl.k, wl.k) - kk_h) > 62)),
     }
 
     # ---- HBM traffic (rank 0, N=1): two rocprofv3 --pmc passes over one child step ------
-    if rank == 0 and world == 1 and args.pmc == "auto" and not args.profile_steps_only:
+    if solo and args.pmc == "auto":
         tr = pmc_traffic(args)
         if tr is not None:
             for key, roof in (("predict", roof_pred), ("eigen", roof_eigen)):
@@ -303,29 +410,189 @@ def main():
                 roof["traffic_note"] = ("HBM bytes per stage pass from rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE "
                                         "(separate passes over one child step of the same workload); "
                                         "traffic = 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of "
-                                        "MI355X_MICROARCH.md (calibrated for 16 B/lane streaming reads; this "
-                                        "kernel's narrower gathers are uncalibrated); Infinity-Cache hits count")
+                                        "MI355X_MICROARCH.md (calibrated for 16 B/lane streaming reads; these "
+                                        "kernels' narrower gathers are uncalibrated); Infinity-Cache hits count")
                 stage_s = pred_s if key == "predict" else eig_s
                 roof["traffic_GBps"] = roof["traffic"] / stage_s / 1e9
         else:
             result["pmc"] = "unavailable (rocprofv3 missing or the collector failed)"
 
-    # ---- knn2 leg (BASELINE config 3; rank 0, N=1; not part of `value`) ----------------
-    if rank == 0 and world == 1 and args.knn2 == "auto" and not args.profile_steps_only:
-        result["knn2"] = knn2_leg(args, ctx, dev, torch)
-
-    # ---- config 5 sample (rank 0, N=1; not part of `value`) ---------------------------
-    if rank == 0 and world == 1 and args.c5 == "auto" and not args.profile_steps_only:
-        result["config5"] = c5_leg(args, ctx, dev, torch, W)
-
     # ---- CPU baseline (rank 0, N=1): the oracle in precompute_local_threads form ---------
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_steps_only:
-        result["cpu_baseline"] = cpu_baseline(args, off, items, ratings, W, k)
+    if want_cpu:
+        result["cpu_baseline"] = cpu_baseline(args, wl, W_host)
+    del W_host
+
+    # ---- secondary legs (rank 0, N=1; not part of `value`) -----------------------------
+    if solo and args.c2 == "auto" and args.config != "c2":
+        wl.plan.close()
+        del wl
+        torch.cuda.empty_cache()
+        result["config2"] = c2_leg(args, ctx, dev_index, dev, torch)
+    if solo and args.knn2 == "auto":
+        torch.cuda.empty_cache()
+        result["knn2"] = knn2_leg(args, ctx, dev, torch)
+    if solo and args.c5 == "auto":
+        torch.cuda.empty_cache()
+        W, _, _ = train_graph(Context, dev_index, dev, torch, CONFIGS["c2"]["seed"], CONFIGS["c2"]["train_users"],
+                              CONFIGS["c2"]["items"])
+        result["config5"] = c5_leg(args, ctx, dev, torch, W.view(CONFIGS["c2"]["items"], -1))
+        del W
 
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def eigen_roofline(k, m_h, eig_s, jstats):
+    kf = k.astype(np.float64)
+    flops = float(np.sum(9.0 * kf ** 3 + 4.0 * kf ** 2))
+    # algorithmic bytes: item ids in, W_u entries (index+weight), sigs/evals/evecs out
+    byt = float(np.sum(4 * kf) + 8 * np.sum(kf * kf) + np.sum(4 * (2 * kf + m_h + kf * m_h)))
+    achieved = flops / eig_s / 1e12
+    exe = float(np.sum(6.0 * kf ** 3)) * jstats["sweeps_mean"]
+    return {
+        "bound": "valu",
+        "roof_note": "fp32 vector roof 157.3 TF/s (the Jacobi kernel is VALU + LDS, no MFMA); algorithmic flops = "
+                     "9k^3 + 4k^2 per user (Golub-Van Loan symmetric QR with vectors, SURVEY 8d)",
+        "kernel": "eigen_kernel<EMAX> (all k-bucket launches of one eigen stage, + the record pack)",
+        "achieved": achieved,
+        "peak": FP32_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": achieved / FP32_PEAK_TFLOPS,
+        "traffic": None,
+        "algorithmic_flops_per_stage": flops,
+        "algorithmic_bytes_per_stage": byt,
+        "algorithmic_GBps": byt / eig_s / 1e9,
+        # one-sided Jacobi executes ~3k^3 FMA (6k^3 flops) per sweep: a dot and a two-column
+        # rotation per pair (DESIGN 3.1); sweeps from cf_debug_stats, mean over users
+        "sweeps_mean": jstats["sweeps_mean"],
+        "executed_flops_per_stage": exe,
+        "executed_TFLOPs": exe / eig_s / 1e12,
+        "executed_frac": exe / eig_s / 1e12 / FP32_PEAK_TFLOPS,
+    }
+
+
+def predict_roofline(acc, pred_s):
+    tf = acc["algorithmic_flops"] / pred_s / 1e12
+    exe = acc["executed_flops"] / pred_s / 1e12
+    return {
+        "bound": "valu",
+        "roof_note": "fp64 roof 78.6 TF/s (VALU = MFMA dense fp64 peak).  algorithmic = a LOWER BOUND of the "
+                     "algorithm this kernel runs (DESIGN 3.2): per user the Gram U^T U (k Lu^2, symmetric) and "
+                     "the projector P = Q Q^T (k^2 Lu, symmetric); per rating the LDL^T of the nc x nc system "
+                     "K (nc^3/3) and its two triangular solves (2 nc^2).  ref_* fields give SURVEY 8d's count of "
+                     "the reference's explicit-inverse work per pair for comparison",
+        "kernel": "predict_kernel<float> (all k-bucket launches of one predict stage)",
+        "achieved": tf,
+        "peak": FP64_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": tf / FP64_PEAK_TFLOPS,
+        "traffic": None,
+        "algorithmic_flops_per_stage": acc["algorithmic_flops"],
+        "executed_flops_per_stage": acc["executed_flops"],
+        "executed_TFLOPs": exe,
+        "executed_frac": exe / FP64_PEAK_TFLOPS,
+        "ref_flops_per_stage": acc["ref_flops"],
+        "ref_equivalent_TFLOPs": acc["ref_flops"] / pred_s / 1e12,
+        "algorithmic_bytes_per_stage": acc["algorithmic_bytes"],
+        "algorithmic_GBps": acc["algorithmic_bytes"] / pred_s / 1e9,
+        "lim_mean": acc["lim_mean"],
+    }
+
+
+def c2_leg(args, ctx, dev_index, dev, torch):
+    """BASELINE config 2 (100k users x 10k items, graph = knn2 over 400k train users) through
+    the same step, plus the out_eigen_ text phases (compute and text-write timed
+    separately): the parallel %g writer (cfh_write_eigen) and the parallel parser
+    (cfh_load_eigen, load_precomputed_data) on the whole C2 record set, on the host's threads."""
+    from collaborative_filtering_amd.api import Context
+
+    cfg = CONFIGS["c2"]
+    a = argparse.Namespace(**vars(args))
+    a.users = cfg["users"]
+    d_W, _, gstats = train_graph(Context, dev_index, dev, torch, cfg["seed"], cfg["train_users"], cfg["items"])
+    wl = Workload(a, cfg, 0, 1, dev, torch, ctx, d_W.view(cfg["items"], cfg["items"]))
+    del d_W
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    for _ in range(2):
+        wl.eigen(sp)
+        wl.pack(sp)
+        wl.predict(sp)
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    reps = 5
+    eig, pred = [], []
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        e[0].record(stream)
+        wl.eigen(sp)
+        wl.pack(sp)
+        e[1].record(stream)
+        wl.predict(sp)
+        e[2].record(stream)
+        e[2].synchronize()
+        eig.append(e[0].elapsed_time(e[1]))
+        pred.append(e[1].elapsed_time(e[2]))
+    step_s = (time.perf_counter() - t0) / reps
+    out = {"workload": f"{cfg['name']}: {wl.U} users x {wl.n_items} items, seed {wl.seed}", "graph": gstats,
+           "users_per_s": wl.U / step_s, "ms_per_step": step_s * 1e3, "predicted_ratings_per_s": wl.n_entries / step_s,
+           "eigen_ms": float(np.median(eig)), "predict_ms": float(np.median(pred)),
+           "eigen_users_per_s": wl.U / float(np.median(eig)) * 1e3,
+           "predict_ratings_per_s": wl.n_entries / float(np.median(pred)) * 1e3,
+           "nc_gt_62_frac": float(np.mean((np.repeat(wl.k, wl.k) - wl.d_kk.cpu().numpy()[:wl.n_entries]) > 62))}
+    # ---- out_eigen_ text phases (host) -----------------------------------------------
+    try:
+        out["text_io"] = text_phases(wl)
+    except OSError as exc:
+        out["text_io"] = f"skipped: {exc}"
+    wl.plan.close()
+    return out
+
+
+def text_phases(wl):
+    import ctypes
+
+    from collaborative_filtering_amd import synth
+    from collaborative_filtering_amd._native import ptr
+
+    L = synth.host_lib()
+    L.cfh_write_eigen.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32] + \
+        [ctypes.c_void_p] * 8
+    L.cfh_write_eigen.restype = ctypes.c_int
+    L.cfh_load_eigen.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64]
+    L.cfh_load_eigen.restype = ctypes.c_int64
+    threads, _ = host_threads()
+    m = wl.d_m.cpu().numpy()[:wl.n_users]
+    sigs = wl.d_sigs.cpu().numpy()
+    evals = wl.d_evals.cpu().numpy()
+    poff = wl.d_poff.cpu().numpy().astype(np.uint64)
+    packed = wl.d_packed.cpu().numpy()
+    uid = np.arange(wl.n_users, dtype=np.uint32)
+    path = os.path.join("/tmp", f"cf_bench_out_eigen_{os.getpid()}").encode()
+    res = {"threads": threads, "records": wl.n_users}
+    try:
+        for fmt, binary in (("text", 0), ("binary", 1)):
+            t = time.perf_counter()
+            rc = L.cfh_write_eigen(path, 0, threads, binary, wl.n_users, ptr(uid), ptr(wl.off), ptr(m),
+                                   ptr(wl.items), ptr(sigs), ptr(evals), ptr(poff), ptr(packed))
+            w_s = time.perf_counter() - t
+            size = os.path.getsize(path.decode())
+            t = time.perf_counter()
+            n = L.cfh_load_eigen(path, threads, None, 0)
+            r_s = time.perf_counter() - t
+            res[fmt] = {"write_s": w_s, "parse_s": r_s, "bytes": size, "write_GBps": size / w_s / 1e9,
+                        "parse_GBps": size / r_s / 1e9, "ok": bool(rc == 0 and n == wl.n_users)}
+    finally:
+        try:
+            os.remove(path.decode())
+        except OSError:
+            pass
+    res["note"] = ("whole C2 record set (download excluded): cfh_write_eigen = the out_eigen_ writer of "
+                   "bin/precompute_local (%g via to_chars, records formatted on `threads` threads), cfh_load_eigen = "
+                   "load_precomputed_data of bin/local_calc_precomp (records parsed in parallel); file in /tmp")
+    return res
 
 
 def c5_leg(args, ctx, dev, torch, W):
@@ -335,21 +602,21 @@ def c5_leg(args, ctx, dev, torch, W):
     predictor (cf_predict_run_f32, own sigs) over every rating of those users: k <= 192 on
     predict_kernel, larger k on the spill predictor.  Reports users/s and ratings/s of the
     mix and the per-path split (HIP events around each plan)."""
-    from collaborative_filtering_amd.api import CF_SIGS_OWN
     from collaborative_filtering_amd import synth
     from collaborative_filtering_amd._native import CF_MAX_K, CF_SPILL_MAX_K
-    from collaborative_filtering_amd.api import evec_offsets
+    from collaborative_filtering_amd.api import CF_SIGS_OWN, evec_offsets
 
     seed = 2026101505
+    n_items = int(W.shape[0])
     sigma = float(np.log(15.0) / 1.6449)            # p95 / median = 15
     k = synth.degrees(seed, args.c5_users, k_median=100.0, sigma=sigma, kmin=20,
                       kmax=min(args.c5_kmax, CF_SPILL_MAX_K))
-    off, items, ratings = synth.user_items(seed, k, args.items, threads=16)
+    off, items, ratings = synth.user_items(seed, k, n_items, threads=16)
     ctx.upload_graph_dense(W)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     out = {"workload": f"BASELINE config 5 sample: {args.c5_users} users, lognormal k (median 100, "
                        f"sigma {sigma:.3f}, p95 {int(np.percentile(k, 95))}, max {int(k.max())}), "
-                       f"{args.items} items, seed {seed}"}
+                       f"{n_items} items (config-2 knn2 graph), seed {seed}"}
     stream = torch.cuda.current_stream(dev)
     total_ms = total_pms = 0.0
     for name, sel in (("lds", k <= CF_MAX_K), ("spill", k > CF_MAX_K)):
@@ -400,9 +667,6 @@ def c5_leg(args, ctx, dev, torch, W):
     out["predict_ms"] = total_pms
     out["ratings_per_s"] = int(k.sum()) / total_pms * 1e3
     return out
-
-
-INT8_PEAK_TOPS = 5000.0    # MI355X int8 MFMA dense (2x bf16 2.5 PF), MI355X_MICROARCH.md
 
 
 def knn2_leg(args, ctx, dev, torch):
@@ -482,7 +746,7 @@ def knn2_leg(args, ctx, dev, torch):
         t = time.perf_counter()
         orc.knn2_rows(off.astype(np.int64), items.astype(np.int32), rats.astype(np.float64), n_items, cal)
         per = (time.perf_counter() - t) / 2
-        n_rows = int(max(2, min(200, args.cpu_seconds / max(per, 1e-3))))
+        n_rows = int(max(2, min(200, args.cpu_seconds * 0.5 / max(per, 1e-3))))
         rows = np.sort(rng.choice(n_items, size=n_rows, replace=False)).astype(np.int32)
         t = time.perf_counter()
         Wr = orc.knn2_rows(off.astype(np.int64), items.astype(np.int32), rats.astype(np.float64), n_items, rows)
@@ -505,7 +769,7 @@ def knn2_leg(args, ctx, dev, torch):
 
 def pmc_traffic(args):
     """FETCH_SIZE and WRITE_SIZE (bytes) summed over the predict_kernel and eigen_kernel
-    launches of one child pass, each counter in its own rocprofv3 run (MI355X_MICROARCH.md:
+    launches of one child step, each counter in its own rocprofv3 run (MI355X_MICROARCH.md:
     FETCH_SIZE costs 3 TCC slots, WRITE_SIZE 2, so they cannot share a pass)."""
     import csv
     import re
@@ -517,15 +781,15 @@ def pmc_traffic(args):
     if prof is None:
         return None
     out = {"predict": [0.0, 0.0], "eigen": [0.0, 0.0]}
-    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--users", str(args.users),
-             "--items", str(args.items), "--k-median", str(args.k_median), "--seed", str(args.seed)]
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", args.config,
+             "--users", str(args.users)]
     env = dict(os.environ, TMPDIR="/tmp")
     for slot, counter in enumerate(("FETCH_SIZE", "WRITE_SIZE")):
         d = tempfile.mkdtemp(prefix="cf_pmc_", dir="/tmp")
         cmd = [prof, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--", *child]
         try:
             subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                           timeout=600, check=True)
+                           timeout=300, check=True)
             path = os.path.join(d, "run_counter_collection.csv")
             for r in csv.DictReader(open(path)):
                 name = r["Kernel_Name"]
@@ -541,94 +805,105 @@ def pmc_traffic(args):
 
 
 def predictor_flops(off, k, m, kk, evals, sigtab):
-    """Flop and byte counts of the predict stage (outside the timed region).
+    """Flop and byte counts of the predict stage (outside the timed region), vectorised.
 
-    algorithmic (the reference's per-pair work): 2cL^2 + 2L^3 + 2cL + 2L^2 + 2L with
-    c = kk and L = lim (compat w_lim = sigtab[r]; the zero-column filter, which drops a column
-    in 0.6% of pairs on this workload, is ignored); bytes = 4cL + 4c + 12 per pair.
+    algorithmic (lower bound of this kernel's algorithm): per user k Lu^2 (Gram,
+    symmetric) + k^2 Lu (P = Q Q^T, symmetric); per pair nc^3/3 + 2 nc^2 (LDL^T of K and the
+    two triangular solves), nc = k - c.
+    ref (the reference's explicit-inverse work per pair): 2cL^2 + 2L^3 + 2cL + 2L^2 +
+    2L with c = kk and L = lim (compat w_lim = sigtab[r]); bytes = 4cL + 4c + 12 per pair.
     executed (this kernel): per user Gram k Lu^2 + LDL^T Lu^3/3 + basis k Lu^2 + 8 k Lu; per pair
-    (nc + 1)(nc + 2) lim + nc^3/3 + 4 nc^2 on the fast path, and for nc > 62 (dense path)
-    2 min(c, nc) L^2 / 2 + L^3 / 3.
+    (nc + 1)(nc + 2) lim + nc^3/3 + 4 nc^2 on the fast path, and for nc > 62 min(c, nc) L^2 + L^3/3.
     """
     off = np.asarray(off, dtype=np.int64)
-    alg = 0.0
-    exe = 0.0
-    byt = 0.0
-    lim_sum = 0.0
-    for u in range(len(k)):
-        b, e = int(off[u]), int(off[u + 1])
-        ku, mu = e - b, int(m[u])
-        if ku == 0 or mu <= 0:
-            continue
-        lim = np.searchsorted(evals[b:b + mu], sigtab[:ku], side="right")   # evals ascending
-        lim = np.minimum(np.maximum(lim, 2), mu).astype(np.float64)
-        c = kk[b:e].astype(np.float64)
-        nc = ku - c
-        alg += float(np.sum(2 * c * lim ** 2 + 2 * lim ** 3 + 2 * c * lim + 2 * lim ** 2 + 2 * lim))
-        byt += float(np.sum(4 * c * lim + 4 * c + 12))
-        lu = float(lim.max())
-        exe += 2 * ku * lu * lu + lu ** 3 / 3 + 8 * ku * lu
-        fast = nc <= 62
-        exe += float(np.sum(((nc + 1) * (nc + 2) * lim + nc ** 3 / 3 + 4 * nc ** 2)[fast]))
-        exe += float(np.sum((np.minimum(c, nc) * lim ** 2 + lim ** 3 / 3)[~fast]))
-        lim_sum += float(lim.sum())
-    return {"algorithmic_flops": alg, "executed_flops": exe, "algorithmic_bytes": byt,
-            "lim_mean": lim_sum / max(float(off[-1]), 1.0)}
+    k = np.asarray(k, dtype=np.int64)
+    n = int(off[-1])
+    uid = np.repeat(np.arange(len(k)), k)
+    row = np.arange(n) - off[:-1][uid]
+    mu = np.asarray(m, dtype=np.int64)[uid]
+    # lim per row = #(stored eigenvalues of the user <= w_lim) (compat table: sigtab[row]), by one
+    # global searchsorted over keys offset by 16 x user (eigenvalues lie in [0, 2], w_lim < 16)
+    mu_k = np.minimum(np.asarray(m, dtype=np.int64), k)          # stored eigenvalues per user
+    valid = row < mu_k[uid]
+    ekeys = (uid * 16.0 + evals[:n].astype(np.float64))[valid]
+    start = np.concatenate([[0], np.cumsum(mu_k)])[:-1]
+    w = sigtab[row].astype(np.float64)
+    lim = np.searchsorted(ekeys, uid * 16.0 + w, side="right") - start[uid]
+    lim = np.minimum(np.maximum(lim, 2), mu).astype(np.float64)
+    c = np.asarray(kk, dtype=np.float64)
+    kr = k[uid].astype(np.float64)
+    nc = kr - c
+    ref = float(np.sum(2 * c * lim ** 2 + 2 * lim ** 3 + 2 * c * lim + 2 * lim ** 2 + 2 * lim))
+    byt = float(np.sum(4 * c * lim + 4 * c + 12))
+    lu = np.zeros(len(k))
+    np.maximum.at(lu, uid, lim)
+    kf = k.astype(np.float64)
+    alg = float(np.sum(kf * lu * lu + kf * kf * lu)) + float(np.sum(nc ** 3 / 3 + 2 * nc ** 2))
+    exe = float(np.sum(2 * kf * lu * lu + lu ** 3 / 3 + 8 * kf * lu))
+    fast = nc <= 62
+    exe += float(np.sum(((nc + 1) * (nc + 2) * lim + nc ** 3 / 3 + 4 * nc ** 2)[fast]))
+    exe += float(np.sum((np.minimum(c, nc) * lim ** 2 + lim ** 3 / 3)[~fast]))
+    return {"algorithmic_flops": alg, "executed_flops": exe, "ref_flops": ref, "algorithmic_bytes": byt,
+            "lim_mean": float(lim.mean()) if n else 0.0}
 
 
-def cpu_baseline(args, off, items, ratings, W, k):
+def cpu_baseline(args, wl, W):
+    """The oracle in precompute_local_threads / local_calc_precomp form (fp64, the reference's
+    dense LU inverse + 2 GEMMs + Householder/QL eigensolver; neigh_program::apply per rating
+    with the explicit-inverse Gram) on a std::thread pool of all the host threads this
+    process may use, over a bounded random sample of the same users."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref as orc
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, hinfo = host_threads()
     rng = np.random.default_rng(1)
-    order = rng.permutation(len(k))
+    order = rng.permutation(wl.n_users)
+    off, items, ratings, k = wl.off, wl.items, wl.ratings, wl.k
 
     def sample_arrays(users):
         ks = k[users].astype(np.int64)
         so = np.zeros(len(users) + 1, dtype=np.int64)
         so[1:] = np.cumsum(ks)
         si = np.concatenate([items[int(off[u]):int(off[u + 1])] for u in users]).astype(np.int32)
-        return so, si
+        sr = np.concatenate([ratings[int(off[u]):int(off[u + 1])] for u in users]).astype(np.float64)
+        return so, si, sr
 
-    # calibrate on a small sample, then size the sample to ~cpu_seconds of wall time
+    # calibrate on a small sample, then size the sample to ~cpu_seconds * 0.6 of wall time
     cal = order[:max(threads * 4, 64)]
-    so, si = sample_arrays(cal)
+    so, si, _ = sample_arrays(cal)
     t = time.perf_counter()
     orc.precompute_batch(so, si, W, n_threads=threads, faithful=True)
     rate = len(cal) / (time.perf_counter() - t)
-    n = int(min(len(k), max(len(cal), rate * args.cpu_seconds * 0.6)))
+    n = int(min(wl.n_users, max(len(cal), rate * args.cpu_seconds * 0.6)))
     users = order[:n]
-    so, si = sample_arrays(users)
+    so, si, sr = sample_arrays(users)
     t = time.perf_counter()
     m, sigs, evals, evecs, eoff = orc.precompute_batch(so, si, W, n_threads=threads, faithful=True)
     eig_s = time.perf_counter() - t
-    # predictor on a sub-sample (single thread, oracle per user)
+    # predictor over the first users of the sample (compat w_lim over the sample's records),
+    # sized to ~cpu_seconds * 0.4
+    npu = max(1, min(n, threads * 2))
     t = time.perf_counter()
-    n_pred = 0
-    budget = args.cpu_seconds * 0.4
-    for j, u in enumerate(users):
-        b, e = int(so[j]), int(so[j + 1])
-        kk_ = e - b
-        mu = int(m[j])
-        U = evecs[int(eoff[j]): int(eoff[j]) + kk_ * mu].reshape(kk_, mu)
-        evj = np.zeros(mu)
-        evj[: min(mu, kk_)] = evals[b: b + min(mu, kk_)]
-        orc.predict_user(si[b:e], ratings[int(off[u]):int(off[u + 1])], evj, U, sigs[:kk_], W)
-        n_pred += kk_
-        if time.perf_counter() - t > budget:
-            break
+    orc.predict_batch(so[:npu + 1], si[:int(so[npu])], sr[:int(so[npu])], m[:npu], evals, eoff[:npu], evecs,
+                      sigs, W, compat=True, n_threads=threads)
+    per_user = (time.perf_counter() - t) / npu
+    npu = int(min(n, max(npu, args.cpu_seconds * 0.4 / max(per_user, 1e-9))))
+    t = time.perf_counter()
+    orc.predict_batch(so[:npu + 1], si[:int(so[npu])], sr[:int(so[npu])], m[:npu], evals, eoff[:npu], evecs,
+                      sigs, W, compat=True, n_threads=threads)
     pred_s = time.perf_counter() - t
+    n_pred = int(so[npu])
     return {
         "value": n / eig_s,
         "unit": "user-subgraph eigendecomps/s",
         "cores": threads,
+        "host": hinfo,
         "kind": "port",
-        "sample": f"{n} users of the same workload (stratified random), oracle compute_eigens with the "
-                  f"reference's dense LU inverse + 2 GEMMs + Householder/QL eigensolver (fp64), "
-                  f"{threads}-thread pool",
+        "sample": f"{n} random users of the same workload, oracle compute_eigens with the reference's dense LU "
+                  f"inverse + 2 GEMMs + Householder/QL eigensolver (fp64), {threads}-thread pool",
         "predicted_ratings_per_s": n_pred / pred_s,
-        "predict_sample": f"{n_pred} predictions, oracle neigh_program::apply (fp64, 1 thread)",
+        "predict_sample": f"{n_pred} predictions ({npu} users), oracle neigh_program::apply (fp64, explicit "
+                          f"PartialPivLU-class inverse per rating, compat w_lim), {threads}-thread pool",
     }
 
 

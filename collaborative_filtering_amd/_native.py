@@ -26,6 +26,7 @@ CF_FILTER_BINOMIAL = 1
 # name -> (restype, argtypes); the list is the ABI contract checked by tests.
 SIGNATURES = {
     "cf_version": (c_int, []),
+    "cf_device_count": (c_int, []),
     "cf_create": (c_int, [c_int, POINTER(c_void_p)]),
     "cf_destroy": (None, [c_void_p]),
     "cf_last_error": (c_char_p, [c_void_p]),
@@ -66,6 +67,11 @@ SIGNATURES = {
     "cf_graph_filter_timing": (c_int, [c_void_p, c_void_p, c_void_p]),
     "cf_local_calc": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p]),
+    "cf_cost_split": (c_int, [c_uint32, c_void_p, c_int, c_void_p]),
+    "cf_pack_eigen_run": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p]),
+    "cf_eigen_batch_multi": (c_int, [c_void_p, c_int, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_void_p, c_uint64, c_void_p]),
 }
 
 _lib = None

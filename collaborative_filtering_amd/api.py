@@ -282,6 +282,46 @@ class Context:
     def plan(self, item_off_host) -> "Plan":
         return Plan(self, item_off_host)
 
+    def pack_eigen_run(self, n_users, d_item_off, d_m, d_evec_off, d_evecs, d_packed_off, d_packed=None,
+                       stream=None):
+        """cf_pack_eigen_run: packed offsets (and, with d_packed, the packed k x m blocks)
+        of the eigen output for the out_eigen_ gather."""
+        self._chk(self.lib.cf_pack_eigen_run(self.h, int(n_users), ptr(d_item_off), ptr(d_m), ptr(d_evec_off),
+                                             ptr(d_evecs), ptr(d_packed_off), ptr(d_packed), c_void_p(stream or 0)),
+                  "cf_pack_eigen_run")
+
+
+def cost_split_native(item_off, n_parts: int) -> np.ndarray:
+    """cf_cost_split: n_parts + 1 contiguous split points balancing sum(k^3)."""
+    item_off = np.ascontiguousarray(item_off, dtype=np.uint64)
+    split = np.zeros(n_parts + 1, dtype=np.uint32)
+    rc = _native.load().cf_cost_split(len(item_off) - 1, ptr(item_off), int(n_parts), ptr(split))
+    if rc != _native.CF_OK:
+        raise NativeError(f"cf_cost_split failed ({rc})")
+    return split.astype(np.int64)
+
+
+def eigen_batch_multi(ctxs, item_off, items):
+    """cf_eigen_batch_multi over contexts `ctxs` (each with the graph uploaded): returns
+    (EigenResult with packed evecs: evec_off = packed offsets, split points)."""
+    lib = _native.load()
+    item_off = np.ascontiguousarray(item_off, dtype=np.uint64)
+    items = np.ascontiguousarray(items, dtype=np.uint32)
+    n_users = len(item_off) - 1
+    _, cap = evec_offsets(item_off)
+    n = int(item_off[-1])
+    m = np.zeros(n_users, dtype=np.int32)
+    sigs = np.zeros(n, dtype=np.float32)
+    evals = np.zeros(n, dtype=np.float32)
+    poff = np.zeros(n_users + 1, dtype=np.uint64)
+    evecs = np.zeros(max(cap, 1), dtype=np.float32)
+    split = np.zeros(len(ctxs) + 1, dtype=np.uint32)
+    arr = (c_void_p * len(ctxs))(*[c.h for c in ctxs])
+    rc = lib.cf_eigen_batch_multi(arr, len(ctxs), n_users, ptr(item_off), ptr(items), ptr(m), ptr(sigs), ptr(evals),
+                                  ptr(poff), ptr(evecs), cap, ptr(split))
+    _check(lib, ctxs[0].h, rc, "cf_eigen_batch_multi")
+    return EigenResult(item_off, poff[:-1].copy(), m, sigs, evals, evecs[: int(poff[-1])]), split.astype(np.int64)
+
 
 class Plan:
     """cf_plan: users bucketed by item count, reusable across eigen/predict runs."""
@@ -320,5 +360,5 @@ class Plan:
                   ptr(d_pred), c_void_p(stream or 0)), "cf_predict_run")
 
 
-__all__ = ["Context", "Plan", "EigenResult", "evec_offsets", "CF_SIGS_OWN", "CF_SIGS_COMPAT", "CF_FILTER_CHEBY",
+__all__ = ["Context", "Plan", "EigenResult", "evec_offsets", "cost_split_native", "eigen_batch_multi", "CF_SIGS_OWN", "CF_SIGS_COMPAT", "CF_FILTER_CHEBY",
            "CF_FILTER_BINOMIAL"]

@@ -51,7 +51,13 @@ int cf_launch_dense_scatter(cf_ctx* ctx, uint32_t n_items, const uint64_t* d_row
 
 extern "C" {
 
-int cf_version(void) { return 1; }
+int cf_version(void) { return 2; }
+
+int cf_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
 
 int cf_create(int device, cf_ctx** out) {
     if (!out) return CF_EINVAL;

@@ -66,16 +66,41 @@ int main(int argc, char** argv) {
             cfcli::die("user " + std::to_string(kv.first) + " rated " + std::to_string(kv.second.size()) +
                        " movies; the eigen path supports k <= " + std::to_string(CF_SPILL_MAX_K));
     }
-    std::vector<uint64_t> eoff(n_users);
+    // --devices N (or CF_DEVICES): ONE global user set range-split across N contexts by k^3
+    // cost, each on GPU (i % visible); the records are gathered to the first GPU over xGMI
+    // and written as one out_eigen_ identical to the one-device run
+    const char* env_dev = std::getenv("CF_DEVICES");
+    const int n_dev = std::max(1, std::atoi(cfcli::opt(argc, argv, "devices", env_dev ? env_dev : "1").c_str()));
+    std::vector<uint64_t> eoff(n_users + 1);
     const uint64_t n_evec = cf_evec_offsets(n_users, off.data(), eoff.data());
     std::vector<int32_t> m(n_users);
     std::vector<float> sigs(off.back()), evals(off.back()), evecs(std::max<uint64_t>(n_evec, 1));
-    cf_ctx* ctx = cfcli::open_device();
-    cfcli::upload_edges(ctx, items, edges);
-    cfcli::check(ctx, cf_eigen_batch(ctx, n_users, off.data(), its.data(), eoff.data(), m.data(), sigs.data(),
-                                     evals.data(), evecs.data()),
-                 "cf_eigen_batch");
-    cf_destroy(ctx);
+    if (n_dev == 1) {
+        cf_ctx* ctx = cfcli::open_device();
+        cfcli::upload_edges(ctx, items, edges);
+        cfcli::check(ctx, cf_eigen_batch(ctx, n_users, off.data(), its.data(), eoff.data(), m.data(), sigs.data(),
+                                         evals.data(), evecs.data()),
+                     "cf_eigen_batch");
+        cf_destroy(ctx);
+    } else {
+        const int visible = cf_device_count();
+        if (visible <= 0) cfcli::die("no usable MI355X device");
+        const char* dev0 = std::getenv("CF_DEVICE");
+        const int base = dev0 ? std::atoi(dev0) : 0;
+        std::vector<cf_ctx*> ctxs(n_dev, nullptr);
+        for (int d = 0; d < n_dev; ++d) {
+            if (cf_create((base + d) % visible, &ctxs[d]) != CF_OK) cfcli::die("cf_create failed");
+            cfcli::upload_edges(ctxs[d], items, edges);
+        }
+        std::vector<uint32_t> split(n_dev + 1);
+        cfcli::check(ctxs[0], cf_eigen_batch_multi(ctxs.data(), n_dev, n_users, off.data(), its.data(), m.data(),
+                                                   sigs.data(), evals.data(), eoff.data(), evecs.data(),
+                                                   evecs.size(), split.data()),
+                     "cf_eigen_batch_multi");
+        for (int d = 0; d < n_dev; ++d)
+            std::printf("device part %d: users %u..%u on GPU %d\n", d, split[d], split[d + 1], (base + d) % visible);
+        for (auto* c : ctxs) cf_destroy(c);
+    }
     // out_eigen_: text records formatted on the reference's n_threads (its first argument,
     // :217-222), or the binary form with --format binary
     const int n_threads = std::max(1, std::atoi(argv[1]));

@@ -86,8 +86,11 @@ void cfh_synth_degrees(uint64_t seed, uint32_t n_users, double k_median, double 
     }
 }
 
-int cfh_synth_user_items(uint64_t seed, uint32_t n_users, uint32_t n_items, double zipf_s,
-                         const uint64_t* item_off, uint32_t* items, float* ratings, int n_threads) {
+// Users u_base .. u_base + n_users - 1 of the population: every user's items and ratings depend
+// only on (seed, global user index), so a rank can generate just its range of a global set.
+int cfh_synth_user_items_at(uint64_t seed, uint32_t u_base, uint32_t n_users, uint32_t n_items,
+                            double zipf_s, const uint64_t* item_off, uint32_t* items, float* ratings,
+                            int n_threads) {
     if (n_items == 0) return -1;
     std::vector<double> cdf(n_items);
     double acc = 0;
@@ -109,7 +112,7 @@ int cfh_synth_user_items(uint64_t seed, uint32_t n_users, uint32_t n_items, doub
         auto& s = seen[t];
         uint64_t ctr = 0;
         uint32_t got = 0;
-        const uint64_t stream = 0x1000000ull + u;
+        const uint64_t stream = 0x1000000ull + u_base + u;
         while (got < k) {
             const double x = u01(seed, stream, ctr++);
             uint32_t it = (uint32_t)(std::lower_bound(cdf.begin(), cdf.end(), x) - cdf.begin());
@@ -125,10 +128,15 @@ int cfh_synth_user_items(uint64_t seed, uint32_t n_users, uint32_t n_items, doub
         std::sort(items + b, items + b + k);
         for (uint32_t j = 0; j < k; ++j) {
             s[items[b + j]] = 0;
-            ratings[b + j] = draw_rating(u01(seed, 0x2000000ull + u, j));
+            ratings[b + j] = draw_rating(u01(seed, 0x2000000ull + u_base + u, j));
         }
     });
     return err.load();
+}
+
+int cfh_synth_user_items(uint64_t seed, uint32_t n_users, uint32_t n_items, double zipf_s,
+                         const uint64_t* item_off, uint32_t* items, float* ratings, int n_threads) {
+    return cfh_synth_user_items_at(seed, 0, n_users, n_items, zipf_s, item_off, items, ratings, n_threads);
 }
 
 // make_synthetic_als_data.cpp:118-178 on splitmix64.  Writes up to `cap` train and

@@ -23,6 +23,9 @@ def host_lib():
         L.cfh_synth_user_items.argtypes = [c_uint64, c_uint32, c_uint32, c_double, c_void_p, c_void_p, c_void_p,
                                            c_int]
         L.cfh_synth_user_items.restype = c_int
+        L.cfh_synth_user_items_at.argtypes = [c_uint64, c_uint32, c_uint32, c_uint32, c_double, c_void_p, c_void_p,
+                                              c_void_p, c_int]
+        L.cfh_synth_user_items_at.restype = c_int
         L.cfh_synth_graph_model.argtypes = [c_uint64, c_uint32, c_double, c_double, c_double, c_void_p, c_int]
         L.cfh_synth_graph_model.restype = c_int
         L.cfh_synth_als.argtypes = [c_uint64, c_uint32, c_uint32, c_uint32, c_double, c_double, c_uint32, c_uint64,
@@ -39,14 +42,17 @@ def degrees(seed: int, n_users: int, k_median: float = 100.0, sigma: float = 0.5
     return k
 
 
-def user_items(seed: int, k: np.ndarray, n_items: int, zipf_s: float = 1.0, threads: int = 8):
-    """Per-user sorted distinct items (Zipf popularity) and 1..5 ratings."""
+def user_items(seed: int, k: np.ndarray, n_items: int, zipf_s: float = 1.0, threads: int = 8, u_base: int = 0):
+    """Per-user sorted distinct items (Zipf popularity) and 1..5 ratings of users
+    u_base .. u_base + len(k) - 1 (a range of a global population: same values as the
+    corresponding slice of the whole population's output)."""
     k = np.asarray(k, dtype=np.uint64)
     off = np.zeros(len(k) + 1, dtype=np.uint64)
     off[1:] = np.cumsum(k)
     items = np.zeros(int(off[-1]), dtype=np.uint32)
     ratings = np.zeros(int(off[-1]), dtype=np.float32)
-    rc = host_lib().cfh_synth_user_items(seed, len(k), n_items, zipf_s, ptr(off), ptr(items), ptr(ratings), threads)
+    rc = host_lib().cfh_synth_user_items_at(seed, int(u_base), len(k), n_items, zipf_s, ptr(off), ptr(items),
+                                            ptr(ratings), threads)
     if rc != 0:
         raise ValueError(f"cfh_synth_user_items failed ({rc})")
     return off, items, ratings

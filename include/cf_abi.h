@@ -55,6 +55,8 @@ typedef struct cf_plan cf_plan;
 
 /* ---- context --------------------------------------------------------------- */
 int cf_version(void);
+/* Number of visible GPUs (0 when none or on error). */
+int cf_device_count(void);
 int cf_create(int device, cf_ctx** out);
 void cf_destroy(cf_ctx* ctx);
 const char* cf_last_error(const cf_ctx* ctx);
@@ -126,6 +128,36 @@ int cf_eigen_batch(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off,
 int cf_eigen_run(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
                  const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m,
                  float* d_sigs, float* d_evals, float* d_evecs, void* stream);
+
+/* ---- multi-GPU eigen stage and the out_eigen_ gather ----------
+ * Replaces the thread pool of precompute_local_threads.cpp:300-314 and the single shared
+ * out_eigen_ (:196-211, read whole by every rank at local_calc_precomp.cpp:485-486,509).
+ *
+ * cf_cost_split: contiguous split points split[0..n_parts] of users 0..n_users-1 balancing
+ * sum(k^3): split[p] = first user whose prefix cost reaches p/n_parts of the total.
+ *
+ * cf_pack_eigen_run: packs the k x m blocks of users 0..n_users-1 (stored in their
+ * cf_evec_slots slots at d_evec_off by cf_eigen_run) into one contiguous run:
+ *   d_packed_off[u] = sum_{v<u} k_v m_v  (n_users + 1 entries, u64, device)
+ *   d_packed[d_packed_off[u] + i*m_u + j] = d_evecs[d_evec_off[u] + i*m_u + j]
+ * With d_packed == NULL only the offsets are written (size the buffer from entry n_users).
+ *
+ * cf_eigen_batch_multi: cf_eigen_batch over ONE global user set on n_dev contexts (one per
+ * GPU, each with the item graph uploaded; several contexts may share a device).  Users are
+ * split by cf_cost_split, every context computes and packs its range concurrently, and the
+ * ranges are gathered to ctxs[0]'s device by peer copies over xGMI.  Outputs as
+ * cf_eigen_batch (m_out, sigs, evals at item_off) except the eigenvectors, which arrive
+ * packed: packed_off[n_users + 1] as above and packed_evecs (capacity packed_cap floats;
+ * the slot total of cf_evec_offsets always suffices).  split_out (optional, n_dev + 1)
+ * receives the ranges.  The records are identical to the one-device run's. */
+int cf_cost_split(uint32_t n_users, const uint64_t* item_off, int n_parts, uint32_t* split);
+int cf_pack_eigen_run(cf_ctx* ctx, uint32_t n_users, const uint64_t* d_item_off, const int32_t* d_m,
+                      const uint64_t* d_evec_off, const float* d_evecs, uint64_t* d_packed_off,
+                      float* d_packed, void* stream);
+int cf_eigen_batch_multi(cf_ctx* const* ctxs, int n_dev, uint32_t n_users, const uint64_t* item_off,
+                         const uint32_t* items, int32_t* m_out, float* sigs, float* evals,
+                         uint64_t* packed_off, float* packed_evecs, uint64_t packed_cap,
+                         uint32_t* split_out);
 
 /* ---- prediction stage: neigh_program::apply (local_calc_precomp.cpp:217-380) ----
  * For every user u and every row r < k of the user's block (test movie items[r] with

@@ -474,6 +474,43 @@ int cfo_predict_user(int k, int m, const int32_t* items, const double* ratings,
     return 0;
 }
 
+// a7 over a batch of users on a std::thread pool: the local_calc_precomp form of the CPU
+// baseline (GraphLab runs neigh_program::apply on --ncpus workers, local_calc_precomp.cpp:
+// 217-380, 484-583).  Per user u (rows item_off[u]..item_off[u+1]): evals at item_off[u]
+// (first m[u] valid), the k x m block at evecs + evec_off[u]; w_lim = sigtab[r] in compat mode
+// (the concatenated table, :414,437,440,271) or sigtab[item_off[u] + r] in own mode.
+// Outputs mse / kk / pred (pred may be null) at item_off[u] + r.
+int cfo_predict_batch(int n_users, const int64_t* item_off, const int32_t* items,
+                      const double* ratings, const int32_t* m, const double* evals,
+                      const int64_t* evec_off, const double* evecs, const double* sigtab,
+                      int compat, const float* W, int64_t n_items, int n_threads,
+                      float* mse_out, int32_t* kk_out, double* pred_out) {
+    std::atomic<int> next(0);
+    auto worker = [&]() {
+        std::vector<int32_t> rows;
+        for (;;) {
+            const int u = next.fetch_add(1);
+            if (u >= n_users) break;
+            const int64_t b = item_off[u];
+            const int k = (int)(item_off[u + 1] - b);
+            if (k <= 0 || m[u] <= 0) continue;
+            rows.resize(k);
+            for (int r = 0; r < k; ++r) rows[r] = r;
+            cfo_predict_user(k, m[u], items + b, ratings + b, evals + b, evecs + evec_off[u],
+                             compat ? sigtab : sigtab + b, W, n_items, k, rows.data(), mse_out + b,
+                             kk_out + b, pred_out ? pred_out + b : nullptr);
+        }
+    };
+    if (n_threads <= 1) {
+        worker();
+    } else {
+        std::vector<std::thread> pool;
+        for (int t = 0; t < n_threads; ++t) pool.emplace_back(worker);
+        for (auto& t : pool) t.join();
+    }
+    return 0;
+}
+
 // a8 assembly: the local graph of movie m (local_calc.cpp:268-334).  Row/column 0 is
 // the movie, rows 1..deg its out-neighbours nbrs[] (compact ids, w > 0.1, ascending:
 // the reference iterates a boost::unordered_map, so its row order is unpinned and the

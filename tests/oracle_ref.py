@@ -33,6 +33,8 @@ def lib():
         L.cfo_compute_eigens.restype = ci
         L.cfo_precompute_batch.argtypes = [ci, vp, vp, ctypes.c_int64, vp, vp, ci, ci, vp, vp, vp, vp]
         L.cfo_predict_user.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, ctypes.c_int64, ci, vp, vp, vp, vp]
+        L.cfo_predict_batch.argtypes = [ci, vp, vp, vp, vp, vp, vp, vp, vp, ci, vp, ctypes.c_int64, ci, vp, vp,
+                                        vp]
         L.cfo_knn2.argtypes = [ci, vp, vp, vp, ci, vp, vp]
         L.cfo_knn2_rows.argtypes = [ci, vp, vp, vp, ci, ci, vp, vp]
         L.cfo_knn3.argtypes = [ci, vp, vp, vp, vp, vp, vp]
@@ -113,6 +115,29 @@ def predict_user(items, ratings, evals, U, sigtab, W, rows=None):
     pred = np.zeros(len(rows))
     lib().cfo_predict_user(k, m, _p(items), _p(ratings), _p(evals), _p(U), _p(sigtab), _p(W), W.shape[0],
                            len(rows), _p(rows), _p(mse), _p(kk), _p(pred))
+    return mse, kk, pred
+
+
+def predict_batch(item_off, items, ratings, m, evals, evec_off, evecs, sigtab, W, compat=True, n_threads=1,
+                  want_pred=False):
+    """neigh_program::apply for every row of every user (thread pool); evals at item_off[u],
+    k x m blocks at evec_off[u].  Returns (mse float32, kk, pred or None) per row."""
+    item_off = np.ascontiguousarray(item_off, dtype=np.int64)
+    items = np.ascontiguousarray(items, dtype=np.int32)
+    ratings = np.ascontiguousarray(ratings, dtype=np.float64)
+    m = np.ascontiguousarray(m, dtype=np.int32)
+    evals = np.ascontiguousarray(evals, dtype=np.float64)
+    evec_off = np.ascontiguousarray(evec_off, dtype=np.int64)
+    evecs = np.ascontiguousarray(evecs, dtype=np.float64)
+    sigtab = np.ascontiguousarray(sigtab, dtype=np.float64)
+    W = np.ascontiguousarray(W, dtype=np.float32)
+    n = int(item_off[-1])
+    mse = np.full(n, np.nan, dtype=np.float32)
+    kk = np.full(n, -1, dtype=np.int32)
+    pred = np.zeros(n) if want_pred else None
+    lib().cfo_predict_batch(len(item_off) - 1, _p(item_off), _p(items), _p(ratings), _p(m), _p(evals),
+                            _p(evec_off), _p(evecs), _p(sigtab), int(compat), _p(W), W.shape[0], int(n_threads),
+                            _p(mse), _p(kk), _p(pred))
     return mse, kk, pred
 
 
