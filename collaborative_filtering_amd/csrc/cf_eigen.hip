@@ -519,11 +519,9 @@ int eigen_join(cf_ctx* ctx, hipStream_t stream) {
     return CF_OK;
 }
 
-int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStream_t caller) {
+int launch_buckets_on(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStream_t caller, bool overlap) {
     hipStream_t stream = caller;
     int nb = 0;
-    const bool overlap = args.mode == kUser && !args.stats;   // diagnostics keep one stream
-    if (overlap) CF_TRY(eigen_fork(ctx, caller));
     for (const cf_bucket& b : plan->buckets) {
         if (b.count == 0) continue;
         args.first = b.first;
@@ -574,8 +572,20 @@ int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStre
         }
         if (rc != CF_OK) return rc;
     }
-    if (overlap) CF_TRY(eigen_join(ctx, caller));
     return CF_OK;
+}
+
+int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStream_t caller) {
+    const bool overlap = args.mode == kUser && !args.stats;   // diagnostics keep one stream
+    if (overlap) CF_TRY(eigen_fork(ctx, caller));
+    const int rc = launch_buckets_on(ctx, plan, args, caller, overlap);
+    // join on every path: buckets already queued on the aux streams must order before the
+    // caller's stream releases or reuses their outputs, also when a later launch failed
+    if (overlap) {
+        const int rj = eigen_join(ctx, caller);
+        if (rc == CF_OK) return rj;
+    }
+    return rc;
 }
 }  // namespace
 
