@@ -32,6 +32,25 @@ def write_movielens(workdir, n_users=240, n_items=120, test_frac=0.25, seed=0, i
     return ml
 
 
+def write_c1(workdir):
+    """BASELINE config 1: make_synthetic_als_data's algorithm (cf_synth.cpp cfh_synth_als,
+    restating make_synthetic_als_data.cpp:118-178 with splitmix64 in place of GraphLab's
+    RNG) with the config's parameters, one file per role like :89-111 (nfiles = 1).
+    Ratings are printed as iostream's default %g (precision 6)."""
+    from collaborative_filtering_amd import workloads as wlm
+    from collaborative_filtering_amd import synth
+
+    c = wlm.C1
+    (tu, tm, tr), (vu, vm, vr) = synth.als(seed=c["seed"], nusers=c["nusers"], nmovies=c["nmovies"], D=c["D"],
+                                           stdev=c["stdev"], alpha=c["alpha"], nvalidate=c["nvalidate"])
+    ml = os.path.join(workdir, "movielens")
+    os.makedirs(ml, exist_ok=True)
+    for suffix, (u, m, r) in (("train", (tu, tm, tr)), ("validate", (vu, vm, vr))):
+        with open(os.path.join(ml, f"graph_0.tsv.{suffix}"), "w") as f:
+            f.writelines(f"{a}\t{b}\t{x:g}\n" for a, b, x in zip(u.tolist(), m.tolist(), r.tolist()))
+    return ml
+
+
 def read_shards(workdir, prefix):
     lines = []
     for f in sorted(glob.glob(os.path.join(workdir, prefix + "*"))):

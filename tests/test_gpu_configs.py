@@ -1,0 +1,399 @@
+"""GPU parity on every BASELINE configuration's own generator and seed.
+
+Each config's workload is built exactly as bench.py builds it (collaborative_filtering_amd/
+workloads.py): the item graph is knn2's output (cf_item_cosine_run, int8 MFMA) over the
+config's train population, the test users come from the same splitmix64 generator.  The
+device path is the TIMED one -- cf_eigen_run -> cf_predict_run_f32 on fp32 eigen blocks in
+HBM, compat w_lim, every k bucket in one call (bucket launches alternating between the two
+aux streams, > 8192 workgroups per bucket at C2/C4) -- and it is checked stage-wise:
+
+* eigen: a deterministic stratified sample (users from every k bucket of the eigen kernels)
+  against the oracle's compute_eigens (SURVEY 8a tolerances: sigs rel 1e-5, m exact unless an
+  eigenvalue sits within 1e-5 of the cut, eigenvalues abs 1e-5, clustered projectors 1e-3,
+  residual / orthonormality 1e-4); size-independent properties (residual, orthonormality,
+  sigs, m vs the cut, sign convention) on ~1000 more users against an L2 built in numpy;
+* predict: the device's OWN fp32 blocks, downloaded and widened to fp64, are fed to the
+  oracle's neigh_program::apply (compat table = the device's concatenated sigs); kk exact,
+  NaN-ness exact, |d mse| <= 1e-6 max(1, mse) where cond(U_CS^T U_CS) <= 1e8; rank-deficient
+  Gram matrices (cond > 1e8) are counted and reported, not compared (their value is rounding
+  noise in the reference too);
+* C3: knn2 rows of the full 20k x 500k problem bit-exact against the oracle's weights_calc;
+* C5: the power-law mix through the LDS and fp64 spill paths in one call;
+* C1: make_synthetic_als_data's algorithm (real-valued ratings, ids 1000..1999) through the
+  drop-in binaries (tests/test_pipeline.py, parametrized "c1").
+
+Parity is pinned to the oracle (tests/oracle_ref.py); the oracle is "parity unpinned"
+against the reference binaries themselves.
+"""
+from __future__ import annotations
+
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import oracle_ref as orc
+from test_gpu_predict import gram_cond
+
+pytestmark = pytest.mark.gpu
+
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def _torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    return torch
+
+
+class FusedRun:
+    """One pass of bench.py's step (eigen -> predict, device-resident) over a user set."""
+
+    def __init__(self, ctx, d_W, n_items, off, items, ratings, sig_mode=None):
+        from collaborative_filtering_amd.api import CF_SIGS_COMPAT, evec_offsets
+
+        torch = _torch()
+        dev = torch.device("cuda", 0)
+        self.torch, self.dev = torch, dev
+        self.n_items = n_items
+        self.off, self.items, self.ratings = off, items, ratings
+        self.k = np.diff(off.astype(np.int64))
+        self.d_W = d_W.view(n_items, n_items)
+        ctx.upload_graph_dense(self.d_W)
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        self.evec_off, n_evec = evec_offsets(off)
+        n, nu = int(off[-1]), len(off) - 1
+        self.d_off, self.d_items, self.d_rat = T(off.view(np.int64)), T(items.view(np.int32)), T(ratings)
+        self.d_eoff = T(self.evec_off.view(np.int64))
+        self.d_m = torch.zeros(nu, dtype=torch.int32, device=dev)
+        self.d_sigs = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.d_evals = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.d_evecs = torch.zeros(max(n_evec, 1), dtype=torch.float32, device=dev)
+        self.d_mse = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.d_kk = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.sig_mode = CF_SIGS_COMPAT if sig_mode is None else sig_mode
+        plan = ctx.plan(off)
+        sp = torch.cuda.current_stream(dev).cuda_stream
+        plan.eigen_run(self.d_off, self.d_items, self.d_eoff, self.d_m, self.d_sigs, self.d_evals, self.d_evecs,
+                       stream=sp)
+        plan.predict_run(self.d_off, self.d_items, self.d_rat, self.d_m, self.d_evals, self.d_eoff, self.d_evecs,
+                         self.d_sigs, self.sig_mode, self.d_mse, self.d_kk, stream=sp)
+        torch.cuda.synchronize(dev)
+        plan.close()
+        self.m = self.d_m.cpu().numpy()
+        self.sigs = self.d_sigs.cpu().numpy()
+        self.mse = self.d_mse.cpu().numpy()
+        self.kk = self.d_kk.cpu().numpy()
+
+    def free(self):
+        del self.d_evecs, self.d_mse, self.d_kk, self.d_sigs, self.d_evals
+        self.torch.cuda.empty_cache()
+
+    def user(self, u):
+        """(items, ratings, W_u float32 k x k, m, sigs, evals[m], U k x m) of user u, from HBM."""
+        b, e = int(self.off[u]), int(self.off[u + 1])
+        k, m = e - b, int(self.m[u])
+        it = self.items[b:e].astype(np.int64)
+        idx = self.torch.from_numpy(it).to(self.dev)
+        Wu = self.d_W.index_select(0, idx).index_select(1, idx).cpu().numpy()
+        ev = np.zeros(m, dtype=np.float32)
+        ev[: min(m, k)] = self.d_evals[b:b + min(m, k)].cpu().numpy()
+        o = int(self.evec_off[u])
+        U = self.d_evecs[o:o + k * m].cpu().numpy().reshape(k, m)
+        return it, self.ratings[b:e], Wu, m, self.sigs[b:e], ev, U
+
+
+# ------------------------------------------------------------------------------------------
+# stage checks shared by the configs
+# ------------------------------------------------------------------------------------------
+def eigen_check(run: FusedRun, users):
+    """Oracle compute_eigens vs the device block of each user (thread pool: ctypes drops the GIL)."""
+
+    def one(u):
+        it, _, Wu, m_g, sig_g, ev_g, U_g = run.user(u)
+        k = len(it)
+        m_ref, sig_ref, _, _, L2 = orc.compute_eigens(Wu.astype(np.float64))
+        ev_full, V_full = orc.eigh(orc.sym_lower(L2))
+        if np.max(np.abs(sig_g - sig_ref) / np.abs(sig_ref)) > 1e-5:
+            return (u, k, "sigs")
+        if m_g != m_ref:
+            smm = np.float32(np.float32(np.max(sig_ref - 0.01)) + 0.01)
+            return None if np.any(np.abs(ev_full - smm) <= 1e-5) else (u, k, f"m {m_g} != {m_ref}")
+        f = orc.compare_eigen_block(L2, m_ref, ev_full, V_full[:, :m_ref], m_g, ev_g, U_g)
+        return (u, k, f) if f else None
+
+    with ThreadPoolExecutor(THREADS) as ex:
+        bad = [r for r in ex.map(one, users) if r]
+    return bad
+
+
+def eigen_properties(run: FusedRun, users, res_tol=1e-4):
+    """Size-independent checks against an L2 assembled in numpy (precompute_local_threads.cpp:
+    114-194): sigs, m vs the cut, ascending kept eigenvalues, residual, orthonormality, and
+    the sign convention (column sums >= 0)."""
+
+    def one(u):
+        it, _, Wu, m, sig_g, ev_g, U_g = run.user(u)
+        k = len(it)
+        W = Wu.astype(np.float64)
+        d = W.sum(axis=1)
+        d[d == 0] = 1.0
+        s = np.sqrt(1.0 / d)
+        L2 = (s[:, None] * (np.diag(d) - W)) * s[None, :]
+        A = np.tril(L2) + np.tril(L2, -1).T
+        sig_ref = np.sqrt(np.sum(L2 * L2, axis=1)) + 0.01
+        if np.max(np.abs(sig_g - sig_ref) / sig_ref) > 1e-5:
+            return (u, "sigs")
+        smm = np.float32(np.float32(np.max(sig_ref - 0.01)) + 0.01)
+        kv = min(m, k)
+        if kv > 2 and not np.all(ev_g[:kv - 1] <= smm + 1e-5):
+            return (u, "m vs cut")
+        if kv < k and m > 2 and not ev_g[kv - 1] <= smm + 1e-5:
+            return (u, "m vs cut (last)")
+        if np.any(np.diff(ev_g[:kv]) < -1e-6):
+            return (u, "order")
+        Ub = U_g[:, :kv].astype(np.float64)
+        R = A @ Ub - Ub * ev_g[None, :kv]
+        res = float(np.max(np.linalg.norm(R, axis=0))) if kv else 0.0
+        orth = float(np.max(np.abs(Ub.T @ Ub - np.eye(kv)))) if kv else 0.0
+        if res > res_tol or orth > res_tol:
+            return (u, f"residual {res:.3g} orth {orth:.3g}")
+        if np.any(Ub.sum(axis=0) < -1e-6):
+            return (u, "sign")
+        return None
+
+    with ThreadPoolExecutor(THREADS) as ex:
+        return [r for r in ex.map(one, users) if r]
+
+
+def predict_check(run: FusedRun, users, max_rows=None, seed=0):
+    """Stage-wise a7 parity on the device's own fp32 blocks.  Returns (good, ill, bad)."""
+    from collaborative_filtering_amd.api import CF_SIGS_COMPAT
+
+    compat = run.sig_mode == CF_SIGS_COMPAT
+    rng = np.random.default_rng(seed)
+
+    def one(u):
+        it, rat, Wu, m, sig_g, ev_g, U_g = run.user(u)
+        k = len(it)
+        b = int(run.off[u])
+        rows = np.arange(k) if max_rows is None or k <= max_rows else \
+            np.sort(rng.choice(k, size=max_rows, replace=False))
+        tab = run.sigs[:k] if compat else sig_g
+        loc = np.arange(k, dtype=np.int32)
+        U = U_g.astype(np.float64)
+        ev = ev_g.astype(np.float64)
+        mse_o, kk_o, _ = orc.predict_user(loc, rat.astype(np.float64), ev, U, tab.astype(np.float64), Wu, rows=rows)
+        good = ill = 0
+        bad = []
+        for t, r in enumerate(rows):
+            g = b + int(r)
+            if run.kk[g] != kk_o[t]:
+                bad.append((u, int(r), "kk", int(run.kk[g]), int(kk_o[t])))
+                continue
+            if kk_o[t] == 0:
+                if not (np.isnan(run.mse[g]) and np.isnan(mse_o[t])):
+                    bad.append((u, int(r), "c=0 not NaN", float(run.mse[g]), float(mse_o[t])))
+                continue
+            cond = gram_cond(loc, ev, U, float(tab[r]), Wu, int(r))
+            if cond <= 1e8:
+                if np.isnan(run.mse[g]) or np.isnan(mse_o[t]):
+                    bad.append((u, int(r), "nan", float(run.mse[g]), float(mse_o[t]), cond))
+                    continue
+                good += 1
+                if abs(float(run.mse[g]) - float(mse_o[t])) > 1e-6 * max(1.0, float(mse_o[t])):
+                    bad.append((u, int(r), "mse", float(run.mse[g]), float(mse_o[t]), cond))
+            else:
+                ill += 1
+        return good, ill, bad
+
+    with ThreadPoolExecutor(THREADS) as ex:
+        res = list(ex.map(one, users))
+    return sum(r[0] for r in res), sum(r[1] for r in res), [b for r in res for b in r[2]]
+
+
+# ------------------------------------------------------------------------------------------
+# fixtures: one fused run per config (module scope: built once, shared by its tests)
+# ------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def c2_run(gpu_ctx):
+    from collaborative_filtering_amd import synth, workloads as wlm
+    from collaborative_filtering_amd.api import Context
+
+    torch = _torch()
+    cfg = wlm.CONFIGS["c2"]
+    d_W, _, _ = wlm.config_graph("c2", Context, 0, torch.device("cuda", 0), torch)
+    k = wlm.user_degrees(cfg)
+    off, items, rat = synth.user_items(cfg["seed"], k, cfg["items"], threads=THREADS)
+    run = FusedRun(gpu_ctx, d_W, cfg["items"], off, items, rat)
+    yield run
+    run.free()
+    del d_W
+
+
+@pytest.fixture(scope="module")
+def c4_graph():
+    from collaborative_filtering_amd import workloads as wlm
+    from collaborative_filtering_amd.api import Context
+
+    torch = _torch()
+    d_W, _, stats = wlm.config_graph("c4", Context, 0, torch.device("cuda", 0), torch)
+    yield d_W, stats
+    del d_W
+    torch.cuda.empty_cache()
+
+
+@pytest.fixture(scope="module")
+def c4_run(gpu_ctx, c4_graph):
+    """The whole 1M-user C4 set, as bench.py's default N=1 step."""
+    from collaborative_filtering_amd import synth, workloads as wlm
+
+    cfg = wlm.CONFIGS["c4"]
+    k = wlm.user_degrees(cfg)
+    off, items, rat = synth.user_items(cfg["seed"], k, cfg["items"], threads=THREADS)
+    run = FusedRun(gpu_ctx, c4_graph[0], cfg["items"], off, items, rat)
+    yield run
+    run.free()
+
+
+def _report(name, good, ill, n_rows):
+    print(f"{name}: {n_rows} predictions compared, {good} well-conditioned equal, {ill} rank-deficient "
+          f"(cond > 1e8, counted)")
+
+
+# ------------------------------------------------------------------------------------------
+# C2: 100k users x 10k items
+# ------------------------------------------------------------------------------------------
+def test_c2_eigen_stratified(c2_run):
+    from collaborative_filtering_amd import workloads as wlm
+
+    users = wlm.stratified_users(c2_run.k, 24, seed=2)
+    assert len(np.unique((c2_run.k[users] + 15) // 16)) == len(np.unique((c2_run.k + 15) // 16))
+    bad = eigen_check(c2_run, users)
+    assert not bad, bad[:10]
+
+
+def test_c2_eigen_properties(c2_run):
+    users = np.random.default_rng(3).choice(len(c2_run.k), size=1000, replace=False)
+    bad = eigen_properties(c2_run, users)
+    assert not bad, bad[:10]
+
+
+def test_c2_predict_stagewise(c2_run):
+    from collaborative_filtering_amd import workloads as wlm
+
+    users = wlm.stratified_users(c2_run.k, 12, seed=4)
+    good, ill, bad = predict_check(c2_run, users)
+    n = int(c2_run.k[users].sum())
+    _report("C2", good, ill, n)
+    assert not bad, bad[:10]
+    assert good >= 0.5 * n, (good, ill, n)
+    # whole-set invariants of the timed path: NaN only where c = 0, kk <= k - 1
+    kk = c2_run.kk
+    kr = np.repeat(c2_run.k, c2_run.k)
+    assert np.all((kk >= 0) & (kk <= kr - 1))
+    assert np.array_equal(np.isnan(c2_run.mse), kk == 0)
+
+
+# ------------------------------------------------------------------------------------------
+# C4: 1M users x 50k items (the metric's own workload)
+# ------------------------------------------------------------------------------------------
+def test_c4_graph_is_knn2_output(c4_graph):
+    _, stats = c4_graph
+    assert stats["knn2_path"] == 1 and stats["edges_w_gt_0.01"] > 10_000_000
+
+
+def test_c4_eigen_stratified(c4_run):
+    from collaborative_filtering_amd import workloads as wlm
+
+    users = wlm.stratified_users(c4_run.k, 24, seed=5)
+    bad = eigen_check(c4_run, users)
+    assert not bad, bad[:10]
+
+
+def test_c4_eigen_properties(c4_run):
+    users = np.random.default_rng(6).choice(len(c4_run.k), size=1000, replace=False)
+    bad = eigen_properties(c4_run, users)
+    assert not bad, bad[:10]
+
+
+def test_c4_predict_stagewise(c4_run):
+    from collaborative_filtering_amd import workloads as wlm
+
+    users = wlm.stratified_users(c4_run.k, 12, seed=7)
+    good, ill, bad = predict_check(c4_run, users)
+    n = int(c4_run.k[users].sum())
+    _report("C4", good, ill, n)
+    assert not bad, bad[:10]
+    assert good >= 0.3 * n, (good, ill, n)
+    kk = c4_run.kk
+    kr = np.repeat(c4_run.k, c4_run.k)
+    assert np.all((kk >= 0) & (kk <= kr - 1))
+    assert np.array_equal(np.isnan(c4_run.mse), kk == 0)
+    # wide complements (nc > 62, the block-wide K path) are in the checked sample
+    b = np.repeat(np.arange(len(c4_run.k)), c4_run.k)
+    sel = np.isin(b, users)
+    assert np.sum((kr - kk)[sel] > 62) > 50
+
+
+# ------------------------------------------------------------------------------------------
+# C5: power-law k through the LDS and spill paths, C4's 50k graph
+# ------------------------------------------------------------------------------------------
+def test_c5_mix_stagewise(gpu_ctx, c4_graph):
+    from collaborative_filtering_amd import synth, workloads as wlm
+    from collaborative_filtering_amd._native import CF_MAX_K
+
+    k_all = wlm.c5_degrees(3000, kmax=1536)
+    rng = np.random.default_rng(8)
+    lds = rng.choice(np.nonzero(k_all <= CF_MAX_K)[0], size=40, replace=False)
+    mid = np.nonzero((k_all > CF_MAX_K) & (k_all <= 420))[0][:14]
+    big = np.nonzero(k_all > 1000)[0][:3]
+    assert len(mid) >= 8 and len(big) == 3
+    users = np.sort(np.concatenate([lds, mid, big]))
+    off_all, items_all, rat_all = synth.user_items(wlm.CONFIGS["c5"]["seed"], k_all, 50_000, threads=THREADS)
+    off, items, rat = wlm.sub_csr(off_all, items_all, rat_all, users)
+    run = FusedRun(gpu_ctx, c4_graph[0], 50_000, off, items, rat)
+    pos = {int(u): i for i, u in enumerate(users)}
+    try:
+        small = [pos[int(u)] for u in np.concatenate([lds, mid])]
+        bad = eigen_check(run, small)
+        assert not bad, bad[:10]
+        bad = eigen_properties(run, [pos[int(u)] for u in big])
+        assert not bad, bad
+        good, ill, badp = predict_check(run, small, max_rows=40, seed=9)
+        _report("C5", good, ill, len(small) * 40)
+        assert not badp, badp[:10]
+        assert good > 200, (good, ill)
+    finally:
+        run.free()
+
+
+# ------------------------------------------------------------------------------------------
+# C3: knn2 at full size, 20k items x 500k train users
+# ------------------------------------------------------------------------------------------
+def test_c3_knn2_rows_bit_exact(gpu_ctx):
+    from collaborative_filtering_amd import workloads as wlm
+    from collaborative_filtering_amd.api import Context
+
+    torch = _torch()
+    dev = torch.device("cuda", 0)
+    kd, off, items, rats = wlm.c3_population(threads=THREADS)
+    n_items = wlm.CONFIGS["c3"]["items"]
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    d_W = torch.empty(n_items * n_items, dtype=torch.float32, device=dev)
+    with Context(0) as kctx:
+        kctx.item_cosine_run(len(kd), n_items, T(off.view(np.int64)), T(items.view(np.int32)), T(rats), 1, d_W)
+        torch.cuda.synchronize(dev)
+        assert kctx.knn2_timing()[2] == 1          # the one-code-plane int8 path
+    W = d_W.view(n_items, n_items)
+    assert torch.equal(W, W.t())
+    rows = np.array([0, 1, 2, 17, 999, 5000, 12345, 19999], dtype=np.int32)   # Zipf head to tail
+    Wr = orc.knn2_rows(off.astype(np.int64), items.astype(np.int32), rats.astype(np.float64), n_items, rows)
+    Wg = W[torch.from_numpy(rows.astype(np.int64)).to(dev)].cpu().numpy()
+    assert np.array_equal(Wg, Wr)
+    assert np.count_nonzero(Wg) > 1000
+    del d_W, W
+    torch.cuda.empty_cache()

@@ -20,14 +20,20 @@ pytestmark = pytest.mark.gpu
 
 
 def gram_cond(items, evals, U, sigtab_row, W, r):
+    """cond(U_CS^T U_CS) of row r as neigh_program::apply forms it (local_calc_precomp.cpp:
+    254-309): C = connected items (w > 0.1), lim = first eigenvalue > w_lim (>= 2, <= m),
+    S = the columns kept by the signed zero-column filter."""
     k, m = U.shape
-    C = [j for j in range(k) if float(W[items[r], items[j]]) > 0.1]
-    lim = 0
-    while lim < m and not evals[lim] > sigtab_row:
-        lim += 1
+    items = np.asarray(items, dtype=np.int64)
+    C = np.nonzero(np.asarray(W[items[r], items], dtype=np.float64) > 0.1)[0]
+    ev = np.asarray(evals[:m], dtype=np.float64)
+    above = np.nonzero(ev > sigtab_row)[0]
+    lim = int(above[0]) if len(above) else m
     lim = min(max(lim, 2), m)
-    keep = [c for c in range(lim) if any(U[i, c] >= 1e-4 for i in C)]
-    if not keep or not C:
+    if len(C) == 0:
+        return np.inf
+    keep = np.nonzero((U[C, :lim] >= 1e-4).any(axis=0))[0]
+    if len(keep) == 0:
         return np.inf
     G = U[np.ix_(C, keep)]
     return np.linalg.cond(G.T @ G)
