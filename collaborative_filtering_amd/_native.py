@@ -10,7 +10,7 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcf_mi355x.so")
+LIB_PATH = os.environ.get("CF_MI355X_LIB") or os.path.join(_HERE, "libcf_mi355x.so")   # override: variant builds (tools/)
 HOST_LIB_PATH = os.path.join(_HERE, "libcf_host.so")
 
 CF_OK = 0

@@ -3,8 +3,8 @@
 // Replaces neigh_program::apply of local_calc_precomp.cpp:217-380.  The reference
 // partitions by movie and copies the whole user block per rating (:234,242); here the
 // test ratings are regrouped BY USER: one 256-thread workgroup walks one user's k
-// test movies against that user's k x m eigen block (L2-resident while it works),
-// so every block is read from HBM once.  For test movie r of user u:
+// test movies against that user's k x m eigen block, so every block is read from HBM
+// once.  For test movie r of user u:
 //
 //   C    = the user's items j with w(movie_r -> item_j) > 0.1        (:132,254-265)
 //   lim  = first eigenvalue index above w_lim, >= 2                   (:271-282)
@@ -14,34 +14,38 @@
 //
 // All arithmetic after the gather is fp64 (the reference's double path).
 //
-// Fast path (per user, then one wave per rating).  The prediction is the value at row
-// r of the least-squares fit of r_C - mean on span(U_CS): it depends on U_S only
-// through an orthonormal basis Q_S of its column span.  Once per user:
-//   Gbar = U^T U over the columns [0, Lu), Lu = max_r lim_r;
-//   Q = U T1 T2 with T = I - su(G - I) - diag(G - I) / 2 (su = strictly upper part),
-//   T1 from Gbar and T2 from (U T1)^T (U T1).  U is near-orthonormal (eigenvectors:
-//   |Gbar - I| ~ 1e-6), each step squares the orthogonality error (1e-6 -> 1e-12 ->
-//   1e-24), and T1, T2 are upper triangular, so the leading lim columns of Q span the
-//   leading lim columns of U and one Q serves every row's prefix S = [0, lim).  All
-//   four products are tiled GEMM-shaped work (no sequential factorisation);
-//   g = Q^T r, h = Q^T 1, the prefix tables PG(i, l) = sum_{j<l} Q_ij g_j,
-//   PH(i, l) = sum_{j<l} Q_ij h_j, and the projector P = Q Q^T (k x k).
-// With P = Q_S Q_S^T (the k x k projector), Cbar = rows not in C (nc of them),
-// y = r - mean, and Q_S^T Q_S = I:
-//   pred - mean = a_r + P_{r,Cbar} K^-1 b,   K = I - P_{Cbar,Cbar}  (nc x nc),
-//   a_r = (P y)_r - P_{r,Cbar} y_Cbar,   b = (P y)_Cbar - P_{Cbar,Cbar} y_Cbar,
-// (Woodbury on U_CS^T U_CS = Q_S^T Q_S - Q_CbarS^T Q_CbarS), where (P y)_i =
-// PG(i, lim) - mean PH(i, lim).  lim is all but constant within a user (mean Lu - lim
-// = 0.08 on the C2 workload), so the entries of P_S = P - sum_{j in [lim, Lu)} Q_j Q_j^T
-// are gathers from P with a (usually empty) tail correction.  A rating therefore costs
-// (nc + 1)(nc + 2) / 2 gathers and an nc x nc LDL^T instead of a lim x lim
-// factorisation.
+// Basis (per user, block-wide, fp64 MFMA GEMMs).  The prediction is the value at row r
+// of the least-squares fit of r_C - mean on span(U_CS): it depends on U_S only through
+// its column span.  With Lu = max_r lim_r:
+//   Q = U T1, T1 = I - su(Gbar - I) - diag(Gbar - I) / 2 from Gbar = U^T U over [0, Lu):
+//     upper triangular, so the leading lim columns of Q span those of U for every lim;
+//   W = an orthonormal basis of the complement of span(Q) (k - Lu columns): Y = (I - Q Q^T)
+//     Omega for a +-1 test matrix Omega, then Cholesky-QR (Y^T Y = L D L^T, W = Y L^-T
+//     D^-1/2);
+//   X = [Q | W] (k x k), then one joint step X <- X T(X^T X) (T upper triangular again:
+//     prefix spans kept) squares the orthogonality error of the whole basis to ~1e-20.
+//   For every lim, X[:, lim:k] is an orthonormal basis of the complement of
+//   span(U[:, :lim]) -- the "tail" columns [lim, Lu) of Q included.
+//
+// Fast path (one wave per rating).  With Cbar = the rows not in C (nc of them, r among
+// them), d = k - lim, B = X[Cbar, lim:k] (nc x d) and y = r - mean on C:
+//   h = X[C, lim:k]^T y_C = (X^T r - mean X^T 1)[lim:k] - B^T y_Cbar
+//   c >= lim (nc <= d, full rank):  pred - mean = -e_r^T K^-1 B h,  K = B B^T  (nc x nc)
+//   c <  lim (nc >  d):             pred - mean = -w_r^T G^-1 h,    G = B^T B  (d x d)
+// K = I - P_CbarCbar (P = X_S X_S^T) is the Woodbury form of U_CS^T U_CS (the same
+// non-unit spectrum), and the first line is exactly the reference's solution.  For c < lim
+// U_CS^T U_CS is singular: the reference's explicit inverse returns rounding noise of its
+// Eigen build, and this kernel returns the minimum-norm least-squares prediction (the
+// pseudo-inverse solution).  Either system has min(nc, d) rows and is the Gram
+// matrix of gathered rows of X: fp64 MFMA on one wave (bordered by B h / e_r or w_r / h),
+// then the wave's bordered LDL^T.  A rating costs ~nc d min(nc, d) MFMA flops instead of a
+// lim x lim factorisation.
 //
 // Dense path (block-wide, the rating's own Gram matrix) for the ratings the fast path
-// does not take: the column filter drops a column, nc > kNcMax, c = 0, a pivot of K
-// below kPivMin while c >= lim (full rank but ill-conditioned: U_CS^T U_CS has an
+// does not take: the column filter drops a column, min(nc, d) > nmax, c = 0, a pivot of
+// K below kPivMin while c >= lim (full rank but ill-conditioned: U_CS^T U_CS has an
 // eigenvalue < kPivMin), or U is not near-orthonormal (max |Gbar - I| > kOrthoMax: no
-// Q for this user).
+// basis for this user).
 // It factors M = U_CS^T U_CS = L D L^T (blocked, right-looking, packed lower triangle
 // in LDS), bordered by t^T and v^T so the factorisation itself yields L^-1 t and
 // L^-1 v and pred = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean.  When the complement is
@@ -49,7 +53,6 @@
 // elimination (and unlike Cholesky) LDL^T carries on through negative pivots, so a
 // numerically indefinite, near-singular M gives the same kind of finite, clamped
 // garbage as the reference's inverse (:314) instead of a NaN.
-
 #include "cf_internal.h"
 #include "cf_ldlt.hpp"   // block-wide systems here use 8-column panels (measured: 16 -> 8 is
                            // 164.3 -> 160.0 ms at C2; the spill paths keep 16)
@@ -58,7 +61,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-constexpr int kNcMax = 62;            // fast path: complement rows (nc + 2 border rows <= 64 lanes)
+constexpr int kNsysMax = 62;          // fast path: system rows (n + 2 border rows <= 64 lanes)
 // fast path: smallest pivot of K = I - P_CbarCbar (its pivots bound the smallest
 // eigenvalue of U_CS^T U_CS in the Q basis, so this admits cond <~ 1e10, where the
 // reference's own explicit inverse is accurate to ~cond * eps; parity is tested to 1e8)
@@ -69,10 +72,16 @@ constexpr double kPivMin = 1e-10;
 constexpr double kOrthoMax = 1e-2;
 constexpr float kOrthoDone = 1e-8f;
 
+// Per-user slot of a chunk (basis kernel -> rating kernel), offsets in doubles from the slot
+// base; the int / u64 arrays live in double-sized cells.
+struct SlotOff {
+    size_t stride;   // doubles per slot
+    int gb, x, q1, ap, gx, hx, misc, cmask, lim, order, cpos;
+};
+
 template <typename T>
 struct PredArgs {
     const uint32_t* order;
-    uint32_t first;
     const uint64_t* item_off;
     const uint32_t* items;
     const float* ratings;
@@ -88,18 +97,15 @@ struct PredArgs {
     int32_t* kk;
     double* pred;
     unsigned long long* phase_cycles;  // diagnostics: per-phase s_memtime totals (or null)
-    int lmax;              // Gram dimension bound of the launch
-    int ncw;               // fast-path bound on nc for this launch
-    int ew;                // doubles of per-wave fast-path matrix E / K
-    int a_elems;           // doubles of the shared factorisation / scratch region
-    double* gbar;          // per-block scratch: Gbar = U^T U (lmax x lmax, full), fp64
-    double* qs;            // per-block scratch: Q ((lmax + 2) x lmax rows: Q, g, h), fp64
-    double* q1;            // per-block scratch: U T1, then P = Q Q^T (lmax x lmax), fp64
-    double* pgh;           // per-block scratch: {PG, PH}(i, l), lmax x (lmax + 1) pairs, fp64
-    double* abig;          // per-block HBM region of the block-wide systems (when !big_lds)
-    size_t abig_elems;     // (lmax + 2)(lmax + 3) / 2
+    int lmax;              // Gram dimension bound of the launch (row stride of the bases)
+    int nmax;              // fast path: largest system min(nc, d) on one wave
+    int ew;                // doubles of per-wave fast-path scratch (system + y + g)
+    int a_elems;           // doubles of the rating kernel's shared factorisation region
     int big_lds;           // 1: the block-wide systems use the LDS region A
+    double* slots;         // per-user slots of the chunk
+    SlotOff so;
 };
+
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -146,7 +152,8 @@ __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK ke
                            double* stage) {
     double* As = stage;
     double* Bs = stage + 16 * kStageLd;
-    const int tid = threadIdx.x;
+    int tid = threadIdx.x;
+    __asm__ volatile("" : "+v"(tid));   // per call: keeps the index math out of the user loop
     const int lane = tid & 63;
     const int wr = (tid >> 6) >> 1, wc = (tid >> 6) & 1;   // this wave's 32 x 32 quadrant
     using RA = decltype(loadA(0, 0));
@@ -160,11 +167,14 @@ __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK ke
             for (int x = 0; x < 2; ++x)
 #pragma unroll
                 for (int y = 0; y < 2; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
-            RA ra[4];
-            RB rb[4];
+            // two 16-deep chunks of raw operands in flight (registers) while a third is staged
+            // in LDS and consumed: the operands come from HBM / the MALL (~2k cycles away),
+            // a chunk's 16 MFMAs per wave take ~1k
+            RA ra0[4], ra1[4];
+            RB rb0[4], rb1[4];
             // unconditional loads from clamped indices: a guarded load would become a
             // branch with its own wait (one full latency per load)
-            auto fetch = [&](int l0) {
+            auto fetch = [&](int l0, RA (&ra)[4], RB (&rb)[4]) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     const int e = tid + kThreads * t;
@@ -174,8 +184,7 @@ __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK ke
                     rb[t] = loadB(min(l0 + lb, K - 1), min(j0 + jb, N - 1));
                 }
             };
-            if (K > 0) fetch(0);
-            for (int l0 = 0; l0 < K; l0 += 16) {
+            auto stage_chunk = [&](int l0, RA (&ra)[4], RB (&rb)[4]) {
                 __syncthreads();   // the previous chunk is consumed
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
@@ -188,7 +197,8 @@ __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK ke
                     Bs[lb * kStageLd + jb] = okb ? xB(l0 + lb, j0 + jb, rb[t]) : 0.0;
                 }
                 __syncthreads();
-                if (l0 + 16 < K) fetch(l0 + 16);
+            };
+            auto mma_chunk = [&]() {
 #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) {
                     const int row = (4 * ks + (lane >> 4)) * kStageLd + (lane & 15);
@@ -204,6 +214,18 @@ __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK ke
                         for (int y = 0; y < 2; ++y)
                             acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
                 }
+            };
+            if (K > 0) fetch(0, ra0, rb0);
+            if (K > 16) fetch(16, ra1, rb1);
+            for (int l0 = 0; l0 < K; l0 += 32) {
+                stage_chunk(l0, ra0, rb0);
+                if (l0 + 32 < K) fetch(l0 + 32, ra0, rb0);
+                mma_chunk();
+                if (l0 + 16 < K) {
+                    stage_chunk(l0 + 16, ra1, rb1);
+                    if (l0 + 48 < K) fetch(l0 + 48, ra1, rb1);
+                    mma_chunk();
+                }
             }
 #pragma unroll
             for (int x = 0; x < 2; ++x)
@@ -218,43 +240,73 @@ __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK ke
         }
 }
 
-template <typename T>
-__global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uint32_t count) {
-    extern __shared__ double dsm[];
-    const int lmax = a.lmax;
-    // A: the factorisation region.  Per user it holds Gbar's LDL^T, then the per-wave
-    //    fast-path scratch, then (dense path) the packed lower triangle of the bordered
-    //    matrix [[M, .], [t^T, .], [v^T, .]] ((lmax + 2) rows).
-    double* A = dsm;
-    double* s_misc = A + a.a_elems;   // [0] mean (dense path), [1] sum of the user's ratings
-    uint32_t* s_item = reinterpret_cast<uint32_t*>(s_misc + 4);
-    float* s_rat = reinterpret_cast<float*>(s_item + CF_MAX_K);
-    int* s_conn = reinterpret_cast<int*>(s_rat + CF_MAX_K);
-    int* s_keep = s_conn + CF_MAX_K;
-    int* s_nconn = s_keep + CF_MAX_K;                      // rows NOT in C (complement)
-    int* s_lim = s_nconn + CF_MAX_K;                       // lim of every row
-    int* s_cpos = s_lim + CF_MAX_K;                        // #rows with U(i, j) >= 1e-4
-    int* s_slow = s_cpos + CF_MAX_K;                       // rows left to the dense path
-    int* s_cnt = s_slow + CF_MAX_K;                        // [0..3] compaction, [4] lim,
-                                                           // [5] Lu, [6] Lq, [7] #dense rows,
-                                                           // [8] next fast-path rating
-    // complement masks: bit i of word 3r + (i >> 6) = item i is NOT an out-neighbour of
-    // item r with w > 0.1 (:254-265); fast-path rating order (largest nc first)
-    uint64_t* s_cmask = reinterpret_cast<uint64_t*>(s_cnt + 12);
-    int* s_order = reinterpret_cast<int*>(s_cmask + 3 * CF_MAX_K);
-    int* s_cbar = s_conn;   // fast path: per-wave complement lists (kWaves x 64), aliases s_conn/s_keep
-    double* Gb = a.gbar + (size_t)blockIdx.x * lmax * lmax;
-    double* Qs = a.qs + (size_t)blockIdx.x * (lmax + 2) * lmax;
-    double* PGH = a.pgh + (size_t)blockIdx.x * lmax * (lmax + 1) * 2;
+// Lower triangle of a Gram matrix on ONE wave, fp64 MFMA: E[tri(i, j)] = sum_{s < inner}
+// val(i, s) val(j, s) for j <= i < nt (nt <= 16 NS).  val(a, s) comes from load(a, s), which
+// must return 0 outside a < nt, s < inner (callers clamp the address and select).  Operand
+// strips of 16 rows x 4 terms: lane l of strip t holds val(16t + (l & 15), s0 + (l >> 4)),
+// which is both the A fragment (A[l&15][l>>4]) of tile row t and the B fragment
+// (B[l>>4][l&15]) of tile column t; the NS(NS+1)/2 lower tiles accumulate in registers.
+// Operands are fetched PF steps (4 PF terms) at a time and the next batch is in flight while
+// the current one's MFMAs issue, so a rating pays ~inner / (4 PF) load round trips.
+template <int NS, int PF, class LOAD>
+__device__ void wave_gram_t(int nt, int inner, LOAD load, double* E) {
+    constexpr int NT = NS * (NS + 1) / 2;
+    const int lane = threadIdx.x & 63;
+    const int li = lane & 15, lk = lane >> 4;
+    f64x4 acc[NT];
+#pragma unroll
+    for (int x = 0; x < NT; ++x) acc[x] = f64x4{0.0, 0.0, 0.0, 0.0};
+    double v[PF][NS], w[PF][NS];
+    auto fetch = [&](int s0) {
+#pragma unroll
+        for (int p = 0; p < PF; ++p)
+#pragma unroll
+            for (int t = 0; t < NS; ++t) w[p][t] = load(16 * t + li, s0 + 4 * p + lk);
+    };
+    fetch(0);
+    for (int s0 = 0; s0 < inner; s0 += 4 * PF) {
+#pragma unroll
+        for (int p = 0; p < PF; ++p)
+#pragma unroll
+            for (int t = 0; t < NS; ++t) v[p][t] = w[p][t];
+        if (s0 + 4 * PF < inner) fetch(s0 + 4 * PF);
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+            if (s0 + 4 * p >= inner) break;   // wave-uniform
+            int x = 0;
+#pragma unroll
+            for (int ti = 0; ti < NS; ++ti)
+#pragma unroll
+                for (int tj = 0; tj <= ti; ++tj, ++x)
+                    acc[x] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[p][ti], v[p][tj], acc[x], 0, 0, 0);
+        }
+    }
+    int x = 0;
+#pragma unroll
+    for (int ti = 0; ti < NS; ++ti)
+#pragma unroll
+        for (int tj = 0; tj <= ti; ++tj, ++x)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = 16 * ti + lk + 4 * q, col = 16 * tj + li;
+                if (row < nt && col <= row) E[tri(row, col)] = acc[x][q];
+            }
+}
 
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    // Diagnostic phase stamps (thread 0 only; no effect on outputs):
-    // {user setup, basis Q, fast ratings, block-wide ratings} cycles, {#fast, #block-wide}
-    // ratings, {Gbar GEMM, block-wide K path} cycles.
-    unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long ph_t = 0;
+template <class LOAD>
+__device__ void wave_gram(int nt, int inner, LOAD load, double* E) {
+    if (nt <= 16)
+        wave_gram_t<1, 16>(nt, inner, load, E);
+    else if (nt <= 32)
+        wave_gram_t<2, 8>(nt, inner, load, E);
+    else if (nt <= 48)
+        wave_gram_t<3, 4>(nt, inner, load, E);
+    else
+        wave_gram_t<4, 4>(nt, inner, load, E);
+}
+
+// Diagnostic phase stamps (thread 0 only; no effect on outputs): {user setup, basis,
+// fast ratings, block-wide ratings} cycles, {#fast, #block-wide} ratings, {Gbar GEMM} cycles.
 #define PHASE_STAMP(ph)                                                   \
     if (a.phase_cycles && tid == 0) {                                     \
         const unsigned long long now = __builtin_amdgcn_s_memtime();      \
@@ -262,8 +314,35 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
         ph_t = now;                                                       \
     }
 
+// ---- kernel 1: per user of a chunk, lim / complement masks / order of the ratings, Gbar,
+// the basis X = [Q | W] and X^T r, X^T 1, into the user's slot ---------------------------
+template <typename T>
+__global__ __launch_bounds__(kThreads, 2) void pred_basis_kernel(PredArgs<T> a, uint32_t first, uint32_t count) {
+    extern __shared__ double dsm[];
+    const int lmax = a.lmax;
+    double* A = dsm;                                       // block_gemm staging
+    double* s_misc = A + kStageElems;                      // [1] sum of the user's ratings
+    uint32_t* s_item = reinterpret_cast<uint32_t*>(s_misc + 4);
+    float* s_rat = reinterpret_cast<float*>(s_item + CF_MAX_K);
+    int* s_lim = reinterpret_cast<int*>(s_rat + CF_MAX_K);   // lim of every row
+    int* s_cpos = s_lim + CF_MAX_K;                        // #rows with U(i, j) >= 1e-4
+    int* s_slow = s_cpos + CF_MAX_K;                       // nc of every row
+    int* s_cnt = s_slow + CF_MAX_K;                        // [5] Lu, [6] orthogonality, [9] failure
+    // complement masks: bit i of word 3r + (i >> 6) = item i is NOT an out-neighbour of
+    // item r with w > 0.1 (:254-265); fast-path rating order (largest nc first)
+    uint64_t* s_cmask = reinterpret_cast<uint64_t*>(s_cnt + 12);
+    int* s_order = reinterpret_cast<int*>(s_cmask + 3 * CF_MAX_K);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long ph_t = 0;
+
     for (uint32_t ub = blockIdx.x; ub < count; ub += gridDim.x) {
-        const uint32_t u = a.order[a.first + ub];
+        double* slot = a.slots + (size_t)ub * a.so.stride;
+        double* Gb = slot + a.so.gb;
+        const uint32_t u = a.order[first + ub];
         const uint64_t base = a.item_off[u];
         const int k = (int)(a.item_off[u + 1] - base);
         const int m = a.m[u];
@@ -271,11 +350,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
         const T* ev = a.evals + base;
         __syncthreads();
         PHASE_STAMP(-1);
-        if (tid == 0) {
-            s_cnt[5] = 0;
-            s_cnt[7] = 0;
-            s_cnt[8] = 0;
-        }
+        if (tid == 0) s_cnt[5] = 0;
         for (int j = tid; j < m; j += kThreads) A[j] = (double)ev[j];   // evals staged in A
         __syncthreads();
         for (int i = tid; i < k; i += kThreads) {
@@ -381,121 +456,240 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
         const int Lq = (__int_as_float(s_cnt[6]) <= (float)kOrthoMax) ? Lu : 0;
         PHASE_STAMP(0);
 
-        // Q = U T1 T2 ..., T(l, j) = -G(l, j) (l < j), 1.5 - G(j, j) / 2 (l = j), 0 (l > j),
-        // T1 from Gbar, each further T from the Gram of the previous product (held in the
-        // PGH buffer until the prefix tables are built); stop once that Gram is within
-        // kOrthoDone of I (two steps for eigenvectors, |Gbar - I| ~ 1e-6).
-        double* Q1 = a.q1 + (size_t)blockIdx.x * lmax * lmax;
-        double* G2 = PGH;
+        // ---- basis X = [Q | W] (file header): Q = U T1, W by Cholesky-QR of (I - Q Q^T)
+        // Omega, one joint T step on X; then X^T r and X^T 1 --------------------------------
+        double* Q1 = slot + a.so.q1;
+        double* Xb = slot + a.so.x;
+        double* AP = slot + a.so.ap;
+        const int ld = lmax;
+        double* Xf = Xb;   // the final basis
+        int Lx = 0;        // 0: no basis (every rating of the user takes the dense path)
         if (Lq > 0) {
             const auto tri_end = [&](int j0) { return min(Lq, j0 + 64); };
             block_gemm<true, false>(
                 k, Lq, [&](int i, int l) { return U[(size_t)i * m + l]; }, as_double,
                 [&](int l, int j) { return Gb[(size_t)l * lmax + j]; }, tri_T, tri_end, all_blocks,
-                [&](int i, int j, double v) { Q1[(size_t)i * Lq + j] = v; }, stage);
-            double* X = Q1;
-            double* Y = Qs;
-            for (int it = 0; it < 3; ++it) {
-                __syncthreads();
-                if (tid == 0) s_cnt[6] = 0;
-                __syncthreads();
-                float dv = 0.0f;
+                [&](int i, int j, double v) { Xb[(size_t)i * ld + j] = v; }, stage);
+            __syncthreads();
+            if (tid == 0) s_cnt[9] = 0;
+            const int du = k - Lq;
+            if (du > 0) {
+                // Omega(i, j) = +-1 from a hash of (user, i, j): deterministic per user
+                const uint32_t seed = u * 0x9E3779B1u + 0x7F4A7C15u;
+                const auto omega = [seed](int i, int j) -> double {
+                    uint32_t h = seed ^ ((uint32_t)i * 0x85EBCA6Bu) ^ ((uint32_t)j * 0xC2B2AE35u);
+                    h ^= h >> 16;
+                    h *= 0x7FEB352Du;
+                    h ^= h >> 15;
+                    h *= 0x846CA68Bu;
+                    h ^= h >> 16;
+                    return (h & 1u) ? 1.0 : -1.0;
+                };
+                const auto om = [&](int l, int j) { return omega(l, j); };
+                // Q^T Omega (Lq x du) -> Q1
                 block_gemm<false, false>(
-                    Lq, Lq, [&](int i, int l) { return X[(size_t)l * Lq + i]; }, as_double,
-                    [&](int l, int j) { return X[(size_t)l * Lq + j]; }, as_double, [&](int) { return k; },
-                    lower_blocks,
-                    [&](int i, int j, double v) {
-                        if (j > i) return;
-                        G2[(size_t)i * Lq + j] = v;
-                        G2[(size_t)j * Lq + i] = v;
-                        const float d = (float)fabs(v - (i == j ? 1.0 : 0.0));
-                        dv = fmaxf(dv, d == d ? d : 3.0e38f);
-                    },
+                    Lq, du, [&](int i, int l) { return Xb[(size_t)l * ld + i]; }, as_double, om, as_double,
+                    [&](int) { return k; }, all_blocks, [&](int i, int j, double v) { Q1[(size_t)i * ld + j] = v; },
                     stage);
-                for (int off = 32; off >= 1; off >>= 1) dv = fmaxf(dv, __shfl_xor(dv, off));
-                if (lane == 0) atomicMax(&s_cnt[6], __float_as_int(dv));
                 __syncthreads();
-                const bool last = it == 2 || __int_as_float(s_cnt[6]) <= kOrthoDone;
+                // Y = Omega - Q (Q^T Omega) (k x du) -> Xb[:, Lq:k]
                 block_gemm<true, false>(
-                    k, Lq, [&](int i, int l) { return X[(size_t)i * Lq + l]; }, as_double,
-                    [&](int l, int j) { return G2[(size_t)l * Lq + j]; }, tri_T, tri_end, all_blocks,
-                    [&](int i, int j, double v) { Y[(size_t)i * Lq + j] = v; }, stage);
-                if (last) {
-                    if (Y != Qs) {
-                        __syncthreads();
-                        for (int e = tid; e < k * Lq; e += kThreads) Qs[e] = Y[e];
+                    k, du, [&](int i, int l) { return Xb[(size_t)i * ld + l]; }, as_double,
+                    [&](int l, int j) { return Q1[(size_t)l * ld + j]; }, as_double, [&](int) { return Lq; },
+                    all_blocks, [&](int i, int j, double v) { Xb[(size_t)i * ld + Lq + j] = omega(i, j) - v; }, stage);
+                __syncthreads();
+                // Y^T Y (du x du, packed lower) -> AP, L D L^T in place
+                block_gemm<false, false>(
+                    du, du, [&](int i, int l) { return Xb[(size_t)l * ld + Lq + i]; }, as_double,
+                    [&](int l, int j) { return Xb[(size_t)l * ld + Lq + j]; }, as_double, [&](int) { return k; },
+                    lower_blocks, [&](int i, int j, double v) { if (j <= i) AP[tri(i, j)] = v; }, stage);
+                __syncthreads();
+                ldlt_bordered<kThreads, 16>(AP, du, du);
+                // W row i = D^-1/2 L^-1 y_i, in place (each thread its own rows)
+                double dmax = 0.0;
+                for (int j = 0; j < du; ++j) dmax = fmax(dmax, AP[tri(j, j)]);
+                bool fail = false;
+                for (int i = tid; i < k; i += kThreads) {
+                    double* xi = Xb + (size_t)i * ld + Lq;
+                    for (int j = 1; j < du; ++j) {
+                        const double* Lj = AP + tri(j, 0);
+                        double z = xi[j];
+                        for (int t = 0; t < j; ++t) z = fma(-Lj[t], xi[t], z);
+                        xi[j] = z;
                     }
-                    break;
-                }
-                double* tmp = X;
-                X = Y;
-                Y = tmp;
-            }
-        }
-        __syncthreads();
-        // g, h (global rows k, k + 1 of Qs, and staged in A: T2 is no longer needed)
-        double* s_g = A;
-        double* s_h = A + Lq;
-        for (int j = tid; j < Lq; j += kThreads) {
-            double g = 0.0, h = 0.0;
-            for (int i0 = 0; i0 < k; i0 += 8) {
-                double v[8];
-#pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    const double q = Qs[(size_t)min(i0 + t, k - 1) * Lq + j];
-                    v[t] = i0 + t < k ? q : 0.0;
-                }
-#pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    g = fma(v[t], (double)s_rat[min(i0 + t, k - 1)], g);   // v[t] = 0 past k
-                    h += v[t];
-                }
-            }
-            Qs[(size_t)k * Lq + j] = g;
-            Qs[(size_t)(k + 1) * Lq + j] = h;
-            s_g[j] = g;
-            s_h[j] = h;
-        }
-        __syncthreads();
-        for (int i = tid; i < k; i += kThreads) {
-            const double* qi = Qs + (size_t)i * Lq;
-            double2* out = reinterpret_cast<double2*>(PGH) + (size_t)i * (Lq + 1);
-            double pg = 0.0, ph = 0.0;
-            out[0] = make_double2(0.0, 0.0);
-            for (int j0 = 0; j0 < Lq; j0 += 8) {
-                double v[8];
-#pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    const double q = qi[min(j0 + t, Lq - 1)];
-                    v[t] = j0 + t < Lq ? q : 0.0;
-                }
-#pragma unroll
-                for (int t = 0; t < 8; ++t)
-                    if (j0 + t < Lq) {
-                        pg = fma(v[t], s_g[j0 + t], pg);
-                        ph = fma(v[t], s_h[j0 + t], ph);
-                        out[j0 + t + 1] = make_double2(pg, ph);
+                    for (int j = 0; j < du; ++j) {
+                        const double dj = AP[tri(j, j)];
+                        fail |= !(dj > 1e-12 * dmax);
+                        xi[j] = dj > 0.0 ? xi[j] / sqrt(dj) : 0.0;
                     }
+                }
+                if (__syncthreads_or(fail) && tid == 0) s_cnt[9] = 1;
+                __syncthreads();
             }
+            // joint T steps on X (k columns): X^T X packed in AP, X <- X T (ping-pong Xb/Q1)
+            double* Xs = Xb;
+            double* Xd = Q1;
+            if (s_cnt[9] == 0) {
+                for (int it = 0; it < 3; ++it) {
+                    if (tid == 0) s_cnt[6] = 0;
+                    __syncthreads();
+                    float dv = 0.0f;
+                    block_gemm<false, false>(
+                        k, k, [&](int i, int l) { return Xs[(size_t)l * ld + i]; }, as_double,
+                        [&](int l, int j) { return Xs[(size_t)l * ld + j]; }, as_double, [&](int) { return k; },
+                        lower_blocks,
+                        [&](int i, int j, double v) {
+                            if (j > i) return;
+                            AP[tri(i, j)] = v;
+                            const float dd = (float)fabs(v - (i == j ? 1.0 : 0.0));
+                            dv = fmaxf(dv, dd == dd ? dd : 3.0e38f);
+                        },
+                        stage);
+                    for (int off = 32; off >= 1; off >>= 1) dv = fmaxf(dv, __shfl_xor(dv, off));
+                    if (lane == 0) atomicMax(&s_cnt[6], __float_as_int(dv));
+                    __syncthreads();
+                    const float dev_x = __int_as_float(s_cnt[6]);
+                    if (!(dev_x <= (float)kOrthoMax)) break;   // no basis: Lx stays 0
+                    const auto k_end = [&](int j0) { return min(k, j0 + 64); };
+                    block_gemm<true, false>(
+                        k, k, [&](int i, int l) { return Xs[(size_t)i * ld + l]; }, as_double,
+                        [&](int l, int j) { return AP[tri(max(l, j), min(l, j))]; }, tri_T, k_end, all_blocks,
+                        [&](int i, int j, double v) { Xd[(size_t)i * ld + j] = v; }, stage);
+                    __syncthreads();
+                    double* tmp = Xs;
+                    Xs = Xd;
+                    Xd = tmp;
+                    if (dev_x <= kOrthoDone) {
+                        Lx = k;
+                        break;
+                    }
+                }
+            }
+            Xf = Xs;
         }
-        double* Pm = Q1;   // U T1 is consumed: P = Q Q^T takes its place
-        if (Lq > 0)
-            block_gemm<true, true>(
-                k, k, [&](int i, int l) { return Qs[(size_t)i * Lq + l]; }, as_double,
-                [&](int l, int j) { return Qs[(size_t)j * Lq + l]; }, as_double, [&](int) { return Lq; }, lower_blocks,
-                [&](int i, int j, double v) {
-                    if (j > i) return;
-                    Pm[(size_t)i * k + j] = v;
-                    Pm[(size_t)j * k + i] = v;
-                },
-                stage);
+        // X^T r and X^T 1, the rating-level arrays and the flags into the slot
+        double* s_gx = slot + a.so.gx;
+        double* s_hx = slot + a.so.hx;
+        if (Lx > 0)
+            for (int j = tid; j < k; j += kThreads) {
+                double g0 = 0.0, g1 = 0.0, h0 = 0.0, h1 = 0.0;
+                int i = 0;
+                for (; i + 1 < k; i += 2) {
+                    const double x0 = Xf[(size_t)i * ld + j], x1 = Xf[(size_t)(i + 1) * ld + j];
+                    g0 = fma(x0, (double)s_rat[i], g0);
+                    g1 = fma(x1, (double)s_rat[i + 1], g1);
+                    h0 += x0;
+                    h1 += x1;
+                }
+                if (i < k) {
+                    const double x0 = Xf[(size_t)i * ld + j];
+                    g0 = fma(x0, (double)s_rat[i], g0);
+                    h0 += x0;
+                }
+                s_gx[j] = g0 + g1;
+                s_hx[j] = h0 + h1;
+            }
         __syncthreads();
         PHASE_STAMP(1);
+        {
+            int* lim_g = reinterpret_cast<int*>(slot + a.so.lim);
+            int* ord_g = reinterpret_cast<int*>(slot + a.so.order);
+            int* cpos_g = reinterpret_cast<int*>(slot + a.so.cpos);
+            uint64_t* cm_g = reinterpret_cast<uint64_t*>(slot + a.so.cmask);
+            for (int i = tid; i < k; i += kThreads) {
+                lim_g[i] = s_lim[i];
+                ord_g[i] = s_order[i];
+            }
+            for (int i = tid; i < 3 * k; i += kThreads) cm_g[i] = s_cmask[i];
+            for (int j = tid; j < Lu; j += kThreads) cpos_g[j] = s_cpos[j];
+            if (tid == 0) {
+                double* misc = slot + a.so.misc;
+                misc[0] = s_misc[1];
+                misc[1] = (double)Lx;
+                misc[2] = (double)Lq;
+                misc[3] = Xf == Q1 ? 1.0 : 0.0;
+            }
+        }
+    }
+    if (a.phase_cycles && tid == 0)
+        for (int ph = 0; ph < 8; ++ph) atomicAdd(&a.phase_cycles[ph], ph_acc[ph]);
+}
 
-        // ---- fast path: one wave per rating ------------------------------------------
+// ---- kernel 2: per user of a chunk, every rating from the slot: the fast path (one wave per
+// rating) and the dense path (block-wide) -------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kThreads, 2) void pred_rating_kernel(PredArgs<T> a, uint32_t first, uint32_t count) {
+    extern __shared__ double dsm[];
+    const int lmax = a.lmax;
+    // A: the factorisation region: the per-wave fast-path scratch, then (dense path) the
+    //    packed lower triangle of the bordered matrix [[M, .], [t^T, .], [v^T, .]].
+    double* A = dsm;
+    double* s_misc = A + a.a_elems;   // [0] mean (dense path), [1] sum of the user's ratings
+    double* s_gx = s_misc + 4;                              // X^T r (k)
+    double* s_hx = s_gx + CF_MAX_K;                         // X^T 1 (k)
+    uint32_t* s_item = reinterpret_cast<uint32_t*>(s_hx + CF_MAX_K);
+    float* s_rat = reinterpret_cast<float*>(s_item + CF_MAX_K);
+    int* s_conn = reinterpret_cast<int*>(s_rat + CF_MAX_K);
+    int* s_keep = s_conn + CF_MAX_K;
+    int* s_nconn = s_keep + CF_MAX_K;                      // rows NOT in C (complement)
+    int* s_lim = s_nconn + CF_MAX_K;                       // lim of every row
+    int* s_cpos = s_lim + CF_MAX_K;                        // #rows with U(i, j) >= 1e-4
+    int* s_slow = s_cpos + CF_MAX_K;                       // rows left to the dense path
+    int* s_cnt = s_slow + CF_MAX_K;                        // [0..3] compaction, [4] flag,
+                                                           // [7] #dense rows, [8] next rating
+    uint64_t* s_cmask = reinterpret_cast<uint64_t*>(s_cnt + 12);
+    int* s_order = reinterpret_cast<int*>(s_cmask + 3 * CF_MAX_K);
+    int* s_cb = s_order + CF_MAX_K;                        // kWaves x CF_MAX_K
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long ph_t = 0;
+
+    for (uint32_t ub = blockIdx.x; ub < count; ub += gridDim.x) {
+        double* slot = a.slots + (size_t)ub * a.so.stride;
+        const double* Gb = slot + a.so.gb;
+        double* AP = slot + a.so.ap;
+        const uint32_t u = a.order[first + ub];
+        const uint64_t base = a.item_off[u];
+        const int k = (int)(a.item_off[u + 1] - base);
+        const int m = a.m[u];
+        const T* U = a.evecs + a.evec_off[u];
+        const double* misc = slot + a.so.misc;
+        const int Lx = (int)misc[1];
+        const int Lq = (int)misc[2];
+        const double* Xf = slot + (misc[3] != 0.0 ? a.so.q1 : a.so.x);
+        const int ld = lmax;
+        __syncthreads();
+        {
+            const int* lim_g = reinterpret_cast<const int*>(slot + a.so.lim);
+            const int* ord_g = reinterpret_cast<const int*>(slot + a.so.order);
+            const int* cpos_g = reinterpret_cast<const int*>(slot + a.so.cpos);
+            const uint64_t* cm_g = reinterpret_cast<const uint64_t*>(slot + a.so.cmask);
+            for (int i = tid; i < k; i += kThreads) {
+                s_item[i] = a.items[base + i];
+                s_rat[i] = a.ratings[base + i];
+                s_lim[i] = lim_g[i];
+                s_order[i] = ord_g[i];
+                s_gx[i] = slot[a.so.gx + i];
+                s_hx[i] = slot[a.so.hx + i];
+            }
+            for (int i = tid; i < 3 * k; i += kThreads) s_cmask[i] = cm_g[i];
+            for (int j = tid; j < min(m, k + 2); j += kThreads) s_cpos[j] = j < Lq ? cpos_g[j] : 0;
+            if (tid == 0) {
+                s_misc[1] = misc[0];
+                s_cnt[7] = 0;
+                s_cnt[8] = 0;
+            }
+        }
+        __syncthreads();
+        PHASE_STAMP(-1);
+
+        // ---- fast path: one wave per rating, in the complement coordinates of its prefix --
         {
             double* Ew = A + (size_t)wave * a.ew;
-            int* cb = s_cbar + wave * 64;
+            int* cb = s_cb + wave * CF_MAX_K;
             const double sum_all = s_misc[1];
             // ratings are claimed from s_order one ahead (LDS counter)
             auto claim = [&]() {
@@ -511,26 +705,28 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                 const int r = s_order[idx];
                 idx = claim();
                 const unsigned long long rt0 = a.phase_cycles ? __builtin_amdgcn_s_memtime() : 0ull;
-                int nc = 0;
+                // Cbar in ascending row order (the position of r in it), its rating sum
+                int nc = 0, posr = 0;
                 double sc = 0.0;
 #pragma unroll
                 for (int t = 0; t < 3; ++t) {
                     const int i = 64 * t + lane;
                     const unsigned long long bal = s_cmask[3 * r + t];
-                    const bool out = (bal >> lane) & 1ull;
-                    if (out) {
-                        const int pos = nc + __popcll(bal & ((1ull << lane) - 1ull));
-                        if (pos < 64) cb[pos] = i;
+                    if ((bal >> lane) & 1ull) {
+                        cb[nc + __popcll(bal & ((1ull << lane) - 1ull))] = i;
                         sc += (double)s_rat[i];
                     }
+                    if ((r >> 6) == t) posr = nc + __popcll(bal & ((1ull << (r & 63)) - 1ull));
                     nc += __popcll(bal);
                 }
                 sc = wave_sum(sc);
                 const int c = k - nc;
                 const int lim = s_lim[r];
-                bool slow = c == 0 || nc > a.ncw || lim > Lq || m < 2;
-                // too many complement rows for one wave: the block-wide K path (bit 16)
-                const bool wide = !(c == 0 || lim > Lq || m < 2) && nc > a.ncw;
+                const int d = k - lim;
+                const bool kmode = nc <= d;   // c >= lim: full rank
+                const int n = kmode ? nc : d;
+                const bool r_out = (s_cmask[3 * r + (r >> 6)] >> (r & 63)) & 1ull;   // r in Cbar (w(r,r) <= 0.1)
+                bool slow = c == 0 || Lx == 0 || m < 2 || n > a.nmax || !r_out;
                 WAVE_SYNC();
                 if (!slow) {
                     // column j < lim is dropped (:284-304) iff every row with
@@ -547,89 +743,79 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                     slow = __ballot(drop) != 0ull;
                 }
                 if (slow) {
-                    if (lane == 0) s_slow[atomicAdd(&s_cnt[7], 1)] = r | (wide ? 0x10000 : 0);
+                    if (lane == 0) s_slow[atomicAdd(&s_cnt[7], 1)] = r;
                     continue;
                 }
                 const double mu = (sum_all - sc) / (double)c;   // mean over C (:311)
                 const unsigned long long sp0 = a.phase_cycles ? __builtin_amdgcn_s_memtime() : 0ull;
-
-                // E = P_S over the rows [Cbar..., r] (np rows, packed lower): gathers
-                // from P, minus the tail sum_{j in [lim, Lq)} Q_aj Q_bj when lim < Lq.
-                const int np = nc + 1;
-                const int nent = np * (np + 1) / 2;
-                // border-row inputs, issued ahead of the P gathers: (PG, PH)(i, lim) of row
-                // cb[lane] (lane < nc) or r (lane 63), and y_q = r_q - mu of the complement
-                const double2* pgh_lim = reinterpret_cast<const double2*>(PGH) + lim;
-                const double2 py = pgh_lim[(size_t)(lane < nc ? cb[lane] : r) * (Lq + 1)];
-                double* sy = Ew + (a.ew - 64);
-                if (lane < nc) sy[lane] = (double)s_rat[cb[lane]] - mu;
-                auto entry_rows = [&](int e, int& ia, int& ib) {
-                    int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-                    while (ra * (ra + 1) / 2 > e) --ra;
-                    while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
-                    const int rb = e - ra * (ra + 1) / 2;
-                    ia = ra < nc ? cb[ra] : r;
-                    ib = rb < nc ? cb[rb] : r;
-                };
-                for (int e0 = 0; e0 < nent; e0 += 4 * 64) {   // four gathers in flight per lane
-                    double v[4];
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        int ia, ib;
-                        entry_rows(min(e0 + 64 * t + lane, nent - 1), ia, ib);
-                        v[t] = Pm[(size_t)ia * k + ib];
-                    }
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        if (e0 + 64 * t + lane < nent) Ew[e0 + 64 * t + lane] = v[t];
-                }
-                if (lim < Lq) {   // rare (mean Lu - lim = 0.08): the tail of P_S
-                    for (int e = lane; e < nent; e += 64) {
-                        int ia, ib;
-                        entry_rows(e, ia, ib);
-                        const double* xa = Qs + (size_t)ia * Lq;
-                        const double* xb = Qs + (size_t)ib * Lq;
-                        double v = Ew[e];
-                        for (int j = lim; j < Lq; ++j) v = fma(-xa[j], xb[j], v);
-                        Ew[e] = v;
-                    }
-                }
+                // The system and its border rows come out of ONE Gram pass over gathered rows of
+                // X (B = X[Cbar, lim:k]) with one extra operand (g = (X^T r - mu X^T 1)[lim:k],
+                // y = r - mu on Cbar), so h = g - B^T y is never formed on its own:
+                //   K-mode: Gram of the rows {B, g^T} -> K and B g; b = B h = B g - K y;
+                //   G-mode: Gram of the columns {B, y} -> G and B^T y; h = g - B^T y.
+                double* aux = Ew + (n + 2) * (n + 3) / 2;   // [0, nc): y; [nc, nc + d): g
+                for (int q = lane; q < nc; q += 64) aux[q] = (double)s_rat[cb[q]] - mu;
+                for (int j = lane; j < d; j += 64) aux[nc + j] = s_gx[lim + j] - mu * s_hx[lim + j];
                 WAVE_SYNC();
-
-                // Border rows: row nc = P_{r,Cbar} (already in place), row nc + 1 := b.
-                // a_r on lane 63 (never a border lane's register).
-                double bl = 0.0, ar = 0.0;
-                if (lane < nc) {
-                    bl = py.x - mu * py.y;
-                    for (int q = 0; q < nc; ++q) {
-                        const double eq = q <= lane ? Ew[tri(lane, q)] : Ew[tri(q, lane)];
-                        bl = fma(-eq, sy[q], bl);
+                const double* yv = aux;
+                const double* gv = aux + nc;
+                if (kmode) {
+                    wave_gram(nc + 1, d,
+                              [&](int ar, int s) {
+                                  const int s2 = min(s, d - 1);
+                                  const double vg = Xf[(size_t)cb[min(ar, nc - 1)] * ld + lim + s2];
+                                  const double vl = gv[s2];
+                                  return s < d ? (ar < nc ? vg : (ar == nc ? vl : 0.0)) : 0.0;
+                              },
+                              Ew);
+                    WAVE_SYNC();
+                    // b_a = (B g)_a - sum_q K_aq y_q into border row n; row n + 1 = e_r
+                    double ba = 0.0;
+                    if (lane < n) {
+                        ba = Ew[tri(n, lane)];
+                        for (int q = 0; q < n; ++q) {
+                            const double kq = q <= lane ? Ew[tri(lane, q)] : Ew[tri(q, lane)];
+                            ba = fma(-kq, yv[q], ba);
+                        }
                     }
-                }
-                if (lane == 63) {
-                    ar = py.x - mu * py.y;
-                    for (int q = 0; q < nc; ++q) ar = fma(-Ew[tri(nc, q)], sy[q], ar);
-                }
-                WAVE_SYNC();
-                if (lane < nc) {
-                    Ew[tri(nc + 1, lane)] = bl;
-                    for (int q = 0; q <= lane; ++q) Ew[tri(lane, q)] = (q == lane ? 1.0 : 0.0) - Ew[tri(lane, q)];
+                    WAVE_SYNC();
+                    if (lane < n) {
+                        Ew[tri(n, lane)] = ba;
+                        Ew[tri(n + 1, lane)] = lane == posr ? 1.0 : 0.0;
+                    }
+                } else {
+                    if (d > 0)
+                        wave_gram(d + 1, nc,
+                                  [&](int ar, int s) {
+                                      const int s2 = min(s, nc - 1);
+                                      const double vg = Xf[(size_t)cb[s2] * ld + lim + min(ar, d - 1)];
+                                      const double vl = yv[s2];
+                                      return s < nc ? (ar < d ? vg : (ar == d ? vl : 0.0)) : 0.0;
+                                  },
+                                  Ew);
+                    WAVE_SYNC();
+                    // row n = w_r, row n + 1 = h = g - B^T y (row d of the Gram)
+                    if (lane < n) {
+                        const double h = gv[lane] - Ew[tri(n, lane)];
+                        Ew[tri(n + 1, lane)] = h;
+                        Ew[tri(n, lane)] = Xf[(size_t)r * ld + lim + lane];
+                    }
                 }
                 WAVE_SYNC();
                 const unsigned long long sp1 = a.phase_cycles ? __builtin_amdgcn_s_memtime() : 0ull;
                 if (a.phase_cycles) wacc[0] += sp1 - sp0;
-                // LDL^T of K (nc columns), border rows nc (P_{r,Cbar}) and nc + 1 (b);
+                // LDL^T of the n x n system, border rows n and n + 1;
                 // lane i owns row i.  Panels of 4 columns, no per-column sync:
                 //  1. every lane factors the 4x4 diagonal block redundantly in registers;
                 //  2. each row below it solves against that block (its 4 entries of L);
                 //  3. the rank-4 trailing update A22 -= L21 D L21^T is one
                 //     v_mfma_f64_16x16x4 per 16x16 lower tile (k = 4 = the panel width).
                 // An exactly zero pivot is skipped (its column of L is 0), as in cf_ldlt.hpp.
-                const int nrows = nc + 2;
+                const int nrows = n + 2;
                 double minpiv = 1.0;
                 const int li = lane & 15, lk = lane >> 4;
-                for (int j0 = 0; j0 < nc; j0 += 4) {
-                    const int pw = min(4, nc - j0);
+                for (int j0 = 0; j0 < n; j0 += 4) {
+                    const int pw = min(4, n - j0);
                     double Lm[4][4], Dv[4], Di[4];
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
@@ -684,8 +870,8 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                     }
                     WAVE_SYNC();
                     const int r0 = j0 + pw;
-                    if (r0 < nc) {
-                        const int ntr = (nrows - r0 + 15) >> 4, ntc = (nc - r0 + 15) >> 4;
+                    if (r0 < n) {
+                        const int ntr = (nrows - r0 + 15) >> 4, ntc = (n - r0 + 15) >> 4;
                         const double dk = lk == 0 ? Dv[0] : lk == 1 ? Dv[1] : lk == 2 ? Dv[2] : Dv[3];
                         const int kc = j0 + min(lk, pw - 1);
                         for (int ti = 0; ti < ntr; ++ti) {
@@ -700,14 +886,14 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
 #pragma unroll
                                 for (int x = 0; x < 2; ++x) {
                                     const int col = r0 + 16 * (tq0 + x) + li;
-                                    const double bv = Ew[tri(min(col, nc - 1), kc)];
-                                    bop[x] = (col < nc && lk < pw) ? bv : 0.0;
+                                    const double bv = Ew[tri(min(col, n - 1), kc)];
+                                    bop[x] = (col < n && lk < pw) ? bv : 0.0;
 #pragma unroll
                                     for (int q = 0; q < 4; ++q) {
                                         const int row = r0 + 16 * ti + lk + 4 * q;
                                         const int rc = min(row, nrows - 1);
                                         const double v = Ew[tri(rc, min(col, rc))];
-                                        acc[x][q] = (tq0 + x <= tmax && row < nrows && col < nc && col <= row) ? v : 0.0;
+                                        acc[x][q] = (tq0 + x <= tmax && row < nrows && col < n && col <= row) ? v : 0.0;
                                     }
                                 }
                                 acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop, bop[0], acc[0], 0, 0, 0);
@@ -718,7 +904,7 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
 #pragma unroll
                                     for (int q = 0; q < 4; ++q) {
                                         const int row = r0 + 16 * ti + lk + 4 * q;
-                                        if (tq0 + x <= tmax && row < nrows && col < nc && col <= row)
+                                        if (tq0 + x <= tmax && row < nrows && col < n && col <= row)
                                             Ew[tri(row, col)] = acc[x][q];
                                     }
                                 }
@@ -729,25 +915,21 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
                 }
                 if (a.phase_cycles) wacc[1] += __builtin_amdgcn_s_memtime() - sp1;
                 double dot = 0.0;
-                if (lane < nc) dot = Ew[tri(nc, lane)] * Ew[tri(nc + 1, lane)] * Ew[tri(lane, lane)];
+                if (lane < n) dot = Ew[tri(n, lane)] * Ew[tri(n + 1, lane)] * Ew[tri(lane, lane)];
                 dot = wave_sum(dot);
-                ar = __shfl(ar, 63);
                 WAVE_SYNC();
-                // Full-rank but ill-conditioned (c >= lim): the dense path, whose error
-                // matches the reference's.  Rank-deficient (c < lim: U_CS^T U_CS is
-                // singular in exact arithmetic, the reference's inverse returns rounding
-                // noise) stays here: b is orthogonal to null(K) exactly as t is to null(M),
-                // so this is the same kind of noise-amplified value.
-                if (!(minpiv >= kPivMin) && c >= lim) {
+                // Full rank but ill-conditioned (c >= lim, a pivot of K below kPivMin): the
+                // dense path, whose error matches the reference's
+                if (kmode && !(minpiv >= kPivMin)) {
                     if (lane == 0) s_slow[atomicAdd(&s_cnt[7], 1)] = r;
                     continue;
                 }
                 if (lane == 0) {
-                    double pred = mu + ar + dot;
+                    double pred = mu - dot;
                     if (pred > 5) pred = 5;
                     if (pred < 1) pred = 1;
-                    const double d = (double)s_rat[r] - pred;
-                    a.mse[base + r] = (float)(d * d);
+                    const double e = (double)s_rat[r] - pred;
+                    a.mse[base + r] = (float)(e * e);
                     a.kk[base + r] = c;
                     if (a.pred) a.pred[base + r] = pred;
                 }
@@ -779,12 +961,12 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
         PHASE_STAMP(2);
 
         // The block-wide systems live in LDS when the bucket's full triangle fits beside two
-        // resident blocks per CU, else in this block's HBM region (L2-resident while used).
-        // (The per-wave fast-path scratch in A is dead by now: a system that fits in A --
-        // (n + 2)(n + 3)/2 doubles for n rows -- uses it whatever big_lds says.)
-        double* const Ahbm = a.abig + (size_t)blockIdx.x * a.abig_elems;
-        // ---- block-wide paths: the K system of the fast path for large complements, and
-        // the rating's own bordered Gram matrix (dense) for everything else ---------------
+        // resident blocks per CU, else in this block's HBM region AP (L2-resident while
+        // used; the basis no longer needs it).  (The per-wave fast-path scratch in A is dead
+        // by now: a system that fits in A -- (n + 2)(n + 3)/2 doubles for n rows -- uses it
+        // whatever big_lds says.)
+        double* const Ahbm = AP;
+        // ---- dense path: the rating's own bordered Gram matrix, block-wide -----------------
         for (int si = 0; si < nslow; ++si) {
             const int r = s_slow[si] & 0xffff;
             // connected set C: the user's items that are out-neighbours of movie r (:254-265)
@@ -795,105 +977,6 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
             const bool use_complement = nc < c;
             const int lim = s_lim[r];
             double* AW = (a.big_lds || (size_t)(nc + 2) * (nc + 3) / 2 <= (size_t)a.a_elems) ? A : Ahbm;
-
-            bool wide = (s_slow[si] >> 16) != 0;
-            const unsigned long long tw0 = (a.phase_cycles && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
-            if (wide) {   // block-uniform
-                bool drop = false;   // the column filter, as in the fast path
-                if (tid < lim && s_cpos[tid] <= nc) {
-                    int hit = 0;
-                    for (int q = 0; q < nc; ++q) hit += (double)U[(size_t)s_nconn[q] * m + tid] >= 0.0001;
-                    drop = hit == s_cpos[tid];
-                }
-                wide = !__syncthreads_or(drop);
-            }
-            if (wide) {
-                // E = P_S over the rows [Cbar..., r] into AW (packed), then the bordered K
-                // system exactly as in the fast path, factored by the blocked LDL^T.
-                const int np = nc + 1;
-                for (int e = tid; e < np * (np + 1) / 2; e += kThreads) {
-                    int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-                    while (ra * (ra + 1) / 2 > e) --ra;
-                    while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
-                    const int rb = e - ra * (ra + 1) / 2;
-                    const int ia = ra < nc ? s_nconn[ra] : r;
-                    const int ib = rb < nc ? s_nconn[rb] : r;
-                    double v = Pm[(size_t)ia * k + ib];
-                    const double* xa = Qs + (size_t)ia * Lq;
-                    const double* xb = Qs + (size_t)ib * Lq;
-                    for (int j = lim; j < Lq; ++j) v = fma(-xa[j], xb[j], v);
-                    AW[e] = v;
-                }
-                if (wave == 0) {
-                    double sc = 0.0;
-                    for (int q = lane; q < nc; q += 64) sc += (double)s_rat[s_nconn[q]];
-                    sc = wave_sum(sc);
-                    if (lane == 0) s_misc[0] = (s_misc[1] - sc) / (double)c;
-                }
-                __syncthreads();
-                const double mu = s_misc[0];
-                const double2* pgh_lim = reinterpret_cast<const double2*>(PGH) + lim;
-                // b_a = (Py)_a - sum_q E_aq y_q for the rows a of Cbar, a_r likewise as row nc:
-                // g lanes per row (g = 4 / 2 / 1 as (nc + 1) g fits the block), shuffle-reduced
-                {
-                    const int nrw = nc + 1;
-                    const int g = nrw * 4 <= kThreads ? 4 : (nrw * 2 <= kThreads ? 2 : 1);
-                    const int ra = tid / g, part = tid - ra * g;
-                    double v = 0.0;
-                    if (ra < nrw)
-                        for (int q = part; q < nc; q += g) {
-                            const double eq = q <= ra ? AW[tri(ra, q)] : AW[tri(q, ra)];
-                            v = fma(-eq, (double)s_rat[s_nconn[q]] - mu, v);
-                        }
-                    if (g >= 4) v += __shfl_xor(v, 2);
-                    if (g >= 2) v += __shfl_xor(v, 1);
-                    if (ra < nrw && part == 0) {
-                        const double2 py = pgh_lim[(size_t)(ra < nc ? s_nconn[ra] : r) * (Lq + 1)];
-                        v += py.x - mu * py.y;
-                        if (ra < nc)
-                            AW[tri(nc + 1, ra)] = v;   // row nc + 1 is read by nobody before the sync
-                        else
-                            s_misc[2] = v;
-                    }
-                }
-                __syncthreads();
-                for (int e = tid; e < nc * (nc + 1) / 2; e += kThreads) {
-                    int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-                    while (ra * (ra + 1) / 2 > e) --ra;
-                    while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
-                    AW[e] = (e == tri(ra, ra) ? 1.0 : 0.0) - AW[e];   // K = I - P_CbarCbar
-                }
-                __syncthreads();
-                ldlt_bordered<kThreads, 8>(AW, nc, nc + 2);
-                if (wave == 0) {
-                    double minpiv = 1.0, dot = 0.0;
-                    for (int j = lane; j < nc; j += 64) {
-                        const double dj = AW[tri(j, j)];
-                        minpiv = fmin(minpiv, dj);
-                        dot = fma(AW[tri(nc, j)] * AW[tri(nc + 1, j)], dj, dot);
-                    }
-                    dot = wave_sum(dot);
-                    for (int off = 32; off >= 1; off >>= 1) minpiv = fmin(minpiv, __shfl_xor(minpiv, off));
-                    if (lane == 0) {
-                        s_misc[3] = dot;
-                        s_cnt[4] = minpiv >= kPivMin ? 1 : 0;
-                    }
-                }
-                __syncthreads();
-                wide = !(s_cnt[4] == 0 && c >= lim);   // ill-conditioned full rank: dense
-                if (wide && tid == 0) {
-                    double pred = mu + s_misc[2] + s_misc[3];
-                    if (pred > 5) pred = 5;
-                    if (pred < 1) pred = 1;
-                    const double d = (double)s_rat[r] - pred;
-                    a.mse[base + r] = (float)(d * d);
-                    a.kk[base + r] = c;
-                    if (a.pred) a.pred[base + r] = pred;
-                }
-                __syncthreads();
-                if (a.phase_cycles && tid == 0) ph_acc[7] += __builtin_amdgcn_s_memtime() - tw0;
-                if (wide) continue;
-            }
 
             // zero-column filter: keep column j < lim iff some U(C, j) >= 1e-4 (:284-304)
             bool keep = false;
@@ -1034,59 +1117,69 @@ __global__ __launch_bounds__(kThreads, 2) void predict_kernel(PredArgs<T> a, uin
         }
         PHASE_STAMP(3);
     }
-    // slots 0-7 (thread 0 of the block); 8-10 are added per rating / user by lane 0 of
+    // slots 0-7 (thread 0 of the block); 8-15 are added per rating / user by lane 0 of
     // every wave
     if (a.phase_cycles && tid == 0)
         for (int ph = 0; ph < 8; ++ph) atomicAdd(&a.phase_cycles[ph], ph_acc[ph]);
 }
 
-// Scratch doubles per workgroup and workgroups of a bucket launch (see launch_predict_bucket).
-inline int predict_blocks(uint32_t count) { return (int)std::min<uint32_t>(count, 8192u); }
-inline size_t predict_per_block(int lmax) {
-    const size_t big = (size_t)(lmax + 2) * (lmax + 3) / 2;
-    return (size_t)lmax * lmax + (size_t)(lmax + 2) * lmax + (size_t)lmax * (lmax + 1) * 2 +
-           (size_t)lmax * lmax + big;
+// Chunks of up to kChunk users per (basis, rating) launch pair; each user of a chunk owns a
+// slot (SlotOff) holding Gbar, X, Q1 (the basis's second buffer), the packed triangle AP and
+// the per-row arrays, ~1 MB at lmax = 192.
+constexpr uint32_t kChunk = 8192;
+inline int fast_tri(int n) { return (n + 2) * (n + 3) / 2; }
+inline SlotOff slot_layout(int lmax) {
+    SlotOff so{};
+    size_t o = 0;
+    const size_t l2 = (size_t)lmax * lmax;
+    so.gb = (int)o; o += l2;
+    so.x = (int)o; o += l2;
+    so.q1 = (int)o; o += l2;
+    so.ap = (int)o; o += (size_t)(lmax + 2) * (lmax + 3) / 2;
+    so.gx = (int)o; o += lmax;
+    so.hx = (int)o; o += lmax;
+    so.misc = (int)o; o += 4;
+    so.cmask = (int)o; o += 3 * (size_t)lmax;                 // u64 per cell
+    so.lim = (int)o; o += (lmax + 1) / 2;                    // ints, two per cell
+    so.order = (int)o; o += (lmax + 1) / 2;
+    so.cpos = (int)o; o += (lmax + 1) / 2;
+    so.stride = (o + 15) & ~(size_t)15;                      // 128-byte aligned slots
+    return so;
+}
+inline size_t basis_lds() {
+    return sizeof(double) * (kStageElems + 4) + CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 3 * sizeof(int)) +
+           12 * sizeof(int) + CF_MAX_K * (3 * sizeof(uint64_t) + sizeof(int));
+}
+inline size_t rating_lds_fixed() {
+    return sizeof(double) * (4 + 2 * CF_MAX_K) +                                      // s_misc, s_gx, s_hx
+           CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 6 * sizeof(int)) + 12 * sizeof(int) +
+           CF_MAX_K * (3 * sizeof(uint64_t) + sizeof(int)) + kWaves * CF_MAX_K * sizeof(int);   // cmask, order, cb
 }
 
+// Launch geometry of a bucket (everything but the chunk).
 template <typename T>
-int launch_predict_bucket(cf_ctx* ctx, PredArgs<T> args, uint32_t count, int lmax, double* scratch,
-                          size_t scratch_bytes, hipStream_t stream) {
+int setup_bucket(cf_ctx* ctx, PredArgs<T>& args, int lmax, size_t& rating_lds) {
     args.lmax = lmax;
-    const size_t lds_fixed = sizeof(double) * 4 + CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 6 * sizeof(int)) +
-                             12 * sizeof(int) + CF_MAX_K * (3 * sizeof(uint64_t) + sizeof(int));   // s_cmask, s_order
+    const size_t lds_fixed = rating_lds_fixed();
     const int big = (lmax + 2) * (lmax + 3) / 2;
-    // The full (lmax + 2)-row triangle of the block-wide systems in LDS would leave one
-    // 4-wave block per CU for k > 128; there it moves to HBM and the LDS keeps only the
-    // basis GEMM staging and the per-wave fast-path systems (nc <= 60), two blocks per CU.
-    args.ncw = std::min(kNcMax, lmax);
-    args.ew = (args.ncw + 2) * (args.ncw + 3) / 2 + 64;   // + y of the complement rows
-    args.big_lds = sizeof(double) * (size_t)std::max({big, kWaves * args.ew, kStageElems}) + lds_fixed <= 81920;
-    if (!args.big_lds) {
-        args.ncw = std::min(60, lmax);
-        args.ew = (args.ncw + 2) * (args.ncw + 3) / 2 + 64;
-    }
-    args.a_elems = std::max({args.big_lds ? big : 0, kWaves * args.ew, kStageElems, 2 * lmax});
-    args.abig_elems = (size_t)big;
-    const size_t lds = sizeof(double) * (size_t)args.a_elems + lds_fixed;
-    if (lds > 163840) return cf_set_error(ctx, CF_ERANGE, "predict bucket exceeds LDS");
-    // Up to 8192 workgroups (~one user each for most buckets): the hardware dispatcher then
-    // balances the per-user cost (~k^3) dynamically.  Measured at C2: 2048 -> 160.2 ms,
-    // 4096 -> 155.7, 8192 -> 152.3, 16384 / all users -> 152.5.  Scratch: ~1.6 MB per
-    // workgroup at k <= 192 (13 GB of the 288 GB).
-    int blocks = (int)std::min<uint32_t>(count, 8192u);
-    const size_t per_block = (size_t)lmax * lmax + (size_t)(lmax + 2) * lmax + (size_t)lmax * (lmax + 1) * 2 +
-                             (size_t)lmax * lmax + (args.big_lds ? 0 : (size_t)big);
-    if ((size_t)blocks * per_block * sizeof(double) > scratch_bytes)
-        return cf_set_error(ctx, CF_EINVAL, "predict scratch undersized");
-    args.gbar = scratch;
-    args.qs = args.gbar + (size_t)blocks * lmax * lmax;
-    args.pgh = args.qs + (size_t)blocks * (lmax + 2) * lmax;
-    args.q1 = args.pgh + (size_t)blocks * lmax * (lmax + 1) * 2;
-    args.abig = args.q1 + (size_t)blocks * lmax * lmax;
-    CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)predict_kernel<T>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(predict_kernel<T>, dim3(blocks), dim3(kThreads), lds, stream, args, count);
-    CF_HIP_CHECK(ctx, hipGetLastError());
+    // Per wave: the bordered system triangle of up to nmax rows plus y and g beside it.
+    // nmax is the largest that keeps two 4-wave blocks per CU (<= 80 KiB each); the
+    // block-wide systems use the LDS only where their full (lmax + 2)-row triangle fits as
+    // well, else the slot's HBM region AP.
+    const auto per_wave = [&](int n) { return fast_tri(n) + 2 * lmax; };   // + y (nc) and g (d)
+    int nmax = std::min(kNsysMax, lmax);
+    while (nmax > 8 && sizeof(double) * (size_t)(kWaves * per_wave(nmax)) + lds_fixed > 81920) --nmax;
+    args.nmax = nmax;
+    args.ew = per_wave(nmax);
+    args.big_lds = sizeof(double) * (size_t)std::max(big, kWaves * args.ew) + lds_fixed <= 81920;
+    args.a_elems = std::max({args.big_lds ? big : 0, kWaves * args.ew, 2 * lmax});
+    args.so = slot_layout(lmax);
+    rating_lds = sizeof(double) * (size_t)args.a_elems + lds_fixed;
+    if (rating_lds > 163840) return cf_set_error(ctx, CF_ERANGE, "predict bucket exceeds LDS");
+    CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)pred_rating_kernel<T>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)rating_lds));
+    CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)pred_basis_kernel<T>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)basis_lds()));
     return CF_OK;
 }
 
@@ -1116,15 +1209,14 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
     args.pred = d_pred;
     args.phase_cycles = ctx->d_phase;
     int rc = CF_OK;
-    // Scratch for every LDS bucket, sized once (largest bucket) per stream; the bucket launches
+    // Slots for one chunk of the largest LDS bucket, per stream; the chunks of every bucket
     // alternate between two context-owned streams (fork/join by events with the caller's
-    // stream) so one bucket's tail overlaps the next -- each stream has its own scratch copy.
-    // Diagnostics (phase counters) keep one stream.
+    // stream) so one chunk's tail overlaps the next.  Diagnostics keep one stream.
     size_t need = 0;
     for (const cf_bucket& b : plan->buckets)
         if (b.count && b.emax != kSpillBucket)
-            need = std::max(need, (size_t)predict_blocks(b.count) *
-                                      predict_per_block(std::max<int>(2, 16 * b.emax)) * sizeof(double));
+            need = std::max(need, (size_t)std::min(b.count, kChunk) *
+                                      slot_layout(std::max<int>(2, 16 * b.emax)).stride * sizeof(double));
     const bool overlap = !ctx->d_phase;
     const size_t copies = overlap ? cf_ctx::kAuxStreams : 1;
     if (need * copies > ctx->scratch_bytes) {
@@ -1159,12 +1251,25 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
             }
             continue;
         }
-        args.first = b.first;
-        const int lmax = std::max<int>(2, 16 * b.emax);
-        const int si = overlap ? (nb++ % cf_ctx::kAuxStreams) : 0;
-        rc = launch_predict_bucket<T>(ctx, args, b.count, lmax,
-                                      reinterpret_cast<double*>(static_cast<char*>(ctx->d_scratch) + si * need), need,
-                                      overlap ? ctx->aux_stream[si] : stream);
+        size_t rating_lds = 0;
+        rc = setup_bucket<T>(ctx, args, std::max<int>(2, 16 * b.emax), rating_lds);
+        if (rc != CF_OK) break;
+        for (uint32_t c0 = 0; c0 < b.count && rc == CF_OK; c0 += kChunk) {
+            const uint32_t cnt = std::min(kChunk, b.count - c0);
+            const int si = overlap ? (nb++ % cf_ctx::kAuxStreams) : 0;
+            hipStream_t st = overlap ? ctx->aux_stream[si] : stream;
+            args.slots = reinterpret_cast<double*>(static_cast<char*>(ctx->d_scratch) + si * need);
+            if ((size_t)cnt * args.so.stride * sizeof(double) > need) {
+                rc = cf_set_error(ctx, CF_EINVAL, "predict scratch undersized");
+                break;
+            }
+            // one workgroup per user of the chunk: the hardware dispatcher balances the
+            // per-user cost (~k^3) dynamically
+            hipLaunchKernelGGL(pred_basis_kernel<T>, dim3(cnt), dim3(kThreads), basis_lds(), st, args, b.first + c0, cnt);
+            hipLaunchKernelGGL(pred_rating_kernel<T>, dim3(cnt), dim3(kThreads), rating_lds, st, args, b.first + c0,
+                               cnt);
+            if (hipGetLastError() != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, "predict launch failed");
+        }
         if (rc != CF_OK) break;
     }
     if (overlap)
