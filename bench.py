@@ -479,11 +479,11 @@ def predict_roofline(acc, pred_s):
     return {
         "bound": "valu",
         "roof_note": "fp64 roof 78.6 TF/s (VALU = MFMA dense fp64 peak).  algorithmic = a LOWER BOUND of the "
-                     "algorithm this kernel runs (DESIGN 3.2): per user the Gram U^T U (k Lu^2, symmetric) and "
-                     "the projector P = Q Q^T (k^2 Lu, symmetric); per rating the LDL^T of the nc x nc system "
-                     "K (nc^3/3) and its two triangular solves (2 nc^2).  ref_* fields give SURVEY 8d's count of "
+                     "algorithm these kernels run (DESIGN 3.2): per user the Gram U^T U (k Lu^2, symmetric) and "
+                     "one k x k Gram of the basis X (k^3); per rating the Gram of its min(nc, d)-row system "
+                     "(ns^2 max(nc, d)) and its LDL^T (ns^3/3).  ref_* fields give SURVEY 8d's count of "
                      "the reference's explicit-inverse work per pair for comparison",
-        "kernel": "predict_kernel<float> (all k-bucket launches of one predict stage)",
+        "kernel": "pred_basis_kernel<float> + pred_rating_kernel<float> (all chunk launches of one predict stage)",
         "achieved": tf,
         "peak": FP64_PEAK_TFLOPS,
         "unit": "TFLOP/s",
@@ -793,7 +793,7 @@ def pmc_traffic(args):
             path = os.path.join(d, "run_counter_collection.csv")
             for r in csv.DictReader(open(path)):
                 name = r["Kernel_Name"]
-                key = "predict" if re.search(r"predict_kernel<", name) else \
+                key = "predict" if re.search(r"pred_(basis|rating)_kernel<|spill_(basis|predict)_kernel<", name) else \
                       "eigen" if re.search(r"eigen_kernel<", name) else None
                 if key and r["Counter_Name"] == counter:
                     out[key][slot] += float(r["Counter_Value"]) * 1024.0   # the counter is in KiB
@@ -808,12 +808,11 @@ def predictor_flops(off, k, m, kk, evals, sigtab):
     """Flop and byte counts of the predict stage (outside the timed region), vectorised.
 
     algorithmic (lower bound of this kernel's algorithm): per user k Lu^2 (Gram,
-    symmetric) + k^2 Lu (P = Q Q^T, symmetric); per pair nc^3/3 + 2 nc^2 (LDL^T of K and the
-    two triangular solves), nc = k - c.
+    symmetric) + k^3 (one Gram of the k x k basis X); per pair ns^2 max(nc, d) + ns^3 / 3 (the
+    Gram of its system and the LDL^T), nc = k - c, d = k - lim, ns = min(nc, d).
     ref (the reference's explicit-inverse work per pair): 2cL^2 + 2L^3 + 2cL + 2L^2 +
     2L with c = kk and L = lim (compat w_lim = sigtab[r]); bytes = 4cL + 4c + 12 per pair.
-    executed (this kernel): per user Gram k Lu^2 + LDL^T Lu^3/3 + basis k Lu^2 + 8 k Lu; per pair
-    (nc + 1)(nc + 2) lim + nc^3/3 + 4 nc^2 on the fast path, and for nc > 62 min(c, nc) L^2 + L^3/3.
+    executed (this kernel, pred_basis_kernel + pred_rating_kernel): see the comments below.
     """
     off = np.asarray(off, dtype=np.int64)
     k = np.asarray(k, dtype=np.int64)
@@ -838,11 +837,19 @@ def predictor_flops(off, k, m, kk, evals, sigtab):
     lu = np.zeros(len(k))
     np.maximum.at(lu, uid, lim)
     kf = k.astype(np.float64)
-    alg = float(np.sum(kf * lu * lu + kf * kf * lu)) + float(np.sum(nc ** 3 / 3 + 2 * nc ** 2))
-    exe = float(np.sum(2 * kf * lu * lu + lu ** 3 / 3 + 8 * kf * lu))
-    fast = nc <= 62
-    exe += float(np.sum(((nc + 1) * (nc + 2) * lim + nc ** 3 / 3 + 4 * nc ** 2)[fast]))
-    exe += float(np.sum((np.minimum(c, nc) * lim ** 2 + lim ** 3 / 3)[~fast]))
+    du = kf - lu                                   # complement columns of the basis X = [Q | W]
+    d = kr - lim                                   # complement width of the rating's prefix
+    ns = np.minimum(nc, d)                         # rows of the rating's system (K or G form)
+    # lower bound: per user the Gram U^T U (k Lu^2) and one k x k Gram of the basis (k^3, the
+    # orthogonality check every basis needs); per rating the Gram of its gathered system
+    # (ns^2 max(nc, d), symmetric) and its LDL^T (ns^3 / 3)
+    alg = float(np.sum(kf * lu * lu + kf ** 3)) + float(np.sum(ns * ns * np.maximum(nc, d) + ns ** 3 / 3))
+    # executed (block_gemm computes whole 64 x 64 blocks; lower-triangle products ~half):
+    # Gram k Lu^2, Q = U T1 k Lu^2, Q^T Omega and Y 4 k Lu du, Y^T Y k du^2 + du^3 / 3, W k du^2,
+    # one joint T step 2 k^3, X^T r and X^T 1 4 k^2; per rating the bordered Gram and LDL^T
+    exe = float(np.sum(2 * kf * lu * lu + 4 * kf * lu * du + 2 * kf * du * du + du ** 3 / 3 + 2 * kf ** 3
+                       + 4 * kf * kf))
+    exe += float(np.sum((ns + 1) * (ns + 2) * np.maximum(nc, d) + ns ** 3 / 3 + 4 * ns ** 2))
     return {"algorithmic_flops": alg, "executed_flops": exe, "ref_flops": ref, "algorithmic_bytes": byt,
             "lim_mean": float(lim.mean()) if n else 0.0}
 

@@ -50,6 +50,9 @@ SIGNATURES = {
     "cf_predict_precomp": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_void_p,
                                    c_void_p]),
+    "cf_predict_precomp_sel": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_void_p,
+                                       c_void_p, c_void_p]),
     "cf_predict_run_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                    c_void_p]),
@@ -60,6 +63,7 @@ SIGNATURES = {
                                c_void_p]),
     "cf_item_cosine_run": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_int, c_float,
                                    c_int, c_void_p, c_void_p]),
+    "cf_knn2_exactness": (c_int, [c_void_p, c_void_p, c_void_p]),
     "cf_knn2_timing": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "cf_knn_predict": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "cf_graph_filter": (c_int, [c_void_p, c_int, c_uint32, ctypes.c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,

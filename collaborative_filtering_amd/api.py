@@ -6,7 +6,7 @@ Inputs are numpy arrays (host) or torch CUDA tensors for the *_run device paths.
 """
 from __future__ import annotations
 
-from ctypes import byref, c_float, c_int, c_uint32, c_void_p
+from ctypes import byref, c_double, c_float, c_int, c_uint32, c_void_p
 from dataclasses import dataclass
 
 import numpy as np
@@ -227,6 +227,13 @@ class Context:
         self._chk(self.lib.cf_knn2_timing(self.h, byref(a), byref(b), byref(c)),
                   "cf_knn2_timing")
         return a.value, b.value, c.value
+
+    def knn2_exactness(self):
+        """(max accumulator, exact) of the last knn2 launch: exact is True when the
+        reference's float accumulators (knn2.cpp:129-140) stay <= 2^24 (cf_knn2_exactness)."""
+        a, e = c_double(), c_int()
+        self._chk(self.lib.cf_knn2_exactness(self.h, byref(a), byref(e)), "cf_knn2_exactness")
+        return a.value, bool(e.value)
 
     # -- knn_program + error_vertex_data (knn3.cpp:185-256) ------------------------
     def knn_predict(self, user_off, items, ratings):

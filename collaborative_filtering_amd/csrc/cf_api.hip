@@ -84,6 +84,7 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_phase) (void)hipFree(ctx->d_phase);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_knn) (void)hipFree(ctx->d_knn);
+    if (ctx->d_knn_acc) (void)hipFree(ctx->d_knn_acc);
     if (ctx->d_spill) (void)hipFree(ctx->d_spill);
     if (ctx->d_pspill) (void)hipFree(ctx->d_pspill);
     if (ctx->d_tri) (void)hipFree(ctx->d_tri);
@@ -368,7 +369,7 @@ int cf_predict_run_f64(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_
     if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_predict_run_f64: no item graph uploaded");
     CF_TRY(set_device(ctx));
     return cf_launch_predict<double>(ctx, plan, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off,
-                                     d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, (hipStream_t)stream);
+                                     d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, nullptr, (hipStream_t)stream);
 }
 
 int cf_predict_run_f32(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,
@@ -379,13 +380,21 @@ int cf_predict_run_f32(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_
     if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_predict_run_f32: no item graph uploaded");
     CF_TRY(set_device(ctx));
     return cf_launch_predict<float>(ctx, plan, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off,
-                                    d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, (hipStream_t)stream);
+                                    d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, nullptr, (hipStream_t)stream);
 }
 
 int cf_predict_precomp(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, const uint32_t* items,
                        const float* ratings, const int32_t* m, const double* evals, const uint64_t* evec_off,
                        const double* evecs, const double* sigtab, uint64_t sigtab_len, int sig_mode,
                        float* mse, int32_t* kk, double* pred) {
+    return cf_predict_precomp_sel(ctx, n_users, item_off, items, ratings, m, evals, evec_off, evecs, sigtab,
+                                  sigtab_len, sig_mode, nullptr, mse, kk, pred);
+}
+
+int cf_predict_precomp_sel(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, const uint32_t* items,
+                           const float* ratings, const int32_t* m, const double* evals, const uint64_t* evec_off,
+                           const double* evecs, const double* sigtab, uint64_t sigtab_len, int sig_mode,
+                           const uint8_t* row_sel, float* mse, int32_t* kk, double* pred) {
     if (!ctx || !item_off || !items || !ratings || !m || !evals || !evec_off || !evecs || !sigtab || !mse || !kk)
         return cf_set_error(ctx, CF_EINVAL, "cf_predict_precomp: null argument");
     if (sig_mode != CF_SIGS_OWN && sig_mode != CF_SIGS_COMPAT)
@@ -408,7 +417,7 @@ int cf_predict_precomp(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, 
         if (items[e] >= ctx->n_items) return cf_set_error(ctx, CF_EINVAL, "item index outside the graph");
     cf_plan* plan = nullptr;
     CF_TRY(cf_plan_create(ctx, n_users, item_off, &plan));
-    DevBuf doff, ditems, drat, dm, deval, deoff, devec, dsig, dmse, dkk, dpred;
+    DevBuf doff, ditems, drat, dm, deval, deoff, devec, dsig, dmse, dkk, dpred, dsel;
     int rc = dev_alloc(ctx, doff, sizeof(uint64_t) * (n_users + 1));
     if (rc == CF_OK) rc = dev_alloc(ctx, ditems, sizeof(uint32_t) * n_entries);
     if (rc == CF_OK) rc = dev_alloc(ctx, drat, sizeof(float) * n_entries);
@@ -420,6 +429,7 @@ int cf_predict_precomp(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, 
     if (rc == CF_OK) rc = dev_alloc(ctx, dmse, sizeof(float) * n_entries);
     if (rc == CF_OK) rc = dev_alloc(ctx, dkk, sizeof(int32_t) * n_entries);
     if (rc == CF_OK && pred) rc = dev_alloc(ctx, dpred, sizeof(double) * n_entries);
+    if (rc == CF_OK && row_sel) rc = dev_alloc(ctx, dsel, std::max<uint64_t>(n_entries, 1));
     hipError_t e = hipSuccess;
     if (rc == CF_OK) {
         auto h2d = [&](void* d, const void* h, size_t bytes) {
@@ -433,13 +443,21 @@ int cf_predict_precomp(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, 
         h2d(deoff.p, evec_off, sizeof(uint64_t) * n_users);
         h2d(devec.p, evecs, sizeof(double) * n_evec);
         h2d(dsig.p, sigtab, sizeof(double) * sigtab_len);
+        if (row_sel) {
+            h2d(dsel.p, row_sel, n_entries);
+            // rows not selected keep the caller's outputs: seed the device copies with them
+            h2d(dmse.p, mse, sizeof(float) * n_entries);
+            h2d(dkk.p, kk, sizeof(int32_t) * n_entries);
+            if (pred) h2d(dpred.p, pred, sizeof(double) * n_entries);
+        }
         if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("predict H2D: ") + hipGetErrorString(e));
     }
     if (rc == CF_OK)
         rc = cf_launch_predict<double>(ctx, plan, (const uint64_t*)doff.p, (const uint32_t*)ditems.p,
                                        (const float*)drat.p, (const int32_t*)dm.p, (const double*)deval.p,
                                        (const uint64_t*)deoff.p, (const double*)devec.p, (const double*)dsig.p,
-                                       sig_mode, (float*)dmse.p, (int32_t*)dkk.p, (double*)dpred.p, nullptr);
+                                       sig_mode, (float*)dmse.p, (int32_t*)dkk.p, (double*)dpred.p,
+                                       (const uint8_t*)dsel.p, nullptr);
     if (rc == CF_OK) {
         e = hipDeviceSynchronize();
         if (e == hipSuccess && n_entries) e = hipMemcpy(mse, dmse.p, sizeof(float) * n_entries, hipMemcpyDeviceToHost);
@@ -479,6 +497,20 @@ int cf_knn2_timing(cf_ctx* ctx, float* plane_ms, float* gemm_ms, int* path) {
     if (plane_ms) *plane_ms = a;
     if (gemm_ms) *gemm_ms = b;
     if (path) *path = ctx->knn_path;
+    return CF_OK;
+}
+
+int cf_knn2_exactness(cf_ctx* ctx, double* max_accumulator, int* exact) {
+    if (!ctx) return CF_EINVAL;
+    if (!ctx->d_knn_acc || !ctx->knn_ev[2]) return cf_set_error(ctx, CF_ESTATE, "cf_knn2_exactness: no knn2 launch yet");
+    CF_TRY(set_device(ctx));
+    CF_HIP_CHECK(ctx, hipEventSynchronize(ctx->knn_ev[2]));
+    unsigned int bits = 0;
+    CF_HIP_CHECK(ctx, hipMemcpy(&bits, ctx->d_knn_acc, sizeof(bits), hipMemcpyDeviceToHost));
+    float v;
+    std::memcpy(&v, &bits, sizeof(v));
+    if (max_accumulator) *max_accumulator = (double)v;
+    if (exact) *exact = ctx->knn_path != 3 && (double)v <= 16777216.0;
     return CF_OK;
 }
 

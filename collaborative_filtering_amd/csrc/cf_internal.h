@@ -43,7 +43,8 @@ struct cf_ctx {
     bool tri_debug = false;
     // knn2 stage events (plane build start, GEMM start, GEMM end) of the last launch.
     hipEvent_t knn_ev[3] = {nullptr, nullptr, nullptr};
-    int knn_path = 0;   // 1 code plane, 2 three int8 planes, 3 fp32 planes
+    int knn_path = 0;
+    unsigned int* d_knn_acc = nullptr;   // knn2: largest accumulator of the last launch (float bits)   // 1 code plane, 2 three int8 planes, 3 fp32 planes
     // bucket overlap (eigen, predict): kAuxStreams non-blocking streams, a join event per
     // stream and one fork event (cf_eigen.hip, cf_predict.hip)
     static constexpr int kAuxStreams = 2;   // measured: 3 streams no faster at C2
@@ -185,14 +186,15 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
                       const uint32_t* d_items, const float* d_ratings, const int32_t* d_m,
                       const T* d_evals, const uint64_t* d_evec_off, const T* d_evecs,
                       const T* d_sigtab, int sig_mode, float* d_mse, int32_t* d_kk,
-                      double* d_pred, hipStream_t stream);
+                      double* d_pred, const uint8_t* d_row_sel, hipStream_t stream);
 
 // Predictor for the spill bucket (CF_MAX_K < k <= CF_SPILL_MAX_K), cf_predict_spill.hip.
 template <typename T>
 int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, const uint64_t* d_item_off,
                             const uint32_t* d_items, const float* d_ratings, const int32_t* d_m,
                             const T* d_evals, const uint64_t* d_evec_off, const T* d_evecs, const T* d_sigtab,
-                            int sig_mode, float* d_mse, int32_t* d_kk, double* d_pred, hipStream_t stream);
+                            int sig_mode, float* d_mse, int32_t* d_kk, double* d_pred, const uint8_t* d_row_sel,
+                            hipStream_t stream);
 
 int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64_t* d_user_off,
                    const uint32_t* d_item, const float* d_rating, int integer_ratings, float w_min,

@@ -79,6 +79,7 @@ struct Knn2Args {
     float w_min;
     int cnt_min;
     float* w_out;       // n_items x n_items
+    unsigned int* acc_max;   // max over the diagonal of max(den1, cnt) (float bits), see knn2_store
 };
 
 // Epilogue for one 32x32 accumulator block: lane holds column c = lane&31 and rows
@@ -101,6 +102,12 @@ __device__ __forceinline__ void knn2_store(const Knn2Args& a, uint32_t a0, uint3
         }
         a.w_out[(size_t)row * a.n_items + col] = w;
         if (!diag_tile) a.w_out[(size_t)col * a.n_items + row] = w;          // w(b,a) == w(a,b)
+        // 2^24 guard (SURVEY hard part 7): the diagonal den1 = sum of r^2 over the item's
+        // raters bounds every accumulator of every pair through that item (den1, den2
+        // directly, |num| by Cauchy-Schwarz, all partial sums included); cnt is counted
+        // likewise.  The reference's float accumulators (knn2.cpp:129-140) are exact iff
+        // the maximum stays <= 2^24.  One vector atomic per item.
+        if (row == col) atomicMax(a.acc_max, __float_as_uint(fmaxf(fabsf((float)den1[reg]), (float)cnt[reg])));
     }
 }
 
@@ -192,6 +199,7 @@ struct Knn2CodeArgs {
     float w_min;
     int cnt_min;
     float* w_out;
+    unsigned int* acc_max;
 };
 
 __device__ __forceinline__ bool code_tile(uint32_t b, uint32_t nt, uint32_t nsb, uint32_t& ta, uint32_t& tb) {
@@ -300,6 +308,7 @@ __global__ __launch_bounds__(512, 1) void knn2_code_kernel(Knn2CodeArgs a) {
     e.w_min = a.w_min;
     e.cnt_min = a.cnt_min;
     e.w_out = a.w_out;
+    e.acc_max = a.acc_max;
     const bool diag = ta == tb;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -401,6 +410,8 @@ int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64
     if (n_items == 0) return CF_OK;
     for (hipEvent_t& e : ctx->knn_ev)
         if (!e) CF_HIP_CHECK(ctx, hipEventCreate(&e));
+    if (!ctx->d_knn_acc) CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_knn_acc, sizeof(unsigned int)));
+    CF_HIP_CHECK(ctx, hipMemsetAsync(ctx->d_knn_acc, 0, sizeof(unsigned int), stream));
     CF_HIP_CHECK(ctx, hipEventRecord(ctx->knn_ev[0], stream));
     // Integer ratings: which values occur decides between one code plane (<= 7 values)
     // and the three-plane int8 form.  The scan reads the ratings once (n x 4 B).
@@ -447,6 +458,7 @@ int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64
         a.w_min = w_min;
         a.cnt_min = cnt_min;
         a.w_out = d_w_out;
+        a.acc_max = ctx->d_knn_acc;
         const uint32_t grid = a.n_super * (a.n_super + 1) / 2 * 256;
         ctx->knn_path = 1;
         CF_HIP_CHECK(ctx, hipEventRecord(ctx->knn_ev[1], stream));
@@ -481,6 +493,7 @@ int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64
     a.w_min = w_min;
     a.cnt_min = cnt_min;
     a.w_out = d_w_out;
+    a.acc_max = ctx->d_knn_acc;
     const uint32_t ntp = a.n_tiles * (a.n_tiles + 1) / 2;
     ctx->knn_path = integer_ratings ? 2 : 3;
     CF_HIP_CHECK(ctx, hipEventRecord(ctx->knn_ev[1], stream));

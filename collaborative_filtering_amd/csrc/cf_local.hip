@@ -171,6 +171,25 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
     CF_TRY(set_device(ctx));
     const uint32_t n_items = ctx->n_items;
     const uint64_t n_test = test_off[n_items];
+    if (n_test && (!test_user || !test_rating)) return cf_set_error(ctx, CF_EINVAL, "cf_local_calc: null test arrays");
+    // every id the kernels read must lie inside the uploaded graph, and lookup_rating
+    // binary-searches each item's test users, so they must be strictly ascending
+    if (n_movies && movie_off[0] != 0) return cf_set_error(ctx, CF_EINVAL, "cf_local_calc: movie_off[0] != 0");
+    for (uint32_t v = 0; v < n_movies; ++v) {
+        if (movie_off[v + 1] < movie_off[v]) return cf_set_error(ctx, CF_EINVAL, "cf_local_calc: movie_off not monotone");
+        for (uint64_t i = movie_off[v]; i < movie_off[v + 1]; ++i)
+            if (movie_items[i] >= n_items)
+                return cf_set_error(ctx, CF_EINVAL, "cf_local_calc: unit " + std::to_string(v) + " names item " +
+                                                        std::to_string(movie_items[i]) + " outside the graph");
+    }
+    if (test_off[0] != 0) return cf_set_error(ctx, CF_EINVAL, "cf_local_calc: test_off[0] != 0");
+    for (uint32_t m = 0; m < n_items; ++m) {
+        if (test_off[m + 1] < test_off[m]) return cf_set_error(ctx, CF_EINVAL, "cf_local_calc: test_off not monotone");
+        for (uint64_t t = test_off[m] + 1; t < test_off[m + 1]; ++t)
+            if (test_user[t] <= test_user[t - 1])
+                return cf_set_error(ctx, CF_EINVAL, "cf_local_calc: test users of item " + std::to_string(m) +
+                                                        " are not strictly ascending");
+    }
     // units with n >= 3 and their (movie, test user) pairs (:269-272, :394)
     std::vector<uint64_t> sq_off(n_movies + 1, 0);
     std::vector<uint32_t> pair_movie, pair_user;

@@ -85,6 +85,7 @@ struct PredArgs {
     const uint64_t* item_off;
     const uint32_t* items;
     const float* ratings;
+    const uint8_t* row_sel;   // rows to predict (null: all; bin/local_calc_precomp --pct)
     const int32_t* m;
     const T* evals;
     const uint64_t* evec_off;
@@ -704,6 +705,7 @@ __global__ __launch_bounds__(kThreads, 2) void pred_rating_kernel(PredArgs<T> a,
             while (idx < k) {
                 const int r = s_order[idx];
                 idx = claim();
+                if (a.row_sel && !a.row_sel[base + r]) continue;   // movie not sampled (wave-uniform)
                 const unsigned long long rt0 = a.phase_cycles ? __builtin_amdgcn_s_memtime() : 0ull;
                 // Cbar in ascending row order (the position of r in it), its rating sum
                 int nc = 0, posr = 0;
@@ -1190,12 +1192,13 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
                       const uint32_t* d_items, const float* d_ratings, const int32_t* d_m,
                       const T* d_evals, const uint64_t* d_evec_off, const T* d_evecs,
                       const T* d_sigtab, int sig_mode, float* d_mse, int32_t* d_kk,
-                      double* d_pred, hipStream_t stream) {
+                      double* d_pred, const uint8_t* d_row_sel, hipStream_t stream) {
     PredArgs<T> args{};
     args.order = plan->d_order;
     args.item_off = d_item_off;
     args.items = d_items;
     args.ratings = d_ratings;
+    args.row_sel = d_row_sel;
     args.m = d_m;
     args.evals = d_evals;
     args.evec_off = d_evec_off;
@@ -1243,7 +1246,7 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
         if (b.emax == kSpillBucket) {   // k > CF_MAX_K: HBM-workspace predictor, alone, first
             hipStream_t st = overlap ? ctx->aux_stream[0] : stream;
             rc = cf_launch_predict_spill<T>(ctx, plan, b, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off,
-                                            d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, st);
+                                            d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, d_row_sel, st);
             if (rc != CF_OK) break;
             if (overlap) {
                 CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[0], st));
@@ -1283,8 +1286,8 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
 template int cf_launch_predict<float>(cf_ctx*, const cf_plan*, const uint64_t*, const uint32_t*,
                                       const float*, const int32_t*, const float*, const uint64_t*,
                                       const float*, const float*, int, float*, int32_t*, double*,
-                                      hipStream_t);
+                                      const uint8_t*, hipStream_t);
 template int cf_launch_predict<double>(cf_ctx*, const cf_plan*, const uint64_t*, const uint32_t*,
                                        const float*, const int32_t*, const double*,
                                        const uint64_t*, const double*, const double*, int, float*,
-                                       int32_t*, double*, hipStream_t);
+                                       int32_t*, double*, const uint8_t*, hipStream_t);

@@ -55,6 +55,7 @@ struct SpArgs {
     const uint64_t* item_off;
     const uint32_t* items;
     const float* ratings;
+    const uint8_t* row_sel;   // rows to predict (null: all)
     const int32_t* m;
     const T* evals;
     const uint64_t* evec_off;
@@ -388,6 +389,7 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
         const uint64_t base = a.item_off[u];
         const int k = (int)(a.item_off[u + 1] - base);
         if (r >= k) continue;   // block-uniform
+        if (a.row_sel && !a.row_sel[base + r]) continue;   // --pct: movie not sampled (block-uniform)
         const int m = a.m[u];
         const T* U = a.evecs + a.evec_off[u];
         const size_t kk2 = (size_t)a.kmax * a.kmax;
@@ -720,7 +722,8 @@ template <typename T>
 int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, const uint64_t* d_item_off,
                             const uint32_t* d_items, const float* d_ratings, const int32_t* d_m,
                             const T* d_evals, const uint64_t* d_evec_off, const T* d_evecs, const T* d_sigtab,
-                            int sig_mode, float* d_mse, int32_t* d_kk, double* d_pred, hipStream_t stream) {
+                            int sig_mode, float* d_mse, int32_t* d_kk, double* d_pred, const uint8_t* d_row_sel,
+                            hipStream_t stream) {
     if (b.count == 0) return CF_OK;
     const int kmax = (int)b.kmax;
     if (kmax > CF_SPILL_MAX_K) return cf_set_error(ctx, CF_ERANGE, "predict spill: k above CF_SPILL_MAX_K");
@@ -730,6 +733,7 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
     a.item_off = d_item_off;
     a.items = d_items;
     a.ratings = d_ratings;
+    a.row_sel = d_row_sel;
     a.m = d_m;
     a.evals = d_evals;
     a.evec_off = d_evec_off;
@@ -788,11 +792,11 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
 template int cf_launch_predict_spill<float>(cf_ctx*, const cf_plan*, const cf_bucket&, const uint64_t*,
                                             const uint32_t*, const float*, const int32_t*, const float*,
                                             const uint64_t*, const float*, const float*, int, float*, int32_t*,
-                                            double*, hipStream_t);
+                                            double*, const uint8_t*, hipStream_t);
 template int cf_launch_predict_spill<double>(cf_ctx*, const cf_plan*, const cf_bucket&, const uint64_t*,
                                              const uint32_t*, const float*, const int32_t*, const double*,
                                              const uint64_t*, const double*, const double*, int, float*,
-                                             int32_t*, double*, hipStream_t);
+                                             int32_t*, double*, const uint8_t*, hipStream_t);
 
 int cf_launch_local_predict_spill(cf_ctx* ctx, uint32_t n_pairs, int nmax, const uint32_t* d_pair_movie,
                                   const uint32_t* d_pair_user, const uint64_t* d_pair_out, const uint64_t* d_item_off,

@@ -42,6 +42,18 @@ int main(int argc, char** argv) {
     cf_ctx* ctx = cfcli::open_device();
     cfcli::check(ctx, cf_item_cosine(ctx, users.size(), n, off.data(), it.data(), r.data(), 0.01f, 5, 0, W.data()),
                  "cf_item_cosine");
+    {
+        double acc = 0.0;
+        int exact = 0, path = 0;
+        float pa = 0.0f, pb = 0.0f;
+        cfcli::check(ctx, cf_knn2_exactness(ctx, &acc, &exact), "cf_knn2_exactness");
+        cfcli::check(ctx, cf_knn2_timing(ctx, &pa, &pb, &path), "cf_knn2_timing");
+        if (!exact && path != 3)
+            std::fprintf(stderr,
+                         "knn2: warning: an accumulator reaches %.0f > 2^24; the reference's float sums "
+                         "(knn2.cpp:129-140) are no longer exact there, these weights are the exact ones\n",
+                         acc);
+    }
     cf_destroy(ctx);
     cfio::ShardWriter fin(".", "out_fin", nshards);
     size_t written = 0;

@@ -4,7 +4,8 @@
 //            sigs up to its own, so w_lim for row r is the r-th sig of the whole file
 //   :122-136 out_fin_ edges (out-neighbour iff float weight > 0.1)
 //   :138-160 out_test_rat_ vertices
-//   :217-380 neigh_program::apply per test rating -> cf_predict_precomp (HIP, fp64)
+//   :217-380 neigh_program::apply per test rating of the sampled movies (:221)
+//            -> cf_predict_precomp_sel (HIP, fp64)
 //   :393-404 writer "movie user mse kk" -> out_res_<i>_of_<N>
 // Options: --pct P (percent of movie vertices, sampled like rand()%100 < P; default
 // 100), --seed S (default: time, as the reference), --compat ref|fixed (fixed = each
@@ -79,26 +80,41 @@ int main(int argc, char** argv) {
         eacc += r.evecs.size();
     }
     if (evecs.empty()) evecs.push_back(0.0);
+    // movie vertices sampled like rand() % 100 < pct in apply (:221), BEFORE prediction:
+    // only the rows of sampled movies are predicted (cf_predict_precomp_sel)
+    std::mt19937 rng(seed);
+    std::map<uint32_t, std::vector<std::pair<uint32_t, double>>> movies(test.begin(), test.end());
+    std::unordered_map<uint32_t, bool> sampled;
+    for (auto& kv : movies) sampled[kv.first] = (unsigned)(rng() % 100) < (unsigned)pct;
+    std::vector<uint8_t> sel(its.size(), 0);
+    {
+        size_t e = 0;
+        for (uint32_t u = 0; u < n_users; ++u)
+            for (uint32_t mv : recs[u].movies) {
+                auto it = sampled.find(mv);
+                sel[e++] = it != sampled.end() && it->second;
+            }
+    }
     const bool ref = compat != "fixed";
-    std::vector<float> mse(its.size());
-    std::vector<int32_t> kk(its.size());
+    std::vector<float> mse(its.size(), std::numeric_limits<float>::quiet_NaN());
+    std::vector<int32_t> kk(its.size(), 0);
     cf_ctx* ctx = cfcli::open_device();
     cfcli::upload_edges(ctx, items, edges);
     if (n_users)
-        cfcli::check(ctx, cf_predict_precomp(ctx, n_users, off.data(), its.data(), rats.data(), m.data(), evals.data(),
-                                             eoff.data(), evecs.data(), ref ? concat.data() : own_sigs.data(),
-                                             ref ? concat.size() : own_sigs.size(),
-                                             ref ? CF_SIGS_COMPAT : CF_SIGS_OWN, mse.data(), kk.data(), nullptr),
-                     "cf_predict_precomp");
+        cfcli::check(ctx, cf_predict_precomp_sel(ctx, n_users, off.data(), its.data(), rats.data(), m.data(),
+                                                 evals.data(), eoff.data(), evecs.data(),
+                                                 ref ? concat.data() : own_sigs.data(),
+                                                 ref ? concat.size() : own_sigs.size(),
+                                                 ref ? CF_SIGS_COMPAT : CF_SIGS_OWN, pct >= 100 ? nullptr : sel.data(),
+                                                 mse.data(), kk.data(), nullptr),
+                     "cf_predict_precomp_sel");
     cf_destroy(ctx);
 
     // rows per test movie vertex (:230-361), sampled per vertex (:221)
-    std::mt19937 rng(seed);
-    std::map<uint32_t, std::vector<std::pair<uint32_t, double>>> movies(test.begin(), test.end());
     cfio::ShardWriter res(".", "out_res", nshards);
     size_t rows = 0, missing = 0;
     for (auto& kv : movies) {
-        if ((unsigned)(rng() % 100) >= (unsigned)pct) continue;
+        if (!sampled[kv.first]) continue;
         const uint32_t movie = kv.first;
         std::string& out = res.shard(movie);
         for (auto& ur : kv.second) {

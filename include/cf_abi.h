@@ -179,6 +179,15 @@ int cf_predict_precomp(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off,
                        const double* evals, const uint64_t* evec_off, const double* evecs,
                        const double* sigtab, uint64_t sigtab_len, int sig_mode,
                        float* mse, int32_t* kk, double* pred);
+/* cf_predict_precomp over the rows with row_sel[item_off[u] + r] != 0 only (row_sel NULL =
+ * every row); the other rows' mse / kk / pred keep the values the caller passed in.  This is
+ * the per-vertex sampling of local_calc_precomp --pct (rand() % 100 < pct before apply,
+ * local_calc_precomp.cpp:221): unsampled movies cost no per-rating work. */
+int cf_predict_precomp_sel(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off,
+                           const uint32_t* items, const float* ratings, const int32_t* m,
+                           const double* evals, const uint64_t* evec_off, const double* evecs,
+                           const double* sigtab, uint64_t sigtab_len, int sig_mode,
+                           const uint8_t* row_sel, float* mse, int32_t* kk, double* pred);
 int cf_predict_run_f64(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
                        const uint32_t* d_items, const float* d_ratings, const int32_t* d_m,
                        const double* d_evals, const uint64_t* d_evec_off,
@@ -210,6 +219,14 @@ int cf_item_cosine_run(cf_ctx* ctx, uint32_t n_users, uint32_t n_items,
  * plane (<= 7 distinct integer ratings), 2 three int8 planes, 3 fp32 planes.
  * Waits for the launch to finish. */
 int cf_knn2_timing(cf_ctx* ctx, float* plane_ms, float* gemm_ms, int* path);
+/* The 2^24 guard of the last cf_item_cosine(_run) (SURVEY hard part 7): the reference sums
+ * num, den1, den2 and cnt in float (knn2.cpp:129-140), which is exact for integer ratings
+ * only while every partial sum stays <= 2^24.  max_accumulator = the largest such sum (the
+ * per-item sum of r^2 or rater count, which bounds every pair's); exact = 1 when the
+ * reference's floats are exact, so its weights equal this kernel's integer-accumulated
+ * ones bit for bit, 0 otherwise (always 0 on the fp32 path of real-valued ratings, whose
+ * reference sums are in hash order).  Waits for the launch to finish. */
+int cf_knn2_exactness(cf_ctx* ctx, double* max_accumulator, int* exact);
 /* local_calc vertex_program::apply (local_calc.cpp:262-526) on the uploaded graph (raw
  * out_fin_ weights; edges count iff w > 0.1, graph_loader :113).  Movie unit v lists
  * movie_items[movie_off[v] .. movie_off[v+1]) = [m, the out-neighbours of m with w > 0.1]

@@ -51,6 +51,29 @@ def test_knn2_integer_value_sets(gpu_ctx, values):
     assert np.array_equal(Wg, Wo)
 
 
+@pytest.mark.parametrize("n_users,values", [(3000, [1, 2, 3, 4, 5]),            # code plane, exact
+                                            (140_000, [-11, 11]),               # code plane, > 2^24
+                                            (140_000, list(range(-11, 12)))])   # three planes, > 2^24
+def test_knn2_exactness_guard(gpu_ctx, n_users, values):
+    """cf_knn2_exactness (SURVEY hard part 7): the largest accumulator the reference would sum
+    in float is the per-item max of (sum r^2, rater count), and the reference is exact iff
+    that stays <= 2^24.  140k users rating item 0 with |r| = 11 push it to 16.94M > 2^24."""
+    rng = np.random.default_rng(n_users + len(values))
+    n_items = 8
+    items = np.stack([np.zeros(n_users, np.int64), 1 + np.arange(n_users) % (n_items - 1)], 1).reshape(-1)
+    rats = rng.choice(np.asarray(values, np.float64), size=2 * n_users)
+    if n_users > 100_000:
+        rats[0::2] = np.where(rng.random(n_users) < 0.5, -11.0, 11.0)
+    off = np.arange(0, 2 * n_users + 1, 2, dtype=np.uint64)
+    gpu_ctx.item_cosine(n_items, off, items.astype(np.uint32), rats.astype(np.float32), want_matrix=True)
+    acc, exact = gpu_ctx.knn2_exactness()
+    sumsq = np.bincount(items, weights=rats * rats, minlength=n_items)
+    cnt = np.bincount(items, minlength=n_items)
+    want = float(max(sumsq.max(), cnt.max()))
+    assert acc == np.float32(want)
+    assert exact == (want <= 2.0 ** 24)
+
+
 def test_knn2_real_valued(gpu_ctx):
     """make_synthetic_als_data-style real ratings: fp32 MFMA path; accumulation order is
     unpinned in the reference (hash order), so weights agree to a relative 1e-5."""

@@ -192,6 +192,23 @@ def test_stage_local_calc_precomp(work):
     assert n_good + n_c0 + n_ill == n_rows and n_good >= 100, (n_good, n_c0, n_ill)
 
 
+def test_stage_local_calc_precomp_pct(work):
+    """--pct samples movie vertices before prediction (local_calc_precomp.cpp:221): with the
+    same seed, the rows written are exactly every test rating of the sampled movies, with the
+    values of the full run (the predictor is row-independent), and nothing else."""
+    full = pu.parse_res(pu.read_shards(work, "out_res_"))   # --pct 100 of the stage above
+    trat = pu.parse_vertex_ratings(pu.read_shards(work, "out_test_rat_"))
+    run(work, "local_calc_precomp", "--pct", "20", "--seed", "7")
+    part = pu.parse_res(pu.read_shards(work, "out_res_"))
+    movies = {m for m, _ in part}
+    assert 0 < len(movies) < len(trat)
+    assert set(part) == {(m, u) for m in movies for u in trat[m]}
+    for key, (g_mse, g_kk) in part.items():
+        f_mse, f_kk = full[key]
+        assert g_kk == f_kk and (g_mse == f_mse or (np.isnan(g_mse) and np.isnan(f_mse))), (key, g_mse, f_mse)
+    run(work, "local_calc_precomp", "--pct", "100", "--seed", "1")   # restore for later stages
+
+
 def test_stage_knn3(work):
     out = run(work, "knn3")
     avg = float(out.strip().split("Knn Average MSE:")[1])

@@ -7,7 +7,7 @@ import csv
 import re
 import sys
 
-STAGES = {"predict": re.compile(r"predict_kernel<|spill_predict_kernel|spill_basis_kernel"),
+STAGES = {"predict": re.compile(r"pred_basis_kernel<|pred_rating_kernel<|predict_kernel<|spill_predict_kernel|spill_basis_kernel"),
           "eigen": re.compile(r"eigen_kernel<|eigen_spill_kernel|pack_copy_kernel|pack_offsets_kernel")}
 
 
