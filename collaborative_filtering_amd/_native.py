@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("CF_MI355X_LIB") or os.path.join(_HERE, "libcf_mi355x.
 HOST_LIB_PATH = os.path.join(_HERE, "libcf_host.so")
 
 CF_OK = 0
+CF_ERANGE = -4
 CF_SIGS_OWN = 0
 CF_SIGS_COMPAT = 1
 CF_MAX_K = 192
@@ -63,6 +64,11 @@ SIGNATURES = {
                                c_void_p]),
     "cf_item_cosine_run": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_int, c_float,
                                    c_int, c_void_p, c_void_p]),
+    "cf_knn_regroup": (c_int, [c_void_p, c_uint64, c_uint32, c_uint32] + [c_void_p] * 12 + [c_uint64]),
+    "cf_knn_regroup_run": (c_int, [c_void_p, c_uint64, c_uint32, c_uint32] + [c_void_p] * 12 + [c_uint64, c_void_p]),
+    "cf_fold_order": (c_int, [c_void_p, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p]),
+    "cf_fold_order_run": (c_int, [c_void_p, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "cf_prep_timing": (c_int, [c_void_p, c_void_p]),
     "cf_knn2_exactness": (c_int, [c_void_p, c_void_p, c_void_p]),
     "cf_knn2_timing": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "cf_knn_predict": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -12,7 +12,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _native
-from ._native import CF_FILTER_BINOMIAL, CF_FILTER_CHEBY, CF_SIGS_COMPAT, CF_SIGS_OWN, NativeError, ptr
+from ._native import CF_ERANGE, CF_FILTER_BINOMIAL, CF_FILTER_CHEBY, CF_SIGS_COMPAT, CF_SIGS_OWN, NativeError, ptr
 
 
 def _check(lib, ctx, rc, what):
@@ -234,6 +234,58 @@ class Context:
         a, e = c_double(), c_int()
         self._chk(self.lib.cf_knn2_exactness(self.h, byref(a), byref(e)), "cf_knn2_exactness")
         return a.value, bool(e.value)
+
+    # -- data prep: knn regroup (knn.cpp:83-357), k-fold order (fold_cross_validation.py) --
+    def knn_regroup(self, n_users, n_movies, user, movie, rating, validate=None, edg_cap=None):
+        """GPU regroup of ratings in read order (compact ids): returns a dict of the train and
+        test CSR lists per movie (users ascending, last rating read wins) and the sorted unique
+        co-rated movie lists (both roles, self excluded).  edg_cap=None sizes the co-rated
+        output from a first call (CF_ERANGE) when n_movies^2 is too large to preallocate."""
+        user = np.ascontiguousarray(user, dtype=np.uint32)
+        movie = np.ascontiguousarray(movie, dtype=np.uint32)
+        rating = np.ascontiguousarray(rating, dtype=np.float32)
+        val = None if validate is None else np.ascontiguousarray(validate, dtype=np.uint8)
+        n = len(user)
+        out = {k: np.zeros(n_movies + 1, np.uint64) for k in ("train_off", "test_off", "edg_off")}
+        for k in ("train_user", "test_user"):
+            out[k] = np.zeros(max(n, 1), np.uint32)
+        for k in ("train_rating", "test_rating"):
+            out[k] = np.zeros(max(n, 1), np.float32)
+        cap = int(edg_cap) if edg_cap is not None else min(n_movies * max(n_movies - 1, 0), 1 << 24)
+        while True:
+            edg = np.zeros(max(cap, 1), np.uint32)
+            rc = self.lib.cf_knn_regroup(self.h, n, n_users, n_movies, ptr(user), ptr(movie), ptr(rating),
+                                         ptr(val) if val is not None else None, ptr(out["train_off"]),
+                                         ptr(out["train_user"]), ptr(out["train_rating"]), ptr(out["test_off"]),
+                                         ptr(out["test_user"]), ptr(out["test_rating"]), ptr(out["edg_off"]),
+                                         ptr(edg), cap)
+            need = int(out["edg_off"][-1])
+            if rc == CF_ERANGE and edg_cap is None and need > cap:
+                cap = need
+                continue
+            self._chk(rc, "cf_knn_regroup")
+            break
+        out["edg_movie"] = edg[:need]
+        for k, o in (("train", "train_off"), ("test", "test_off")):
+            m = int(out[o][-1])
+            out[k + "_user"] = out[k + "_user"][:m]
+            out[k + "_rating"] = out[k + "_rating"][:m]
+        return out
+
+    def fold_order(self, user, rank):
+        """Rating indices ordered by (rank[user[i]], i) on the GPU (cf_fold_order)."""
+        user = np.ascontiguousarray(user, dtype=np.uint32)
+        rank = np.ascontiguousarray(rank, dtype=np.uint32)
+        order = np.zeros(max(len(user), 1), np.uint32)
+        self._chk(self.lib.cf_fold_order(self.h, len(user), len(rank), ptr(user), ptr(rank), ptr(order)),
+                  "cf_fold_order")
+        return order[:len(user)]
+
+    def prep_timing(self):
+        """Device ms of the last regroup / fold-order call (HIP events)."""
+        t = c_float()
+        self._chk(self.lib.cf_prep_timing(self.h, byref(t)), "cf_prep_timing")
+        return t.value
 
     # -- knn_program + error_vertex_data (knn3.cpp:185-256) ------------------------
     def knn_predict(self, user_off, items, ratings):

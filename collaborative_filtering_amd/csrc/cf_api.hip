@@ -85,6 +85,9 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_knn) (void)hipFree(ctx->d_knn);
     if (ctx->d_knn_acc) (void)hipFree(ctx->d_knn_acc);
+    if (ctx->d_prep) (void)hipFree(ctx->d_prep);
+    for (hipEvent_t& e : ctx->prep_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->d_spill) (void)hipFree(ctx->d_spill);
     if (ctx->d_pspill) (void)hipFree(ctx->d_pspill);
     if (ctx->d_tri) (void)hipFree(ctx->d_tri);

@@ -43,8 +43,12 @@ struct cf_ctx {
     bool tri_debug = false;
     // knn2 stage events (plane build start, GEMM start, GEMM end) of the last launch.
     hipEvent_t knn_ev[3] = {nullptr, nullptr, nullptr};
-    int knn_path = 0;
-    unsigned int* d_knn_acc = nullptr;   // knn2: largest accumulator of the last launch (float bits)   // 1 code plane, 2 three int8 planes, 3 fp32 planes
+    int knn_path = 0;   // 1 code plane, 2 three int8 planes, 3 fp32 planes
+    unsigned int* d_knn_acc = nullptr;   // knn2: largest accumulator of the last launch (float bits)
+    // data prep (cf_prep.hip): sort / bitmap scratch, grown on demand; events of the last call
+    void* d_prep = nullptr;
+    size_t prep_bytes = 0;
+    hipEvent_t prep_ev[2] = {nullptr, nullptr};
     // bucket overlap (eigen, predict): kAuxStreams non-blocking streams, a join event per
     // stream and one fork event (cf_eigen.hip, cf_predict.hip)
     static constexpr int kAuxStreams = 2;   // measured: 3 streams no faster at C2

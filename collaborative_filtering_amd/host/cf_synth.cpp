@@ -13,6 +13,7 @@
 //                         (u + 2654435761) % nusers stepping, movie id offset +nusers)
 //   cfh_synth_graph_model expected knn2 output for a Zipf train population (dense)
 
+#include "cf_pyrand.hpp"
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -229,6 +230,14 @@ int cfh_synth_graph_model(uint64_t seed, uint32_t n_items, double zipf_s, double
         }
     });
     return 0;
+}
+
+// random.seed(seed); x = list(range(n)); random.shuffle(x) -> perm (cf_pyrand.hpp)
+void cfh_py_shuffle(uint64_t seed, uint32_t n, uint32_t* perm) {
+    std::vector<uint32_t> x(n);
+    for (uint32_t i = 0; i < n; ++i) x[i] = i;
+    pyrand::MT(seed).shuffle(x);
+    for (uint32_t i = 0; i < n; ++i) perm[i] = x[i];
 }
 
 }  // extern "C"

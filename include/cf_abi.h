@@ -252,6 +252,40 @@ int cf_knn_predict(cf_ctx* ctx, uint32_t n_users, const uint64_t* user_off,
                    const uint32_t* items, const float* ratings, double* pred,
                    float* movie_mse, uint32_t* movie_count);
 
+/* ---- data prep: knn regroup and k-fold split on the GPU --------
+ * cf_knn_regroup replaces the three GraphLab programs of knn.cpp (vertex_program :160-205,
+ * vertex2/3_program :212-298) and feeds its writers (:303-357).  Input: n ratings in read
+ * order with compact ids user[i] < n_users (in the order of the reference's remapped ids,
+ * uimax - id, :103) and movie[i] < n_movies (ascending movie id), rating[i], and
+ * validate[i] != 0 for the .validate role (NULL = all train, :88-92).  Output per movie m:
+ *   train_user/train_rating[train_off[m] .. train_off[m+1]) : its train ratings, users
+ *       ascending, one per user (the last one read wins: map assignment, :183-187);
+ *   test_*  likewise for the validate role (ratings_test);
+ *   edg_movie[edg_off[m] .. edg_off[m+1]) : the sorted unique movies co-rated with m by any
+ *       of its raters, both roles, m itself excluded (:224-227, 271-274, 342-351).
+ * train_* / test_* need room for n entries, edg_movie for edg_cap; when the co-rated lists
+ * need more than edg_cap entries edg_off is still complete and the call returns CF_ERANGE
+ * (the device variant drops the excess writes: check d_edg_off[n_movies] <= edg_cap). */
+int cf_knn_regroup(cf_ctx* ctx, uint64_t n, uint32_t n_users, uint32_t n_movies, const uint32_t* user,
+                   const uint32_t* movie, const float* rating, const uint8_t* validate, uint64_t* train_off,
+                   uint32_t* train_user, float* train_rating, uint64_t* test_off, uint32_t* test_user,
+                   float* test_rating, uint64_t* edg_off, uint32_t* edg_movie, uint64_t edg_cap);
+int cf_knn_regroup_run(cf_ctx* ctx, uint64_t n, uint32_t n_users, uint32_t n_movies, const uint32_t* d_user,
+                       const uint32_t* d_movie, const float* d_rating, const uint8_t* d_validate,
+                       uint64_t* d_train_off, uint32_t* d_train_user, float* d_train_rating,
+                       uint64_t* d_test_off, uint32_t* d_test_user, float* d_test_rating, uint64_t* d_edg_off,
+                       uint32_t* d_edg_movie, uint64_t edg_cap, void* stream);
+/* User-disjoint k-fold split (fold_cross_validation.py:31-57): rank[u] is user u's position
+ * in the shuffled key list (a permutation of 0..n_users-1); order receives the rating indices
+ * sorted by (rank[user[i]], i), i.e. the concatenation u0.test, u1.test, ... of the script
+ * (each user's lines in read order).  The fold boundaries are rank ranges (host). */
+int cf_fold_order(cf_ctx* ctx, uint64_t n, uint32_t n_users, const uint32_t* user, const uint32_t* rank,
+                  uint32_t* order);
+int cf_fold_order_run(cf_ctx* ctx, uint64_t n, uint32_t n_users, const uint32_t* d_user, const uint32_t* d_rank,
+                      uint32_t* d_order, void* stream);
+/* Device time (HIP events) of the last cf_knn_regroup(_run) / cf_fold_order(_run); waits. */
+int cf_prep_timing(cf_ctx* ctx, float* ms);
+
 /* ---- graph-signal polynomial filters ------------------------ */
 #define CF_FILTER_CHEBY 0     /* cheby.cpp:152-274 (Chebyshev recurrence on [0, 2]) */
 #define CF_FILTER_BINOMIAL 1  /* binomials.cpp:145-253 (quadratic factors, overlapping windows) */
