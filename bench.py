@@ -65,6 +65,8 @@ def parse():
                    help="N=1 secondary leg: BASELINE config 2 (100k x 10k) steps and the out_eigen_ text phases")
     p.add_argument("--knn2", choices=["auto", "off", "only"], default="auto",
                    help="BASELINE config 3 knn2 leg (N=1, rank 0): int8 MFMA item cosine, 20k items x 500k users")
+    p.add_argument("--prep", choices=["auto", "off", "only"], default="auto",
+                   help="data-prep leg (N=1, rank 0): GPU knn regroup + k-fold order on the config-2 ratings")
     p.add_argument("--knn2-users", type=int, default=500_000)
     p.add_argument("--knn2-items", type=int, default=20_000)
     p.add_argument("--knn2-reps", type=int, default=3)
@@ -226,6 +228,10 @@ def main():
     if args.knn2 == "only":
         with Context(dev_index) as kctx:
             print(json.dumps(knn2_leg(args, kctx, dev, torch)), flush=True)
+        return
+    if args.prep == "only":
+        with Context(dev_index) as pctx:
+            print(json.dumps(prep_leg(args, pctx, dev, torch)), flush=True)
         return
 
     cfg = CONFIGS[args.config]
@@ -431,6 +437,9 @@ def main():
     if solo and args.knn2 == "auto":
         torch.cuda.empty_cache()
         result["knn2"] = knn2_leg(args, ctx, dev, torch)
+    if solo and args.prep == "auto":
+        torch.cuda.empty_cache()
+        result["prep"] = prep_leg(args, ctx, dev, torch)
     if solo and args.c5 == "auto":
         torch.cuda.empty_cache()
         W, _, _ = train_graph(Context, dev_index, dev, torch, CONFIGS["c2"]["seed"], CONFIGS["c2"]["train_users"],
@@ -669,6 +678,89 @@ def c5_leg(args, ctx, dev, torch, W):
     return out
 
 
+def prep_leg(args, ctx, dev, torch):
+    """SURVEY 8f item 3, data prep on the GPU: the knn regroup (cf_knn_regroup_run: per-movie
+    train / test lists with last-read-wins, sorted unique co-rated lists) and the k-fold order
+    (cf_fold_order_run, 5 folds) over the config-2 ratings (100k users x 10k items, ~10.7M
+    ratings, 20% of each user's ratings in the validate role).  HBM-bound: SURVEY 8d's 24 B
+    per rating (12 read + 12 written) plus 4 B per co-rated entry written.  Inputs resident,
+    HIP events around each call; the CPU baseline is the oracle restatement on a sample."""
+    from collaborative_filtering_amd import synth
+    from collaborative_filtering_amd._native import ptr
+
+    cfg = CONFIGS["c2"]
+    seed, n_users, n_items = cfg["seed"], cfg["users"], cfg["items"]
+    k = synth.degrees(seed, n_users, k_median=100.0, sigma=0.5, kmin=20, kmax=180)
+    off, items, rats = synth.user_items(seed, k, n_items, threads=16)
+    n = int(off[-1])
+    user = np.repeat(np.arange(n_users, dtype=np.uint32), k.astype(np.int64))
+    validate = (np.random.default_rng(seed).random(n) < 0.2).astype(np.uint8)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    d_user, d_movie, d_rat, d_val = T(user.view(np.int32)), T(items.view(np.int32)), T(rats), T(validate)
+    U32 = lambda m: torch.empty(max(m, 1), dtype=torch.int32, device=dev)
+    OFF = lambda: torch.empty(n_items + 1, dtype=torch.int64, device=dev)
+    F32 = lambda m: torch.empty(max(m, 1), dtype=torch.float32, device=dev)
+    tro, teo, eo = OFF(), OFF(), OFF()
+    tru, teu, trr, ter = U32(n), U32(n), F32(n), F32(n)
+    cap = n_items * (n_items - 1)
+    edg = U32(cap)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    L = ctx.lib
+    reg_ms, fold_ms = [], []
+    rank = np.random.default_rng(5).permutation(n_users).astype(np.uint32)
+    d_rank, d_order = T(rank.view(np.int32)), U32(n)
+    for rep in range(3):
+        rc = L.cf_knn_regroup_run(ctx.h, n, n_users, n_items, ptr(d_user), ptr(d_movie), ptr(d_rat), ptr(d_val),
+                                  ptr(tro), ptr(tru), ptr(trr), ptr(teo), ptr(teu), ptr(ter), ptr(eo), ptr(edg),
+                                  cap, ctypes_void(sp))
+        ctx._chk(rc, "cf_knn_regroup_run")
+        reg_ms.append(ctx.prep_timing())
+        rc = L.cf_fold_order_run(ctx.h, n, n_users, ptr(d_user), ptr(d_rank), ptr(d_order), ctypes_void(sp))
+        ctx._chk(rc, "cf_fold_order_run")
+        fold_ms.append(ctx.prep_timing())
+    n_tr, n_te, n_edg = int(tro[-1].item()), int(teo[-1].item()), int(eo[-1].item())
+    reg_s, fold_s = float(np.median(reg_ms[1:])) / 1e3, float(np.median(fold_ms[1:])) / 1e3
+    byt = 24.0 * n + 4.0 * n_edg
+    # full-size properties: every rating kept once (no duplicates in this set), the fold order
+    # is a permutation grouped by rank
+    order = d_order[:n].cpu().numpy().view(np.uint32)
+    ok_fold = bool(np.array_equal(np.sort(order), np.arange(n, dtype=np.uint32)) and
+                   np.all(np.diff(rank[user[order]].astype(np.int64)) >= 0))
+    out = {
+        "workload": f"config-2 ratings: {n_users} users x {n_items} items, {n} ratings (20% validate), seed {seed}",
+        "regroup_ms": reg_s * 1e3, "fold_order_ms": fold_s * 1e3,
+        "ratings_per_s": n / reg_s, "train": n_tr, "test": n_te, "corated_entries": n_edg,
+        "kept_all": n_tr + n_te == n, "fold_order_grouped": ok_fold,
+        "roofline": {"bound": "hbm", "kernel": "cf_knn_regroup_run (radix sorts, co-rated bitmap, row writes)",
+                     "achieved": byt / reg_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": byt / reg_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes": byt,
+                     "note": "24 B per rating (SURVEY 8d: 12 read + 12 written) + 4 B per co-rated entry; the "
+                             "two sorts and the bitmap are several passes over that"},
+    }
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        from oracle import cf_prep_oracle as prep
+
+        m = 300_000
+        t = time.perf_counter()
+        prep.knn_regroup(n_items, user[:m], items[:m], rats[:m], validate[:m])
+        dt = time.perf_counter() - t
+        out["cpu_baseline"] = {"value": m / dt, "unit": "ratings/s", "cores": 1, "kind": "port",
+                               "sample": f"first {m} ratings, oracle/cf_prep_oracle.knn_regroup (Python maps, "
+                                         "the reference's map semantics), 1 thread"}
+    del d_user, d_movie, d_rat, d_val, tru, teu, trr, ter, edg, d_order
+    torch.cuda.empty_cache()
+    return out
+
+
+def ctypes_void(p):
+    import ctypes
+
+    return ctypes.c_void_p(p or 0)
+
+
 def knn2_leg(args, ctx, dev, torch):
     """BASELINE config 3: knn2 weights_calc (knn2.cpp:127-164) over I items x U train users,
     integer ratings 1..5, on the int8 MFMA path; the dense item-weight matrix stays in HBM.
@@ -709,6 +801,22 @@ def knn2_leg(args, ctx, dev, torch):
     W_s = d_W.view(n_items, n_items)
     sym = bool(torch.equal(W_s, W_s.t()))
     nnz = int((W_s > 0).sum().item())
+    # K-chunk streaming: the same launch in 4 user chunks with the int32 tile
+    # partials carried in HBM; the weights must be the same bits
+    chunk = -(-n_users // 4 // 128) * 128
+    d_W2 = torch.empty_like(d_W)
+    ctx.set_knn2_chunk(chunk)
+    try:
+        e0.record(stream)
+        ctx.item_cosine_run(n_users, n_items, d_off, d_items, d_rat, 1, d_W2, stream=sp)
+        e1.record(stream)
+        e1.synchronize()
+        chunked = {"users_per_chunk": chunk, "chunks": ctx.knn2_chunks(), "call_ms": e0.elapsed_time(e1),
+                   "bit_identical": bool(torch.equal(d_W, d_W2))}
+    finally:
+        ctx.set_knn2_chunk(0)
+    del d_W2
+    acc, exact = ctx.knn2_exactness()
     out = {
         "workload": f"BASELINE config 3: knn2 item cosine, {n_items} items x {n_users} train users, "
                     f"mean deg {float(kd.mean()):.1f}, integer ratings 1..5 (Zipf(1) items, seed {seed})",
@@ -720,6 +828,9 @@ def knn2_leg(args, ctx, dev, torch):
         "useful_pair_updates": float(np.sum(kd.astype(np.float64) ** 2)),
         "edges_w_gt_0.01": nnz,
         "symmetric": sym,
+        "k_chunked": chunked,
+        "max_float_accumulator": acc,
+        "reference_floats_exact": exact,
         "roofline": {
             "bound": "mfma",
             "kernel": "knn2_code_kernel (v_mfma_i32_32x32x32_i8)",

@@ -69,6 +69,8 @@ SIGNATURES = {
     "cf_fold_order": (c_int, [c_void_p, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p]),
     "cf_fold_order_run": (c_int, [c_void_p, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "cf_prep_timing": (c_int, [c_void_p, c_void_p]),
+    "cf_set_knn2_chunk": (c_int, [c_void_p, c_uint32]),
+    "cf_knn2_chunks": (c_int, [c_void_p, c_void_p]),
     "cf_knn2_exactness": (c_int, [c_void_p, c_void_p, c_void_p]),
     "cf_knn2_timing": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "cf_knn_predict": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -228,6 +228,15 @@ class Context:
                   "cf_knn2_timing")
         return a.value, b.value, c.value
 
+    def set_knn2_chunk(self, users_per_chunk: int = 0):
+        """Force the knn2 K-chunk size (users, multiple of 128; 0 = automatic by free HBM)."""
+        self._chk(self.lib.cf_set_knn2_chunk(self.h, int(users_per_chunk)), "cf_set_knn2_chunk")
+
+    def knn2_chunks(self):
+        n = c_int()
+        self._chk(self.lib.cf_knn2_chunks(self.h, byref(n)), "cf_knn2_chunks")
+        return n.value
+
     def knn2_exactness(self):
         """(max accumulator, exact) of the last knn2 launch: exact is True when the
         reference's float accumulators (knn2.cpp:129-140) stay <= 2^24 (cf_knn2_exactness)."""

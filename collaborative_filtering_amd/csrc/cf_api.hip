@@ -85,6 +85,7 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_knn) (void)hipFree(ctx->d_knn);
     if (ctx->d_knn_acc) (void)hipFree(ctx->d_knn_acc);
+    if (ctx->d_knn_part) (void)hipFree(ctx->d_knn_part);
     if (ctx->d_prep) (void)hipFree(ctx->d_prep);
     for (hipEvent_t& e : ctx->prep_ev)
         if (e) (void)hipEventDestroy(e);
@@ -500,6 +501,18 @@ int cf_knn2_timing(cf_ctx* ctx, float* plane_ms, float* gemm_ms, int* path) {
     if (plane_ms) *plane_ms = a;
     if (gemm_ms) *gemm_ms = b;
     if (path) *path = ctx->knn_path;
+    return CF_OK;
+}
+
+int cf_set_knn2_chunk(cf_ctx* ctx, uint32_t users_per_chunk) {
+    if (!ctx) return CF_EINVAL;
+    ctx->knn_chunk_users = users_per_chunk;
+    return CF_OK;
+}
+
+int cf_knn2_chunks(cf_ctx* ctx, int* n_chunks) {
+    if (!ctx || !n_chunks) return CF_EINVAL;
+    *n_chunks = ctx->knn_chunks;
     return CF_OK;
 }
 

@@ -44,7 +44,12 @@ struct cf_ctx {
     // knn2 stage events (plane build start, GEMM start, GEMM end) of the last launch.
     hipEvent_t knn_ev[3] = {nullptr, nullptr, nullptr};
     int knn_path = 0;   // 1 code plane, 2 three int8 planes, 3 fp32 planes
-    unsigned int* d_knn_acc = nullptr;   // knn2: largest accumulator of the last launch (float bits)
+    unsigned int* d_knn_acc = nullptr;
+    // knn2 K-chunk streaming: tile partial sums, forced chunk size (0 = by free HBM), chunks used
+    void* d_knn_part = nullptr;
+    size_t knn_part_bytes = 0;
+    uint32_t knn_chunk_users = 0;
+    int knn_chunks = 0;   // knn2: largest accumulator of the last launch (float bits)
     // data prep (cf_prep.hip): sort / bitmap scratch, grown on demand; events of the last call
     void* d_prep = nullptr;
     size_t prep_bytes = 0;

@@ -200,6 +200,11 @@ struct Knn2CodeArgs {
     int cnt_min;
     float* w_out;
     unsigned int* acc_max;
+    // K-chunk streaming (users beyond one HBM-resident plane): int32 partial sums of the four
+    // products per tile, 256 KB per 128 x 128 tile; acc_in: start from them, acc_out: store
+    // them instead of running the epilogue (the last chunk has acc_out = 0)
+    int* part;
+    int acc_in, acc_out;
 };
 
 __device__ __forceinline__ bool code_tile(uint32_t b, uint32_t nt, uint32_t nsb, uint32_t& ta, uint32_t& tb) {
@@ -260,8 +265,25 @@ __global__ __launch_bounds__(512, 1) void knn2_code_kernel(Knn2CodeArgs a) {
     };
 
     v16i num[2], den1[2], den2[2], cnt[2];
+    // partial-sum slot of this wave: [tile][wave][block i][product][reg][lane] (coalesced per reg)
+    const uint64_t tile = (uint64_t)ta * a.n_tiles - (uint64_t)ta * (ta - 1) / 2 + (tb - ta);
+    int* part = a.part ? a.part + ((tile * 8 + wave) * 8) * 1024 + lane : nullptr;
+    auto part_io = [&](bool load) {
+        v16i* acc[4] = {num, den1, den2, cnt};
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    int* q = part + ((i * 4 + p) * 16 + g) * 64;
+                    if (load) acc[p][i][g] = *q;
+                    else *q = acc[p][i][g];
+                }
+    };
 #pragma unroll
     for (int i = 0; i < 2; ++i) num[i] = den1[i] = den2[i] = cnt[i] = v16i{};
+    if (a.acc_in) part_io(true);
 
     const int rdA = (wy * 64 + r) * KC_ROW + 16 * h, rdB = (wx * 32 + r) * KC_ROW + 16 * h;
     const uint64_t n_stage = a.ldu / KC_U;
@@ -302,6 +324,10 @@ __global__ __launch_bounds__(512, 1) void knn2_code_kernel(Knn2CodeArgs a) {
         }
         if (s + 1 < n_stage) lstore(buf ^ 1);
         __syncthreads();
+    }
+    if (a.acc_out) {
+        part_io(false);
+        return;
     }
     Knn2Args e{};
     e.n_items = a.n_items;
@@ -436,37 +462,79 @@ int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64
             if (mask >> b & 1) vals[n_vals++] = b - 11;
     }
     if (integer_ratings && n_vals <= 7) {
-        const uint64_t ldu = ((uint64_t)n_users + KC_U - 1) / KC_U * KC_U;
-        const size_t plane = (size_t)n_items * ldu;
+        // Users in K chunks when one code plane of every user would not fit (SURVEY 8f item 3:
+        // 1M x 50k is a 50 GB plane; the int32 partials are 256 KB per tile, 20 GB at 50k
+        // items): a plane per chunk, partial sums carried across chunks in HBM, the epilogue
+        // on the last chunk.  cf_set_knn2_chunk forces a chunk size (tests).
+        const uint64_t n_tiles = (n_items + KC_T - 1) / KC_T;
+        const uint64_t ldu_all = ((uint64_t)n_users + KC_U - 1) / KC_U * KC_U;
+        uint64_t chunk = ldu_all;
+        if (ctx->knn_chunk_users) {
+            chunk = std::max<uint64_t>(KC_U, (uint64_t)ctx->knn_chunk_users / KC_U * KC_U);
+        } else {
+            size_t free_b = 0, total_b = 0;
+            CF_HIP_CHECK(ctx, hipMemGetInfo(&free_b, &total_b));
+            const size_t avail = (free_b + ctx->knn_bytes) / 10 * 6;   // leave room for the caller
+            if ((size_t)n_items * ldu_all > avail) {
+                const size_t parts = n_tiles * (n_tiles + 1) / 2 * 262144;
+                if (parts >= avail) return cf_set_error(ctx, CF_ENOMEM, "knn2: tile partial sums exceed HBM");
+                chunk = std::max<uint64_t>(KC_U, (avail - parts) / n_items / KC_U * KC_U);
+            }
+        }
+        chunk = std::min(chunk, ldu_all);
+        const uint64_t n_chunks = n_users ? (n_users + chunk - 1) / chunk : 1;
+        const size_t plane = (size_t)n_items * chunk;
         CF_TRY(knn2_alloc(ctx, std::max<size_t>(plane, 16)));
         int8_t* C = (int8_t*)ctx->d_knn;
-        CF_HIP_CHECK(ctx, hipMemsetAsync(C, 0, plane, stream));
+        int* part = nullptr;
+        if (n_chunks > 1) {
+            const size_t pb = n_tiles * (n_tiles + 1) / 2 * 262144;
+            if (pb > ctx->knn_part_bytes) {
+                if (ctx->d_knn_part) (void)hipFree(ctx->d_knn_part);
+                ctx->d_knn_part = nullptr;
+                ctx->knn_part_bytes = 0;
+                if (hipMalloc(&ctx->d_knn_part, pb) != hipSuccess)
+                    return cf_set_error(ctx, CF_ENOMEM, "knn2 tile partial sums (" + std::to_string(pb) + " bytes)");
+                ctx->knn_part_bytes = pb;
+            }
+            part = (int*)ctx->d_knn_part;
+        }
         CodeMap map{};
         for (int c = 1; c <= n_vals; ++c) map.code[vals[c - 1] + 11] = (int8_t)c;
-        if (n_users) {
-            hipLaunchKernelGGL(plane_code_kernel, dim3(n_users), dim3(64), 0, stream, n_users, d_user_off, d_item,
-                               d_rating, ldu, map, C);
-            CF_HIP_CHECK(ctx, hipGetLastError());
-        }
         Knn2CodeArgs a{};
         a.C = C;
-        a.ldu = ldu;
+        a.ldu = chunk;
         a.n_items = n_items;
-        a.n_tiles = (n_items + KC_T - 1) / KC_T;
+        a.n_tiles = (uint32_t)n_tiles;
         a.n_super = (a.n_tiles + 15) / 16;
         code_tables(vals, n_vals, a.tR_lo, a.tR_hi, a.tS_lo, a.tS_hi, a.tB_lo, a.tB_hi);
         a.w_min = w_min;
         a.cnt_min = cnt_min;
         a.w_out = d_w_out;
         a.acc_max = ctx->d_knn_acc;
+        a.part = part;
         const uint32_t grid = a.n_super * (a.n_super + 1) / 2 * 256;
         ctx->knn_path = 1;
-        CF_HIP_CHECK(ctx, hipEventRecord(ctx->knn_ev[1], stream));
-        hipLaunchKernelGGL(knn2_code_kernel, dim3(grid), dim3(512), 0, stream, a);
-        CF_HIP_CHECK(ctx, hipGetLastError());
+        ctx->knn_chunks = (int)n_chunks;
+        for (uint64_t c = 0; c < n_chunks; ++c) {
+            const uint64_t u0 = c * chunk;
+            const uint32_t nu = (uint32_t)std::min<uint64_t>(chunk, n_users - std::min<uint64_t>(u0, n_users));
+            CF_HIP_CHECK(ctx, hipMemsetAsync(C, 0, plane, stream));
+            if (nu) {
+                hipLaunchKernelGGL(plane_code_kernel, dim3(nu), dim3(64), 0, stream, nu, d_user_off + u0, d_item,
+                                   d_rating, chunk, map, C);
+                CF_HIP_CHECK(ctx, hipGetLastError());
+            }
+            a.acc_in = c > 0;
+            a.acc_out = c + 1 < n_chunks;
+            if (c == 0) CF_HIP_CHECK(ctx, hipEventRecord(ctx->knn_ev[1], stream));
+            hipLaunchKernelGGL(knn2_code_kernel, dim3(grid), dim3(512), 0, stream, a);
+            CF_HIP_CHECK(ctx, hipGetLastError());
+        }
         CF_HIP_CHECK(ctx, hipEventRecord(ctx->knn_ev[2], stream));
         return CF_OK;
     }
+    ctx->knn_chunks = 1;
     const uint64_t ldu = ((uint64_t)n_users + 31) / 32 * 32;
     const size_t esz = integer_ratings ? 1 : 4;
     const size_t plane = (size_t)n_items * ldu * esz;

@@ -28,10 +28,30 @@
 // with the script's `n_usr_done > num_usr / num_div` rule).
 
 #include <hipcub/hipcub.hpp>
+#include <rocprim/rocprim.hpp>
 
 #include "cf_internal.h"
 
 namespace {
+
+// Sorts run rocprim's stable merge-sort path at every size (radix_sort_config with an unbounded
+// merge-sort limit).  Inside a PyTorch process this library is served by torch's bundled HIP
+// runtime, under which rocprim's onesweep radix path fails to launch (hipErrorInvalidValue, in
+// both its gfx950-tuned and generic configurations), while the merge path runs; standalone on
+// the ROCm 7.2 runtime all of them run (tools/probe_sort.hip, 10.7M u64 keys + u32 values,
+// 47 bits: onesweep 0.94 ms, merge sort 0.86 ms).
+using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config,
+                                           (size_t)1 << 40>;
+
+template <class K, class V>
+hipError_t sort_pairs(void* tmp, size_t& bytes, const K* ki, K* ko, const V* vi, V* vo, uint64_t n, int bits,
+                      hipStream_t st) {
+    return rocprim::radix_sort_pairs<SortCfg>(tmp, bytes, ki, ko, vi, vo, (unsigned int)n, 0u, (unsigned int)bits, st);
+}
+template <class K>
+hipError_t sort_keys(void* tmp, size_t& bytes, const K* ki, K* ko, uint64_t n, int bits, hipStream_t st) {
+    return rocprim::radix_sort_keys<SortCfg>(tmp, bytes, ki, ko, (unsigned int)n, 0u, (unsigned int)bits, st);
+}
 
 inline int bits_for(uint64_t n) {   // bits to represent 0 .. n-1 (>= 1)
     int b = 1;
@@ -222,17 +242,18 @@ int prep_events(cf_ctx* ctx) {
     return CF_OK;
 }
 
-// cub temporary-storage sizes for n items
-size_t cub_bytes(uint64_t n, uint64_t nseg) {
+// cub temporary-storage sizes, queried with exactly the arguments of the real calls (rocprim
+// sizes its onesweep storage from the bit range and the stream's target)
+size_t cub_bytes(uint64_t n, uint64_t nseg, int bits_a, int bits_b, int bits_fold, hipStream_t st) {
     size_t a = 0, b = 0, c = 0, d = 0, e = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                             (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
-    (void)hipcub::DeviceRadixSort::SortKeys(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)n);
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, d, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)nseg);
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, e, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                             (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
-    return std::max({a, b, c, d, e});
+    (void)sort_pairs(nullptr, a, (const uint64_t*)nullptr, (uint64_t*)nullptr, (const uint32_t*)nullptr,
+                     (uint32_t*)nullptr, n, bits_a, st);
+    (void)sort_keys(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr, n, bits_b, st);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, st);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, d, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)nseg, st);
+    (void)sort_pairs(nullptr, e, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                     (uint32_t*)nullptr, n, bits_fold, st);
+    return std::max({a, b, c, d, e}) + 4096;
 }
 
 // widen u32 counts into u64 for the offset scans
@@ -259,7 +280,8 @@ int cf_knn_regroup_run(cf_ctx* ctx, uint64_t n, uint32_t n_users, uint32_t n_mov
     hipStream_t st = (hipStream_t)stream_;
     const uint64_t nseg = 2 * (uint64_t)n_movies + 1;
     const uint32_t words = (n_movies + 31) / 32;
-    const size_t cub = cub_bytes(n, std::max<uint64_t>(nseg, (uint64_t)n_users + 1));
+    const int bits_a = 32 + bits_for(nseg), bits_b = 32 + bits_for((uint64_t)n_users + 1);
+    const size_t cub = cub_bytes(n, std::max<uint64_t>(nseg, (uint64_t)n_users + 1), bits_a, bits_b, 1, st);
     const size_t need = 2 * 8 * (n + 64) + 3 * 4 * (n + 64) + 4 * (n + 64) + 8 * 2 * (nseg + 64) +
                         (4 + 8) * ((uint64_t)n_users + 64) + 4 * (uint64_t)n_movies * words + 8 * (n_movies + 64) +
                         cub + 16 * 256 + 4 * (n + 64);
@@ -287,8 +309,8 @@ int cf_knn_regroup_run(cf_ctx* ctx, uint64_t n, uint32_t n_users, uint32_t n_mov
     // ---- 1. per-movie train / test lists ----------------------------------------------
     if (n) {
         hipLaunchKernelGGL(regroup_keys_kernel, G, B, 0, st, n, d_user, d_movie, d_validate, n_movies, key_a, idx_a);
-        const int end_bit = 32 + bits_for(nseg);
-        CF_HIP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, tb, key_a, key_b, idx_a, idx_b, (int)n, 0, end_bit, st));
+        CF_HIP_CHECK(ctx, hipGetLastError());
+        CF_HIP_CHECK(ctx, sort_pairs(tmp, tb, key_a, key_b, idx_a, idx_b, n, bits_a, st));
         hipLaunchKernelGGL(run_flag_kernel, G, B, 0, st, n, key_b, 0, keep);
         CF_HIP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tb, keep, pos, (int)n, st));
     }
@@ -304,8 +326,7 @@ int cf_knn_regroup_run(cf_ctx* ctx, uint64_t n, uint32_t n_users, uint32_t n_mov
     CF_HIP_CHECK(ctx, hipMemsetAsync(ucnt, 0, sizeof(uint32_t) * ((uint64_t)n_users + 1), st));
     if (n) {
         hipLaunchKernelGGL(user_keys_kernel, G, B, 0, st, n, d_user, d_movie, key_a);
-        const int end_bit = 32 + bits_for((uint64_t)n_users + 1);
-        CF_HIP_CHECK(ctx, hipcub::DeviceRadixSort::SortKeys(tmp, tb, key_a, key_b, (int)n, 0, end_bit, st));
+        CF_HIP_CHECK(ctx, sort_keys(tmp, tb, key_a, key_b, n, bits_b, st));
         hipLaunchKernelGGL(run_flag_kernel, G, B, 0, st, n, key_b, 1, keep);
         CF_HIP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tb, keep, pos, (int)n, st));
         hipLaunchKernelGGL(user_sets_kernel, G, B, 0, st, n, key_b, keep, pos, ucnt, kuser);
@@ -395,7 +416,8 @@ int cf_fold_order_run(cf_ctx* ctx, uint64_t n, uint32_t n_users, const uint32_t*
     CF_TRY(set_device(ctx));
     CF_TRY(prep_events(ctx));
     hipStream_t st = (hipStream_t)stream_;
-    const size_t cub = cub_bytes(n, 1);
+    const int bits_f = bits_for(std::max<uint64_t>(n_users, 1));
+    const size_t cub = cub_bytes(n, 1, 64, 64, bits_f, st);
     CF_TRY(prep_reserve(ctx, 3 * 4 * (n + 64) + cub + 1024));
     Carve cv{static_cast<char*>(ctx->d_prep)};
     uint32_t* key_a = cv.take<uint32_t>(n);
@@ -406,8 +428,7 @@ int cf_fold_order_run(cf_ctx* ctx, uint64_t n, uint32_t n_users, const uint32_t*
     CF_HIP_CHECK(ctx, hipEventRecord(ctx->prep_ev[0], st));
     if (n) {
         hipLaunchKernelGGL(fold_keys_kernel, grid_for(n), dim3(256), 0, st, n, d_user, d_rank, key_a, idx);
-        CF_HIP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, tb, key_a, key_b, idx, d_order, (int)n, 0,
-                                                             bits_for(std::max<uint64_t>(n_users, 1)), st));
+        CF_HIP_CHECK(ctx, sort_pairs(tmp, tb, key_a, key_b, idx, d_order, n, bits_f, st));
         CF_HIP_CHECK(ctx, hipGetLastError());
     }
     CF_HIP_CHECK(ctx, hipEventRecord(ctx->prep_ev[1], st));

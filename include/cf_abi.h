@@ -227,6 +227,14 @@ int cf_knn2_timing(cf_ctx* ctx, float* plane_ms, float* gemm_ms, int* path);
  * ones bit for bit, 0 otherwise (always 0 on the fp32 path of real-valued ratings, whose
  * reference sums are in hash order).  Waits for the launch to finish. */
 int cf_knn2_exactness(cf_ctx* ctx, double* max_accumulator, int* exact);
+/* K-chunk streaming of the one-code-plane knn2 path: when the int8 code
+ * plane of all users (n_items x n_users bytes) exceeds ~60% of free HBM, users are processed
+ * in chunks with the four int32 products carried per 128 x 128 tile in HBM between chunks
+ * (256 KB per tile) and the epilogue on the last chunk: the weights are identical.
+ * cf_set_knn2_chunk forces users_per_chunk (rounded down to a multiple of 128; 0 = automatic);
+ * cf_knn2_chunks reports the chunk count of the last launch. */
+int cf_set_knn2_chunk(cf_ctx* ctx, uint32_t users_per_chunk);
+int cf_knn2_chunks(cf_ctx* ctx, int* n_chunks);
 /* local_calc vertex_program::apply (local_calc.cpp:262-526) on the uploaded graph (raw
  * out_fin_ weights; edges count iff w > 0.1, graph_loader :113).  Movie unit v lists
  * movie_items[movie_off[v] .. movie_off[v+1]) = [m, the out-neighbours of m with w > 0.1]

@@ -74,6 +74,24 @@ def test_knn2_exactness_guard(gpu_ctx, n_users, values):
     assert exact == (want <= 2.0 ** 24)
 
 
+@pytest.mark.parametrize("chunk", [128, 384, 1000])
+def test_knn2_k_chunk_streaming(gpu_ctx, chunk):
+    """Users in K chunks (int32 tile partials carried in HBM between chunks): the same bits as
+    the one-plane launch and the oracle, whatever the chunk size (a ragged last chunk too)."""
+    n_users, n_items = 3000, 700
+    off, items, rats = synth_train(n_users, n_items, seed=77, zero_frac=0.03)
+    Wo, _ = orc.knn2(off.astype(np.int64), items.astype(np.int32), rats, n_items)
+    try:
+        gpu_ctx.set_knn2_chunk(chunk)
+        Wg = gpu_ctx.item_cosine(n_items, off, items, rats.astype(np.float32))
+        assert gpu_ctx.knn2_chunks() == -(-n_users // (chunk // 128 * 128))
+    finally:
+        gpu_ctx.set_knn2_chunk(0)
+    assert np.array_equal(Wg, Wo)
+    acc, exact = gpu_ctx.knn2_exactness()
+    assert exact and acc > 0
+
+
 def test_knn2_real_valued(gpu_ctx):
     """make_synthetic_als_data-style real ratings: fp32 MFMA path; accumulation order is
     unpinned in the reference (hash order), so weights agree to a relative 1e-5."""
