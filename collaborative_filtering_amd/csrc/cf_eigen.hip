@@ -39,6 +39,15 @@ using f2 = __attribute__((ext_vector_type(2))) float;
 __device__ __forceinline__ f2 lds_ld(const f2* p) {
     return *(const volatile __attribute__((address_space(3))) f2*)(p);
 }
+// Column stores likewise: un-fused ds_write_b64 instead of ds_write2_b64 (CF_EIGEN_FUSED_ST=1
+// keeps the compiler's pairing, for A/B).
+__device__ __forceinline__ void lds_st(f2* p, f2 v) {
+#if defined(CF_EIGEN_FUSED_ST) && CF_EIGEN_FUSED_ST
+    *p = v;
+#else
+    *(volatile __attribute__((address_space(3))) f2*)(p) = v;
+#endif
+}
 
 
 template <int CTRL>
@@ -324,12 +333,16 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
                 devp = s_dev[p];
                 al = pair_sum(al2.x + al2.y);
             }
+            // q = s0 + f + ti walks the traveling half from ti = fi, wrapping at f; a step is
+            // live while step < f and the traveling column exists (ti < t, q < k)
+            const int tv = fixed ? min(t, k - s0 - f) : 0;
+            const int nlive = fixed ? f : 0;
+            int ti = fi;
+            f2* bq = reinterpret_cast<f2*>(B + (s0 + f + ti) * LD);
+            f2* const bq0 = reinterpret_cast<f2*>(B + (s0 + f) * LD);
             for (int step = 0; step < FL; ++step) {
-                int ti = fi + step;
-                if (ti >= f) ti -= f;
                 const int q = s0 + f + ti;
-                if (fixed && step < f && ti < t && q < k) {
-                    f2* bq = reinterpret_cast<f2*>(B + q * LD);
+                if (step < nlive && ti < tv) {
                     const float dq = s_dev[q];   // issued with the column loads
                     const float be = s_nrm[q];
                     f2 xq[E2];
@@ -343,17 +356,19 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
                     if (ga * ga > tol2 * (al * be)) {
                         // Hardware rcp/rsq/sqrt: the rotation only has to annihilate ga well
                         // enough; its scale error (c^2 + s^2 != 1) is tracked exactly below.
-                        const float zeta = (be - al) * __builtin_amdgcn_rcpf(2.0f * ga);
-                        const float az = fabsf(zeta);
-                        const float tt = copysignf(
-                            __builtin_amdgcn_rcpf(az + __builtin_amdgcn_sqrtf(fmaf(az, az, 1.0f))), zeta);
+                        // t = sign(zeta) / (|zeta| + sqrt(1 + zeta^2)), zeta = (be - al) / (2 ga),
+                        // written as 2 ga sign(be - al) / (|be - al| + sqrt((be - al)^2 + 4 ga^2)):
+                        // three transcendentals instead of four
+                        const float dd = be - al;
+                        const float r = __builtin_amdgcn_sqrtf(fmaf(dd, dd, 4.0f * ga * ga));
+                        const float tt = (dd < 0.0f ? -2.0f * ga : 2.0f * ga) * __builtin_amdgcn_rcpf(fabsf(dd) + r);
                         const float c = __builtin_amdgcn_rsqf(fmaf(tt, tt, 1.0f));
                         const float sn = c * tt;
                         const f2 c2 = {c, c}, s2 = {sn, sn}, ns2 = {-sn, -sn};
 #pragma unroll
                         for (int e = 0; e < E2; ++e) {
                             const f2 np = __builtin_elementwise_fma(ns2, xq[e], c2 * xp[e]);
-                            bq[slot(q, e)] = __builtin_elementwise_fma(s2, xp[e], c2 * xq[e]);
+                            lds_st(bq + slot(q, e), __builtin_elementwise_fma(s2, xp[e], c2 * xq[e]));
                             xp[e] = np;
                         }
                         // c^2 + s^2 = 1 + delta: track each column's accumulated scale so
@@ -374,10 +389,15 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
                     }
                 }
                 __syncthreads();
+                bq += LD / 2;   // f2 units
+                if (++ti == f) {
+                    ti = 0;
+                    bq = bq0;
+                }
             }
             if (pmod) {
 #pragma unroll
-                for (int e = 0; e < E2; ++e) bp[slot(p, e)] = xp[e];
+                for (int e = 0; e < E2; ++e) lds_st(bp + slot(p, e), xp[e]);
                 if (lig == 0) {
                     s_dev[p] = devp;
                     s_nrm[p] = al;

@@ -50,6 +50,7 @@ def _run_local_case(gpu_ctx, G, test, check_movies=None, spill_gap=1e-2):
     mse, kk, pred, wlim, lim = gpu_ctx.local_calc(np.array(moff), np.array(mitems), toff, np.array(tuser),
                                                   np.array(trat))
     n_cmp = n_wl = 0
+    cat = {"c=0": 0, "tie": 0, "rank-deficient": 0, "ill-conditioned": 0, "small gap": 0}
     sizes = []
     bad = []
     for mv, nbrs in units:
@@ -75,6 +76,7 @@ def _run_local_case(gpu_ctx, G, test, check_movies=None, spill_gap=1e-2):
                 bad.append((mv, t, "kk", kk[g], kk_o[t]))
                 continue
             if kk_o[t] == 0:
+                cat["c=0"] += 1
                 if not (np.isnan(mse[g]) and np.isnan(mse_o[t])):
                     bad.append((mv, t, "c=0 not NaN", mse[g], mse_o[t]))
                 continue
@@ -84,20 +86,30 @@ def _run_local_case(gpu_ctx, G, test, check_movies=None, spill_gap=1e-2):
                 continue
             tie = np.min(np.abs(ev - wl_o[t])) < 1e-4
             if lim[g] != lim_o[t]:
+                cat["tie"] += 1
                 if not tie:
                     bad.append((mv, t, "lim", lim[g], lim_o[t]))
                 continue
             C = [i for i in range(len(nbrs) + 1) if i > 0 and R[i, t] != 0]
             Uc = V[np.ix_(C, range(lim_o[t]))]
-            if len(C) < lim_o[t] or np.linalg.cond(Uc.T @ Uc) > 1e4:
+            if len(C) < lim_o[t]:
+                # singular U_C^T U_C: both sides return rounding noise; pinned: finite, clamped
+                cat["rank-deficient"] += 1
+                if not (np.isfinite(mse[g]) and 1.0 <= pred[g] <= 5.0):
+                    bad.append((mv, t, "rank-deficient not finite/clamped", float(mse[g]), float(pred[g])))
+                continue
+            if np.linalg.cond(Uc.T @ Uc) > 1e4:
+                cat["ill-conditioned"] += 1
                 continue
             # the span of the first lim eigenvectors is determined to ~eps / gap at the cut
             gap = ev[lim_o[t]] - ev[lim_o[t] - 1] if lim_o[t] < len(ev) else 1.0
             if gap < (spill_gap if len(nbrs) + 1 > 192 else 1e-2):
+                cat["small gap"] += 1
                 continue
             n_cmp += 1
             if abs(float(mse[g]) - float(mse_o[t])) > 1e-3 * max(1.0, float(mse_o[t])):
                 bad.append((mv, t, "mse", float(mse[g]), float(mse_o[t]), float(pred[g]), pred_o[t], gap))
+    print(f"categories outside the mse comparison: {cat}")
     return n_wl, n_cmp, sizes, bad
 
 
@@ -105,7 +117,8 @@ def test_local_calc_matches_oracle(gpu_ctx):
     G, test = build_case(7)
     n_wl, n_cmp, _, bad = _run_local_case(gpu_ctx, G, test)
     assert not bad, bad[:10]
-    assert n_wl > 200 and n_cmp > 20, (n_wl, n_cmp)
+    # measured (r2): 767 w_lim values, 719 predictions compared -- most rows are comparable
+    assert n_wl > 600 and n_cmp > 0.8 * n_wl, (n_wl, n_cmp)
     print(f"w_lim compared {n_wl}, predictions compared {n_cmp}")
 
 
@@ -121,5 +134,7 @@ def test_local_calc_spill_units(gpu_ctx):
     n_wl, n_cmp, sizes, bad = _run_local_case(gpu_ctx, G, test, check_movies=set(range(24)), spill_gap=1e-3)
     assert not bad, bad[:10]
     assert sum(s > 192 for s in sizes) >= 5 and sum(s <= 192 for s in sizes) >= 5, sizes
-    assert n_wl > 200 and n_cmp > 20, (n_wl, n_cmp)
+    # measured (r2): 1277 w_lim values, 553 predictions compared (dense n ~ 200 graphs leave
+    # many ratings rank-deficient or without a 1e-3 gap at the lim cut)
+    assert n_wl > 1000 and n_cmp > 400, (n_wl, n_cmp)
     print(f"spill units: sizes {sorted(sizes)}; w_lim compared {n_wl}, predictions compared {n_cmp}")
