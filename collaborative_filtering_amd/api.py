@@ -419,6 +419,20 @@ class Plan:
                                   ptr(d_sigs), ptr(d_evals), ptr(d_evecs), c_void_p(stream or 0)),
                "cf_eigen_run")
 
+    def step_run(self, d_item_off, d_items, d_ratings, d_evec_off, d_m, d_sigs, d_evals, d_evecs, sig_mode,
+                 d_mse, d_kk, d_pred=None, stream=None):
+        """cf_step_run: eigen + predictor (fp32 eigen outputs, sigtab = d_sigs) with per-bucket overlap."""
+        c = self.ctx
+        c._chk(c.lib.cf_step_run(c.h, self.h, ptr(d_item_off), ptr(d_items), ptr(d_ratings), ptr(d_evec_off),
+                                 ptr(d_m), ptr(d_sigs), ptr(d_evals), ptr(d_evecs), int(sig_mode), ptr(d_mse),
+                                 ptr(d_kk), ptr(d_pred), c_void_p(stream or 0)), "cf_step_run")
+
+    def step_timing(self):
+        """(eigen_ms, total_ms) of the last cf_step_run (waits for it)."""
+        a, b = c_float(), c_float()
+        self.ctx._chk(self.ctx.lib.cf_step_timing(self.ctx.h, byref(a), byref(b)), "cf_step_timing")
+        return a.value, b.value
+
     def predict_run(self, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off, d_evecs, d_sigtab,
                     sig_mode, d_mse, d_kk, d_pred=None, stream=None, fp64=False):
         c = self.ctx

@@ -96,6 +96,11 @@ void cf_destroy(cf_ctx* ctx) {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t& e : ctx->aux_event)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t* arr : {ctx->step_bucket_ev, ctx->step_sync_ev, ctx->step_time_ev})
+        for (int i = 0; i < (arr == ctx->step_bucket_ev ? 16 : arr == ctx->step_sync_ev ? 4 : 3); ++i)
+            if (arr[i]) (void)hipEventDestroy(arr[i]);
+    for (hipStream_t& st : ctx->step_stream)
+        if (st) (void)hipStreamDestroy(st);
     for (hipStream_t& st : ctx->aux_stream)
         if (st) (void)hipStreamDestroy(st);
     delete ctx;
@@ -247,6 +252,7 @@ int cf_plan_create(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, cf_p
     cf_plan* plan = new (std::nothrow) cf_plan();
     if (!plan) return cf_set_error(ctx, CF_ENOMEM, "plan allocation");
     plan->n_users = n_users;
+    plan->h_item_off.assign(item_off, item_off + n_users + 1);
     // Bucket by emax = ceil(k/16); within a bucket, largest k first (cost ~ k^3).
     // by[0]: the spill path (CF_MAX_K < k <= CF_SPILL_MAX_K), launched first.
     std::vector<std::vector<uint32_t>> by(13);
@@ -304,6 +310,7 @@ void cf_plan_destroy(cf_plan* plan) {
     if (plan->d_order) (void)hipFree(plan->d_order);
     if (plan->d_tri_roff) (void)hipFree(plan->d_tri_roff);
     if (plan->d_tri_hoff) (void)hipFree(plan->d_tri_hoff);
+    cf_plan_destroy(plan->prefix);
     delete plan;
 }
 
@@ -385,6 +392,30 @@ int cf_predict_run_f32(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_
     CF_TRY(set_device(ctx));
     return cf_launch_predict<float>(ctx, plan, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off,
                                     d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, nullptr, (hipStream_t)stream);
+}
+
+int cf_step_run(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,
+                const float* d_ratings, const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals,
+                float* d_evecs, int sig_mode, float* d_mse, int32_t* d_kk, double* d_pred, void* stream) {
+    if (!ctx || !plan) return cf_set_error(ctx, CF_EINVAL, "cf_step_run: null");
+    if (sig_mode != CF_SIGS_OWN && sig_mode != CF_SIGS_COMPAT) return cf_set_error(ctx, CF_EINVAL, "cf_step_run: bad sig_mode");
+    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_step_run: no item graph uploaded");
+    CF_TRY(set_device(ctx));
+    return cf_launch_step(ctx, plan, d_item_off, d_items, d_ratings, d_evec_off, d_m, d_sigs, d_evals, d_evecs,
+                          sig_mode, d_mse, d_kk, d_pred, (hipStream_t)stream);
+}
+
+int cf_step_timing(cf_ctx* ctx, float* eigen_ms, float* total_ms) {
+    if (!ctx) return CF_EINVAL;
+    if (!ctx->step_time_ev[2]) return cf_set_error(ctx, CF_ESTATE, "cf_step_timing: no cf_step_run yet");
+    CF_TRY(set_device(ctx));
+    CF_HIP_CHECK(ctx, hipEventSynchronize(ctx->step_time_ev[2]));
+    float a = 0.0f, b = 0.0f;
+    CF_HIP_CHECK(ctx, hipEventElapsedTime(&a, ctx->step_time_ev[0], ctx->step_time_ev[1]));
+    CF_HIP_CHECK(ctx, hipEventElapsedTime(&b, ctx->step_time_ev[0], ctx->step_time_ev[2]));
+    if (eigen_ms) *eigen_ms = a;
+    if (total_ms) *total_ms = b;
+    return CF_OK;
 }
 
 int cf_predict_precomp(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, const uint32_t* items,

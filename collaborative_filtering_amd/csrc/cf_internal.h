@@ -59,6 +59,12 @@ struct cf_ctx {
     static constexpr int kAuxStreams = 2;   // measured: 3 streams no faster at C2
     hipStream_t aux_stream[kAuxStreams] = {};
     hipEvent_t aux_event[kAuxStreams + 1] = {};
+    // fused step (cf_step_run): two predictor streams beside the two aux (eigen) streams, an
+    // event per eigen bucket, and timing events {start, eigen done, end}
+    hipStream_t step_stream[2] = {};
+    hipEvent_t step_bucket_ev[16] = {};
+    hipEvent_t step_sync_ev[4] = {};
+    hipEvent_t step_time_ev[3] = {};
     // graph filter (cf_graph_filter): device time of the last call's supersteps, its edges
     float filter_ms = 0.0f;
     uint64_t filter_nnz = 0;
@@ -102,6 +108,8 @@ struct cf_plan {
     uint32_t* d_order = nullptr;     // device copy
     std::vector<cf_bucket> buckets;
     uint32_t kmax = 0;
+    std::vector<uint64_t> h_item_off;   // host copy of the user offsets (cf_step_run's compat prefix)
+    cf_plan* prefix = nullptr;          // cf_step_run: plan of the users whose sigs form the compat table
 };
 
 int cf_set_error(cf_ctx* ctx, int code, const std::string& msg);
@@ -198,6 +206,12 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
                       double* d_pred, const uint8_t* d_row_sel, hipStream_t stream);
 
 // Predictor for the spill bucket (CF_MAX_K < k <= CF_SPILL_MAX_K), cf_predict_spill.hip.
+// cf_eigen_run + cf_predict_run_f32 with the predictor of each k-bucket started as soon as that
+// bucket's eigenpairs exist (cf_predict.hip).
+int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,
+                   const float* d_ratings, const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals,
+                   float* d_evecs, int sig_mode, float* d_mse, int32_t* d_kk, double* d_pred, hipStream_t stream);
+
 template <typename T>
 int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, const uint64_t* d_item_off,
                             const uint32_t* d_items, const float* d_ratings, const int32_t* d_m,

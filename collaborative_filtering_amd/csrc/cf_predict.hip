@@ -466,13 +466,15 @@ __global__ __launch_bounds__(kThreads, 2) void pred_basis_kernel(PredArgs<T> a, 
         double* Xf = Xb;   // the final basis
         int Lx = 0;        // 0: no basis (every rating of the user takes the dense path)
         if (Lq > 0) {
+            // the W-failure flag is cleared before the barrier that ends the Q product, so every
+            // thread reads it cleared below also when there is no complement (du == 0)
+            if (tid == 0) s_cnt[9] = 0;
             const auto tri_end = [&](int j0) { return min(Lq, j0 + 64); };
             block_gemm<true, false>(
                 k, Lq, [&](int i, int l) { return U[(size_t)i * m + l]; }, as_double,
                 [&](int l, int j) { return Gb[(size_t)l * lmax + j]; }, tri_T, tri_end, all_blocks,
                 [&](int i, int j, double v) { Xb[(size_t)i * ld + j] = v; }, stage);
             __syncthreads();
-            if (tid == 0) s_cnt[9] = 0;
             const int du = k - Lq;
             if (du > 0) {
                 // Omega(i, j) = +-1 from a hash of (user, i, j): deterministic per user
@@ -1280,6 +1282,145 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
             CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[i], ctx->aux_stream[i]));
             CF_HIP_CHECK(ctx, hipStreamWaitEvent(stream, ctx->aux_event[i], 0));
         }
+    return rc;
+}
+
+// Fused step: cf_eigen_run + cf_predict_run_f32 with per-bucket overlap.  Eigen buckets
+// alternate between the context's two aux streams (as cf_eigen_run); each records an event,
+// and the predictor chunks of that bucket start on the two predictor streams as soon as it
+// fires, so a bucket's prediction (fp64 MFMA, latency-bound) runs beside the next buckets'
+// Jacobi sweeps (fp32 VALU + LDS) instead of after all of them.  In compat mode every user's
+// w_lim reads the global sig table (the sigs of the first users, local_calc_precomp.cpp:414,
+// 437,440), so those users' eigen pass runs first on its own (a prefix plan; their bucket
+// later rewrites the same bits).  Events: step_time_ev = {start, eigen done, end}.
+int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,
+                   const float* d_ratings, const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals,
+                   float* d_evecs, int sig_mode, float* d_mse, int32_t* d_kk, double* d_pred, hipStream_t stream) {
+    if (ctx->eigen_method != CF_EIGEN_JACOBI || ctx->d_stats || ctx->d_phase || plan->buckets.size() > 16) {
+        // diagnostics / the tridiagonal solver: the two stages one after the other
+        CF_TRY(cf_launch_eigen(ctx, plan, d_item_off, d_items, d_evec_off, d_m, d_sigs, d_evals, d_evecs, stream));
+        return cf_launch_predict<float>(ctx, plan, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off, d_evecs,
+                                        d_sigs, sig_mode, d_mse, d_kk, d_pred, nullptr, stream);
+    }
+    if (!ctx->aux_stream[0])
+        for (int i = 0; i < cf_ctx::kAuxStreams; ++i) {
+            CF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->aux_stream[i], hipStreamNonBlocking));
+            CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->aux_event[i], hipEventDisableTiming));
+        }
+    if (!ctx->aux_event[cf_ctx::kAuxStreams])
+        CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->aux_event[cf_ctx::kAuxStreams], hipEventDisableTiming));
+    if (!ctx->step_stream[0]) {
+        for (hipStream_t& st : ctx->step_stream) CF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        for (hipEvent_t& e : ctx->step_bucket_ev) CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (hipEvent_t& e : ctx->step_sync_ev) CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (hipEvent_t& e : ctx->step_time_ev) CF_HIP_CHECK(ctx, hipEventCreate(&e));
+    }
+    hipStream_t* es = ctx->aux_stream;   // eigen
+    hipStream_t* ps = ctx->step_stream;  // predict
+    // compat prefix: the users whose sigs cover rows [0, kmax) of the concatenated table
+    cf_plan* pre = nullptr;
+    if (sig_mode == CF_SIGS_COMPAT && plan->n_users) {
+        if (!plan->prefix) {
+            uint32_t j = 0;
+            while (j < plan->n_users && plan->h_item_off[j] < plan->kmax) ++j;
+            CF_TRY(cf_plan_create(ctx, j, plan->h_item_off.data(), &const_cast<cf_plan*>(plan)->prefix));
+        }
+        pre = plan->prefix;
+    }
+    PredArgs<float> args{};
+    args.order = plan->d_order;
+    args.item_off = d_item_off;
+    args.items = d_items;
+    args.ratings = d_ratings;
+    args.m = d_m;
+    args.evals = d_evals;
+    args.evec_off = d_evec_off;
+    args.evecs = d_evecs;
+    args.sigtab = d_sigs;
+    args.sig_mode = sig_mode;
+    args.graph = ctx->d_graph;
+    args.n_items = ctx->n_items;
+    args.mse = d_mse;
+    args.kk = d_kk;
+    args.pred = d_pred;
+    size_t need = 0;
+    for (const cf_bucket& b : plan->buckets)
+        if (b.count && b.emax != kSpillBucket)
+            need = std::max(need, (size_t)std::min(b.count, kChunk) *
+                                      slot_layout(std::max<int>(2, 16 * b.emax)).stride * sizeof(double));
+    if (need * 2 > ctx->scratch_bytes) {
+        if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+        ctx->d_scratch = nullptr;
+        ctx->scratch_bytes = 0;
+        CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_scratch, need * 2));
+        ctx->scratch_bytes = need * 2;
+    }
+    // fork every stream from the caller's
+    CF_HIP_CHECK(ctx, hipEventRecord(ctx->step_time_ev[0], stream));
+    CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[cf_ctx::kAuxStreams], stream));
+    for (int i = 0; i < 2; ++i) {
+        CF_HIP_CHECK(ctx, hipStreamWaitEvent(es[i], ctx->aux_event[cf_ctx::kAuxStreams], 0));
+        CF_HIP_CHECK(ctx, hipStreamWaitEvent(ps[i], ctx->aux_event[cf_ctx::kAuxStreams], 0));
+    }
+    int rc = CF_OK;
+    if (pre) {   // prefix users first, then every predictor stream waits for their sigs
+        rc = cf_launch_eigen(ctx, pre, d_item_off, d_items, d_evec_off, d_m, d_sigs, d_evals, d_evecs, ps[0]);
+        if (rc == CF_OK) CF_HIP_CHECK(ctx, hipEventRecord(ctx->step_sync_ev[0], ps[0]));
+        if (rc == CF_OK) CF_HIP_CHECK(ctx, hipStreamWaitEvent(ps[1], ctx->step_sync_ev[0], 0));
+    }
+    int nb = 0, nc = 0;
+    for (size_t bi = 0; bi < plan->buckets.size() && rc == CF_OK; ++bi) {
+        const cf_bucket& b = plan->buckets[bi];
+        if (b.count == 0) continue;
+        hipStream_t est = es[nb++ % 2];
+        if (b.emax == kSpillBucket) {   // spill eigen alone first (it fills the chip), as cf_launch_eigen
+            rc = cf_launch_eigen_spill(ctx, plan, b, d_item_off, d_items, d_evec_off, d_m, d_sigs, d_evals, d_evecs,
+                                       es[0]);
+            if (rc != CF_OK) break;
+            CF_HIP_CHECK(ctx, hipEventRecord(ctx->step_bucket_ev[bi], es[0]));
+            CF_HIP_CHECK(ctx, hipStreamWaitEvent(es[1], ctx->step_bucket_ev[bi], 0));
+            CF_HIP_CHECK(ctx, hipStreamWaitEvent(ps[0], ctx->step_bucket_ev[bi], 0));
+            rc = cf_launch_predict_spill<float>(ctx, plan, b, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off,
+                                                d_evecs, d_sigs, sig_mode, d_mse, d_kk, d_pred, nullptr, ps[0]);
+            continue;
+        }
+        rc = cf_launch_eigen_flagged(ctx, plan, b.emax, b.first, b.count, nullptr, d_item_off, d_items, d_evec_off,
+                                     d_m, d_sigs, d_evals, d_evecs, est);
+        if (rc != CF_OK) break;
+        CF_HIP_CHECK(ctx, hipEventRecord(ctx->step_bucket_ev[bi], est));
+        size_t rating_lds = 0;
+        rc = setup_bucket<float>(ctx, args, std::max<int>(2, 16 * b.emax), rating_lds);
+        if (rc != CF_OK) break;
+        bool waited[2] = {false, false};
+        for (uint32_t c0 = 0; c0 < b.count; c0 += kChunk) {
+            const uint32_t cnt = std::min(kChunk, b.count - c0);
+            const int si = nc++ % 2;
+            if (!waited[si]) {
+                CF_HIP_CHECK(ctx, hipStreamWaitEvent(ps[si], ctx->step_bucket_ev[bi], 0));
+                waited[si] = true;
+            }
+            args.slots = reinterpret_cast<double*>(static_cast<char*>(ctx->d_scratch) + si * need);
+            hipLaunchKernelGGL(pred_basis_kernel<float>, dim3(cnt), dim3(kThreads), basis_lds(), ps[si], args,
+                               b.first + c0, cnt);
+            hipLaunchKernelGGL(pred_rating_kernel<float>, dim3(cnt), dim3(kThreads), rating_lds, ps[si], args,
+                               b.first + c0, cnt);
+            if (hipGetLastError() != hipSuccess) {
+                rc = cf_set_error(ctx, CF_EHIP, "step predict launch failed");
+                break;
+            }
+        }
+    }
+    // join: eigen streams -> "eigen done" event on the caller, then the predictor streams
+    for (int i = 0; i < 2; ++i) {
+        CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[i], es[i]));
+        CF_HIP_CHECK(ctx, hipStreamWaitEvent(stream, ctx->aux_event[i], 0));
+    }
+    CF_HIP_CHECK(ctx, hipEventRecord(ctx->step_time_ev[1], stream));
+    for (int i = 0; i < 2; ++i) {
+        CF_HIP_CHECK(ctx, hipEventRecord(ctx->step_sync_ev[1 + i], ps[i]));
+        CF_HIP_CHECK(ctx, hipStreamWaitEvent(stream, ctx->step_sync_ev[1 + i], 0));
+    }
+    CF_HIP_CHECK(ctx, hipEventRecord(ctx->step_time_ev[2], stream));
     return rc;
 }
 

@@ -199,6 +199,18 @@ int cf_predict_run_f32(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_
                        const float* d_evecs, const float* d_sigtab, int sig_mode,
                        float* d_mse, int32_t* d_kk, double* d_pred, void* stream);
 
+/* ---- fused step ------------------------------------------------------------------
+ * cf_eigen_run followed by cf_predict_run_f32 on the SAME outputs (sigtab = d_sigs), with the
+ * predictor of every k-bucket started as soon as that bucket's eigenpairs exist, on streams of
+ * its own, so prediction overlaps the remaining eigen buckets.  Outputs are identical to the
+ * two calls in sequence.  Ordered on `stream` like the *_run calls.  cf_step_timing: device
+ * time of the last cf_step_run from its start to the last eigen bucket and to its end. */
+int cf_step_run(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,
+                const float* d_ratings, const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs,
+                float* d_evals, float* d_evecs, int sig_mode, float* d_mse, int32_t* d_kk,
+                double* d_pred, void* stream);
+int cf_step_timing(cf_ctx* ctx, float* eigen_ms, float* total_ms);
+
 /* ---- kNN stage ------------------------------------------------------------------
  * knn2 weights_calc (knn2.cpp:127-164): for every item pair a != b over the users
  * present in both train lists, cnt > cnt_min ? w = num/(sqrtf(den1)*sqrtf(den2)) : 0,

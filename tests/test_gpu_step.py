@@ -1,0 +1,48 @@
+"""cf_step_run (eigen + predictor with per-bucket overlap on separate streams) writes exactly
+what cf_eigen_run followed by cf_predict_run_f32 writes: same kernels, same inputs, only the
+launch order across streams differs.  Both w_lim modes; users in every LDS bucket plus spill
+users (k > 192) so the spill eigen / predictor run inside the fused schedule too."""
+import numpy as np
+import pytest
+
+from collaborative_filtering_amd import synth
+from collaborative_filtering_amd.api import CF_SIGS_COMPAT, CF_SIGS_OWN, evec_offsets
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("sig_mode", [CF_SIGS_COMPAT, CF_SIGS_OWN])
+def test_step_run_equals_sequential(gpu_ctx, sig_mode):
+    torch = pytest.importorskip("torch")
+    seed, n_items = 2026101502, 2000
+    k = synth.degrees(seed, 6000, k_median=90.0, sigma=0.6, kmin=2, kmax=180)
+    k[[5, 777, 4000]] = [260, 201, 230]          # spill users
+    off, items, rats = synth.user_items(seed, k, n_items, threads=8)
+    W = synth.graph_model(seed, n_items, threads=8)
+    gpu_ctx.upload_graph_dense(W)
+    plan = gpu_ctx.plan(off)
+    dev = torch.device("cuda")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    eoff, ne = evec_offsets(off)
+    n, U = int(off[-1]), len(k)
+
+    def fresh():
+        return dict(m=torch.zeros(U, dtype=torch.int32, device=dev), sigs=torch.zeros(n, device=dev),
+                    evals=torch.zeros(n, device=dev), evecs=torch.zeros(ne, device=dev),
+                    mse=torch.zeros(n, device=dev), kk=torch.zeros(n, dtype=torch.int32, device=dev),
+                    pred=torch.zeros(n, dtype=torch.float64, device=dev))
+
+    d_off, d_items, d_rat, d_eoff = T(off.view(np.int64)), T(items.view(np.int32)), T(rats), T(eoff.view(np.int64))
+    a, b = fresh(), fresh()
+    plan.eigen_run(d_off, d_items, d_eoff, a["m"], a["sigs"], a["evals"], a["evecs"])
+    plan.predict_run(d_off, d_items, d_rat, a["m"], a["evals"], d_eoff, a["evecs"], a["sigs"], sig_mode,
+                     a["mse"], a["kk"], a["pred"])
+    plan.step_run(d_off, d_items, d_rat, d_eoff, b["m"], b["sigs"], b["evals"], b["evecs"], sig_mode,
+                  b["mse"], b["kk"], b["pred"])
+    eig_ms, tot_ms = plan.step_timing()
+    torch.cuda.synchronize()
+    assert 0 < eig_ms <= tot_ms
+    for key in a:
+        x, y = a[key].cpu().numpy(), b[key].cpu().numpy()
+        assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), key   # bitwise, NaNs included
+    plan.close()
