@@ -46,3 +46,35 @@ def test_step_run_equals_sequential(gpu_ctx, sig_mode):
         x, y = a[key].cpu().numpy(), b[key].cpu().numpy()
         assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), key   # bitwise, NaNs included
     plan.close()
+
+
+def test_pipeline_is_deterministic(gpu_ctx):
+    """Three runs of cf_eigen_run -> cf_predict_run_f32 on fresh buffers write the same bits.
+    (A barrier race in the predictor's basis kernel once corrupted ~0.1% of the k >= 100 users
+    differently from run to run; this would have caught it.)"""
+    torch = pytest.importorskip("torch")
+    seed, n_items = 2026101502, 2000
+    k = synth.degrees(seed, 6000, k_median=90.0, sigma=0.6, kmin=2, kmax=180)
+    k[[11, 1234, 5000]] = [240, 199, 310]          # spill users (persistent-workgroup kernels)
+    off, items, rats = synth.user_items(seed, k, n_items, threads=8)
+    gpu_ctx.upload_graph_dense(synth.graph_model(seed, n_items, threads=8))
+    plan = gpu_ctx.plan(off)
+    dev = torch.device("cuda")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    eoff, ne = evec_offsets(off)
+    n, U = int(off[-1]), len(k)
+    d_off, d_items, d_rat, d_eoff = T(off.view(np.int64)), T(items.view(np.int32)), T(rats), T(eoff.view(np.int64))
+    runs = []
+    for _ in range(3):
+        o = dict(m=torch.zeros(U, dtype=torch.int32, device=dev), sigs=torch.zeros(n, device=dev),
+                 evals=torch.zeros(n, device=dev), evecs=torch.zeros(ne, device=dev),
+                 mse=torch.zeros(n, device=dev), kk=torch.zeros(n, dtype=torch.int32, device=dev))
+        plan.eigen_run(d_off, d_items, d_eoff, o["m"], o["sigs"], o["evals"], o["evecs"])
+        plan.predict_run(d_off, d_items, d_rat, o["m"], o["evals"], d_eoff, o["evecs"], o["sigs"], CF_SIGS_OWN,
+                         o["mse"], o["kk"])
+        torch.cuda.synchronize()
+        runs.append({key: v.cpu().numpy() for key, v in o.items()})
+    for r in runs[1:]:
+        for key in r:
+            assert np.array_equal(r[key].view(np.uint8), runs[0][key].view(np.uint8)), key
+    plan.close()
