@@ -18,6 +18,12 @@ for s in $steps; do
     timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- \
       python3 bench.py --steps 3 --warmup 1 --profile-steps-only > gpurun_out/prof_$tag.log 2>&1 || { echo PROF_FAILED; tail -n 20 gpurun_out/prof_$tag.log; exit 1; }
     tail -n 1 gpurun_out/prof_$tag.log | cut -c1-300 ;;
+  dist)
+    # N = 2 rehearsal on one GPU: two ranks share the device over gloo (the driver's 8-GPU runs use RCCL)
+    CF_DIST_BACKEND=gloo timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+      --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 2 --warmup 1 --users 200000 \
+      --no-cpu-baseline --pmc off > gpurun_out/dist2_$tag.log 2>&1 || { echo DIST_FAILED; tail -n 30 gpurun_out/dist2_$tag.log; exit 1; }
+    grep '"metric"' gpurun_out/dist2_$tag.log | cut -c1-400 ;;
   esac
 done
 echo ROUND_OK
