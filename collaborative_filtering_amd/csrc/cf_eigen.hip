@@ -33,8 +33,13 @@ namespace {
 constexpr int kGroup = 8;   // lanes per column pair (half a DPP row)
 // Stopping rule: iterate while a sweep made a rotation with |gamma| > kSigRot * tol * sqrt(al be)
 // (rotations above tol are always applied).  A numpy model of this kernel on C2 users kept the
-// same eigenvalue error and final off-diagonal level with 1-2 fewer sweeps (of ~10) at 4.
-constexpr float kSigRot2 = 16.0f;
+// same eigenvalue error and final off-diagonal level with 1-2 fewer sweeps (of ~10) at
+// kSigRot = 4..16; on the GPU (C2 mix) 4 / 8 / 16 gave 8.47 / 8.22 / 7.95 sweeps with the same
+// parity (profiles/r02/eigen_ab_v4_kappa.txt).  kSigRot2 = kSigRot^2 = 256.
+#ifndef CF_EIGEN_SIGROT2
+#define CF_EIGEN_SIGROT2 256.0f
+#endif
+constexpr float kSigRot2 = CF_EIGEN_SIGROT2;
 
 using f2 = __attribute__((ext_vector_type(2))) float;
 // A column read as volatile 8-byte loads: plain loads 64 B apart get fused into

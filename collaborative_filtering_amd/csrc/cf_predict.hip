@@ -413,8 +413,8 @@ __global__ __launch_bounds__(kThreads, 2) void pred_basis_kernel(PredArgs<T> a, 
             s_order[rank] = i;
         }
 
-        // Gbar = U^T U over the columns [0, Lu), all k rows: full copy in Gb (the dense
-        // path's complement form reads it); max |Gbar - I| (non-negative floats order
+        // Gbar = U^T U over the columns [0, Lu), all k rows: its upper triangle in Gb (the
+        // dense path's complement form reads it symmetrically); max |Gbar - I| (non-negative floats order
         // as their bit patterns) decides whether this user gets a basis.  All products
         // of this phase are block_gemm calls staged through A (free until the fast path).
         double* stage = A;
@@ -432,8 +432,7 @@ __global__ __launch_bounds__(kThreads, 2) void pred_basis_kernel(PredArgs<T> a, 
             [&](int l, int j) { return U[(size_t)l * m + j]; }, as_double, [&](int) { return k; }, lower_blocks,
             [&](int i, int j, double v) {
                 if (j > i) return;
-                Gb[(size_t)i * lmax + j] = v;
-                Gb[(size_t)j * lmax + i] = v;
+                Gb[(size_t)j * lmax + i] = v;   // upper triangle only: T1 reads G(l, j), l <= j
                 const float d = (float)fabs(v - (i == j ? 1.0 : 0.0));
                 dev = fmaxf(dev, d == d ? d : 3.0e38f);
             },
@@ -1067,7 +1066,8 @@ __global__ __launch_bounds__(kThreads, 2) void pred_rating_kernel(PredArgs<T> a,
                             const int ia = 4 * ta + x, ib = 4 * tb + y;
                             if (ia < L && ib <= ia)
                                 AW[tri(ia, ib)] = use_complement
-                                                     ? Gb[(size_t)ca[x] * lmax + cb[y]] - acc[x][y]
+                                                     ? Gb[(size_t)min(ca[x], cb[y]) * lmax + max(ca[x], cb[y])] -
+                                                           acc[x][y]
                                                      : acc[x][y];
                         }
                 }
