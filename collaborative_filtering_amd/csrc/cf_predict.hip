@@ -76,7 +76,7 @@ constexpr float kOrthoDone = 1e-8f;
 // base; the int / u64 arrays live in double-sized cells.
 struct SlotOff {
     size_t stride;   // doubles per slot
-    int gb, x, q1, ap, gx, hx, misc, cmask, lim, order, cpos;
+    int gb, x, q1, ap, gx, hx, misc, cmask, lim, order, cpos, pmask;
 };
 
 template <typename T>
@@ -441,16 +441,29 @@ __global__ __launch_bounds__(kThreads, 2) void pred_basis_kernel(PredArgs<T> a, 
         if (lane == 0) atomicMax(&s_cnt[6], __float_as_int(dev));
         __syncthreads();
         if (a.phase_cycles && tid == 0) ph_acc[6] += __builtin_amdgcn_s_memtime() - tg0;
-        for (int j = tid; j < Lu; j += kThreads) {
-            int cnt = 0;
-            for (int i0 = 0; i0 < k; i0 += 8) {
-                double v[8];
+        // per column j < Lu: the rows with U(i, j) >= 1e-4 as a 3-word mask (the rating
+        // kernel's column filter is then P_j & ~Cbar == 0 per column) and their count
+        {
+            uint64_t* pm_g = reinterpret_cast<uint64_t*>(slot + a.so.pmask);
+            for (int j = tid; j < Lu; j += kThreads) {
+                int cnt = 0;
 #pragma unroll
-                for (int t = 0; t < 8; ++t) v[t] = (double)U[(size_t)min(i0 + t, k - 1) * m + j];
+                for (int w = 0; w < 3; ++w) {
+                    uint64_t bits = 0;
+                    const int iend = min(k, 64 * w + 64);
+                    for (int i0 = 64 * w; i0 < iend; i0 += 8) {
+                        double v[8];
 #pragma unroll
-                for (int t = 0; t < 8; ++t) cnt += (i0 + t < k) && v[t] >= 0.0001;
+                        for (int t = 0; t < 8; ++t) v[t] = (double)U[(size_t)min(i0 + t, k - 1) * m + j];
+#pragma unroll
+                        for (int t = 0; t < 8; ++t)
+                            if (i0 + t < iend && v[t] >= 0.0001) bits |= 1ull << (i0 + t - 64 * w);
+                    }
+                    pm_g[3 * j + w] = bits;
+                    cnt += __popcll(bits);
+                }
+                s_cpos[j] = cnt;
             }
-            s_cpos[j] = cnt;
         }
         __syncthreads();
         const int Lq = (__int_as_float(s_cnt[6]) <= (float)kOrthoMax) ? Lu : 0;
@@ -642,6 +655,7 @@ __global__ __launch_bounds__(kThreads, 2) void pred_rating_kernel(PredArgs<T> a,
     uint64_t* s_cmask = reinterpret_cast<uint64_t*>(s_cnt + 12);
     int* s_order = reinterpret_cast<int*>(s_cmask + 3 * CF_MAX_K);
     int* s_cb = s_order + CF_MAX_K;                        // kWaves x CF_MAX_K
+    uint64_t* s_pmask = reinterpret_cast<uint64_t*>(s_cb + kWaves * CF_MAX_K);   // 3 x CF_MAX_K
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -679,6 +693,8 @@ __global__ __launch_bounds__(kThreads, 2) void pred_rating_kernel(PredArgs<T> a,
             }
             for (int i = tid; i < 3 * k; i += kThreads) s_cmask[i] = cm_g[i];
             for (int j = tid; j < min(m, k + 2); j += kThreads) s_cpos[j] = j < Lq ? cpos_g[j] : 0;
+            const uint64_t* pm_g = reinterpret_cast<const uint64_t*>(slot + a.so.pmask);
+            for (int i = tid; i < 3 * min(m, k + 2); i += kThreads) s_pmask[i] = i < 3 * Lq ? pm_g[i] : 0ull;
             if (tid == 0) {
                 s_misc[1] = misc[0];
                 s_cnt[7] = 0;
@@ -735,14 +751,9 @@ __global__ __launch_bounds__(kThreads, 2) void pred_rating_kernel(PredArgs<T> a,
                     // column j < lim is dropped (:284-304) iff every row with
                     // U(i, j) >= 1e-4 lies in Cbar
                     bool drop = false;
-                    for (int j = lane; j < lim; j += 64) {
-                        const int cp = s_cpos[j];
-                        if (cp <= nc) {
-                            int hit = 0;
-                            for (int q = 0; q < nc; ++q) hit += (double)U[(size_t)cb[q] * m + j] >= 0.0001;
-                            drop |= hit == cp;
-                        }
-                    }
+                    const uint64_t c0 = ~s_cmask[3 * r], c1 = ~s_cmask[3 * r + 1], c2 = ~s_cmask[3 * r + 2];
+                    for (int j = lane; j < lim; j += 64)
+                        drop |= ((s_pmask[3 * j] & c0) | (s_pmask[3 * j + 1] & c1) | (s_pmask[3 * j + 2] & c2)) == 0ull;
                     slow = __ballot(drop) != 0ull;
                 }
                 if (slow) {
@@ -1147,6 +1158,7 @@ inline SlotOff slot_layout(int lmax) {
     so.lim = (int)o; o += (lmax + 1) / 2;                    // ints, two per cell
     so.order = (int)o; o += (lmax + 1) / 2;
     so.cpos = (int)o; o += (lmax + 1) / 2;
+    so.pmask = (int)o; o += 3 * (size_t)lmax;                 // u64 per cell
     so.stride = (o + 15) & ~(size_t)15;                      // 128-byte aligned slots
     return so;
 }
@@ -1157,7 +1169,8 @@ inline size_t basis_lds() {
 inline size_t rating_lds_fixed() {
     return sizeof(double) * (4 + 2 * CF_MAX_K) +                                      // s_misc, s_gx, s_hx
            CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 6 * sizeof(int)) + 12 * sizeof(int) +
-           CF_MAX_K * (3 * sizeof(uint64_t) + sizeof(int)) + kWaves * CF_MAX_K * sizeof(int);   // cmask, order, cb
+           CF_MAX_K * (3 * sizeof(uint64_t) + sizeof(int)) + kWaves * CF_MAX_K * sizeof(int) +   // cmask, order, cb
+           3 * CF_MAX_K * sizeof(uint64_t);                                                   // pmask
 }
 
 // Launch geometry of a bucket (everything but the chunk).
