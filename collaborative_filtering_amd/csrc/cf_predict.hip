@@ -632,8 +632,12 @@ __global__ __launch_bounds__(kThreads, 2) void pred_basis_kernel(PredArgs<T> a, 
 
 // ---- kernel 2: per user of a chunk, every rating from the slot: the fast path (one wave per
 // rating) and the dense path (block-wide) -------------------------------------------------
+#ifndef CF_PRED_RATING_OCC
+#define CF_PRED_RATING_OCC 2   // rating-kernel blocks per CU (registers and the LDS budget below)
+#endif
+constexpr size_t kRatingLds = 163840 / CF_PRED_RATING_OCC;
 template <typename T>
-__global__ __launch_bounds__(kThreads, 2) void pred_rating_kernel(PredArgs<T> a, uint32_t first, uint32_t count) {
+__global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_rating_kernel(PredArgs<T> a, uint32_t first, uint32_t count) {
     extern __shared__ double dsm[];
     const int lmax = a.lmax;
     // A: the factorisation region: the per-wave fast-path scratch, then (dense path) the
@@ -1185,10 +1189,10 @@ int setup_bucket(cf_ctx* ctx, PredArgs<T>& args, int lmax, size_t& rating_lds) {
     // well, else the slot's HBM region AP.
     const auto per_wave = [&](int n) { return fast_tri(n) + 2 * lmax; };   // + y (nc) and g (d)
     int nmax = std::min(kNsysMax, lmax);
-    while (nmax > 8 && sizeof(double) * (size_t)(kWaves * per_wave(nmax)) + lds_fixed > 81920) --nmax;
+    while (nmax > 8 && sizeof(double) * (size_t)(kWaves * per_wave(nmax)) + lds_fixed > kRatingLds) --nmax;
     args.nmax = nmax;
     args.ew = per_wave(nmax);
-    args.big_lds = sizeof(double) * (size_t)std::max(big, kWaves * args.ew) + lds_fixed <= 81920;
+    args.big_lds = sizeof(double) * (size_t)std::max(big, kWaves * args.ew) + lds_fixed <= kRatingLds;
     args.a_elems = std::max({args.big_lds ? big : 0, kWaves * args.ew, 2 * lmax});
     args.so = slot_layout(lmax);
     rating_lds = sizeof(double) * (size_t)args.a_elems + lds_fixed;

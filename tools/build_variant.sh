@@ -8,6 +8,6 @@ for f in collaborative_filtering_amd/csrc/*.hip; do
   b=$(basename $f .hip)
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Icollaborative_filtering_amd/csrc "$@" -c $f -o $out/$b.o &
 done
-wait
+wait || exit 1
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o collaborative_filtering_amd/variants/libcf_$name.so $out/*.o
 echo built collaborative_filtering_amd/variants/libcf_$name.so
