@@ -71,6 +71,9 @@ constexpr double kPivMin = 1e-10;
 // ~1e-16 for any U within kOrthoMax of orthonormal
 constexpr double kOrthoMax = 1e-2;
 constexpr float kOrthoDone = 1e-8f;
+#ifndef CF_PRED_BASIS_OCC
+#define CF_PRED_BASIS_OCC 2    // basis-kernel blocks per CU (registers; its LDS is ~30 KB)
+#endif
 
 // Per-user slot of a chunk (basis kernel -> rating kernel), offsets in doubles from the slot
 // base; the int / u64 arrays live in double-sized cells.
@@ -318,7 +321,7 @@ __device__ void wave_gram(int nt, int inner, LOAD load, double* E) {
 // ---- kernel 1: per user of a chunk, lim / complement masks / order of the ratings, Gbar,
 // the basis X = [Q | W] and X^T r, X^T 1, into the user's slot ---------------------------
 template <typename T>
-__global__ __launch_bounds__(kThreads, 2) void pred_basis_kernel(PredArgs<T> a, uint32_t first, uint32_t count) {
+__global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel(PredArgs<T> a, uint32_t first, uint32_t count) {
     extern __shared__ double dsm[];
     const int lmax = a.lmax;
     double* A = dsm;                                       // block_gemm staging
