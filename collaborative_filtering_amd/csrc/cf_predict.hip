@@ -443,7 +443,9 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
         for (int off = 32; off >= 1; off >>= 1) dev = fmaxf(dev, __shfl_xor(dev, off));
         if (lane == 0) atomicMax(&s_cnt[6], __float_as_int(dev));
         __syncthreads();
+#ifndef CF_PRED_BASIS_PROBE
         if (a.phase_cycles && tid == 0) ph_acc[6] += __builtin_amdgcn_s_memtime() - tg0;
+#endif
         // per column j < Lu: the rows with U(i, j) >= 1e-4 as a 3-word mask (the rating
         // kernel's column filter is then P_j & ~Cbar == 0 per column) and their count
         {
@@ -490,6 +492,9 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
                 [&](int l, int j) { return Gb[(size_t)l * lmax + j]; }, tri_T, tri_end, all_blocks,
                 [&](int i, int j, double v) { Xb[(size_t)i * ld + j] = v; }, stage);
             __syncthreads();
+#ifdef CF_PRED_BASIS_PROBE
+            const unsigned long long tw0 = (a.phase_cycles && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
+#endif
             const int du = k - Lq;
             if (du > 0) {
                 // Omega(i, j) = +-1 from a hash of (user, i, j): deterministic per user
@@ -544,6 +549,10 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
                 if (__syncthreads_or(fail) && tid == 0) s_cnt[9] = 1;
                 __syncthreads();
             }
+#ifdef CF_PRED_BASIS_PROBE   // diagnostics: slot 7 = complement build, slot 6 = joint steps
+            if (a.phase_cycles && tid == 0) ph_acc[7] += __builtin_amdgcn_s_memtime() - tw0;
+            const unsigned long long tj0 = (a.phase_cycles && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
+#endif
             // joint T steps on X (k columns): X^T X packed in AP, X <- X T (ping-pong Xb/Q1)
             double* Xs = Xb;
             double* Xd = Q1;
@@ -584,6 +593,9 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
                 }
             }
             Xf = Xs;
+#ifdef CF_PRED_BASIS_PROBE
+            if (a.phase_cycles && tid == 0) ph_acc[6] += __builtin_amdgcn_s_memtime() - tj0;
+#endif
         }
         // X^T r and X^T 1, the rating-level arrays and the flags into the slot
         double* s_gx = slot + a.so.gx;
