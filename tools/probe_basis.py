@@ -1,7 +1,8 @@
 """Predictor basis-kernel sub-phases on the config-4 shard (run with CF_MI355X_LIB = a build with
 -DCF_PRED_BASIS_PROBE=1): the share of the basis phase spent building the complement W (Omega
 products, Cholesky-QR, the row solve) and in the joint orthogonalisation step."""
-import runpy, sys
+import os, runpy, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.argv = ["probe_c4.py", sys.argv[1] if len(sys.argv) > 1 else "125000"]
 import collaborative_filtering_amd.api as api
 orig = api.Context.debug_phases
