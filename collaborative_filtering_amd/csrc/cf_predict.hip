@@ -527,21 +527,51 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
                     [&](int l, int j) { return Xb[(size_t)l * ld + Lq + j]; }, as_double, [&](int) { return k; },
                     lower_blocks, [&](int i, int j, double v) { if (j <= i) AP[tri(i, j)] = v; }, stage);
                 __syncthreads();
-                ldlt_bordered<kThreads, 16>(AP, du, du);
+                // factor and solve with L in LDS when it fits the (now idle) GEMM staging
+                double* LP = AP;
+#ifndef CF_PRED_COMPLEMENT_GLOBAL
+                if (tri(du, 0) <= kStageElems) {
+                    LP = stage;
+                    for (int i = tid; i < tri(du, 0); i += kThreads) LP[i] = AP[i];
+                    __syncthreads();
+                }
+#endif
+                ldlt_bordered<kThreads, 16>(LP, du, du);
                 // W row i = D^-1/2 L^-1 y_i, in place (each thread its own rows)
                 double dmax = 0.0;
-                for (int j = 0; j < du; ++j) dmax = fmax(dmax, AP[tri(j, j)]);
+                for (int j = 0; j < du; ++j) dmax = fmax(dmax, LP[tri(j, j)]);
                 bool fail = false;
                 for (int i = tid; i < k; i += kThreads) {
                     double* xi = Xb + (size_t)i * ld + Lq;
-                    for (int j = 1; j < du; ++j) {
-                        const double* Lj = AP + tri(j, 0);
-                        double z = xi[j];
-                        for (int t = 0; t < j; ++t) z = fma(-Lj[t], xi[t], z);
-                        xi[j] = z;
+                    // forward substitution in 16-column panels held in registers: the solved
+                    // entries t < p0 are read once per panel (independent loads, 16 independent
+                    // accumulators) instead of once per column in one dependent chain; each
+                    // entry still accumulates t = 0 .. j-1 in order (bit-identical results)
+                    for (int p0 = 0; p0 < du; p0 += 16) {
+                        const int b = min(16, du - p0);
+                        double acc[16];
+                        int rb[16];
+#pragma unroll
+                        for (int q = 0; q < 16; ++q) {
+                            acc[q] = q < b ? xi[p0 + q] : 0.0;
+                            rb[q] = tri(p0 + min(q, b - 1), 0);
+                        }
+#pragma unroll 2
+                        for (int t = 0; t < p0; ++t) {
+                            const double xt = xi[t];
+#pragma unroll
+                            for (int q = 0; q < 16; ++q) acc[q] = fma(-LP[rb[q] + t], xt, acc[q]);
+                        }
+#pragma unroll
+                        for (int q = 1; q < 16; ++q)
+#pragma unroll
+                            for (int t = 0; t < q; ++t) acc[q] = fma(-LP[rb[q] + p0 + t], acc[t], acc[q]);
+#pragma unroll
+                        for (int q = 0; q < 16; ++q)
+                            if (q < b) xi[p0 + q] = acc[q];
                     }
                     for (int j = 0; j < du; ++j) {
-                        const double dj = AP[tri(j, j)];
+                        const double dj = LP[tri(j, j)];
                         fail |= !(dj > 1e-12 * dmax);
                         xi[j] = dj > 0.0 ? xi[j] / sqrt(dj) : 0.0;
                     }
