@@ -149,13 +149,17 @@ __device__ int block_compact(bool flag, int idx, int* out, int* s_cnt) {
 // whole block; the caller synchronises before reading C.
 constexpr int kStageLd = 80;                       // == 16 (mod 32): the four 16-lane row
                                                    // groups of a fragment read hit disjoint banks
-constexpr int kStageElems = 2 * 16 * kStageLd;
+constexpr int kStageBuf = 2 * 16 * kStageLd;        // one chunk: A then B, 16 x kStageLd each
+#ifdef CF_PRED_GEMM_SINGLE_BUFFER
+constexpr int kStageNbuf = 1;
+#else
+constexpr int kStageNbuf = 2;                       // chunks alternate buffers: one barrier each
+#endif
+constexpr int kStageElems = kStageNbuf * kStageBuf;
 using f64x4 = __attribute__((ext_vector_type(4))) double;
 template <bool A_LFAST, bool B_LFAST, class LA, class XA, class LB, class XB, class FK, class FW, class FO>
 __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK kend, FW want, FO out,
                            double* stage) {
-    double* As = stage;
-    double* Bs = stage + 16 * kStageLd;
     int tid = threadIdx.x;
     __asm__ volatile("" : "+v"(tid));   // per call: keeps the index math out of the user loop
     const int lane = tid & 63;
@@ -188,8 +192,13 @@ __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK ke
                     rb[t] = loadB(min(l0 + lb, K - 1), min(j0 + jb, N - 1));
                 }
             };
-            auto stage_chunk = [&](int l0, RA (&ra)[4], RB (&rb)[4]) {
-                __syncthreads();   // the previous chunk is consumed
+            // with two buffers, chunk c is written to buffer c & 1 after the barrier that
+            // published chunk c - 1, which every wave reaches only after its MFMAs on chunk
+            // c - 2 (the same buffer): one barrier per chunk
+            auto stage_chunk = [&](int l0, RA (&ra)[4], RB (&rb)[4], int b) {
+                double* As = stage + (kStageNbuf - 1) * b * kStageBuf;
+                double* Bs = As + 16 * kStageLd;
+                if (kStageNbuf == 1) __syncthreads();   // the previous chunk is consumed
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     const int e = tid + kThreads * t;
@@ -202,7 +211,9 @@ __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK ke
                 }
                 __syncthreads();
             };
-            auto mma_chunk = [&]() {
+            auto mma_chunk = [&](int b) {
+                const double* As = stage + (kStageNbuf - 1) * b * kStageBuf;
+                const double* Bs = As + 16 * kStageLd;
 #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) {
                     const int row = (4 * ks + (lane >> 4)) * kStageLd + (lane & 15);
@@ -222,15 +233,17 @@ __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK ke
             if (K > 0) fetch(0, ra0, rb0);
             if (K > 16) fetch(16, ra1, rb1);
             for (int l0 = 0; l0 < K; l0 += 32) {
-                stage_chunk(l0, ra0, rb0);
+                stage_chunk(l0, ra0, rb0, 0);
                 if (l0 + 32 < K) fetch(l0 + 32, ra0, rb0);
-                mma_chunk();
+                mma_chunk(0);
                 if (l0 + 16 < K) {
-                    stage_chunk(l0 + 16, ra1, rb1);
+                    stage_chunk(l0 + 16, ra1, rb1, 1);
                     if (l0 + 48 < K) fetch(l0 + 48, ra1, rb1);
-                    mma_chunk();
+                    mma_chunk(1);
                 }
             }
+            // the next output block restarts at buffer 0, which slower waves may still read
+            if (kStageNbuf == 2) __syncthreads();
 #pragma unroll
             for (int x = 0; x < 2; ++x)
 #pragma unroll
