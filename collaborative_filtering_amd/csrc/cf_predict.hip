@@ -72,7 +72,7 @@ constexpr double kPivMin = 1e-10;
 constexpr double kOrthoMax = 1e-2;
 constexpr float kOrthoDone = 1e-8f;
 #ifndef CF_PRED_BASIS_OCC
-#define CF_PRED_BASIS_OCC 2    // basis-kernel blocks per CU (registers; its LDS is ~30 KB)
+#define CF_PRED_BASIS_OCC 2    // basis-kernel blocks per CU (registers; its LDS is ~50 KB)
 #endif
 
 // Per-user slot of a chunk (basis kernel -> rating kernel), offsets in doubles from the slot
@@ -333,6 +333,10 @@ __device__ void wave_gram(int nt, int inner, LOAD load, double* E) {
 
 // ---- kernel 1: per user of a chunk, lim / complement masks / order of the ratings, Gbar,
 // the basis X = [Q | W] and X^T r, X^T 1, into the user's slot ---------------------------
+#ifndef CF_PRED_MASK_ROWS
+#define CF_PRED_MASK_ROWS 8
+#endif
+constexpr int kMaskRows = CF_PRED_MASK_ROWS;   // graph rows gathered per wave at once
 template <typename T>
 __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel(PredArgs<T> a, uint32_t first, uint32_t count) {
     extern __shared__ double dsm[];
@@ -375,12 +379,17 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
             s_rat[i] = a.ratings[base + i];
             // lim = first eigenvalue index above w_lim, clamped to [2, m] (:271-282)
             const double w_lim = (double)a.sigtab[a.sig_mode == CF_SIGS_COMPAT ? (uint64_t)i : base + i];
+            // eight evals per probe, so the LDS reads of a probe are in flight together
             int lim = m;
-            for (int j = 0; j < m; ++j)
-                if (A[j] > w_lim) {
-                    lim = j;
+            for (int j0 = 0; j0 < m; j0 += 8) {
+                unsigned above = 0;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) above |= (j0 + t < m && A[min(j0 + t, m - 1)] > w_lim) ? 1u << t : 0u;
+                if (above) {
+                    lim = j0 + __builtin_ctz(above);
                     break;
                 }
+            }
             lim = min(max(lim, 2), m);
             s_lim[i] = lim;
             atomicMax(&s_cnt[5], lim);
@@ -393,18 +402,18 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
         }
         __syncthreads();
         const int Lu = s_cnt[5];
-        // complement masks, four graph rows in flight per wave (unconditional clamped
+        // complement masks, kMaskRows graph rows in flight per wave (unconditional clamped
         // loads, see block_gemm), then nc of every row in s_slow (free until the fast path)
-        for (int r0 = 4 * wave; r0 < k; r0 += 4 * kWaves) {
-            float gv[4][3];
+        for (int r0 = kMaskRows * wave; r0 < k; r0 += kMaskRows * kWaves) {
+            float gv[kMaskRows][3];
 #pragma unroll
-            for (int x = 0; x < 4; ++x) {
+            for (int x = 0; x < kMaskRows; ++x) {
                 const float* nrow = a.graph + (size_t)s_item[min(r0 + x, k - 1)] * a.n_items;
 #pragma unroll
                 for (int t = 0; t < 3; ++t) gv[x][t] = nrow[s_item[min(64 * t + lane, k - 1)]];
             }
 #pragma unroll
-            for (int x = 0; x < 4; ++x) {
+            for (int x = 0; x < kMaskRows; ++x) {
                 int nc = 0;
 #pragma unroll
                 for (int t = 0; t < 3; ++t) {
@@ -469,12 +478,12 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
                 for (int w = 0; w < 3; ++w) {
                     uint64_t bits = 0;
                     const int iend = min(k, 64 * w + 64);
-                    for (int i0 = 64 * w; i0 < iend; i0 += 8) {
-                        double v[8];
+                    for (int i0 = 64 * w; i0 < iend; i0 += 16) {
+                        double v[16];
 #pragma unroll
-                        for (int t = 0; t < 8; ++t) v[t] = (double)U[(size_t)min(i0 + t, k - 1) * m + j];
+                        for (int t = 0; t < 16; ++t) v[t] = (double)U[(size_t)min(i0 + t, k - 1) * m + j];
 #pragma unroll
-                        for (int t = 0; t < 8; ++t)
+                        for (int t = 0; t < 16; ++t)
                             if (i0 + t < iend && v[t] >= 0.0001) bits |= 1ull << (i0 + t - 64 * w);
                     }
                     pm_g[3 * j + w] = bits;
