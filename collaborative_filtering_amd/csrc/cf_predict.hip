@@ -703,6 +703,11 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
 #define CF_PRED_RATING_OCC 2   // rating-kernel blocks per CU (registers and the LDS budget below)
 #endif
 constexpr size_t kRatingLds = 163840 / CF_PRED_RATING_OCC;
+#ifndef CF_PRED_LDL_PW
+#define CF_PRED_LDL_PW 4   // fast-path LDL^T panel width (4 or 8): columns per trailing update
+#endif
+constexpr int kLdlPw = CF_PRED_LDL_PW;
+static_assert(kLdlPw == 4 || kLdlPw == 8, "panel width: one or two MFMA k-steps");
 template <typename T>
 __global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_rating_kernel(PredArgs<T> a, uint32_t first, uint32_t count) {
     extern __shared__ double dsm[];
@@ -899,13 +904,13 @@ __global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_rating_kern
                 const int nrows = n + 2;
                 double minpiv = 1.0;
                 const int li = lane & 15, lk = lane >> 4;
-                for (int j0 = 0; j0 < n; j0 += 4) {
-                    const int pw = min(4, n - j0);
-                    double Lm[4][4], Dv[4], Di[4];
+                for (int j0 = 0; j0 < n; j0 += kLdlPw) {
+                    const int pw = min(kLdlPw, n - j0);
+                    double Lm[kLdlPw][kLdlPw], Dv[kLdlPw], Di[kLdlPw];
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) {
+                    for (int t = 0; t < kLdlPw; ++t) {
                         // unconditional (clamped) broadcast reads, then select
-                        double at[4];
+                        double at[kLdlPw];
 #pragma unroll
                         for (int u = 0; u <= t; ++u)
                             at[u] = Ew[tri(j0 + min(t, pw - 1), j0 + min(u, pw - 1))];
@@ -927,29 +932,29 @@ __global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_rating_kern
                         Di[t] = d != 0.0 ? 1.0 / d : 0.0;   // exact-zero pivot: column skipped
                     }
 #pragma unroll
-                    for (int t = 0; t < 4; ++t)
+                    for (int t = 0; t < kLdlPw; ++t)
                         if (t < pw) minpiv = fmin(minpiv, Dv[t]);
                     if (lane >= j0 && lane < nrows) {
                         if (lane < j0 + pw) {   // a row of the block: L and D from the factor
 #pragma unroll
-                            for (int t = 0; t < 4; ++t)
+                            for (int t = 0; t < kLdlPw; ++t)
                                 if (lane - j0 == t) {
 #pragma unroll
                                     for (int u = 0; u < t; ++u) Ew[tri(lane, j0 + u)] = Lm[t][u];
                                     Ew[tri(lane, lane)] = Dv[t];
                                 }
                         } else {   // a row below: z L11^T = a_i, l_i = z / D
-                            double z[4];
+                            double z[kLdlPw];
 #pragma unroll
-                            for (int t = 0; t < 4; ++t) z[t] = Ew[tri(lane, j0 + min(t, pw - 1))];
+                            for (int t = 0; t < kLdlPw; ++t) z[t] = Ew[tri(lane, j0 + min(t, pw - 1))];
 #pragma unroll
-                            for (int t = 0; t < 4; ++t) {
+                            for (int t = 0; t < kLdlPw; ++t) {
                                 z[t] = t < pw ? z[t] : 0.0;
 #pragma unroll
                                 for (int s2 = 0; s2 < t; ++s2) z[t] = fma(-z[s2], Lm[t][s2], z[t]);
                             }
 #pragma unroll
-                            for (int t = 0; t < 4; ++t)
+                            for (int t = 0; t < kLdlPw; ++t)
                                 if (t < pw) Ew[tri(lane, j0 + t)] = z[t] * Di[t];
                         }
                     }
@@ -957,22 +962,38 @@ __global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_rating_kern
                     const int r0 = j0 + pw;
                     if (r0 < n) {
                         const int ntr = (nrows - r0 + 15) >> 4, ntc = (n - r0 + 15) >> 4;
-                        const double dk = lk == 0 ? Dv[0] : lk == 1 ? Dv[1] : lk == 2 ? Dv[2] : Dv[3];
-                        const int kc = j0 + min(lk, pw - 1);
+                        // MFMA step s takes the panel's columns 4s .. 4s + 3 (lane group lk)
+                        double dk[kLdlPw / 4];
+                        int kc[kLdlPw / 4];
+#pragma unroll
+                        for (int s4 = 0; s4 < kLdlPw / 4; ++s4) {
+                            double dsel = Dv[4 * s4];
+#pragma unroll
+                            for (int t = 1; t < 4; ++t) dsel = lk == t ? Dv[4 * s4 + t] : dsel;
+                            dk[s4] = dsel;
+                            kc[s4] = j0 + min(4 * s4 + lk, pw - 1);
+                        }
                         for (int ti = 0; ti < ntr; ++ti) {
                             const int arow = r0 + 16 * ti + li;
-                            const double av = Ew[tri(min(arow, nrows - 1), kc)];
-                            const double aop = (arow < nrows && lk < pw) ? -av * dk : 0.0;
+                            double aop[kLdlPw / 4];
+#pragma unroll
+                            for (int s4 = 0; s4 < kLdlPw / 4; ++s4) {
+                                const double av = Ew[tri(min(arow, nrows - 1), kc[s4])];
+                                aop[s4] = (arow < nrows && 4 * s4 + lk < pw) ? -av * dk[s4] : 0.0;
+                            }
                             const int tmax = min(ti, ntc - 1);
                             // two tiles of the row at a time: loads, then MFMAs, then stores
                             for (int tq0 = 0; tq0 <= tmax; tq0 += 2) {
                                 f64x4 acc[2];
-                                double bop[2];
+                                double bop[2][kLdlPw / 4];
 #pragma unroll
                                 for (int x = 0; x < 2; ++x) {
                                     const int col = r0 + 16 * (tq0 + x) + li;
-                                    const double bv = Ew[tri(min(col, n - 1), kc)];
-                                    bop[x] = (col < n && lk < pw) ? bv : 0.0;
+#pragma unroll
+                                    for (int s4 = 0; s4 < kLdlPw / 4; ++s4) {
+                                        const double bv = Ew[tri(min(col, n - 1), kc[s4])];
+                                        bop[x][s4] = (col < n && 4 * s4 + lk < pw) ? bv : 0.0;
+                                    }
 #pragma unroll
                                     for (int q = 0; q < 4; ++q) {
                                         const int row = r0 + 16 * ti + lk + 4 * q;
@@ -981,8 +1002,12 @@ __global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_rating_kern
                                         acc[x][q] = (tq0 + x <= tmax && row < nrows && col < n && col <= row) ? v : 0.0;
                                     }
                                 }
-                                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop, bop[0], acc[0], 0, 0, 0);
-                                if (tq0 + 1 <= tmax) acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop, bop[1], acc[1], 0, 0, 0);
+#pragma unroll
+                                for (int s4 = 0; s4 < kLdlPw / 4; ++s4) {
+                                    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[s4], bop[0][s4], acc[0], 0, 0, 0);
+                                    if (tq0 + 1 <= tmax)
+                                        acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[s4], bop[1][s4], acc[1], 0, 0, 0);
+                                }
 #pragma unroll
                                 for (int x = 0; x < 2; ++x) {
                                     const int col = r0 + 16 * (tq0 + x) + li;
