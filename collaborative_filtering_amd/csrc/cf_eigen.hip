@@ -127,27 +127,34 @@ __device__ __forceinline__ float test_rating(const EigenArgs& a, uint32_t movie,
 // LD == 16 (mod 64) floats: the 4 consecutive columns that the 4 pairs of a
 // half-wave touch in one tournament step start in distinct 16-bank quarters, so the
 // b64 accesses are conflict-free (MI355X_MICROARCH.md, LDS table: b64 bank = (a/4) mod 64).
-template <int EMAX>
+// NARROW (bucket 12 only): at most NC = 188 columns in LDS, so LD = 208 == 16 (mod 64)
+// fits too.  The full 192-column bucket falls back to LD = NR + 8 == 8 (mod 64), whose
+// b64 column accesses are 2-way bank conflicted; every bucket-12 launch whose largest k
+// is <= 188 (all of BASELINE C2/C4: k is clipped at 180) takes the narrow layout.
+template <int EMAX, bool NARROW = false>
 struct EigenGeom {
     static constexpr int NR = 16 * EMAX;
+    static constexpr int NC = NARROW ? 188 : NR;                 // column capacity of B
     static constexpr int E2 = NR / (2 * kGroup);               // float2 chunks per lane
-    // == 16 mod 64 where it fits in LDS; the k <= 192 bucket falls back to NR + 8
-    static constexpr int LD = (NR * (NR + ((16 - NR) % 64 + 64) % 64) + 9 * NR <= 40960 - 4)
-                                  ? NR + ((16 - NR) % 64 + 64) % 64 : NR + 8;
+    static constexpr int LD16 = NR + ((16 - NR) % 64 + 64) % 64;
+    // == 16 mod 64 where it fits in LDS; the full k <= 192 bucket falls back to NR + 8
+    static constexpr int LD = (NC * LD16 + 9 * NR <= 40960 - 4) ? LD16 : NR + 8;
     static constexpr int NT = (NR > 128) ? 1024 : 512;         // 1 pass per step up to NT/8 pairs
 
     static constexpr size_t bytes() {
-        return sizeof(float) * (size_t)NR * LD     // B
+        return sizeof(float) * (size_t)NC * LD     // B
                + sizeof(uint32_t) * NR             // items
                + sizeof(float) * NR * 5            // s, l2 diagonal, sig, mu, scale drift
                + sizeof(int) * NR                  // perm
                + sizeof(int) * 4;                  // flags
     }
 };
+static_assert(EigenGeom<12, true>::LD % 64 == 16, "narrow bucket-12 layout must be conflict-free");
+static_assert(EigenGeom<12, true>::bytes() <= 163840, "narrow bucket-12 layout exceeds 160 KiB LDS");
 
-template <int EMAX>
-__global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a) {
-    using G = EigenGeom<EMAX>;
+template <int EMAX, bool NARROW = false>
+__global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT)) void eigen_kernel(EigenArgs a) {
+    using G = EigenGeom<EMAX, NARROW>;
     constexpr int NR = G::NR;
     constexpr int LD = G::LD;
     // element (row i, column j) of B.  (A row swizzle for the LD == 8 (mod 64) bucket,
@@ -157,7 +164,7 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     constexpr int NT = G::NT;
     extern __shared__ float smem[];
     float* B = smem;
-    uint32_t* s_item = reinterpret_cast<uint32_t*>(B + (size_t)NR * LD);
+    uint32_t* s_item = reinterpret_cast<uint32_t*>(B + (size_t)G::NC * LD);
     float* s_s = reinterpret_cast<float*>(s_item + NR);
     float* s_l2d = s_s + NR;
     float* s_sig = s_l2d + NR;
@@ -180,7 +187,7 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     const uint64_t base = a.item_off[u];
     const int nrows = (int)(a.item_off[u + 1] - base);
     int k = nrows;   // columns of B (kSigma: the unrated rows, set below)
-    if (nrows <= 0 || nrows > NR) {
+    if (nrows <= 0 || nrows > G::NC) {
         if (tid == 0) {
             if (mode == kSigma) a.wlim[unit] = __int_as_float(0x7fc00000);
             else a.m_out[u] = (nrows <= 0) ? 0 : -1;
@@ -189,7 +196,7 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     }
 
     for (int i = tid; i < nrows; i += NT) s_item[i] = a.items[base + i];
-    for (int idx = tid; idx < NR * LD; idx += NT) B[idx] = 0.0f;
+    for (int idx = tid; idx < G::NC * LD; idx += NT) B[idx] = 0.0f;
     __syncthreads();
     if (mode == kSigma) {
         // ---- 1s. B's columns = the unrated rows of the movie's L2 (row 0 counts as
@@ -510,19 +517,31 @@ __global__ __launch_bounds__(EigenGeom<EMAX>::NT) void eigen_kernel(EigenArgs a)
     }
 }
 
-template <int EMAX>
+template <int EMAX, bool NARROW = false>
 int launch_bucket(cf_ctx* ctx, const EigenArgs& args, uint32_t count, hipStream_t stream) {
-    const size_t lds = EigenGeom<EMAX>::bytes();
-    static_assert(EigenGeom<EMAX>::bytes() <= 163840, "eigen bucket exceeds 160 KiB LDS");
+    using G = EigenGeom<EMAX, NARROW>;
+    const size_t lds = G::bytes();
+    static_assert(G::bytes() <= 163840, "eigen bucket exceeds 160 KiB LDS");
     static bool configured = false;
     if (!configured) {
-        CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_kernel<EMAX>,
+        CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_kernel<EMAX, NARROW>,
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         configured = true;
     }
-    hipLaunchKernelGGL(eigen_kernel<EMAX>, dim3(count), dim3(EigenGeom<EMAX>::NT), lds, stream, args);
+    hipLaunchKernelGGL((eigen_kernel<EMAX, NARROW>), dim3(count), dim3(G::NT), lds, stream, args);
     CF_HIP_CHECK(ctx, hipGetLastError());
     return CF_OK;
+}
+
+// Bucket 12 in the conflict-free narrow layout when every unit fits it (kmax = the bucket's
+// largest k; units are sorted largest first).  CF_EIGEN_NARROW=0 keeps the 192-column layout.
+int launch_bucket12(cf_ctx* ctx, const EigenArgs& args, uint32_t count, uint32_t kmax, hipStream_t stream) {
+    static const bool narrow_on = [] {
+        const char* e = getenv("CF_EIGEN_NARROW");
+        return !(e && e[0] == '0');
+    }();
+    if (narrow_on && kmax <= (uint32_t)EigenGeom<12, true>::NC) return launch_bucket<12, true>(ctx, args, count, stream);
+    return launch_bucket<12>(ctx, args, count, stream);
 }
 
 }  // namespace
@@ -600,7 +619,7 @@ int launch_buckets_on(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStrea
             case 9: rc = launch_bucket<9>(ctx, args, b.count, stream); break;
             case 10: rc = launch_bucket<10>(ctx, args, b.count, stream); break;
             case 11: rc = launch_bucket<11>(ctx, args, b.count, stream); break;
-            case 12: rc = launch_bucket<12>(ctx, args, b.count, stream); break;
+            case 12: rc = launch_bucket12(ctx, args, b.count, b.kmax, stream); break;
             default: return cf_set_error(ctx, CF_ERANGE, "eigen bucket out of range (k > 192)");
         }
         if (rc != CF_OK) return rc;
