@@ -69,6 +69,27 @@ def test_eigen_sparse_disconnected(eig_ctx):
     _check_batch(gpu_ctx, W, off, items, "sparse")
 
 
+@pytest.mark.parametrize("density", [0.9, 0.05])
+def test_eigen_bucket12_narrow_and_wide_layouts(gpu_ctx, density):
+    """Bucket 12 (177 <= k <= 192) has two LDS layouts: the conflict-free narrow
+    one (188 columns, LD 208) when the bucket's largest k is <= 188, else the 192-column one
+    (LD 200).  The narrow launch is checked against the oracle, and the same users are run
+    again with a k = 192 user added (forcing the wide layout): their blocks must be
+    bit-identical, since only the LDS addresses differ."""
+    ks = [188, 187, 186, 183, 180, 180, 177]
+    W = cases.item_graph(320, density, seed=41)
+    off, items = cases.user_items(320, ks, seed=42)
+    _check_batch(gpu_ctx, W, off, items, f"narrow{density}")
+    narrow = gpu_ctx.eigen_batch(off, items)
+    extra = np.sort(np.random.default_rng(43).choice(320, size=192, replace=False)).astype(np.uint32)
+    off_w = np.append(off, off[-1] + 192).astype(np.uint64)
+    wide = gpu_ctx.eigen_batch(off_w, np.concatenate([items, extra]))
+    for u in range(len(ks)):
+        assert int(narrow.m[u]) == int(wide.m[u]), u
+        for a, b in zip(narrow.block(u), wide.block(u)):
+            assert np.array_equal(a, b), u
+
+
 def test_eigen_many_users_random_order(eig_ctx):
     gpu_ctx = eig_ctx
     rng = np.random.default_rng(31)
