@@ -270,14 +270,16 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT)) void eigen_kernel(Ei
     __syncthreads();
 
     // ---- 3. B = sym_lower(L2) + I, in place ------------------------------------------
-    for (int i = wave; i < k; i += NW) {
-        const float si = s_s[i];
-        for (int j = lane; j < i; j += 64) {
-            const float v = -(si * B[bidx(i, j)]) * s_s[j];
+    // a wave per column j, lanes down its rows i > j: the lower (i,j) read and write walk
+    // a column (conflict-free); only the mirrored (j,i) store strides by LD
+    for (int j = wave; j < k; j += NW) {
+        const float sj = s_s[j];
+        for (int i = j + 1 + lane; i < k; i += 64) {
+            const float v = -(s_s[i] * B[bidx(i, j)]) * sj;
             B[bidx(i, j)] = v;   // (i,j), lower
             B[bidx(j, i)] = v;   // (j,i), mirrored
         }
-        if (lane == 0) B[bidx(i, i)] = s_l2d[i] + 1.0f;
+        if (lane == 0) B[bidx(j, j)] = s_l2d[j] + 1.0f;
     }
     for (int i = tid; i < k; i += NT) s_dev[i] = 0.0f;
     if (tid == 0) s_flag[0] = 0;
@@ -446,16 +448,29 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT)) void eigen_kernel(Ei
     // (local_calc_precomp.cpp:284-304): a fixed convention makes the all-positive
     // lambda = 0 eigenvector of a connected subgraph survive it instead of being dropped
     // from every rating of the user by the luck of the rotation order.
-    for (int j = tid; j < k; j += NT) {
+    // One 8-lane group per column in the sweep's float2 layout (conflict-free, rows past
+    // nrows are zero), the fp64 partials combined in a fixed butterfly order.
+    for (int j = g; j < k; j += NG) {
+        const f2* bc = reinterpret_cast<const f2*>(B + j * LD);
         double acc = 0.0, sum = 0.0;
-        for (int i = 0; i < nrows; ++i) {
-            const double v = (double)B[bidx(i, j)];
-            acc = fma(v, v, acc);
-            sum += v;
+#pragma unroll
+        for (int e = 0; e < E2; ++e) {
+            const f2 x = lds_ld(bc + kGroup * e + lig);
+            acc = fma((double)x.x, (double)x.x, acc);
+            acc = fma((double)x.y, (double)x.y, acc);
+            sum += (double)x.x;
+            sum += (double)x.y;
         }
-        const double nrm = sqrt(acc);
-        s_mu[j] = (float)(nrm / sqrt(1.0 + (double)s_dev[j]));   // lambda_j + 1
-        s_s[j] = (float)((sum < 0.0 ? -1.0 : 1.0) / nrm);        // unit-normalises v_j
+#pragma unroll
+        for (int o = 1; o < kGroup; o <<= 1) {
+            acc += __shfl_xor(acc, o);
+            sum += __shfl_xor(sum, o);
+        }
+        if (lig == 0) {
+            const double nrm = sqrt(acc);
+            s_mu[j] = (float)(nrm / sqrt(1.0 + (double)s_dev[j]));   // lambda_j + 1
+            s_s[j] = (float)((sum < 0.0 ? -1.0 : 1.0) / nrm);        // unit-normalises v_j
+        }
     }
     __syncthreads();
     if (mode == kSigma) {   // w_lim = sqrt(lambda_min(L2_h L2_h^T)) = sigma_min(L2_h) (:435-436)
@@ -476,19 +491,24 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT)) void eigen_kernel(Ei
         s_perm[rank] = j;
     }
     __syncthreads();
-    if (tid == 0) {
-        int lim = k;   // kLocal keeps every eigenpair (es(ll2), local_calc.cpp:378)
-        if (mode == kUser) {
-            float smm = 0.0f;
-            for (int i = 0; i < k; ++i)
-                if (smm < s_sig[i]) smm = s_sig[i];
-            smm = (float)((double)smm + 0.01);          // (:182)
-            for (lim = 0; lim < k; ++lim)
-                if ((double)(s_mu[s_perm[lim]] - 1.0f) > (double)smm) break;  // (:186-188)
-            if (lim < 2) lim = 2;                        // (:190-191)
+    if (mode == kUser) {
+        // lim = first sorted position with lambda > smm (:186-188).  lambda = mu - 1 is
+        // monotone in mu and the order is ascending in mu, so it equals the count of
+        // eigenpairs with !(lambda > smm): one block-wide count instead of a serial walk.
+        float smm = 0.0f;
+        for (int i = 0; i < k; ++i)
+            if (smm < s_sig[i]) smm = s_sig[i];
+        smm = (float)((double)smm + 0.01);              // (:182)
+        const bool below = tid < k && !((double)(s_mu[tid] - 1.0f) > (double)smm);
+        int lim = __syncthreads_count(below);
+        if (lim < 2) lim = 2;                            // (:190-191)
+        if (tid == 0) {
+            s_flag[1] = lim;
+            a.m_out[u] = lim;
         }
-        s_flag[1] = lim;
-        a.m_out[u] = lim;
+    } else if (tid == 0) {
+        s_flag[1] = k;   // kLocal keeps every eigenpair (es(ll2), local_calc.cpp:378)
+        a.m_out[u] = k;
     }
     __syncthreads();
     const int m = s_flag[1];
