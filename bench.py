@@ -142,7 +142,7 @@ class Workload:
     def __init__(self, args, cfg, rank, world, dev, torch, ctx, W_dev):
         from collaborative_filtering_amd import synth
         from collaborative_filtering_amd.api import evec_offsets
-        from collaborative_filtering_amd.multi import cost_split
+        from collaborative_filtering_amd.multi import compat_prefix_users, cost_split
 
         self.torch = torch
         self.U = args.users or cfg["users"]
@@ -175,6 +175,20 @@ class Workload:
         self.d_poff = torch.zeros(self.n_users + 1, dtype=torch.int64, device=dev)
         self.d_packed = None
         self.ctx = ctx
+        # compat w_lim reads the GLOBAL concatenated sig table (local_calc_precomp.cpp:414,437,440):
+        # its rows [0, kmax) are the sigs of the first j users of the global set.  Rank 0 owns them
+        # (its d_sigs); every other rank recomputes those users in its step (multi.compat_prefix_users)
+        self.pre = None
+        j = compat_prefix_users(k_all)
+        if (lo > 0 or hi < j) and j > 0:
+            poff, pitems, _ = synth.user_items(self.seed, k_all[:j], self.n_items, threads=16, u_base=0)
+            peoff, pn = evec_offsets(poff)
+            self.pre = {"plan": ctx.plan(poff), "off": T(poff.view(np.int64)), "items": T(pitems.view(np.int32)),
+                        "eoff": T(peoff.view(np.int64)), "m": torch.zeros(j, dtype=torch.int32, device=dev),
+                        "sigs": torch.zeros(int(poff[-1]), dtype=torch.float32, device=dev),
+                        "evals": torch.zeros(int(poff[-1]), dtype=torch.float32, device=dev),
+                        "evecs": torch.zeros(max(pn, 1), dtype=torch.float32, device=dev), "users": j}
+        self.prefix_users = j
 
     def eigen(self, sp):
         self.plan.eigen_run(self.d_off, self.d_items, self.d_eoff, self.d_m, self.d_sigs, self.d_evals, self.d_evecs,
@@ -197,12 +211,21 @@ class Workload:
         self.plan.step_run(self.d_off, self.d_items, self.d_rat, self.d_eoff, self.d_m, self.d_sigs, self.d_evals,
                            self.d_evecs, CF_SIGS_COMPAT, self.d_mse, self.d_kk, stream=sp)
 
+    def sig_table(self, sp):
+        """The compat sig table of this rank: its own d_sigs on rank 0 (the global set's first
+        users are its first users); elsewhere the prefix users' sigs, recomputed on this GPU."""
+        if self.pre is None:
+            return self.d_sigs
+        p = self.pre
+        p["plan"].eigen_run(p["off"], p["items"], p["eoff"], p["m"], p["sigs"], p["evals"], p["evecs"], stream=sp)
+        return p["sigs"]
+
     def predict(self, sp):
         from collaborative_filtering_amd.api import CF_SIGS_COMPAT
 
-        # compat w_lim: the concatenated sigs table of the records in user order (d_sigs)
+        tab = self.sig_table(sp)
         self.plan.predict_run(self.d_off, self.d_items, self.d_rat, self.d_m, self.d_evals, self.d_eoff, self.d_evecs,
-                              self.d_sigs, CF_SIGS_COMPAT, self.d_mse, self.d_kk, stream=sp)
+                              tab, CF_SIGS_COMPAT, self.d_mse, self.d_kk, stream=sp)
 
 
 def main():
@@ -243,6 +266,10 @@ def main():
             print(json.dumps(prep_leg(args, pctx, dev, torch)), flush=True)
         return
 
+    if args.fused == "on" and world > 1:
+        # cf_step_run builds its compat table from the rank's own first users; ranks > 0 need the
+        # global set's (Workload.sig_table), which only the two-call step provides
+        raise SystemExit("--fused on is single-rank only")
     cfg = CONFIGS[args.config]
     solo = rank == 0 and world == 1 and not args.profile_steps_only and not args.pmc_child
     want_cpu = solo and not args.no_cpu_baseline
@@ -269,9 +296,12 @@ def main():
             coll_dev = dev if backend == "nccl" else torch.device("cpu")
             gather_state["n_packed"] = int(wl.d_poff[-1].item())
             gather_state["counts"] = exchange_counts([wl.n_users, wl.n_entries, wl.n_entries,
-                                                      gather_state["n_packed"]], device=coll_dev)
+                                                      gather_state["n_packed"], wl.n_entries, wl.n_entries],
+                                                     device=coll_dev)
+        # both record kinds: the eigen records (out_eigen_) and the prediction rows (out_res_:
+        # mse, kk), as the reference saves out_res_ from every rank (local_calc_precomp.cpp:576)
         parts = [wl.d_m[:wl.n_users], wl.d_sigs[:wl.n_entries], wl.d_evals[:wl.n_entries],
-                 wl.d_packed[:gather_state["n_packed"]]]
+                 wl.d_packed[:gather_state["n_packed"]], wl.d_mse[:wl.n_entries], wl.d_kk[:wl.n_entries]]
         if backend != "nccl":
             parts = [p_.cpu() for p_ in parts]
         return gather_to_rank0(parts, gather_state["counts"])
@@ -449,6 +479,12 @@ def main():
         "kk_mean": float(kk_h.mean()),
         "nan_predictions": int(np.isnan(mse_h).sum()),
         "nc_gt_62_frac": float(np.mean((np.repeat(wl.k, wl.k) - kk_h) > 62)),
+        "rank_deficient_predictions": {
+            "rows": pred_acc["rank_deficient_rows"], "frac": pred_acc["rank_deficient_frac"],
+            "c0_rows": pred_acc["c0_rows"],
+            "note": "rank 0's rows with 0 < c < lim (U_CS^T U_CS singular): the reference's explicit inverse "
+                    "returns rounding noise clamped to [1, 5] there, this kernel the minimum-norm least-squares "
+                    "prediction; tests pin kk, finiteness and the clamp range on them, not the value"},
     }
 
     # ---- HBM traffic (rank 0, N=1): two rocprofv3 --pmc passes over one child step ------
@@ -1008,8 +1044,13 @@ def predictor_flops(off, k, m, kk, evals, sigtab):
     exe = float(np.sum(2 * kf * lu * lu + 4 * kf * lu * du + 2 * kf * du * du + du ** 3 / 3 + 2 * kf ** 3
                        + 4 * kf * kf))
     exe += float(np.sum((ns + 1) * (ns + 2) * np.maximum(nc, d) + ns ** 3 / 3 + 4 * ns ** 2))
+    # structurally rank-deficient rows: 0 < c < lim, so U_CS^T U_CS (lim' x lim', rank <= c) is
+    # singular before the column filter -- the reference returns rounding noise there, this
+    # kernel the minimum-norm least-squares prediction
+    rdef = int(np.sum((c > 0) & (c < lim)))
     return {"algorithmic_flops": alg, "executed_flops": exe, "ref_flops": ref, "algorithmic_bytes": byt,
-            "lim_mean": float(lim.mean()) if n else 0.0}
+            "lim_mean": float(lim.mean()) if n else 0.0, "rank_deficient_rows": rdef,
+            "rank_deficient_frac": rdef / max(n, 1), "c0_rows": int(np.sum(c == 0))}
 
 
 def cpu_baseline(args, wl, W):

@@ -54,6 +54,9 @@ SIGNATURES = {
     "cf_predict_precomp_sel": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_void_p,
                                        c_void_p, c_void_p]),
+    "cf_predict_precomp_multi": (c_int, [c_void_p, c_int, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p]),
     "cf_step_run": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "cf_step_timing": (c_int, [c_void_p, c_void_p, c_void_p]),

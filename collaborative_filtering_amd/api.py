@@ -391,6 +391,36 @@ def eigen_batch_multi(ctxs, item_off, items):
     return EigenResult(item_off, poff[:-1].copy(), m, sigs, evals, evecs[: int(poff[-1])]), split.astype(np.int64)
 
 
+def predict_precomp_multi(ctxs, item_off, items, ratings, m, evals, evec_off, evecs, sigtab,
+                          sig_mode=CF_SIGS_COMPAT, row_sel=None, want_pred=False):
+    """cf_predict_precomp_multi: neigh_program::apply over one user set on contexts `ctxs`
+    (each with the graph uploaded; users range-split by k^3, the global compat table on every
+    context).  Host numpy arrays as Context.predict_precomp; returns (mse, kk[, pred], split)."""
+    lib = _native.load()
+    item_off = np.ascontiguousarray(item_off, dtype=np.uint64)
+    items = np.ascontiguousarray(items, dtype=np.uint32)
+    ratings = np.ascontiguousarray(ratings, dtype=np.float32)
+    m = np.ascontiguousarray(m, dtype=np.int32)
+    evals = np.ascontiguousarray(evals, dtype=np.float64)
+    evec_off = np.ascontiguousarray(evec_off, dtype=np.uint64)
+    evecs = np.ascontiguousarray(evecs, dtype=np.float64)
+    sigtab = np.ascontiguousarray(sigtab, dtype=np.float64)
+    sel = None if row_sel is None else np.ascontiguousarray(row_sel, dtype=np.uint8)
+    n_users = len(item_off) - 1
+    n = int(item_off[-1])
+    mse = np.zeros(n, dtype=np.float32)
+    kk = np.zeros(n, dtype=np.int32)
+    pred = np.zeros(n, dtype=np.float64) if want_pred else None
+    split = np.zeros(len(ctxs) + 1, dtype=np.uint32)
+    arr = (c_void_p * len(ctxs))(*[c.h for c in ctxs])
+    rc = lib.cf_predict_precomp_multi(arr, len(ctxs), n_users, ptr(item_off), ptr(items), ptr(ratings), ptr(m),
+                                      ptr(evals), ptr(evec_off), ptr(evecs), ptr(sigtab), len(sigtab), int(sig_mode),
+                                      ptr(sel), ptr(mse), ptr(kk), ptr(pred), ptr(split))
+    _check(lib, ctxs[0].h, rc, "cf_predict_precomp_multi")
+    out = (mse, kk, pred) if want_pred else (mse, kk)
+    return out + (split.astype(np.int64),)
+
+
 class Plan:
     """cf_plan: users bucketed by item count, reusable across eigen/predict runs."""
 
@@ -442,5 +472,6 @@ class Plan:
                   ptr(d_pred), c_void_p(stream or 0)), "cf_predict_run")
 
 
-__all__ = ["Context", "Plan", "EigenResult", "evec_offsets", "cost_split_native", "eigen_batch_multi", "CF_SIGS_OWN", "CF_SIGS_COMPAT", "CF_FILTER_CHEBY",
+__all__ = ["Context", "Plan", "EigenResult", "evec_offsets", "cost_split_native", "eigen_batch_multi",
+           "predict_precomp_multi", "CF_SIGS_OWN", "CF_SIGS_COMPAT", "CF_FILTER_CHEBY",
            "CF_FILTER_BINOMIAL"]

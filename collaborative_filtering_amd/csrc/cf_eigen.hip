@@ -706,7 +706,8 @@ int cf_launch_local_sigma(cf_ctx* ctx, const cf_plan* pair_plan, const uint64_t*
     return launch_all_buckets(ctx, pair_plan, args, stream);
 }
 
-static int launch_emax(cf_ctx* ctx, int emax, const EigenArgs& args, uint32_t count, hipStream_t stream) {
+static int launch_emax(cf_ctx* ctx, int emax, const EigenArgs& args, uint32_t count, uint32_t kmax,
+                       hipStream_t stream) {
     switch (emax) {
         case 1: return launch_bucket<1>(ctx, args, count, stream);
         case 2: return launch_bucket<2>(ctx, args, count, stream);
@@ -719,7 +720,7 @@ static int launch_emax(cf_ctx* ctx, int emax, const EigenArgs& args, uint32_t co
         case 9: return launch_bucket<9>(ctx, args, count, stream);
         case 10: return launch_bucket<10>(ctx, args, count, stream);
         case 11: return launch_bucket<11>(ctx, args, count, stream);
-        case 12: return launch_bucket<12>(ctx, args, count, stream);
+        case 12: return launch_bucket12(ctx, args, count, kmax, stream);   // the layout cf_launch_eigen picks
         default: return cf_set_error(ctx, CF_ERANGE, "eigen bucket out of range (k > 192)");
     }
 }
@@ -745,7 +746,10 @@ int cf_launch_eigen_flagged(cf_ctx* ctx, const cf_plan* plan, int emax, uint32_t
     args.tol_scale = ctx->tol_scale;
     args.max_sweeps = ctx->max_sweeps;
     args.only_flag = flag;
-    return launch_emax(ctx, emax, args, count, stream);
+    // units are sorted largest k first within a bucket, so the range's first unit has its kmax
+    const uint32_t u0 = plan->h_order[first];
+    const uint32_t kmax = (uint32_t)(plan->h_item_off[u0 + 1] - plan->h_item_off[u0]);
+    return launch_emax(ctx, emax, args, count, kmax, stream);
 }
 
 int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,

@@ -1472,10 +1472,17 @@ int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
         CF_HIP_CHECK(ctx, hipStreamWaitEvent(ps[i], ctx->aux_event[cf_ctx::kAuxStreams], 0));
     }
     int rc = CF_OK;
+    // after the fork a failed event call sets rc and skips the rest, so the join below always
+    // orders the caller's stream after every kernel already queued on es / ps
+#define CF_STEP_CHECK(expr)                                                                            \
+    if (rc == CF_OK) {                                                                                 \
+        const hipError_t _e = (expr);                                                                  \
+        if (_e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    }
     if (pre) {   // prefix users first, then every predictor stream waits for their sigs
         rc = cf_launch_eigen(ctx, pre, d_item_off, d_items, d_evec_off, d_m, d_sigs, d_evals, d_evecs, ps[0]);
-        if (rc == CF_OK) CF_HIP_CHECK(ctx, hipEventRecord(ctx->step_sync_ev[0], ps[0]));
-        if (rc == CF_OK) CF_HIP_CHECK(ctx, hipStreamWaitEvent(ps[1], ctx->step_sync_ev[0], 0));
+        CF_STEP_CHECK(hipEventRecord(ctx->step_sync_ev[0], ps[0]));
+        CF_STEP_CHECK(hipStreamWaitEvent(ps[1], ctx->step_sync_ev[0], 0));
     }
     int nb = 0, nc = 0;
     for (size_t bi = 0; bi < plan->buckets.size() && rc == CF_OK; ++bi) {
@@ -1486,9 +1493,9 @@ int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
             rc = cf_launch_eigen_spill(ctx, plan, b, d_item_off, d_items, d_evec_off, d_m, d_sigs, d_evals, d_evecs,
                                        es[0]);
             if (rc != CF_OK) break;
-            CF_HIP_CHECK(ctx, hipEventRecord(ctx->step_bucket_ev[bi], es[0]));
-            CF_HIP_CHECK(ctx, hipStreamWaitEvent(es[1], ctx->step_bucket_ev[bi], 0));
-            CF_HIP_CHECK(ctx, hipStreamWaitEvent(ps[0], ctx->step_bucket_ev[bi], 0));
+            CF_STEP_CHECK(hipEventRecord(ctx->step_bucket_ev[bi], es[0]));
+            CF_STEP_CHECK(hipStreamWaitEvent(es[1], ctx->step_bucket_ev[bi], 0));
+            CF_STEP_CHECK(hipStreamWaitEvent(ps[0], ctx->step_bucket_ev[bi], 0));
             rc = cf_launch_predict_spill<float>(ctx, plan, b, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off,
                                                 d_evecs, d_sigs, sig_mode, d_mse, d_kk, d_pred, nullptr, ps[0]);
             continue;
@@ -1496,7 +1503,7 @@ int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
         rc = cf_launch_eigen_flagged(ctx, plan, b.emax, b.first, b.count, nullptr, d_item_off, d_items, d_evec_off,
                                      d_m, d_sigs, d_evals, d_evecs, est);
         if (rc != CF_OK) break;
-        CF_HIP_CHECK(ctx, hipEventRecord(ctx->step_bucket_ev[bi], est));
+        CF_STEP_CHECK(hipEventRecord(ctx->step_bucket_ev[bi], est));
         size_t rating_lds = 0;
         rc = setup_bucket<float>(ctx, args, std::max<int>(2, 16 * b.emax), rating_lds);
         if (rc != CF_OK) break;
@@ -1505,9 +1512,10 @@ int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
             const uint32_t cnt = std::min(kChunk, b.count - c0);
             const int si = nc++ % 2;
             if (!waited[si]) {
-                CF_HIP_CHECK(ctx, hipStreamWaitEvent(ps[si], ctx->step_bucket_ev[bi], 0));
+                CF_STEP_CHECK(hipStreamWaitEvent(ps[si], ctx->step_bucket_ev[bi], 0));
                 waited[si] = true;
             }
+            if (rc != CF_OK) break;
             args.slots = reinterpret_cast<double*>(static_cast<char*>(ctx->d_scratch) + si * need);
             hipLaunchKernelGGL(pred_basis_kernel<float>, dim3(cnt), dim3(kThreads), basis_lds(), ps[si], args,
                                b.first + c0, cnt);
@@ -1519,6 +1527,7 @@ int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
             }
         }
     }
+#undef CF_STEP_CHECK
     // join: eigen streams -> "eigen done" event on the caller, then the predictor streams
     for (int i = 0; i < 2; ++i) {
         CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[i], es[i]));

@@ -282,27 +282,44 @@ int cf_knn_regroup_run(cf_ctx* ctx, uint64_t n, uint32_t n_users, uint32_t n_mov
     const uint32_t words = (n_movies + 31) / 32;
     const int bits_a = 32 + bits_for(nseg), bits_b = 32 + bits_for((uint64_t)n_users + 1);
     const size_t cub = cub_bytes(n, std::max<uint64_t>(nseg, (uint64_t)n_users + 1), bits_a, bits_b, 1, st);
-    const size_t need = 2 * 8 * (n + 64) + 3 * 4 * (n + 64) + 4 * (n + 64) + 8 * 2 * (nseg + 64) +
-                        (4 + 8) * ((uint64_t)n_users + 64) + 4 * (uint64_t)n_movies * words + 8 * (n_movies + 64) +
-                        cub + 16 * 256 + 4 * (n + 64);
+    // the scratch layout, carved twice: a dry run over a null base sizes the reservation
+    // from exactly the takes the real carve makes
+    struct Layout {
+        uint64_t *key_a, *key_b, *seg_w, *seg_off, *uw, *uoff, *rcnt;
+        uint32_t *idx_a, *idx_b, *keep, *pos, *kuser, *seg_cnt, *ucnt, *bm;
+        void* tmp;
+    };
+    const auto carve = [&](char* base, Layout& L) {
+        Carve cv{base};
+        L.key_a = cv.take<uint64_t>(n);
+        L.key_b = cv.take<uint64_t>(n);
+        L.idx_a = cv.take<uint32_t>(n);
+        L.idx_b = cv.take<uint32_t>(n);
+        L.keep = cv.take<uint32_t>(n);
+        L.pos = cv.take<uint32_t>(n);
+        L.kuser = cv.take<uint32_t>(n);
+        L.seg_cnt = cv.take<uint32_t>(nseg);
+        L.seg_w = cv.take<uint64_t>(nseg);
+        L.seg_off = cv.take<uint64_t>(nseg);
+        L.ucnt = cv.take<uint32_t>((uint64_t)n_users + 1);
+        L.uw = cv.take<uint64_t>((uint64_t)n_users + 1);
+        L.uoff = cv.take<uint64_t>((uint64_t)n_users + 1);
+        L.bm = cv.take<uint32_t>((uint64_t)n_movies * words);
+        L.rcnt = cv.take<uint64_t>((uint64_t)n_movies + 1);
+        L.tmp = cv.take<char>(cub);
+        return cv.used;
+    };
+    Layout lay{};
+    const size_t need = carve(nullptr, lay);
     CF_TRY(prep_reserve(ctx, need));
-    Carve cv{static_cast<char*>(ctx->d_prep)};
-    uint64_t* key_a = cv.take<uint64_t>(n);
-    uint64_t* key_b = cv.take<uint64_t>(n);
-    uint32_t* idx_a = cv.take<uint32_t>(n);
-    uint32_t* idx_b = cv.take<uint32_t>(n);
-    uint32_t* keep = cv.take<uint32_t>(n);
-    uint32_t* pos = cv.take<uint32_t>(n);
-    uint32_t* kuser = cv.take<uint32_t>(n);
+    if (carve(static_cast<char*>(ctx->d_prep), lay) > ctx->prep_bytes)
+        return cf_set_error(ctx, CF_EINVAL, "cf_knn_regroup_run: scratch layout exceeds the reservation");
+    uint64_t *key_a = lay.key_a, *key_b = lay.key_b, *seg_w = lay.seg_w, *seg_off = lay.seg_off, *uw = lay.uw,
+             *uoff = lay.uoff, *rcnt = lay.rcnt;
+    uint32_t *idx_a = lay.idx_a, *idx_b = lay.idx_b, *keep = lay.keep, *pos = lay.pos, *kuser = lay.kuser,
+             *seg_cnt = lay.seg_cnt, *ucnt = lay.ucnt, *bm = lay.bm;
     float* krat = reinterpret_cast<float*>(idx_a);   // idx_a is dead after the first sort
-    uint32_t* seg_cnt = cv.take<uint32_t>(nseg);
-    uint64_t* seg_w = cv.take<uint64_t>(nseg);
-    uint64_t* seg_off = cv.take<uint64_t>(nseg);
-    uint32_t* ucnt = cv.take<uint32_t>((uint64_t)n_users + 1);
-    uint64_t* uoff = cv.take<uint64_t>((uint64_t)n_users + 1);
-    uint32_t* bm = cv.take<uint32_t>((uint64_t)n_movies * words);
-    uint64_t* rcnt = cv.take<uint64_t>((uint64_t)n_movies + 1);
-    void* tmp = cv.take<char>(cub);
+    void* tmp = lay.tmp;
     size_t tb = cub;
     const dim3 G = grid_for(n), B(256);
     CF_HIP_CHECK(ctx, hipEventRecord(ctx->prep_ev[0], st));
@@ -331,7 +348,6 @@ int cf_knn_regroup_run(cf_ctx* ctx, uint64_t n, uint32_t n_users, uint32_t n_mov
         CF_HIP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tb, keep, pos, (int)n, st));
         hipLaunchKernelGGL(user_sets_kernel, G, B, 0, st, n, key_b, keep, pos, ucnt, kuser);
     }
-    uint64_t* uw = reinterpret_cast<uint64_t*>(key_a);   // key_a is dead after the sort
     hipLaunchKernelGGL(widen_kernel, grid_for((uint64_t)n_users + 1), B, 0, st, (uint64_t)n_users + 1, ucnt, uw);
     CF_HIP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tb, uw, uoff, (int)n_users + 1, st));
     // ---- 3-4. co-rated bitmap, row counts, sorted lists ---------------------------------

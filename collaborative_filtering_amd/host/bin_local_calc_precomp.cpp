@@ -9,7 +9,8 @@
 //   :393-404 writer "movie user mse kk" -> out_res_<i>_of_<N>
 // Options: --pct P (percent of movie vertices, sampled like rand()%100 < P; default
 // 100), --seed S (default: time, as the reference), --compat ref|fixed (fixed = each
-// user's own sigs), --verbosity (accepted, ignored), --nshards N.
+// user's own sigs), --verbosity (accepted, ignored), --nshards N, --devices N (users range-split
+// over N GPU contexts, cf_predict_precomp_multi; out_res_ identical to one device).
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -98,17 +99,45 @@ int main(int argc, char** argv) {
     const bool ref = compat != "fixed";
     std::vector<float> mse(its.size(), std::numeric_limits<float>::quiet_NaN());
     std::vector<int32_t> kk(its.size(), 0);
-    cf_ctx* ctx = cfcli::open_device();
-    cfcli::upload_edges(ctx, items, edges);
-    if (n_users)
-        cfcli::check(ctx, cf_predict_precomp_sel(ctx, n_users, off.data(), its.data(), rats.data(), m.data(),
-                                                 evals.data(), eoff.data(), evecs.data(),
-                                                 ref ? concat.data() : own_sigs.data(),
-                                                 ref ? concat.size() : own_sigs.size(),
-                                                 ref ? CF_SIGS_COMPAT : CF_SIGS_OWN, pct >= 100 ? nullptr : sel.data(),
-                                                 mse.data(), kk.data(), nullptr),
-                     "cf_predict_precomp_sel");
-    cf_destroy(ctx);
+    // --devices N (or CF_DEVICES): the users range-split by k^3 over N contexts, GPU (i % visible)
+    // each -- the reference's ranks each hold the whole out_eigen_ (:485-486, 509) -- with the
+    // global compat table on every context, so out_res_ is identical to the one-device run's
+    const char* env_dev = std::getenv("CF_DEVICES");
+    const int n_dev = std::max(1, std::atoi(cfcli::opt(argc, argv, "devices", env_dev ? env_dev : "1").c_str()));
+    const double* tab = ref ? concat.data() : own_sigs.data();
+    const uint64_t tab_len = ref ? concat.size() : own_sigs.size();
+    const int mode = ref ? CF_SIGS_COMPAT : CF_SIGS_OWN;
+    const uint8_t* rsel = pct >= 100 ? nullptr : sel.data();
+    if (n_dev == 1) {
+        cf_ctx* ctx = cfcli::open_device();
+        cfcli::upload_edges(ctx, items, edges);
+        if (n_users)
+            cfcli::check(ctx, cf_predict_precomp_sel(ctx, n_users, off.data(), its.data(), rats.data(), m.data(),
+                                                     evals.data(), eoff.data(), evecs.data(), tab, tab_len, mode,
+                                                     rsel, mse.data(), kk.data(), nullptr),
+                         "cf_predict_precomp_sel");
+        cf_destroy(ctx);
+    } else {
+        const int visible = cf_device_count();
+        if (visible <= 0) cfcli::die("no usable MI355X device");
+        const char* dev0 = std::getenv("CF_DEVICE");
+        const int base = dev0 ? std::atoi(dev0) : 0;
+        std::vector<cf_ctx*> ctxs(n_dev, nullptr);
+        for (int d = 0; d < n_dev; ++d) {
+            if (cf_create((base + d) % visible, &ctxs[d]) != CF_OK) cfcli::die("cf_create failed");
+            cfcli::upload_edges(ctxs[d], items, edges);
+        }
+        std::vector<uint32_t> split(n_dev + 1);
+        if (n_users)
+            cfcli::check(ctxs[0], cf_predict_precomp_multi(ctxs.data(), n_dev, n_users, off.data(), its.data(),
+                                                           rats.data(), m.data(), evals.data(), eoff.data(),
+                                                           evecs.data(), tab, tab_len, mode, rsel, mse.data(),
+                                                           kk.data(), nullptr, split.data()),
+                         "cf_predict_precomp_multi");
+        for (int d = 0; d < n_dev; ++d)
+            std::printf("device part %d: users %u..%u on GPU %d\n", d, split[d], split[d + 1], (base + d) % visible);
+        for (auto* c : ctxs) cf_destroy(c);
+    }
 
     // rows per test movie vertex (:230-361), sampled per vertex (:221)
     cfio::ShardWriter res(".", "out_res", nshards);

@@ -27,6 +27,23 @@ def cost_split(k: np.ndarray, world: int) -> np.ndarray:
     return np.maximum.accumulate(out)
 
 
+def compat_prefix_users(k, kmax: int | None = None) -> int:
+    """Leading users (file order) whose sigs cover rows [0, kmax) of the compat sig table.
+
+    local_calc_precomp's sigs_min is never cleared (local_calc_precomp.cpp:414, 437, 440), so
+    w_lim of row r of ANY record is the r-th sig of the whole out_eigen_ file (:271): the table a
+    rank needs is the concatenated sigs of the first j users of the GLOBAL set, j = the first
+    index whose prefix of k reaches kmax (the largest k).  Rank 0 owns them; every other rank
+    recomputes those few users' sigs (no exchange: the eigen kernel is deterministic, so the
+    bits equal rank 0's).  The same rule as cf_launch_step's compat prefix (cf_predict.hip)."""
+    k = np.asarray(k, dtype=np.int64)
+    if len(k) == 0:
+        return 0
+    kmax = int(k.max()) if kmax is None else int(kmax)
+    cum = np.cumsum(k)
+    return int(min(len(k), np.searchsorted(cum, kmax, side="left") + 1))
+
+
 def local_slice(item_off: np.ndarray, lo: int, hi: int):
     """Re-based item_off of users [lo, hi) and the entry range they cover."""
     item_off = np.asarray(item_off, dtype=np.uint64)

@@ -188,6 +188,17 @@ int cf_predict_precomp_sel(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_o
                            const double* evals, const uint64_t* evec_off, const double* evecs,
                            const double* sigtab, uint64_t sigtab_len, int sig_mode,
                            const uint8_t* row_sel, float* mse, int32_t* kk, double* pred);
+/* cf_predict_precomp_sel over ONE user set on n_dev contexts (one per GPU, each with the item
+ * graph uploaded; several may share a device), for local_calc_precomp on several GPUs
+ * (local_calc_precomp.cpp:485-486,509: every rank holds the whole out_eigen_).  Users are split
+ * by cf_cost_split; each context predicts its range concurrently.  In CF_SIGS_COMPAT mode every
+ * range reads the same global sig table, so the outputs are bit-identical to the one-context
+ * call.  split_out (optional, n_dev + 1) receives the ranges. */
+int cf_predict_precomp_multi(cf_ctx* const* ctxs, int n_dev, uint32_t n_users, const uint64_t* item_off,
+                             const uint32_t* items, const float* ratings, const int32_t* m, const double* evals,
+                             const uint64_t* evec_off, const double* evecs, const double* sigtab,
+                             uint64_t sigtab_len, int sig_mode, const uint8_t* row_sel, float* mse, int32_t* kk,
+                             double* pred, uint32_t* split_out);
 int cf_predict_run_f64(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
                        const uint32_t* d_items, const float* d_ratings, const int32_t* d_m,
                        const double* d_evals, const uint64_t* d_evec_off,

@@ -236,15 +236,21 @@ def clusters(ev: np.ndarray, gap: float = 1e-3):
 
 
 def compare_eigen_block(L2, m_ref, ev_full_ref, U_ref, m_gpu, ev_gpu, U_gpu, ev_tol=1e-5, proj_tol=1e-3,
-                        res_tol=1e-4, gap=1e-2):
+                        res_tol=1e-4, gap=1e-2, escapes=None):
     """Return a list of failure strings (empty = parity).
 
-    Eigenvectors are compared as clustered projectors.  Clusters group eigenvalues
-    closer than `gap` = 1e-2 (not 1e-3): the fp32 backward error of the GPU solver is
-    ~2e-6, so by Davis-Kahan an isolated vector at gap g moves by ~2e-6/g, i.e. up to
-    2e-3 at g = 1e-3; at g >= 1e-2 the bound is 2e-4 < proj_tol.  A cluster of several
-    vectors just past the gap (the knn2 graphs of configs 2/4 have such spectra) may exceed
-    proj_tol; it then passes only within the Davis-Kahan bound of its own residual.
+    Eigenvectors are compared as clustered projectors.  Clusters group eigenvalues of the
+    ORACLE's spectrum closer than `gap` = 1e-2 (not 1e-3): the fp32 backward error of the GPU
+    solver is ~2e-6, so by Davis-Kahan an isolated vector at gap g moves by ~2e-6/g, i.e. up to
+    2e-3 at g = 1e-3; at g >= 1e-2 the bound is 2e-4 < proj_tol.
+
+    A cluster whose projector error exceeds proj_tol is an ESCAPE: it fails outright beyond
+    10 x proj_tol; between proj_tol and 10 x proj_tol it is appended to `escapes` (a list the
+    caller passes, as (cluster size, error, the oracle spectrum's gap to the rest of the
+    spectrum)) for the caller to count and cap against the clusters compared -- a rule that
+    depends only on the oracle's spectrum, never on the GPU block's own residual.  Without an
+    `escapes` list every escape fails.  `escapes` also receives ("clusters", n) entries with
+    the number of clusters compared, for the caller's ratio.
     """
     fails = []
     k = L2.shape[0]
@@ -265,26 +271,42 @@ def compare_eigen_block(L2, m_ref, ev_full_ref, U_ref, m_gpu, ev_gpu, U_gpu, ev_
         res = np.max(np.linalg.norm(A @ Ug - Ug * ev_gpu[:kv][None, :].astype(np.float64), axis=0))
         if res > res_tol:
             fails.append(f"residual {res:.3g}")
+    n_clusters = 0
     for g in clusters(ev_full_ref, gap):
         if g[-1] >= kv:
             break  # cluster straddles the stored boundary
+        n_clusters += 1
         Pg = Ug[:, g] @ Ug[:, g].T
         Pr = Ur[:, g] @ Ur[:, g].T
         d = np.linalg.norm(Pg - Pr)
         if d > proj_tol:
-            # Davis-Kahan sin-theta bound from the GPU block's OWN residual: with R = A U_g -
-            # U_g diag(lambda_g) over the cluster and delta = the distance from the GPU's
-            # cluster eigenvalues to the rest of the reference spectrum, ||P_gpu - P_ref||_F <=
-            # sqrt(2) ||R||_F / delta.  An fp32 solver's projector may exceed proj_tol only by
-            # as much as its (separately bounded, <= res_tol) residual allows at that gap; a
-            # projector error beyond the bound would be a real defect.
-            R = A @ Ug[:, g] - Ug[:, g] * ev_gpu[g][None, :].astype(np.float64)
             rest = np.delete(ev_full_ref, g)
-            delta = np.min(np.abs(rest[:, None] - ev_gpu[g][None, :].astype(np.float64))) if len(rest) else np.inf
-            dk = np.sqrt(2.0) * np.linalg.norm(R) / delta if delta > 0 else np.inf
-            if d > 1.1 * dk:
-                fails.append(f"projector cluster {g[0]}..{g[-1]} err {d:.3g} (Davis-Kahan bound {dk:.3g})")
+            delta = float(np.min(np.abs(rest[:, None] - ev_full_ref[g][None, :]))) if len(rest) else np.inf
+            if escapes is None or d > 10.0 * proj_tol:
+                fails.append(f"projector cluster {g[0]}..{g[-1]} err {d:.3g} (oracle gap {delta:.3g})")
+            else:
+                escapes.append((len(g), float(d), delta))
+    if escapes is not None:
+        escapes.append(("clusters", n_clusters))
     return fails
+
+
+def escape_summary(escapes):
+    """(clusters compared, escapes, largest escape error) of an `escapes` list."""
+    n = sum(e[1] for e in escapes if e[0] == "clusters")
+    esc = [e for e in escapes if e[0] != "clusters"]
+    return n, len(esc), max((e[1] for e in esc), default=0.0)
+
+
+ESCAPE_CAP = 0.01   # at most 1 % of the compared clusters (and at least 2) may exceed proj_tol
+
+
+def escapes_ok(escapes, label=""):
+    """Report the escape count of a test and check it against ESCAPE_CAP."""
+    n, e, worst = escape_summary(escapes)
+    print(f"{label}: {n} eigenvector clusters compared, {e} above proj_tol 1e-3 (max {worst:.3g}, cap "
+          f"{max(2, int(ESCAPE_CAP * n))})")
+    return e <= max(2, int(ESCAPE_CAP * n))
 
 
 def graph_filter(kind, n, va, vb, w, signal, coeff):

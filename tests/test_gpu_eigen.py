@@ -28,6 +28,7 @@ def _check_batch(ctx, W, item_off, items, label):
     ctx.upload_graph_dense(W)
     res = ctx.eigen_batch(item_off, items)
     bad = []
+    esc = []
     for u in range(len(item_off) - 1):
         b, e = int(item_off[u]), int(item_off[u + 1])
         it = items[b:e].astype(np.int64)
@@ -48,10 +49,11 @@ def _check_batch(ctx, W, item_off, items, label):
         if k == 1:
             assert np.allclose(U_g, [[1.0, 0.0]]) and abs(ev_g[0] - 1.0) < 1e-6 and ev_g[1] == 0
             continue
-        f = orc.compare_eigen_block(L2, m_ref, ev_full, V_full[:, :m_ref], int(res.m[u]), ev_g, U_g)
+        f = orc.compare_eigen_block(L2, m_ref, ev_full, V_full[:, :m_ref], int(res.m[u]), ev_g, U_g, escapes=esc)
         if f:
             bad.append((label, u, k, f))
     assert not bad, bad
+    assert orc.escapes_ok(esc, label), orc.escape_summary(esc)
 
 
 def test_eigen_bucket_edges_dense(eig_ctx):

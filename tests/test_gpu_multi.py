@@ -96,3 +96,125 @@ def test_precompute_local_devices_byte_identical(tmp_path, fmt):
         outs[n_dev] = open(os.path.join(wd, out), "rb").read()
     assert len(outs[1]) > 1000
     assert outs[2] == outs[1] and outs[4] == outs[1]
+
+
+def _c2_subsample(n_users, seed):
+    from collaborative_filtering_amd import synth, workloads as wlm
+    from collaborative_filtering_amd.api import Context
+
+    import torch
+
+    cfg = wlm.CONFIGS["c2"]
+    d_W, _, _ = wlm.config_graph("c2", Context, 0, torch.device("cuda", 0), torch)
+    k_all = wlm.user_degrees(cfg)
+    users = np.sort(np.random.default_rng(seed).choice(len(k_all), size=n_users, replace=False))
+    off_all, items_all, rat_all = synth.user_items(cfg["seed"], k_all, cfg["items"], threads=16)
+    off, items, rat = wlm.sub_csr(off_all, items_all, rat_all, users)
+    return d_W.view(cfg["items"], cfg["items"]), off, items, rat
+
+
+def test_predict_precomp_multi_bit_identical(gpu_ctx):
+    """cf_predict_precomp_multi over 2 and 3 contexts (sharing GPU 0) equals the one-context
+    cf_predict_precomp_sel bit for bit on a C2 subsample in compat mode (every range reads the
+    global concatenated sig table, local_calc_precomp.cpp:414,437,440)."""
+    from collaborative_filtering_amd.api import CF_SIGS_COMPAT, Context, cost_split_native, predict_precomp_multi
+
+    d_W, off, items, rat = _c2_subsample(1500, seed=11)
+    gpu_ctx.upload_graph_dense(d_W)
+    res = gpu_ctx.eigen_batch(off, items)
+    k = np.diff(off.astype(np.int64))
+    evals = res.evals.astype(np.float64)
+    evecs = res.evecs.astype(np.float64)
+    sig = res.sigs.astype(np.float64)
+    ref = gpu_ctx.predict_precomp(off, items, rat, res.m, evals, res.evec_off, evecs, sig, sig_mode=CF_SIGS_COMPAT)
+    assert np.sum(ref[1] > 0) > 1000
+    for n_dev in (2, 3):
+        ctxs = [Context(0) for _ in range(n_dev)]
+        try:
+            for c in ctxs:
+                c.upload_graph_dense(d_W)
+            mse, kk, split = predict_precomp_multi(ctxs, off, items, rat, res.m, evals, res.evec_off, evecs, sig,
+                                                   sig_mode=CF_SIGS_COMPAT)
+        finally:
+            for c in ctxs:
+                c.close()
+        assert np.array_equal(split, cost_split_native(off, n_dev)) and np.all(np.diff(split) > 0)
+        assert int(off[split[1]]) > int(k.max())        # ranges past the first hold no prefix user
+        assert np.array_equal(kk, ref[1])
+        assert np.array_equal(mse, ref[0], equal_nan=True)
+
+
+def test_bench_ranks_equal_single_rank(gpu_ctx):
+    """bench.py's N>1 step on world = 2 and 3 ranks emulated by contexts on GPU 0: each rank's
+    Workload (its cost_split range of the global set, the compat table rebuilt from the global
+    prefix users on ranks > 0) predicts exactly the rows of the one-rank run, bit for bit."""
+    import argparse
+
+    import torch
+
+    import bench
+
+    from collaborative_filtering_amd import workloads as wlm
+    from collaborative_filtering_amd.api import Context as _Ctx
+
+    cfg = dict(bench.CONFIGS["c2"])
+    d_W, _, _ = wlm.config_graph("c2", _Ctx, 0, torch.device("cuda", 0), torch)
+    d_W = d_W.view(cfg["items"], cfg["items"])
+    args = argparse.Namespace(users=6000)
+    dev = torch.device("cuda", 0)
+    sp = torch.cuda.current_stream(dev).cuda_stream
+
+    def run(world):
+        from collaborative_filtering_amd.api import Context
+
+        mse, kk, ms, pre = [], [], [], []
+        for rank in range(world):
+            with Context(0) as ctx:
+                wl = bench.Workload(args, cfg, rank, world, dev, torch, ctx, d_W)
+                wl.eigen(sp)
+                wl.predict(sp)
+                torch.cuda.synchronize(dev)
+                mse.append(wl.d_mse[:wl.n_entries].cpu().numpy())
+                kk.append(wl.d_kk[:wl.n_entries].cpu().numpy())
+                ms.append(wl.d_m[:wl.n_users].cpu().numpy())
+                pre.append(wl.pre is not None)
+                wl.plan.close()
+                if wl.pre:
+                    wl.pre["plan"].close()
+        return np.concatenate(mse), np.concatenate(kk), np.concatenate(ms), pre
+
+    mse1, kk1, m1, pre1 = run(1)
+    assert pre1 == [False]
+    assert np.sum(kk1 > 0) > 100000
+    for world in (2, 3):
+        mse, kk, m, pre = run(world)
+        assert pre == [False] + [True] * (world - 1)
+        assert np.array_equal(m, m1)
+        assert np.array_equal(kk, kk1)
+        assert np.array_equal(mse, mse1, equal_nan=True)
+
+
+def test_local_calc_precomp_devices_byte_identical(tmp_path):
+    """bin/local_calc_precomp --devices 1/2/3 (cf_predict_precomp_multi): one out_res_ set,
+    byte-identical to the one-device run (the reference: every rank reads the whole out_eigen_,
+    local_calc_precomp.cpp:485-486,509, and saves its rows of out_res_, :576)."""
+    import glob
+
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    wd = str(tmp_path)
+    pu.write_movielens(wd, n_users=400, n_items=150, test_frac=0.5, seed=19)
+    _run(wd, "knn")
+    _run(wd, "knn2")
+    _run(wd, "precompute_local", "8")
+    outs = {}
+    for n_dev in (1, 2, 3):
+        log = _run(wd, "local_calc_precomp", "--pct", "100", "--seed", "1", "--devices", str(n_dev))
+        if n_dev > 1:
+            assert log.count("device part") == n_dev
+        files = sorted(glob.glob(os.path.join(wd, "out_res_*")))
+        outs[n_dev] = b"".join(open(f, "rb").read() for f in files)
+    assert outs[1].count(b"\n") > 1000
+    assert outs[2] == outs[1] and outs[3] == outs[1]

@@ -128,6 +128,7 @@ def test_stage_precompute_local(work):
     _, test = movielens_ratings(work)
     assert sorted(r["user"] for r in recs) == sorted({u for ur in test.values() for u in ur})
     bad = []
+    esc = []
     for r in recs:
         mv = r["movies"]
         Wu = np.array([[fin.get((a, b), 0.0) for b in mv] for a in mv])
@@ -143,10 +144,12 @@ def test_stage_precompute_local(work):
             continue
         if k == 1:
             continue
-        f = orc.compare_eigen_block(L2, m, full, V[:, :m], m, r["evals"], r["U"], ev_tol=2e-5, res_tol=2e-4)
+        f = orc.compare_eigen_block(L2, m, full, V[:, :m], m, r["evals"], r["U"], ev_tol=2e-5, res_tol=2e-4,
+                                    escapes=esc)
         if f:
             bad.append((r["user"], f))
     assert not bad, bad[:5]
+    assert orc.escapes_ok(esc, "precompute_local"), orc.escape_summary(esc)
 
 
 def test_stage_local_calc_precomp(work):
