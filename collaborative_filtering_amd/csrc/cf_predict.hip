@@ -519,8 +519,19 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
 #endif
             const int du = k - Lq;
             if (du > 0) {
-                // Omega(i, j) = +-1 from a hash of (user, i, j): deterministic per user
-                const uint32_t seed = u * 0x9E3779B1u + 0x7F4A7C15u;
+                // Omega(i, j) = +-1 from a hash of (the user's content, i, j): the seed mixes k
+                // and three of its item ids, never the user's position in the batch, so a user
+                // gets the same basis bits in any batch or range split (multi-GPU runs equal
+                // the one-GPU run)
+                const auto mix = [](uint32_t h) {
+                    h ^= h >> 16;
+                    h *= 0x7FEB352Du;
+                    h ^= h >> 15;
+                    h *= 0x846CA68Bu;
+                    return h ^ (h >> 16);
+                };
+                const uint32_t seed = mix(mix(mix((uint32_t)k * 0x9E3779B1u + 0x7F4A7C15u) ^ s_item[0]) ^
+                                          s_item[k >> 1]) ^ s_item[k - 1];
                 const auto omega = [seed](int i, int j) -> double {
                     uint32_t h = seed ^ ((uint32_t)i * 0x85EBCA6Bu) ^ ((uint32_t)j * 0xC2B2AE35u);
                     h ^= h >> 16;
