@@ -29,9 +29,9 @@ int main(int argc, char** argv) {
     const int nshards = std::stoi(cfcli::opt(argc, argv, "nshards", "4"));
     const std::string eig_path = cfcli::opt(argc, argv, "eigen", "out_eigen_");
 
-    // text (parsed on --threads threads, default all) or the binary form, detected by its magic
-    std::vector<cfio::EigenRecord> recs =
-        cfio::load_eigen_file(eig_path, std::stoi(cfcli::opt(argc, argv, "threads", "0")));
+    // text (parsed on --threads threads, default all) or the binary form, detected by its magic,
+    // mapped and parsed straight into flat arrays (cfio::load_eigen_flat)
+    const cfio::EigenFlat recs = cfio::load_eigen_flat(eig_path, std::stoi(cfcli::opt(argc, argv, "threads", "0")));
     std::printf("Loaded %zu test users\n", recs.size());
     auto edges = cfio::load_edges(".", "out_fin_");
     for (auto& e : edges) e.w = (double)(float)e.w;   // parsed as float (:129)
@@ -43,7 +43,7 @@ int main(int argc, char** argv) {
         all.push_back(e.b);
     }
     for (auto& kv : test) all.push_back(kv.first);
-    for (auto& r : recs) all.insert(all.end(), r.movies.begin(), r.movies.end());
+    all.insert(all.end(), recs.movies.begin(), recs.movies.end());
     cfio::IdMap items;
     items.build(all);
 
@@ -53,34 +53,38 @@ int main(int argc, char** argv) {
         for (auto& ur : kv.second) urat[ur.first][kv.first] = ur.second;
 
     const uint32_t n_users = (uint32_t)recs.size();
-    std::vector<uint64_t> off(n_users + 1, 0), eoff(n_users);
-    std::vector<uint32_t> its;
-    std::vector<float> rats;
-    std::vector<int32_t> m(n_users);
-    std::vector<double> evals, evecs, own_sigs, concat;
+    // the flat record arrays ARE the predictor's inputs: rows at recs.off, blocks at
+    // recs.evec_off, and the compat table = every record's sigs in file order (recs.sigs);
+    // only the compact ids, ratings and the k-slot eigenvalues are built here
+    const std::vector<uint64_t>& off = recs.off;
+    std::vector<uint64_t> eoff(recs.evec_off.begin(), recs.evec_off.end() - 1);
+    const std::vector<int32_t>& m = recs.m;
+    const double* sig_tab = recs.sigs.data();   // own sigs at off[u] == the compat concatenation
+    std::vector<uint32_t> its(off.back());
+    std::vector<float> rats(off.back());
+    std::vector<double> evals(off.back(), 0.0);
     std::unordered_map<uint32_t, uint32_t> rec_of_user;
-    uint64_t eacc = 0;
     for (uint32_t u = 0; u < n_users; ++u) {
-        const auto& r = recs[u];
-        const uint32_t k = (uint32_t)r.movies.size();
-        if (k > CF_SPILL_MAX_K) cfcli::die("record with k > 3072 is outside the supported buckets");
-        rec_of_user[r.user] = u;   // a later record of the same user replaces it (:472)
-        m[u] = (int32_t)r.evals.size();
-        auto& ur = urat[r.user];
-        for (uint32_t j = 0; j < k; ++j) {
-            its.push_back(items.at[r.movies[j]]);
-            auto it = ur.find(r.movies[j]);
-            rats.push_back(it == ur.end() ? 0.0f : (float)it->second);   // operator[] default 0 (:259)
-            evals.push_back(j < r.evals.size() ? r.evals[j] : 0.0);
-            own_sigs.push_back(r.sigs[j]);
+        const uint64_t k = off[u + 1] - off[u];
+        if (k > CF_SPILL_MAX_K) cfcli::die("record with k > " + std::to_string(CF_SPILL_MAX_K) +
+                                           " is outside the supported buckets");
+        rec_of_user[recs.user[u]] = u;   // a later record of the same user replaces it (:472)
+        auto& ur = urat[recs.user[u]];
+        const uint64_t nm = recs.eval_off[u + 1] - recs.eval_off[u];
+        for (uint64_t j = 0; j < k; ++j) {
+            const uint32_t mv = recs.movies[off[u] + j];
+            its[off[u] + j] = items.at[mv];
+            auto it = ur.find(mv);
+            rats[off[u] + j] = it == ur.end() ? 0.0f : (float)it->second;   // operator[] default 0 (:259)
+            evals[off[u] + j] = j < nm ? recs.evals[recs.eval_off[u] + j] : 0.0;
         }
-        concat.insert(concat.end(), r.sigs.begin(), r.sigs.end());
-        off[u + 1] = its.size();
-        eoff[u] = eacc;
-        evecs.insert(evecs.end(), r.evecs.begin(), r.evecs.end());
-        eacc += r.evecs.size();
     }
-    if (evecs.empty()) evecs.push_back(0.0);
+    std::vector<double> evecs_pad;
+    const double* evecs_p = recs.evecs.data();
+    if (recs.evecs.empty()) {
+        evecs_pad.assign(1, 0.0);
+        evecs_p = evecs_pad.data();
+    }
     // movie vertices sampled like rand() % 100 < pct in apply (:221), BEFORE prediction:
     // only the rows of sampled movies are predicted (cf_predict_precomp_sel)
     std::mt19937 rng(seed);
@@ -91,7 +95,8 @@ int main(int argc, char** argv) {
     {
         size_t e = 0;
         for (uint32_t u = 0; u < n_users; ++u)
-            for (uint32_t mv : recs[u].movies) {
+            for (uint64_t j = off[u]; j < off[u + 1]; ++j) {
+                const uint32_t mv = recs.movies[j];
                 auto it = sampled.find(mv);
                 sel[e++] = it != sampled.end() && it->second;
             }
@@ -104,8 +109,8 @@ int main(int argc, char** argv) {
     // global compat table on every context, so out_res_ is identical to the one-device run's
     const char* env_dev = std::getenv("CF_DEVICES");
     const int n_dev = std::max(1, std::atoi(cfcli::opt(argc, argv, "devices", env_dev ? env_dev : "1").c_str()));
-    const double* tab = ref ? concat.data() : own_sigs.data();
-    const uint64_t tab_len = ref ? concat.size() : own_sigs.size();
+    const double* tab = sig_tab;          // both modes read the same flat array (CF_SIGS_COMPAT by row,
+    const uint64_t tab_len = off.back();  // CF_SIGS_OWN at off[u] + row)
     const int mode = ref ? CF_SIGS_COMPAT : CF_SIGS_OWN;
     const uint8_t* rsel = pct >= 100 ? nullptr : sel.data();
     if (n_dev == 1) {
@@ -113,7 +118,7 @@ int main(int argc, char** argv) {
         cfcli::upload_edges(ctx, items, edges);
         if (n_users)
             cfcli::check(ctx, cf_predict_precomp_sel(ctx, n_users, off.data(), its.data(), rats.data(), m.data(),
-                                                     evals.data(), eoff.data(), evecs.data(), tab, tab_len, mode,
+                                                     evals.data(), eoff.data(), evecs_p, tab, tab_len, mode,
                                                      rsel, mse.data(), kk.data(), nullptr),
                          "cf_predict_precomp_sel");
         cf_destroy(ctx);
@@ -131,7 +136,7 @@ int main(int argc, char** argv) {
         if (n_users)
             cfcli::check(ctxs[0], cf_predict_precomp_multi(ctxs.data(), n_dev, n_users, off.data(), its.data(),
                                                            rats.data(), m.data(), evals.data(), eoff.data(),
-                                                           evecs.data(), tab, tab_len, mode, rsel, mse.data(),
+                                                           evecs_p, tab, tab_len, mode, rsel, mse.data(),
                                                            kk.data(), nullptr, split.data()),
                          "cf_predict_precomp_multi");
         for (int d = 0; d < n_dev; ++d)
@@ -151,11 +156,11 @@ int main(int argc, char** argv) {
             int32_t c = 0;
             auto ri = rec_of_user.find(ur.first);
             if (ri != rec_of_user.end()) {
-                const auto& r = recs[ri->second];
-                for (uint32_t j = 0; j < r.movies.size(); ++j)
-                    if (r.movies[j] == movie) {
-                        e = mse[off[ri->second] + j];
-                        c = kk[off[ri->second] + j];
+                const uint32_t r = ri->second;
+                for (uint64_t j = off[r]; j < off[r + 1]; ++j)
+                    if (recs.movies[j] == movie) {
+                        e = mse[j];
+                        c = kk[j];
                         break;
                     }
             }

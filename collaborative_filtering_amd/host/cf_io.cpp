@@ -7,8 +7,13 @@
 #include <stdexcept>
 #include <thread>
 
+#include <atomic>
+
 #include <dirent.h>
+#include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <charconv>
@@ -49,6 +54,12 @@ std::string join(const std::string& dir, const std::string& name) {
     return ends_with(dir, "/") ? dir + name : dir + "/" + name;
 }
 
+}  // namespace
+
+bool parse_f64(const char*& p, const char* e, double& out);
+
+namespace {
+
 // Tokenizer over one line.
 struct Tok {
     const char* p;
@@ -65,11 +76,7 @@ struct Tok {
     }
     bool f64(double& v) {
         skip();
-        if (p < e && *p == '+') ++p;
-        auto r = std::from_chars(p, e, v);
-        if (r.ec != std::errc()) return false;
-        p = r.ptr;
-        return true;
+        return parse_f64(p, e, v);
     }
 };
 
@@ -108,10 +115,115 @@ std::string read_file(const std::string& path) {
     return ss.str();
 }
 
+// %g, precision 6.  Fast path for values exactly representable as float with 1e-3 <= |v| < 1e6
+// (every eigenvector entry, eigenvalue, sig and mse the writers format, bar the tiny ones): with
+// a 24-bit mantissa, n = |v| * 10^k (k <= 8, 10^k < 2^27) is EXACT in double, so nearbyint(n)
+// is the correctly rounded 6-digit significand with ties to even -- printf's and to_chars'
+// rounding of the exact binary value -- and the digits follow without any conversion error.
+// Everything else takes std::to_chars (tests/test_formats.py compares both on millions of
+// values, ties included).
+char* format_g6(char* p, double v) {
+    static const double kPow[9] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8};
+    const double a = std::fabs(v);
+    if (!(a >= 1e-3 && a < 1e6) || (double)(float)v != v)
+        return std::to_chars(p, p + 32, v, std::chars_format::general, 6).ptr;
+    int k = 0;
+    double n = a;
+    while (n < 1e5) n = a * kPow[++k];      // n in [1e5, 1e6), exact
+    double r = std::nearbyint(n);            // round half even
+    int x = 5 - k;                           // decimal exponent of the leading digit
+    if (r >= 1e6) {                          // 999999.5 -> 1000000: one more digit position
+        r = 1e5;
+        if (++x >= 6) return std::to_chars(p, p + 32, v, std::chars_format::general, 6).ptr;
+    }
+    uint32_t d = (uint32_t)r;
+    char dig[6];
+    for (int i = 5; i >= 0; --i) {
+        dig[i] = (char)('0' + d % 10);
+        d /= 10;
+    }
+    int nd = 6;                              // significant digits left after stripping zeros
+    while (nd > x + 1 && nd > 1 && dig[nd - 1] == '0') --nd;
+    if (v < 0) *p++ = '-';
+    if (x >= 0) {                            // ddd.ddd
+        for (int i = 0; i <= x; ++i) *p++ = dig[i];
+        if (nd > x + 1) {
+            *p++ = '.';
+            for (int i = x + 1; i < nd; ++i) *p++ = dig[i];
+        }
+    } else {                                 // 0.000ddd
+        *p++ = '0';
+        *p++ = '.';
+        for (int i = 0; i < -x - 1; ++i) *p++ = '0';
+        for (int i = 0; i < nd; ++i) *p++ = dig[i];
+    }
+    return p;
+}
+
 void append_g(std::string& out, double v) {
     char buf[64];
-    auto r = std::to_chars(buf, buf + sizeof(buf), v, std::chars_format::general, 6);
-    out.append(buf, r.ptr);
+    out.append(buf, format_g6(buf, v));
+}
+
+// strtod-exact parse of a decimal number: Clinger's fast path (mantissa < 2^53 and a power of
+// ten up to 10^22 are exact doubles, so one multiplication or division is correctly rounded)
+// for the short numbers of these files, std::from_chars otherwise.  Accepts what from_chars
+// accepts plus a leading '+'.
+bool parse_f64(const char*& p, const char* e, double& out) {
+    static const double kPow[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                    1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+    const char* q = p;
+    if (q < e && *q == '+') ++q;
+    const char* start = q;
+    bool neg = false;
+    if (q < e && *q == '-') {
+        neg = true;
+        ++q;
+    }
+    uint64_t w = 0;
+    int nd = 0, ex = 0;
+    bool any = false;
+    while (q < e && (unsigned)(*q - '0') < 10) {
+        if (nd < 19) w = w * 10 + (uint64_t)(*q - '0'), nd += (w != 0);
+        else ++ex;
+        ++q;
+        any = true;
+    }
+    if (q < e && *q == '.') {
+        ++q;
+        while (q < e && (unsigned)(*q - '0') < 10) {
+            if (nd < 19) {
+                w = w * 10 + (uint64_t)(*q - '0');
+                nd += (w != 0);
+                --ex;
+            }
+            ++q;
+            any = true;
+        }
+    }
+    if (q < e && (*q == 'e' || *q == 'E')) {
+        const char* t = q + 1;
+        bool eneg = false;
+        if (t < e && (*t == '+' || *t == '-')) eneg = *t++ == '-';
+        int ev = 0;
+        bool edig = false;
+        while (t < e && (unsigned)(*t - '0') < 10 && ev < 10000) ev = ev * 10 + (*t++ - '0'), edig = true;
+        if (edig) {
+            ex += eneg ? -ev : ev;
+            q = t;
+        }
+    }
+    if (any && nd < 19 && w < (1ull << 53) && ex >= -22 && ex <= 22 && (q == e || (unsigned)(*q - '0') >= 10)) {
+        double d = (double)w;
+        d = ex < 0 ? d / kPow[-ex] : d * kPow[ex];
+        out = neg ? -d : d;
+        p = q;
+        return true;
+    }
+    auto r = std::from_chars(start, e, out);
+    if (r.ec != std::errc()) return false;
+    p = r.ptr;
+    return true;
 }
 
 void append_u(std::string& out, uint64_t v) {
@@ -255,34 +367,6 @@ namespace {
 
 constexpr char kEigenMagic[8] = {'C', 'F', 'E', 'I', 'G', 'E', 'N', '1'};
 
-// One 3-line text record (load_precomputed_data's state machine, local_calc_precomp.cpp:
-// 426-476) from its three line spans; false on a malformed line (the reference asserts).
-bool parse_eigen_record(const char* const* lb, const char* const* le, EigenRecord& cur) {
-    uint32_t kk = 0, mm = 0;
-    bool ok = true;
-    {   // "uid k m" + "movie sig" x k (:426-442)
-        Tok t{lb[0], le[0]};
-        if (!t.u32(cur.user) || !t.u32(kk) || !t.u32(mm)) return false;
-        cur.movies.resize(kk);
-        cur.sigs.resize(kk);
-        for (uint32_t i = 0; i < kk; ++i)
-            if (!t.u32(cur.movies[i]) || !t.f64(cur.sigs[i])) ok = false;   // assert (:434)
-    }
-    {   // m eigenvalues (:444-452)
-        Tok t{lb[1], le[1]};
-        cur.evals.resize(mm);
-        for (uint32_t i = 0; i < mm; ++i)
-            if (!t.f64(cur.evals[i])) ok = false;   // assert (:447)
-    }
-    {   // k x m eigenvectors (:454-476)
-        Tok t{lb[2], le[2]};
-        cur.evecs.resize((size_t)kk * mm);
-        for (size_t i = 0; i < (size_t)kk * mm; ++i)
-            if (!t.f64(cur.evecs[i])) ok = false;   // assert (:462)
-    }
-    return ok;
-}
-
 int resolve_threads(int n_threads) {
     if (n_threads > 0) return n_threads;
     const unsigned h = std::thread::hardware_concurrency();
@@ -301,70 +385,183 @@ void parallel_for(int n, F&& f) {
     for (auto& th : pool) th.join();
 }
 
-std::vector<EigenRecord> load_eigen_binary(const std::string& text, const std::string& path) {
-    std::vector<EigenRecord> out;
-    size_t pos = sizeof(kEigenMagic);
-    auto take = [&](void* dst, size_t bytes) {
-        if (pos + bytes > text.size()) throw std::runtime_error("truncated binary out_eigen_ " + path);
-        std::memcpy(dst, text.data() + pos, bytes);
-        pos += bytes;
-    };
-    uint64_t n = 0;
-    take(&n, sizeof(n));
-    out.resize(n);
-    std::vector<float> buf;
-    for (auto& r : out) {
-        uint32_t hdr[3];
-        take(hdr, sizeof(hdr));
-        const uint32_t k = hdr[1], m = hdr[2];
-        r.user = hdr[0];
-        r.movies.resize(k);
-        take(r.movies.data(), sizeof(uint32_t) * k);
-        auto floats = [&](std::vector<double>& dst, size_t cnt) {
-            buf.resize(cnt);
-            take(buf.data(), sizeof(float) * cnt);
-            dst.assign(buf.begin(), buf.end());
-        };
-        floats(r.sigs, k);
-        floats(r.evals, m);
-        floats(r.evecs, (size_t)k * m);
+// Read-only mapping of a whole file (empty files map to nothing).
+struct Mapped {
+    const char* p = nullptr;
+    size_t n = 0;
+    explicit Mapped(const std::string& path) {
+        const int fd = ::open(path.c_str(), O_RDONLY);
+        if (fd < 0) throw std::runtime_error("cannot open " + path);
+        struct stat st;
+        if (fstat(fd, &st) != 0) {
+            ::close(fd);
+            throw std::runtime_error("cannot stat " + path);
+        }
+        n = (size_t)st.st_size;
+        if (n) {
+            void* v = mmap(nullptr, n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+            if (v == MAP_FAILED) {
+                ::close(fd);
+                throw std::runtime_error("cannot map " + path);
+            }
+            madvise(v, n, MADV_SEQUENTIAL | MADV_WILLNEED);
+            p = static_cast<const char*>(v);
+        }
+        ::close(fd);
     }
-    return out;
+    ~Mapped() {
+        if (p) munmap(const_cast<char*>(p), n);
+    }
+};
+
+template <class T>
+void exclusive_scan_into(std::vector<uint64_t>& off, const std::vector<T>& cnt) {
+    off.assign(cnt.size() + 1, 0);
+    for (size_t i = 0; i < cnt.size(); ++i) off[i + 1] = off[i] + (uint64_t)cnt[i];
+}
+
+void flat_resize(EigenFlat& F, const std::vector<uint32_t>& k) {
+    exclusive_scan_into(F.off, k);
+    std::vector<uint64_t> km(k.size());
+    for (size_t r = 0; r < k.size(); ++r) km[r] = (uint64_t)k[r] * (uint64_t)std::max(F.m[r], 0);
+    exclusive_scan_into(F.eval_off, F.m);
+    exclusive_scan_into(F.evec_off, km);
+    F.movies.resize(F.off.back());
+    F.sigs.resize(F.off.back());
+    F.evals.resize(F.eval_off.back());
+    F.evecs.resize(F.evec_off.back());
+}
+
+void load_flat_binary(const Mapped& f, const std::string& path, int T, EigenFlat& F) {
+    size_t pos = sizeof(kEigenMagic);
+    auto need = [&](size_t bytes) {
+        if (pos + bytes > f.n) throw std::runtime_error("truncated binary out_eigen_ " + path);
+    };
+    need(sizeof(uint64_t));
+    uint64_t n = 0;
+    std::memcpy(&n, f.p + pos, sizeof(n));
+    pos += sizeof(n);
+    // hop over the record headers: uid k m, then k movies, k sigs, m evals, k*m evecs (4 B each)
+    std::vector<size_t> at(n);
+    std::vector<uint32_t> k(n);
+    F.user.resize(n);
+    F.m.resize(n);
+    for (uint64_t r = 0; r < n; ++r) {
+        uint32_t hdr[3];
+        need(sizeof(hdr));
+        std::memcpy(hdr, f.p + pos, sizeof(hdr));
+        F.user[r] = hdr[0];
+        k[r] = hdr[1];
+        F.m[r] = (int32_t)hdr[2];
+        at[r] = pos + sizeof(hdr);
+        const size_t body = 4 * ((size_t)2 * hdr[1] + hdr[2] + (size_t)hdr[1] * hdr[2]);
+        need(sizeof(hdr) + body);
+        pos += sizeof(hdr) + body;
+    }
+    flat_resize(F, k);
+    parallel_for(T, [&](int t) {
+        const size_t r0 = n * t / T, r1 = n * (t + 1) / T;
+        for (size_t r = r0; r < r1; ++r) {
+            const char* q = f.p + at[r];
+            const size_t kk = k[r], mm = (size_t)F.m[r];
+            std::memcpy(F.movies.data() + F.off[r], q, 4 * kk);
+            q += 4 * kk;
+            auto widen = [&](double* dst, size_t cnt) {
+                for (size_t i = 0; i < cnt; ++i) {
+                    float v;
+                    std::memcpy(&v, q + 4 * i, 4);
+                    dst[i] = v;
+                }
+                q += 4 * cnt;
+            };
+            widen(F.sigs.data() + F.off[r], kk);
+            widen(F.evals.data() + F.eval_off[r], mm);
+            widen(F.evecs.data() + F.evec_off[r], kk * mm);
+        }
+    });
+}
+
+void load_flat_text(const Mapped& f, const std::string& path, int T, EigenFlat& F) {
+    // non-empty line spans, found in parallel over byte ranges
+    std::vector<std::vector<const char*>> lb(T), le(T);
+    parallel_for(T, [&](int t) {
+        const char* beg = f.p + f.n * t / T;
+        const char* end = f.p + f.n * (t + 1) / T;
+        // a range owns the lines that START in it
+        if (t > 0 && beg[-1] != '\n') {
+            const char* nl = static_cast<const char*>(std::memchr(beg, '\n', (size_t)(f.p + f.n - beg)));
+            beg = nl ? nl + 1 : f.p + f.n;
+        }
+        const char* fe = f.p + f.n;
+        const char* p = beg;
+        while (p < end) {
+            const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(fe - p)));
+            if (!nl) nl = fe;
+            if (nl > p) {
+                lb[t].push_back(p);
+                le[t].push_back(nl);
+            }
+            p = nl + 1;
+        }
+    });
+    std::vector<const char*> B, E;
+    for (int t = 0; t < T; ++t) {
+        B.insert(B.end(), lb[t].begin(), lb[t].end());
+        E.insert(E.end(), le[t].begin(), le[t].end());
+    }
+    const size_t n = B.size() / 3;   // a trailing partial record is dropped (state machine)
+    std::vector<uint32_t> k(n);
+    F.user.resize(n);
+    F.m.resize(n);
+    std::vector<char> bad(T, 0);
+    parallel_for(T, [&](int t) {   // "uid k m" of every record
+        for (size_t r = n * t / T; r < n * (t + 1) / T; ++r) {
+            Tok tk{B[3 * r], E[3 * r]};
+            uint32_t mm = 0;
+            if (!tk.u32(F.user[r]) || !tk.u32(k[r]) || !tk.u32(mm)) bad[t] = 1;
+            F.m[r] = (int32_t)mm;
+        }
+    });
+    for (char b : bad)
+        if (b) throw std::runtime_error("malformed out_eigen_ record in " + path);
+    flat_resize(F, k);
+    parallel_for(T, [&](int t) {
+        for (size_t r = n * t / T; r < n * (t + 1) / T; ++r) {
+            const size_t kk = k[r], mm = (size_t)F.m[r];
+            bool ok = true;
+            Tok a{B[3 * r], E[3 * r]};
+            uint32_t skip;
+            a.u32(skip), a.u32(skip), a.u32(skip);
+            for (size_t i = 0; i < kk; ++i)   // movie sig pairs (:426-442)
+                ok &= a.u32(F.movies[F.off[r] + i]) && a.f64(F.sigs[F.off[r] + i]);
+            Tok b{B[3 * r + 1], E[3 * r + 1]};   // m eigenvalues (:444-452)
+            for (size_t i = 0; i < mm; ++i) ok &= b.f64(F.evals[F.eval_off[r] + i]);
+            Tok c{B[3 * r + 2], E[3 * r + 2]};   // k x m eigenvectors (:454-476)
+            double* dst = F.evecs.data() + F.evec_off[r];
+            for (size_t i = 0; i < kk * mm; ++i) ok &= c.f64(dst[i]);
+            if (!ok) bad[t] = 1;   // the reference asserts (:434, 447, 462)
+        }
+    });
+    for (char b : bad)
+        if (b) throw std::runtime_error("malformed out_eigen_ record in " + path);
 }
 
 }  // namespace
 
-std::vector<EigenRecord> load_eigen_file(const std::string& path, int n_threads) {
-    const std::string text = read_file(path);
-    if (text.size() >= sizeof(kEigenMagic) && std::memcmp(text.data(), kEigenMagic, sizeof(kEigenMagic)) == 0)
-        return load_eigen_binary(text, path);
-    // non-empty line spans, then records of 3 lines parsed in parallel over record ranges
-    std::vector<const char*> lb, le;
-    {
-        const char* p = text.data();
-        const char* end = p + text.size();
-        while (p < end) {
-            const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(end - p)));
-            if (!nl) nl = end;
-            if (nl > p) {
-                lb.push_back(p);
-                le.push_back(nl);
-            }
-            p = nl + 1;
-        }
+EigenFlat load_eigen_flat(const std::string& path, int n_threads) {
+    Mapped f(path);
+    EigenFlat F;
+    const int T = resolve_threads(n_threads);
+    if (f.n >= sizeof(kEigenMagic) && std::memcmp(f.p, kEigenMagic, sizeof(kEigenMagic)) == 0)
+        load_flat_binary(f, path, T, F);
+    else
+        load_flat_text(f, path, T, F);
+    if (F.off.empty()) {   // no records
+        F.off.assign(1, 0);
+        F.eval_off.assign(1, 0);
+        F.evec_off.assign(1, 0);
     }
-    const size_t n_rec = lb.size() / 3;   // a trailing partial record is dropped (state machine)
-    std::vector<EigenRecord> out(n_rec);
-    const int T = (int)std::min<size_t>((size_t)resolve_threads(n_threads), std::max<size_t>(n_rec, 1));
-    std::vector<char> bad(T, 0);
-    parallel_for(T, [&](int t) {
-        const size_t r0 = n_rec * t / T, r1 = n_rec * (t + 1) / T;
-        for (size_t r = r0; r < r1; ++r)
-            if (!parse_eigen_record(&lb[3 * r], &le[3 * r], out[r])) bad[t] = 1;
-    });
-    for (char b : bad)
-        if (b) throw std::runtime_error("malformed out_eigen_ record in " + path);
-    return out;
+    return F;
 }
 
 void write_eigen_file(const std::string& path, bool append, int n_threads, bool binary, uint32_t n_users,
@@ -390,23 +587,57 @@ void write_eigen_file(const std::string& path, bool append, int n_threads, bool 
         }
         return;
     }
-    // text: contiguous user ranges formatted in parallel, written in order
+    // text: chunks of users formatted in parallel; chunk c lands at the sum of the sizes of
+    // chunks 0..c-1, published along a chain as soon as each chunk is formatted, and every
+    // thread pwrite()s its own chunk there -- formatting and writing overlap, no serial writer
+    f.close();   // created (or truncated) above; appended records start at its current end
+    const int wfd = ::open(path.c_str(), O_WRONLY);
+    if (wfd < 0) throw std::runtime_error("cannot open " + path);
+    const uint64_t base = append ? (uint64_t)::lseek(wfd, 0, SEEK_END) : 0;
     const int T = (int)std::min<uint32_t>((uint32_t)resolve_threads(n_threads), std::max<uint32_t>(n_users, 1));
-    const uint32_t chunk = 4096;   // users per formatting task
+    const uint32_t chunk = 256;    // users per formatting task (~4-8 MB of text at k ~ 100)
     const uint32_t n_chunks = (n_users + chunk - 1) / chunk;
-    for (uint32_t c0 = 0; c0 < n_chunks; c0 += (uint32_t)T) {
-        const int nt = (int)std::min<uint32_t>((uint32_t)T, n_chunks - c0);
-        std::vector<std::string> part(nt);
-        parallel_for(nt, [&](int t) {
-            const uint32_t u0 = (c0 + t) * chunk, u1 = std::min(n_users, u0 + chunk);
+    std::vector<uint64_t> start(n_chunks + 1, 0);
+    std::vector<std::atomic<int>> ready(n_chunks + 1);
+    for (auto& r : ready) r.store(0);
+    ready[0].store(1);
+    std::atomic<bool> failed{false};
+    std::atomic<uint32_t> next{0};
+    parallel_for(T, [&](int) {
+        std::string buf;
+        for (;;) {
+            const uint32_t c = next.fetch_add(1);
+            if (c >= n_chunks) break;
+            buf.clear();
+            const uint32_t u0 = c * chunk, u1 = std::min(n_users, u0 + chunk);
+            uint64_t vals = 0;
+            for (uint32_t u = u0; u < u1; ++u) {
+                const uint64_t k = off[u + 1] - off[u];
+                vals += 2 * k + (uint64_t)m[u] * (k + 1);
+            }
+            buf.reserve(12 * vals + 64);   // %g of 6 digits + sign + separator
             for (uint32_t u = u0; u < u1; ++u) {
                 const uint32_t k = (uint32_t)(off[u + 1] - off[u]);
-                append_eigen_record(part[t], uid[u], k, (uint32_t)m[u], movies + off[u], sigs + off[u],
-                                    evals + off[u], evecs + eoff[u]);
+                append_eigen_record(buf, uid[u], k, (uint32_t)m[u], movies + off[u], sigs + off[u], evals + off[u],
+                                    evecs + eoff[u]);
             }
-        });
-        for (auto& p : part) f.write(p.data(), (std::streamsize)p.size());
-    }
+            // chunks are claimed in order, so the chain below waits only on formatting in flight
+            while (!ready[c].load(std::memory_order_acquire)) std::this_thread::yield();
+            start[c + 1] = start[c] + buf.size();
+            ready[c + 1].store(1, std::memory_order_release);
+            size_t done = 0;
+            while (done < buf.size()) {
+                const ssize_t w = ::pwrite(wfd, buf.data() + done, buf.size() - done, (off_t)(base + start[c] + done));
+                if (w <= 0) {
+                    failed = true;
+                    break;
+                }
+                done += (size_t)w;
+            }
+        }
+    });
+    ::close(wfd);
+    if (failed) throw std::runtime_error("write failed: " + path);
 }
 
 }  // namespace cfio
@@ -429,26 +660,57 @@ extern "C" int cfh_write_eigen(const char* path, int append, int n_threads, int 
 // receives, per record, uid, k, m, then movies, sigs, evals, evecs as doubles (cap doubles).
 extern "C" int64_t cfh_load_eigen(const char* path, int n_threads, double* flat, int64_t cap) {
     try {
-        const auto recs = cfio::load_eigen_file(path, n_threads);
+        const auto F = cfio::load_eigen_flat(path, n_threads);
+        if (!flat) return (int64_t)F.size();
         int64_t pos = 0;
         auto put = [&](double v) {
             if (flat && pos < cap) flat[pos] = v;
             ++pos;
         };
-        for (const auto& r : recs) {
-            put(r.user);
-            put((double)r.movies.size());
-            put((double)r.evals.size());
-            for (auto v : r.movies) put(v);
-            for (auto v : r.sigs) put(v);
-            for (auto v : r.evals) put(v);
-            for (auto v : r.evecs) put(v);
+        for (size_t r = 0; r < F.size(); ++r) {
+            const uint64_t k = F.off[r + 1] - F.off[r];
+            put(F.user[r]);
+            put((double)k);
+            put((double)F.m[r]);
+            for (uint64_t i = F.off[r]; i < F.off[r + 1]; ++i) put(F.movies[i]);
+            for (uint64_t i = F.off[r]; i < F.off[r + 1]; ++i) put(F.sigs[i]);
+            for (uint64_t i = F.eval_off[r]; i < F.eval_off[r + 1]; ++i) put(F.evals[i]);
+            for (uint64_t i = F.evec_off[r]; i < F.evec_off[r + 1]; ++i) put(F.evecs[i]);
         }
         if (flat && pos > cap) return -2;
-        return (int64_t)recs.size();
+        return (int64_t)F.size();
     } catch (const std::exception&) {
         return -1;
     }
+}
+
+// Formatting / parsing probes for tests/test_formats.py: format_g6 (the writers' %g) and
+// parse_f64 (the readers' strtod) over arrays.
+extern "C" int64_t cfh_format_many(const double* v, int64_t n, char* out, int64_t cap) {
+    int64_t pos = 0;
+    char buf[64];
+    for (int64_t i = 0; i < n; ++i) {
+        char* e = cfio::format_g6(buf, v[i]);
+        const int64_t len = e - buf;
+        if (pos + len + 1 > cap) return -1;
+        std::memcpy(out + pos, buf, (size_t)len);
+        pos += len;
+        out[pos++] = '\n';
+    }
+    return pos;
+}
+
+extern "C" int64_t cfh_parse_many(const char* text, int64_t len, double* out, int64_t cap) {
+    const char* p = text;
+    const char* e = text + len;
+    int64_t n = 0;
+    while (p < e && n < cap) {
+        while (p < e && (*p == ' ' || *p == '\n')) ++p;
+        if (p >= e) break;
+        if (!cfio::parse_f64(p, e, out[n])) return -1;
+        ++n;
+    }
+    return n;
 }
 
 // C entry points used by the Python side (tests compare the formatting with printf).

@@ -9,7 +9,9 @@
 
 #include <cstdint>
 #include <string>
+#include <memory>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 namespace cfio {
@@ -24,6 +26,8 @@ std::string read_file(const std::string& path);
 
 // %g with precision 6, exactly as `std::ostream << double` with default flags.
 void append_g(std::string& out, double v);
+char* format_g6(char* p, double v);                        // the same into p, returns the end
+bool parse_f64(const char*& p, const char* e, double& out);   // strtod-exact decimal parse
 void append_u(std::string& out, uint64_t v);
 
 // A movielens rating triplet (user id already remapped to uimax - uid where asked).
@@ -74,21 +78,47 @@ struct IdMap {
     uint32_t size() const { return (uint32_t)ids.size(); }
 };
 
-// out_eigen_ record (README.md:14-19; precompute_local_threads.cpp:196-210).
-struct EigenRecord {
-    uint32_t user = 0;
-    std::vector<uint32_t> movies;   // row order of the block
-    std::vector<double> sigs;
-    std::vector<double> evals;      // m values
-    std::vector<double> evecs;      // k*m row-major
-};
+// out_eigen_ record writer (README.md:14-19; precompute_local_threads.cpp:196-210).
 void append_eigen_record(std::string& out, uint32_t user, uint32_t k, uint32_t m,
                          const uint32_t* movies, const float* sigs, const float* evals,
                          const float* evecs);
-// load_precomputed_data (local_calc_precomp.cpp:406-482): the 3-line state machine, with the
-// records parsed on n_threads threads (0 = hardware concurrency).  A file that starts with
-// "CFEIGEN1" is the binary form written by write_eigen_file(binary = true).
-std::vector<EigenRecord> load_eigen_file(const std::string& path, int n_threads = 0);
+// load_precomputed_data (local_calc_precomp.cpp:406-482; its 3-line state machine for text, or
+// the "CFEIGEN1" binary form of write_eigen_file) straight into flat arrays (no per-record
+// vectors): the file is mapped,
+// record boundaries found in parallel, and every record parsed (text) or widened (binary) into
+// its place on n_threads threads.  Record r of the n in file order: user[r], k = off[r+1] -
+// off[r] movies / sigs at off[r], m[r] eigenvalues at eval_off[r], its k x m row-major block at
+// evec_off[r].
+// Allocator whose resize() leaves elements uninitialised: the loader's threads write (first
+// touch) every element of the big arrays themselves instead of one thread zeroing them first.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        if constexpr (sizeof...(A) == 0) ::new ((void*)p) U;
+        else ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+template <class T>
+using RawVec = std::vector<T, NoInitAlloc<T>>;
+
+struct EigenFlat {
+    std::vector<uint32_t> user;
+    std::vector<uint64_t> off;        // n + 1, prefix of k
+    std::vector<int32_t> m;
+    RawVec<uint32_t> movies;
+    RawVec<double> sigs;
+    std::vector<uint64_t> eval_off;   // n + 1, prefix of m
+    RawVec<double> evals;
+    std::vector<uint64_t> evec_off;   // n + 1, prefix of k * m
+    RawVec<double> evecs;
+    size_t size() const { return user.size(); }
+};
+EigenFlat load_eigen_flat(const std::string& path, int n_threads = 0);
 // out_eigen_ writer (precompute_local_threads.cpp:196-211): text records formatted on
 // n_threads threads (contiguous user ranges, written in user order), or the binary form
 // (the reference's own TODO, README.md:29).

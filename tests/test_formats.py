@@ -28,6 +28,59 @@ def test_g_format_matches_printf():
     assert fmt(math.nan) in ("nan", "-nan")
 
 
+def _many(values):
+    lib = ctypes.CDLL(_native.HOST_LIB_PATH)
+    lib.cfh_format_many.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]
+    lib.cfh_format_many.restype = ctypes.c_int64
+    v = np.ascontiguousarray(values, dtype=np.float64)
+    buf = ctypes.create_string_buffer(32 * len(v) + 16)
+    n = lib.cfh_format_many(v.ctypes.data, len(v), ctypes.addressof(buf), len(buf))
+    assert n > 0
+    return buf.raw[:n].decode().split("\n")[:-1]
+
+
+def test_g6_fast_path_matches_printf():
+    """The writers' %g (format_g6): its exact fast path for float values in [1e-3, 1e6) and the
+    to_chars fallback, against Python's printf-style %g (correctly rounded, ties to even), on
+    2M random floats across the range, exact decimal ties (j / 2^(t+1)), rounding carries
+    (999999.5 -> 1e+06) and the range edges."""
+    rng = np.random.default_rng(5)
+    e = rng.uniform(-4.0, 6.5, 2_000_000)
+    v = (np.sign(rng.standard_normal(e.size)) * 10.0 ** e).astype(np.float32).astype(np.float64)
+    ties = []
+    for t in range(0, 9):   # a = j / 2^(t+1), j odd: a * 10^t ends in .5 exactly
+        j = rng.integers(0, 2 ** 22, 4000) * 2 + 1
+        a = j / 2.0 ** (t + 1)
+        ties.append(a[(a >= 1e-3) & (a < 1e6)])
+    edge = [0.001, 0.0009999999, 999999.5, 999999.4, 99999.95, 9.999995, 0.00999999, 1e-3, 123456.5, 0.5, 1.0,
+            -0.0, 0.0, 1e6, 999999.0]
+    vals = np.concatenate([v] + ties + [np.array(edge, np.float64).astype(np.float32).astype(np.float64),
+                                        np.array([1.0000001, 0.1, 1 / 3.0, 2.0 / 3.0], np.float64)])
+    got = _many(vals)
+    want = ["%g" % x for x in vals]
+    bad = [(x, g, w) for x, g, w in zip(vals, got, want) if g != w]
+    assert not bad, bad[:10]
+
+
+def test_parse_f64_correctly_rounded():
+    """The readers' decimal parse (Clinger fast path + from_chars) returns Python's correctly
+    rounded float() on %g strings, long mantissas and exponents past the fast path."""
+    lib = ctypes.CDLL(_native.HOST_LIB_PATH)
+    lib.cfh_parse_many.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]
+    lib.cfh_parse_many.restype = ctypes.c_int64
+    rng = np.random.default_rng(6)
+    x = rng.standard_normal(300_000) * 10.0 ** rng.integers(-30, 30, 300_000)
+    strs = ["%g" % v for v in x[:100_000]] + ["%.17g" % v for v in x[100_000:200_000]] + \
+           ["%.12e" % v for v in x[200_000:]] + ["+1.5", "-0", "0.000123", "1e5", ".5", "12345678901234567890",
+                                                "1.2345678901234567890123", "4.9e-324"]
+    text = " ".join(strs).encode()
+    out = np.zeros(len(strs))
+    n = lib.cfh_parse_many(text, len(text), out.ctypes.data, len(out))
+    assert n == len(strs)
+    want = np.array([float(t) for t in strs])
+    assert np.array_equal(out.view(np.uint64), want.view(np.uint64))
+
+
 def _records(n_users, seed):
     rng = np.random.default_rng(seed)
     k = rng.integers(1, 40, n_users).astype(np.int64)
@@ -77,7 +130,7 @@ def test_eigen_text_parallel_writer_and_reader(tmp_path):
     """Text out_eigen_ formatted on 7 threads is byte-identical to 1 thread (records in user
     order), and the parallel parser returns the same records as the serial one."""
     lib = _host()
-    recs = _records(9000, 1)   # > 2 formatting chunks of 4096 users
+    recs = _records(9000, 1)   # > 4 formatting chunks of 2048 users, pwrite()n out of order
     _write(lib, tmp_path / "t1", recs, 1, False)
     _write(lib, tmp_path / "t7", recs, 7, False)
     b1, b7 = (tmp_path / "t1").read_bytes(), (tmp_path / "t7").read_bytes()
