@@ -75,7 +75,7 @@ def parse():
     p.add_argument("--c5", choices=["auto", "off", "only"], default="auto",
                    help="BASELINE config 5 sample (N=1, rank 0): power-law k mix through the LDS + spill paths")
     p.add_argument("--c5-users", type=int, default=1000)
-    p.add_argument("--c5-kmax", type=int, default=1536, help="clip of the config-5 sample (its p95 ~1.5k)")
+    p.add_argument("--c5-kmax", type=int, default=5000, help="cap of the config-5 degrees (SURVEY 8d: 5000)")
     return p.parse_args()
 
 
@@ -253,9 +253,9 @@ def main():
 
     if args.c5 == "only":
         with Context(dev_index) as cctx:
-            W, _, _ = train_graph(Context, dev_index, dev, torch, CONFIGS["c2"]["seed"], CONFIGS["c2"]["train_users"],
-                                  CONFIGS["c2"]["items"])
-            print(json.dumps(c5_leg(args, cctx, dev, torch, W.view(CONFIGS["c2"]["items"], -1))), flush=True)
+            W, _, _ = train_graph(Context, dev_index, dev, torch, CONFIGS["c4"]["seed"], CONFIGS["c4"]["train_users"],
+                                  CONFIGS["c4"]["items"])
+            print(json.dumps(c5_leg(args, cctx, dev, torch, W.view(CONFIGS["c4"]["items"], -1))), flush=True)
         return
     if args.knn2 == "only":
         with Context(dev_index) as kctx:
@@ -525,9 +525,9 @@ def main():
         result["prep"] = prep_leg(args, ctx, dev, torch)
     if solo and args.c5 == "auto":
         torch.cuda.empty_cache()
-        W, _, _ = train_graph(Context, dev_index, dev, torch, CONFIGS["c2"]["seed"], CONFIGS["c2"]["train_users"],
-                              CONFIGS["c2"]["items"])
-        result["config5"] = c5_leg(args, ctx, dev, torch, W.view(CONFIGS["c2"]["items"], -1))
+        W, _, _ = train_graph(Context, dev_index, dev, torch, CONFIGS["c4"]["seed"], CONFIGS["c4"]["train_users"],
+                              CONFIGS["c4"]["items"])
+        result["config5"] = c5_leg(args, ctx, dev, torch, W.view(CONFIGS["c4"]["items"], -1))
         del W
 
     if rank == 0:
@@ -689,8 +689,8 @@ def text_phases(wl):
 
 def c5_leg(args, ctx, dev, torch, W):
     """BASELINE config 5, bounded sample: a power-law degree mix (lognormal k, median 100,
-    p95 ~1.5k, clipped to [20, --c5-kmax]) through cf_eigen_run -- k <= 192 on the LDS
-    Jacobi path, larger k on the fp64 spill path -- on the config-2 item graph, then the
+    p95 ~1.5k, clipped to [20, --c5-kmax = 5000]) through cf_eigen_run -- k <= 192 on the LDS
+    Jacobi path, larger k on the fp64 spill path -- on the config-4 (50k-item) graph, then the
     predictor (cf_predict_run_f32, own sigs) over every rating of those users: k <= 192 on
     predict_kernel, larger k on the spill predictor.  Reports users/s and ratings/s of the
     mix and the per-path split (HIP events around each plan)."""
@@ -708,7 +708,7 @@ def c5_leg(args, ctx, dev, torch, W):
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     out = {"workload": f"BASELINE config 5 sample: {args.c5_users} users, lognormal k (median 100, "
                        f"sigma {sigma:.3f}, p95 {int(np.percentile(k, 95))}, max {int(k.max())}), "
-                       f"{n_items} items (config-2 knn2 graph), seed {seed}"}
+                       f"{n_items} items (config-4 knn2 graph), seed {seed}"}
     stream = torch.cuda.current_stream(dev)
     total_ms = total_pms = 0.0
     for name, sel in (("lds", k <= CF_MAX_K), ("spill", k > CF_MAX_K)):

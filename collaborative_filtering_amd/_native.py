@@ -18,7 +18,7 @@ CF_ERANGE = -4
 CF_SIGS_OWN = 0
 CF_SIGS_COMPAT = 1
 CF_MAX_K = 192
-CF_SPILL_MAX_K = 3072
+CF_SPILL_MAX_K = 5000
 CF_EIGEN_TRIDIAG = 0
 CF_EIGEN_JACOBI = 1
 CF_FILTER_CHEBY = 0

@@ -91,6 +91,11 @@ void cf_destroy(cf_ctx* ctx) {
         if (e) (void)hipEventDestroy(e);
     if (ctx->d_spill) (void)hipFree(ctx->d_spill);
     if (ctx->d_pspill) (void)hipFree(ctx->d_pspill);
+    if (ctx->pspill_meta_ev) {
+        (void)hipEventSynchronize(ctx->pspill_meta_ev);
+        (void)hipEventDestroy(ctx->pspill_meta_ev);
+    }
+    if (ctx->h_pspill_meta) (void)hipHostFree(ctx->h_pspill_meta);
     if (ctx->d_tri) (void)hipFree(ctx->d_tri);
     for (hipEvent_t& e : ctx->knn_ev)
         if (e) (void)hipEventDestroy(e);

@@ -38,7 +38,6 @@ namespace {
 
 constexpr int SP_T = 512;
 constexpr int SP_W = SP_T / 64;
-constexpr int SP_N = CF_SPILL_MAX_K;
 constexpr int SP_QB = 16;                        // QL iterations applied per pass over Z
 constexpr int SP_NB = 32;                        // Householder panel width (dlatrd block)
 constexpr int SP_CC = 32;                        // columns staged per trailing-update step
@@ -59,24 +58,36 @@ struct SpillArgs {
     float* evecs;
     double* work;
     uint64_t work_stride;    // doubles per workgroup slot (>= kmax^2)
+    uint64_t big_off;        // BIG launches: rc, rs, tau (kmax doubles each) at this slot offset
     unsigned int* counter;   // next spill user (zeroed before the launch)
     unsigned long long* phase;   // 8 counters (cf_debug_spill), summed by thread 0
     cf_spill_local loc;      // a8 modes (loc.mode = 0: compute_eigens of a user)
 };
 
-struct SpillSmem {
-    double d[SP_N];
-    double e[SP_N];
-    double rc[SP_N];
-    double rs[SP_N];
-    double tau[SP_N];
+// LDS of one workgroup.  NL = the largest k of the launch's layout.  Up to SP_NL (3072) the
+// per-row vectors rc / rs / tau live in LDS too; a BIG launch (SP_NL < k <= CF_SPILL_MAX_K)
+// keeps d / e (the QL recurrence's operands) and sig / perm in LDS and moves rc / rs / tau to
+// the user's HBM slot, with the 32-column staging tiles (which alias rc in the LDS layout) in
+// a dedicated region.
+constexpr int SP_NL = 3072;
+constexpr int SP_STAGE = 2 * 32 * 33;             // the largest staging use: two 32 x 33 tiles
+template <int NL, bool BIG>
+struct SpillSmemT {
+    double d[NL];
+    double e[NL];
+    double rc[BIG ? 1 : NL];
+    double rs[BIG ? 1 : NL];
+    double tau[BIG ? 1 : NL];
+    double stage[BIG ? SP_STAGE : 1];
     double vj[SP_NB], wj[SP_NB], xv[SP_NB], xw[SP_NB];
     double part[8 * 64];
-    float sig[SP_N];
-    int perm[SP_N];
+    float sig[NL];
+    int perm[NL];
     double red[SP_W + 4];
     int flag[4];
 };
+static_assert(sizeof(SpillSmemT<SP_NL, false>) <= 163840, "spill LDS");
+static_assert(sizeof(SpillSmemT<CF_SPILL_MAX_K, true>) <= 163840, "big spill LDS");
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -105,11 +116,17 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
     return t;
 }
 
+template <int NL, bool BIG>
 __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    SpillSmem& S = *reinterpret_cast<SpillSmem*>(smem_raw);
+    SpillSmemT<NL, BIG>& S = *reinterpret_cast<SpillSmemT<NL, BIG>*>(smem_raw);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     double* M = a.work + (size_t)blockIdx.x * a.work_stride;
+    // per-row vectors and the staging tiles (see SpillSmemT)
+    double* const rc = BIG ? M + a.big_off : S.rc;
+    double* const rs = BIG ? M + a.big_off + NL : S.rs;
+    double* const tau = BIG ? M + a.big_off + 2 * NL : S.tau;
+    double* const stage = BIG ? S.stage : S.rc;
     const double eps = 2.220446049250313e-16;   // 2^-52 (tql2)
 
     for (;;) {
@@ -209,18 +226,18 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 ds += (double)w;
             }
             ds = wave_sum(ds);
-            if (lane == 0) S.rs[i] = (ds == 0.0 && mode == 0) ? 1.0 : ds;   // (:137-140)
+            if (lane == 0) rs[i] = (ds == 0.0 && mode == 0) ? 1.0 : ds;   // (:137-140)
         }
         __syncthreads();
-        for (int i = tid; i < n; i += SP_T) S.rc[i] = sqrt(1.0 / S.rs[i]);   // (:149-153)
+        for (int i = tid; i < n; i += SP_T) rc[i] = sqrt(1.0 / rs[i]);   // (:149-153)
         __syncthreads();
         float* L2out = mode == 1 ? a.loc.l2 + a.loc.l2_off[u] : nullptr;
         for (int i = wave; i < n; i += SP_W) {
-            const double si = S.rc[i], di = S.rs[i];
+            const double si = rc[i], di = rs[i];
             double sq = 0.0;
             for (int j = lane; j < n; j += 64) {
                 const double l = (j == i ? di : 0.0) - (double)Wt[(size_t)i * n + j];
-                const double l2 = (si * l) * S.rc[j];   // (:155)
+                const double l2 = (si * l) * rc[j];   // (:155)
                 sq += l2 * l2;
                 if (L2out) L2out[(size_t)i * n + j] = (float)l2;   // unsymmetrised, for the w_lim pass
                 if (j <= i) {
@@ -283,11 +300,11 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 if (tid == 0) {
                     S.d[j] = ajj;
                     S.e[j] = beta;
-                    S.tau[j] = tj;
+                    tau[j] = tj;
                 }
                 for (int r = j + 1 + tid; r < n; r += SP_T) {
                     const double vr = (r == j + 1) ? 1.0 : colj[r] * scal;
-                    S.rc[r] = vr;
+                    rc[r] = vr;
                     colj[r] = vr;
                 }
                 __syncthreads();
@@ -302,7 +319,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     const int t = q >> 1;
                     const double* src = (q & 1) ? M + (size_t)(p + t) * n : Wp + (size_t)t * n;
                     double s = 0.0;
-                    for (int r = r0 + lane; r < n; r += 64) s += src[r] * S.rc[r];
+                    for (int r = r0 + lane; r < n; r += 64) s += src[r] * rc[r];
                     s = wave_sum(s);
                     if (lane == 0) {
                         if (q & 1)
@@ -334,17 +351,17 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                             for (int t = 0; t < 16; ++t) x[t] = mr[(size_t)(c + t) * n];
 #pragma unroll
                             for (int t = 0; t < 16; t += 4) {
-                                p0 += x[t] * S.rc[c + t];
-                                p1 += x[t + 1] * S.rc[c + t + 1];
-                                p2 += x[t + 2] * S.rc[c + t + 2];
-                                p3 += x[t + 3] * S.rc[c + t + 3];
+                                p0 += x[t] * rc[c + t];
+                                p1 += x[t + 1] * rc[c + t + 1];
+                                p2 += x[t + 2] * rc[c + t + 2];
+                                p3 += x[t + 3] * rc[c + t + 3];
                             }
                         }
-                        for (; c < c_hi; ++c) p0 += mr[(size_t)c * n] * S.rc[c];
+                        for (; c < c_hi; ++c) p0 += mr[(size_t)c * n] * rc[c];
                     }
                     const double ps = (p0 + p1) + (p2 + p3);
                     if (segs == 1) {
-                        if (r < n) S.rs[r] = ps;
+                        if (r < n) rs[r] = ps;
                     } else {
                         S.part[sg * (nrb * 64) + rb * 64 + lane] = ps;
                     }
@@ -354,7 +371,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 for (int r = r0 + tid; r < n; r += SP_T) {
                     double y;
                     if (segs == 1) {
-                        y = S.rs[r];
+                        y = rs[r];
                     } else {
                         y = 0.0;
                         for (int sg = 0; sg < segs; ++sg) y += S.part[sg * (nrb * 64) + (r - r0)];
@@ -362,11 +379,11 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     for (int t = 0; t < jj; ++t)
                         y -= M[(size_t)(p + t) * n + r] * S.xv[t] + Wp[(size_t)t * n + r] * S.xw[t];
                     y *= tj;
-                    S.rs[r] = y;
-                    yv += y * S.rc[r];
+                    rs[r] = y;
+                    yv += y * rc[r];
                 }
                 const double a2 = -0.5 * tj * block_sum(yv, S.red);
-                for (int r = tid; r < n; r += SP_T) Wp[(size_t)jj * n + r] = r >= r0 ? S.rs[r] + a2 * S.rc[r] : 0.0;
+                for (int r = tid; r < n; r += SP_T) Wp[(size_t)jj * n + r] = r >= r0 ? rs[r] + a2 * rc[r] : 0.0;
                 __syncthreads();
             }
             // trailing update A(q:n, q:n) -= V W^T + W V^T (q = p + jb), full square so the
@@ -377,7 +394,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             const int mq = n - q;
             if (mq > 0) {
                 const int nrb = (mq + 63) >> 6;
-                double* stg = S.rc;   // [SP_CC][2 * SP_NB]: V(c, t) then W(c, t)
+                double* stg = stage;   // [SP_CC][2 * SP_NB]: V(c, t) then W(c, t)
                 for (int pass = 0; pass < nrb; pass += SP_W) {
                     const int rb = pass + wave;
                     const int r = q + rb * 64 + lane;
@@ -720,7 +737,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         const unsigned long long t4 = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
         // ---- 4a. Z to row-major (in place, 32 x 32 tile pairs through LDS) ------------------
         {
-            double* buf = S.rc;   // two 32 x 33 tiles
+            double* buf = stage;   // two 32 x 33 tiles
             const int nt = (n + 31) >> 5;
             for (int I = 0; I < nt; ++I) {
                 for (int J = I; J < nt; ++J) {
@@ -745,8 +762,8 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         // V (T (V^T Z)).  Lane per column of the row-major Z; V rows staged in LDS and read as
         // wave-uniform broadcasts, the jb-vectors V^T z and T (V^T z) live in registers.
         {
-            double* Tm = S.rc;              // [SP_NB][SP_NB]
-            double* Gm = S.rc + SP_NB * SP_NB;
+            double* Tm = stage;              // [SP_NB][SP_NB]
+            double* Gm = stage + SP_NB * SP_NB;
             double* Vs = S.e;               // [SP_RC][SP_NB + 1]
             constexpr int VLD = SP_NB + 1;
             for (int p = ((n - 2) / SP_NB) * SP_NB; p >= 0; p -= SP_NB) {
@@ -765,7 +782,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 for (int idx = tid; idx < SP_NB * SP_NB; idx += SP_T) Tm[idx] = 0.0;
                 __syncthreads();
                 for (int i = 0; i < jb; ++i) {
-                    const double ti = S.tau[p + i];
+                    const double ti = tau[p + i];
                     if (tid < i) {
                         double s = 0.0;
                         for (int s_ = tid; s_ < i; ++s_) s += Tm[tid * SP_NB + s_] * Gm[s_ * SP_NB + i];
@@ -862,7 +879,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     s1 += Zb[(size_t)(r + 1) * n + c];
                 }
                 if (r < n) s0 += Zb[(size_t)r * n + c];
-                S.rs[c] = (s0 + s1) < 0.0 ? -1.0 : 1.0;
+                rs[c] = (s0 + s1) < 0.0 ? -1.0 : 1.0;
             }
         }
         __syncthreads();
@@ -887,7 +904,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         for (size_t idx = tid; idx < (size_t)n * mm; idx += SP_T) {
             const int i = (int)(idx / mm), r = (int)(idx - (size_t)i * mm);
             const int j = S.perm[r];
-            Wt[idx] = (float)(Zb[(size_t)i * n + j] * S.rs[j]);
+            Wt[idx] = (float)(Zb[(size_t)i * n + j] * rs[j]);
         }
         __syncthreads();
         if (a.phase && tid == 0) {
@@ -912,9 +929,16 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     if (b.count == 0) return CF_OK;
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    const uint64_t stride = 2ull * b.kmax * b.kmax + (uint64_t)SP_NB * b.kmax + 4ull * SP_QB * (b.kmax + 2 * SP_QB + 4) + 64;
+    const bool big = b.kmax > (uint32_t)SP_NL;
+    if (b.kmax > (uint32_t)CF_SPILL_MAX_K) return cf_set_error(ctx, CF_ERANGE, "spill eigen: k above CF_SPILL_MAX_K");
+    const uint64_t base_stride =
+        2ull * b.kmax * b.kmax + (uint64_t)SP_NB * b.kmax + 4ull * SP_QB * (b.kmax + 2 * SP_QB + 4) + 64;
+    const uint64_t stride = base_stride + (big ? 3ull * CF_SPILL_MAX_K : 0ull);
     const uint64_t slot_bytes = stride * sizeof(double);
-    const uint64_t budget = 24ull << 30;   // workspace cap; fewer resident users beyond it
+    // workspace cap: a fifth of the free HBM (>= 24 GB), fewer resident users beyond it
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    const uint64_t budget = std::max<uint64_t>(24ull << 30, (uint64_t)free_b / 5);
     uint32_t grid = std::min<uint32_t>(b.count, (uint32_t)n_cu);
     grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(grid, budget / slot_bytes));
     const size_t need = (size_t)grid * slot_bytes + 256;
@@ -946,14 +970,21 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     a.counter = reinterpret_cast<unsigned int*>(ctx->d_spill);
     a.work = reinterpret_cast<double*>(static_cast<char*>(ctx->d_spill) + 256);
     a.work_stride = stride;
+    a.big_off = base_stride;
     if (loc) a.loc = *loc;
     a.phase = ctx->spill_debug ? reinterpret_cast<unsigned long long*>(static_cast<char*>(ctx->d_spill) + 64) : nullptr;
     CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), stream));
-    const size_t lds = sizeof(SpillSmem);
-    static_assert(sizeof(SpillSmem) <= 163840, "spill LDS");
-    CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_spill_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)lds));
-    hipLaunchKernelGGL(eigen_spill_kernel, dim3(grid), dim3(SP_T), lds, stream, a);
+    if (big) {
+        const size_t lds = sizeof(SpillSmemT<CF_SPILL_MAX_K, true>);
+        CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_spill_kernel<CF_SPILL_MAX_K, true>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((eigen_spill_kernel<CF_SPILL_MAX_K, true>), dim3(grid), dim3(SP_T), lds, stream, a);
+    } else {
+        const size_t lds = sizeof(SpillSmemT<SP_NL, false>);
+        CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_spill_kernel<SP_NL, false>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((eigen_spill_kernel<SP_NL, false>), dim3(grid), dim3(SP_T), lds, stream, a);
+    }
     CF_HIP_CHECK(ctx, hipGetLastError());
     return CF_OK;
 }

@@ -36,6 +36,10 @@ struct cf_ctx {
     // predictor spill-path workspace (per-user Q / Gbar slots, per-workgroup LDL^T), grown on demand.
     void* d_pspill = nullptr;
     size_t pspill_bytes = 0;
+    // its per-chunk slot tables: pinned host staging buffer and the event of the last copy
+    void* h_pspill_meta = nullptr;
+    size_t pspill_meta_bytes = 0;
+    hipEvent_t pspill_meta_ev = nullptr;
     // tridiagonal eigen path scratch (T, QL records), grown on demand; eigen method
     void* d_tri = nullptr;
     size_t tri_bytes = 0;

@@ -33,6 +33,8 @@
 //
 // Output per rating (row r of user u, entry base + r): mse = (float)(r - clamp(pred))^2,
 // kk = |C|, pred (:318-359).
+#include <cstring>
+
 #include "cf_internal.h"
 #include "cf_ldlt.hpp"
 
@@ -67,10 +69,11 @@ struct SpArgs {
     float* mse;
     int32_t* kk;
     double* pred;
-    double* ws;              // per slot: Q0, Q1 (Q and P = Q Q^T), Gbar, Gt (kmax^2 each), g, h, PG, PH
-    size_t slot_d;
-    int* wsi;                // per slot: lim[kmax], cpos[kmax], hdr[4] = {Lu, basis, qsel, -}
-    size_t slot_i;
+    double* ws;              // per slot: Q0, Q1 (Q and P = Q Q^T), Gbar, Gt (k^2 each), g, h, PG, PH
+    const uint64_t* soff;    // per slot s of the chunk (nu + 1): doubles offset of its slot in ws
+    int* wsi;                // per slot: lim[k], cpos[k], hdr[4] = {Lu, basis, qsel, -}
+    const uint64_t* sioff;   // per slot (nu + 1): ints offset of its slot in wsi
+    const uint64_t* roff;    // per slot (nu + 1): first work item (= row) of the slot; roff[nu] items
     double* fa;              // per workgroup factorisation region
     size_t fa_d;
     unsigned int* counter;   // work-item counter of the predict kernel
@@ -224,15 +227,15 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
     const int k = (int)(a.item_off[u + 1] - base);
     const int m = a.m[u];
     const T* U = a.evecs + a.evec_off[u];
-    const size_t kk2 = (size_t)a.kmax * a.kmax;
-    double* slot = a.ws + s * a.slot_d;
+    const size_t kk2 = (size_t)k * k;   // slots are sized by the user's own k (soff)
+    double* slot = a.ws + a.soff[s];
     double* Qb[2] = {slot, slot + kk2};
     double* Gb = slot + 2 * kk2;   // Gbar = U^T U over [0, Lu), full, ld Lu
     double* Gt = slot + 3 * kk2;   // Gram of the current Q (steps > 0)
     double* gh = slot + 4 * kk2;   // g[Lu], h[Lu], PG[k], PH[k]
-    int* lim = a.wsi + s * a.slot_i;
-    int* cpos = lim + a.kmax;
-    int* hdr = cpos + a.kmax;
+    int* lim = a.wsi + a.sioff[s];
+    int* cpos = lim + k;
+    int* hdr = cpos + k;
 
     for (int j = tid; j < m; j += kT) s_ev[j] = (double)a.evals[base + j];
     if (tid == 0) s_hdr[0] = 2;
@@ -362,9 +365,10 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
     __shared__ double s_misc[4];
     __shared__ int s_tmp[kW];
     __shared__ unsigned int s_item;
+    __shared__ unsigned int s_slot;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     double* fa = a.fa + (size_t)blockIdx.x * a.fa_d;
-    const uint32_t total = a.nu * (uint32_t)a.kmax;
+    const uint64_t total = a.roff[a.nu];   // one work item per (slot, row)
     // Diagnostic counters (thread 0, s_memtime; no effect on outputs): cycles of
     // {0 sets + mean, 1 column filter, 2 P entries, 3 b and K, 4 Woodbury LDL^T, 5 dense
     // path}, counts {6 Woodbury, 7 dense, 8 sum nc (Woodbury), 9 np > 64,
@@ -378,25 +382,36 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
         pt = now;                                                           \
     }
     for (;;) {
-        if (tid == 0) s_item = atomicAdd(a.counter, 1u);
+        if (tid == 0) {
+            // claim an item, and find its slot in the chunk's row prefix (binary search)
+            const uint32_t w = atomicAdd(a.counter, 1u);
+            uint32_t lo = 0, hi = a.nu;
+            if (w < total)
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (a.roff[mid] <= w) lo = mid;
+                    else hi = mid;
+                }
+            s_item = w;
+            s_slot = lo;
+        }
         __syncthreads();
         const uint32_t w = s_item;
+        const uint32_t s = s_slot;
         __syncthreads();
         if (w >= total) break;   // every wave of every block reaches this exit
-        const uint32_t s = w / (uint32_t)a.kmax;
-        const int r = (int)(w - s * (uint32_t)a.kmax);
+        const int r = (int)(w - a.roff[s]);
         const uint32_t u = a.order[a.first + s];
         const uint64_t base = a.item_off[u];
         const int k = (int)(a.item_off[u + 1] - base);
-        if (r >= k) continue;   // block-uniform
         if (a.row_sel && !a.row_sel[base + r]) continue;   // --pct: movie not sampled (block-uniform)
         const int m = a.m[u];
         const T* U = a.evecs + a.evec_off[u];
-        const size_t kk2 = (size_t)a.kmax * a.kmax;
-        const double* slot = a.ws + s * a.slot_d;
-        const int* lim_t = a.wsi + s * a.slot_i;
-        const int* cpos = lim_t + a.kmax;
-        const int* hdr = cpos + a.kmax;
+        const size_t kk2 = (size_t)k * k;
+        const double* slot = a.ws + a.soff[s];
+        const int* lim_t = a.wsi + a.sioff[s];
+        const int* cpos = lim_t + k;
+        const int* hdr = cpos + k;
         const int Lu = hdr[0];
         const bool basis = hdr[1] != 0;
         const double* Q = slot + (hdr[2] ? kk2 : 0);
@@ -746,25 +761,61 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
     a.kk = d_kk;
     a.pred = d_pred;
     a.phase = ctx->d_phase;
-    // workspace: counter | factorisation regions | user slots (doubles) | slot ints
-    const size_t kk2 = (size_t)kmax * kmax;
-    a.slot_d = 4 * kk2 + 4 * (size_t)kmax;
-    a.slot_i = 2 * (size_t)kmax + 4;
+    // workspace: counter | chunk tables | factorisation regions | user slots (doubles) | slot
+    // ints.  Every user's slot is sized by its OWN k (4 k^2 + 4 k doubles, 2 k + 4 ints): a
+    // config-5 bucket spans k = 193 .. 5000, and kmax-sized slots would hold ~100x fewer users.
     a.fa_d = (size_t)(kmax + 2) * (kmax + 3) / 2;
-    // Slots: as many users per chunk as a third of the free HBM holds (288 GB per GPU: all
-    // of a config-5 shard's spill users at once, so the basis launch fills the chip),
-    // at least 8 GB.
     size_t free_b = 0, total_b = 0;
     CF_HIP_CHECK(ctx, hipMemGetInfo(&free_b, &total_b));
-    const size_t kSlotBudget = std::max<size_t>((size_t)8 << 30, (free_b + ctx->pspill_bytes) / 3);
-    const size_t kFaBudget = (size_t)4 << 30;
-    const uint32_t slots = (uint32_t)std::max<size_t>(1, std::min<size_t>(b.count, kSlotBudget / (a.slot_d * 8)));
+    const size_t avail = free_b + ctx->pspill_bytes;
+    // slots: as many users per chunk as a third of the free HBM holds (288 GB per GPU: all of
+    // a config-5 shard's spill users at once, so the basis launch fills the chip), >= 8 GB;
+    // factorisation regions: a tenth of it (>= 4 GB), 32 .. 512 persistent workgroups
+    const size_t kSlotBudget = std::max<size_t>((size_t)8 << 30, avail / 3);
+    const size_t kFaBudget = std::max<size_t>((size_t)4 << 30, avail / 10);
     const int blocks = (int)std::max<size_t>(32, std::min<size_t>(512, kFaBudget / (a.fa_d * 8)));
     const size_t fa_bytes = (size_t)blocks * a.fa_d * sizeof(double);
-    const size_t ws_bytes = (size_t)slots * a.slot_d * sizeof(double);
-    const size_t need = 256 + fa_bytes + ws_bytes + (size_t)slots * a.slot_i * sizeof(int);
+    // chunks over the bucket's users (plan order: largest k first), each within the budget
+    struct Chunk {
+        uint32_t u0, nu;
+        size_t meta;   // index of its tables in `meta` (3 x (nu + 1))
+    };
+    std::vector<Chunk> chunks;
+    std::vector<uint64_t> meta;
+    size_t ws_max = 0, wsi_max = 0;
+    for (uint32_t u0 = 0; u0 < b.count;) {
+        Chunk c{u0, 0, meta.size()};
+        uint64_t sd = 0, si = 0, rows = 0;
+        std::vector<uint64_t> t_sd{0}, t_si{0}, t_r{0};
+        while (u0 + c.nu < b.count) {
+            const uint32_t u = plan->h_order[b.first + u0 + c.nu];
+            const uint64_t k = plan->h_item_off[u + 1] - plan->h_item_off[u];
+            const uint64_t d = 4 * k * k + 4 * k;
+            if (c.nu > 0 && (sd + d) * sizeof(double) > kSlotBudget) break;
+            sd += d;
+            si += 2 * k + 4;
+            rows += k;
+            t_sd.push_back(sd);
+            t_si.push_back(si);
+            t_r.push_back(rows);
+            ++c.nu;
+        }
+        meta.insert(meta.end(), t_sd.begin(), t_sd.end());
+        meta.insert(meta.end(), t_si.begin(), t_si.end());
+        meta.insert(meta.end(), t_r.begin(), t_r.end());
+        ws_max = std::max(ws_max, (size_t)sd);
+        wsi_max = std::max(wsi_max, (size_t)si);
+        chunks.push_back(c);
+        u0 += c.nu;
+    }
+    const size_t meta_bytes = ((meta.size() * sizeof(uint64_t) + 255) / 256) * 256;
+    const size_t ws_bytes = ws_max * sizeof(double);
+    const size_t need = 256 + meta_bytes + fa_bytes + ws_bytes + wsi_max * sizeof(int);
     if (need > ctx->pspill_bytes) {
-        if (ctx->d_pspill) (void)hipFree(ctx->d_pspill);
+        if (ctx->d_pspill) {
+            CF_HIP_CHECK(ctx, hipStreamSynchronize(stream));   // earlier launches may still read it
+            (void)hipFree(ctx->d_pspill);
+        }
         ctx->d_pspill = nullptr;
         ctx->pspill_bytes = 0;
         CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_pspill, need));
@@ -772,17 +823,36 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
     }
     char* p = reinterpret_cast<char*>(ctx->d_pspill);
     a.counter = reinterpret_cast<unsigned int*>(p);
-    a.fa = reinterpret_cast<double*>(p + 256);
-    a.ws = reinterpret_cast<double*>(p + 256 + fa_bytes);
-    a.wsi = reinterpret_cast<int*>(p + 256 + fa_bytes + ws_bytes);
-    for (uint32_t u0 = 0; u0 < b.count; u0 += slots) {
-        a.first = b.first + u0;
-        a.nu = std::min(slots, b.count - u0);
+    uint64_t* d_meta = reinterpret_cast<uint64_t*>(p + 256);
+    a.fa = reinterpret_cast<double*>(p + 256 + meta_bytes);
+    a.ws = reinterpret_cast<double*>(p + 256 + meta_bytes + fa_bytes);
+    a.wsi = reinterpret_cast<int*>(p + 256 + meta_bytes + fa_bytes + ws_bytes);
+    // the tables go up in one asynchronous copy from the context's pinned staging buffer; the
+    // previous call's copy out of it has completed before it is overwritten (its event)
+    const size_t meta_n = meta.size() * sizeof(uint64_t);
+    if (ctx->pspill_meta_ev) CF_HIP_CHECK(ctx, hipEventSynchronize(ctx->pspill_meta_ev));
+    else CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->pspill_meta_ev, hipEventDisableTiming));
+    if (meta_n > ctx->pspill_meta_bytes) {
+        if (ctx->h_pspill_meta) (void)hipHostFree(ctx->h_pspill_meta);
+        ctx->h_pspill_meta = nullptr;
+        ctx->pspill_meta_bytes = 0;
+        CF_HIP_CHECK(ctx, hipHostMalloc(&ctx->h_pspill_meta, meta_n));
+        ctx->pspill_meta_bytes = meta_n;
+    }
+    std::memcpy(ctx->h_pspill_meta, meta.data(), meta_n);
+    CF_HIP_CHECK(ctx, hipMemcpyAsync(d_meta, ctx->h_pspill_meta, meta_n, hipMemcpyHostToDevice, stream));
+    CF_HIP_CHECK(ctx, hipEventRecord(ctx->pspill_meta_ev, stream));
+    for (const Chunk& c : chunks) {
+        a.first = b.first + c.u0;
+        a.nu = c.nu;
+        a.soff = d_meta + c.meta;
+        a.sioff = a.soff + (c.nu + 1);
+        a.roff = a.sioff + (c.nu + 1);
+        const uint64_t items = meta[c.meta + 2 * (c.nu + 1) + c.nu];
         CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), stream));
         hipLaunchKernelGGL(spill_basis_kernel<T>, dim3(a.nu), dim3(kT), 0, stream, a);
         CF_HIP_CHECK(ctx, hipGetLastError());
-        const uint32_t items = a.nu * (uint32_t)kmax;
-        hipLaunchKernelGGL(spill_predict_kernel<T>, dim3((unsigned)std::min<uint32_t>(blocks, items)), dim3(kT), 0,
+        hipLaunchKernelGGL(spill_predict_kernel<T>, dim3((unsigned)std::min<uint64_t>(blocks, items)), dim3(kT), 0,
                            stream, a);
         CF_HIP_CHECK(ctx, hipGetLastError());
     }

@@ -8,7 +8,7 @@
 // space of all ids seen (the reference's 2000x2000 matrix is only defined for ids
 // < 2000); users are written in ascending uid order with their movies ascending (the
 // reference's order is boost::unordered_map order); k <= 192 runs on the LDS path,
-// 192 < k <= 3072 on the fp64 spill path.
+// 192 < k <= 5000 (CF_SPILL_MAX_K) on the fp64 spill path.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>

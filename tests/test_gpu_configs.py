@@ -432,3 +432,33 @@ def test_c3_knn2_rows_bit_exact(gpu_ctx):
     assert np.count_nonzero(Wg) > 1000
     del d_W, W
     torch.cuda.empty_cache()
+
+
+def test_c5_tail_k_up_to_5000(gpu_ctx, c4_graph):
+    """C5 as specified: its lognormal tail reaches the k = 5000 cap.  Users with k = 2000,
+    3100, 4000 and 5000 (Zipf items of the 50k C4 graph) through the timed fused path: the
+    fp64 spill solver (k > 3072 in its BIG layout: rc / rs / tau in the HBM slot) and the
+    spill predictor (per-user slots).  Size-independent properties at full size on every
+    user (residual, orthonormality, sigs, m vs the cut, order, sign); oracle parity at
+    k = 2000 (m exact unless at the cut, eigenvalues 1e-5, clustered projectors, residual)
+    and stage-wise predictor parity on rows of that user."""
+    from collaborative_filtering_amd import synth, workloads as wlm
+
+    ks = np.array([2000, 3100, 4000, 5000], dtype=np.uint32)
+    off, items, rat = synth.user_items(wlm.CONFIGS["c5"]["seed"] + 7, ks, 50_000, threads=THREADS)
+    run = FusedRun(gpu_ctx, c4_graph[0], 50_000, off, items, rat)
+    try:
+        assert np.all(run.m[:4] >= 2) and np.all(run.m[:4] <= ks)
+        bad = eigen_properties(run, [0, 1, 2, 3])
+        assert not bad, bad
+        bad = eigen_check(run, [0], "C5 k=2000")
+        assert not bad, bad
+        kk = run.kk
+        kr = np.repeat(run.k, run.k)
+        assert np.all((kk >= 0) & (kk <= kr - 1))
+        assert np.array_equal(np.isnan(run.mse), kk == 0)
+        good, ill, badp = predict_check(run, [0], max_rows=6, seed=10)
+        _report("C5 k=2000", good, ill, 6)
+        assert not badp, badp
+    finally:
+        run.free()
