@@ -21,6 +21,8 @@ CF_MAX_K = 192
 CF_SPILL_MAX_K = 5000
 CF_EIGEN_TRIDIAG = 0
 CF_EIGEN_JACOBI = 1
+CF_GRAPH_DENSE = 0
+CF_GRAPH_CSR = 1
 CF_FILTER_CHEBY = 0
 CF_FILTER_BINOMIAL = 1
 
@@ -40,6 +42,10 @@ SIGNATURES = {
     "cf_item_graph_upload": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p]),
     "cf_item_graph_upload_dense": (c_int, [c_void_p, c_uint32, c_void_p, c_int]),
     "cf_item_graph_device": (c_void_p, [c_void_p, POINTER(c_uint32)]),
+    "cf_set_graph_layout": (c_int, [c_void_p, c_int]),
+    "cf_graph_info": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "cf_item_cosine_edges": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int,
+                                     c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
     "cf_plan_create": (c_int, [c_void_p, c_uint32, c_void_p, POINTER(c_void_p)]),
     "cf_plan_destroy": (None, [c_void_p]),
     "cf_evec_slots": (c_uint64, [c_uint32]),

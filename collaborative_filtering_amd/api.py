@@ -156,6 +156,43 @@ class Context:
                   "cf_item_graph_upload")
         self.n_items = n_items
 
+    def set_graph_layout(self, layout: str = "dense"):
+        """'dense' (n^2 fp32) or 'csr' (row pointers, ascending columns, weights) for the next
+        graph upload (cf_set_graph_layout)."""
+        code = {"dense": _native.CF_GRAPH_DENSE, "csr": _native.CF_GRAPH_CSR}[layout]
+        self._chk(self.lib.cf_set_graph_layout(self.h, code), "cf_set_graph_layout")
+
+    def graph_info(self):
+        """(layout name, n_items, stored edges) of the resident graph."""
+        lay, n, nnz = c_int(), c_uint32(), np.zeros(1, np.uint64)
+        self._chk(self.lib.cf_graph_info(self.h, byref(lay), byref(n), ptr(nnz)), "cf_graph_info")
+        return ("csr" if lay.value == _native.CF_GRAPH_CSR else "dense"), n.value, int(nnz[0])
+
+    def item_cosine_edges(self, n_items, user_off, items, ratings, w_min=0.01, cnt_min=5, adopt=False):
+        """knn2 as the compacted edge list (cf_item_cosine_edges): (edge_off[n_items + 1],
+        targets, weights) per source, targets ascending."""
+        user_off = np.ascontiguousarray(user_off, dtype=np.uint64)
+        items = np.ascontiguousarray(items, dtype=np.uint32)
+        ratings = np.ascontiguousarray(ratings, dtype=np.float32)
+        eoff = np.zeros(n_items + 1, np.uint64)
+        cnt = np.zeros(1, np.uint64)
+        cap = 1 << 20
+        while True:
+            col = np.zeros(cap, np.uint32)
+            w = np.zeros(cap, np.float32)
+            rc = self.lib.cf_item_cosine_edges(self.h, len(user_off) - 1, n_items, ptr(user_off), ptr(items),
+                                               ptr(ratings), float(w_min), int(cnt_min), int(adopt), ptr(eoff),
+                                               ptr(col), ptr(w), cap, ptr(cnt))
+            if rc == CF_ERANGE and int(cnt[0]) > cap:
+                cap = int(cnt[0])
+                continue
+            self._chk(rc, "cf_item_cosine_edges")
+            break
+        if adopt:
+            self.n_items = n_items
+        n = int(cnt[0])
+        return eoff, col[:n], w[:n]
+
     def graph_device_ptr(self) -> int:
         n = c_uint32()
         p = self.lib.cf_item_graph_device(self.h, byref(n))

@@ -80,6 +80,9 @@ void cf_destroy(cf_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->d_graph) (void)hipFree(ctx->d_graph);
+    if (ctx->d_grp) (void)hipFree(ctx->d_grp);
+    if (ctx->d_gcol) (void)hipFree(ctx->d_gcol);
+    if (ctx->d_gw) (void)hipFree(ctx->d_gw);
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
     if (ctx->d_phase) (void)hipFree(ctx->d_phase);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
@@ -167,71 +170,7 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps) {
     return CF_OK;
 }
 
-int cf_item_graph_upload(cf_ctx* ctx, uint32_t n_items, const uint64_t* row_ptr, const uint32_t* col,
-                         const float* w) {
-    if (!ctx || !row_ptr || (row_ptr[n_items] > 0 && (!col || !w)))
-        return cf_set_error(ctx, CF_EINVAL, "cf_item_graph_upload: null argument");
-    CF_TRY(set_device(ctx));
-    const uint64_t nnz = row_ptr[n_items];
-    const size_t dense_bytes = (size_t)n_items * n_items * sizeof(float);
-    if (ctx->d_graph) {
-        (void)hipFree(ctx->d_graph);
-        ctx->d_graph = nullptr;
-        ctx->n_items = 0;
-    }
-    float* dense = nullptr;
-    if (hipMalloc(&dense, std::max<size_t>(dense_bytes, 16)) != hipSuccess)
-        return cf_set_error(ctx, CF_ENOMEM, "cf_item_graph_upload: dense graph allocation failed");
-    DevBuf drp, dcol, dw;
-    int rc = dev_alloc(ctx, drp, sizeof(uint64_t) * (n_items + 1));
-    if (rc == CF_OK) rc = dev_alloc(ctx, dcol, sizeof(uint32_t) * nnz);
-    if (rc == CF_OK) rc = dev_alloc(ctx, dw, sizeof(float) * nnz);
-    if (rc != CF_OK) {
-        (void)hipFree(dense);
-        return rc;
-    }
-    hipError_t e = hipMemset(dense, 0, dense_bytes);
-    if (e == hipSuccess) e = hipMemcpy(drp.p, row_ptr, sizeof(uint64_t) * (n_items + 1), hipMemcpyHostToDevice);
-    if (e == hipSuccess && nnz) e = hipMemcpy(dcol.p, col, sizeof(uint32_t) * nnz, hipMemcpyHostToDevice);
-    if (e == hipSuccess && nnz) e = hipMemcpy(dw.p, w, sizeof(float) * nnz, hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-        (void)hipFree(dense);
-        return cf_set_error(ctx, CF_EHIP, std::string("graph upload: ") + hipGetErrorString(e));
-    }
-    rc = cf_launch_dense_scatter(ctx, n_items, (const uint64_t*)drp.p, (const uint32_t*)dcol.p,
-                                 (const float*)dw.p, dense, nullptr);
-    if (rc == CF_OK && hipDeviceSynchronize() != hipSuccess)
-        rc = cf_set_error(ctx, CF_EHIP, "graph scatter failed");
-    if (rc != CF_OK) {
-        (void)hipFree(dense);
-        return rc;
-    }
-    ctx->d_graph = dense;
-    ctx->n_items = n_items;
-    return CF_OK;
-}
-
-int cf_item_graph_upload_dense(cf_ctx* ctx, uint32_t n_items, const float* w_dense, int on_device) {
-    if (!ctx || (!w_dense && n_items)) return cf_set_error(ctx, CF_EINVAL, "cf_item_graph_upload_dense: null");
-    CF_TRY(set_device(ctx));
-    const size_t bytes = (size_t)n_items * n_items * sizeof(float);
-    if (ctx->d_graph) {
-        (void)hipFree(ctx->d_graph);
-        ctx->d_graph = nullptr;
-        ctx->n_items = 0;
-    }
-    float* dense = nullptr;
-    if (hipMalloc(&dense, std::max<size_t>(bytes, 16)) != hipSuccess)
-        return cf_set_error(ctx, CF_ENOMEM, "dense graph allocation failed");
-    hipError_t e = hipMemcpy(dense, w_dense, bytes, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-        (void)hipFree(dense);
-        return cf_set_error(ctx, CF_EHIP, std::string("dense graph copy: ") + hipGetErrorString(e));
-    }
-    ctx->d_graph = dense;
-    ctx->n_items = n_items;
-    return CF_OK;
-}
+// cf_item_graph_upload / cf_item_graph_upload_dense: cf_graph.hip (dense or CSR layout).
 
 const float* cf_item_graph_device(const cf_ctx* ctx, uint32_t* n_items) {
     if (!ctx) return nullptr;
@@ -323,7 +262,7 @@ int cf_eigen_run(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, c
                  const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals, float* d_evecs,
                  void* stream) {
     if (!ctx || !plan) return cf_set_error(ctx, CF_EINVAL, "cf_eigen_run: null");
-    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_eigen_run: no item graph uploaded");
+    if (!has_graph(ctx)) return cf_set_error(ctx, CF_ESTATE, "cf_eigen_run: no item graph uploaded");
     CF_TRY(set_device(ctx));
     return cf_launch_eigen(ctx, plan, d_item_off, d_items, d_evec_off, d_m, d_sigs, d_evals, d_evecs,
                            (hipStream_t)stream);
@@ -333,7 +272,7 @@ int cf_eigen_batch(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, cons
                    const uint64_t* evec_off, int32_t* m_out, float* sigs, float* evals, float* evecs) {
     if (!ctx || !item_off || !evec_off || !m_out || !sigs || !evals || !evecs)
         return cf_set_error(ctx, CF_EINVAL, "cf_eigen_batch: null argument");
-    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_eigen_batch: no item graph uploaded");
+    if (!has_graph(ctx)) return cf_set_error(ctx, CF_ESTATE, "cf_eigen_batch: no item graph uploaded");
     CF_TRY(set_device(ctx));
     const uint64_t n_entries = item_off[n_users];
     for (uint64_t e = 0; e < n_entries; ++e)
@@ -382,7 +321,7 @@ int cf_predict_run_f64(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_
                        const uint64_t* d_evec_off, const double* d_evecs, const double* d_sigtab, int sig_mode,
                        float* d_mse, int32_t* d_kk, double* d_pred, void* stream) {
     if (!ctx || !plan) return cf_set_error(ctx, CF_EINVAL, "cf_predict_run_f64: null");
-    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_predict_run_f64: no item graph uploaded");
+    if (!has_graph(ctx)) return cf_set_error(ctx, CF_ESTATE, "cf_predict_run_f64: no item graph uploaded");
     CF_TRY(set_device(ctx));
     return cf_launch_predict<double>(ctx, plan, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off,
                                      d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, nullptr, (hipStream_t)stream);
@@ -393,7 +332,7 @@ int cf_predict_run_f32(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_
                        const uint64_t* d_evec_off, const float* d_evecs, const float* d_sigtab, int sig_mode,
                        float* d_mse, int32_t* d_kk, double* d_pred, void* stream) {
     if (!ctx || !plan) return cf_set_error(ctx, CF_EINVAL, "cf_predict_run_f32: null");
-    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_predict_run_f32: no item graph uploaded");
+    if (!has_graph(ctx)) return cf_set_error(ctx, CF_ESTATE, "cf_predict_run_f32: no item graph uploaded");
     CF_TRY(set_device(ctx));
     return cf_launch_predict<float>(ctx, plan, d_item_off, d_items, d_ratings, d_m, d_evals, d_evec_off,
                                     d_evecs, d_sigtab, sig_mode, d_mse, d_kk, d_pred, nullptr, (hipStream_t)stream);
@@ -404,7 +343,7 @@ int cf_step_run(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, co
                 float* d_evecs, int sig_mode, float* d_mse, int32_t* d_kk, double* d_pred, void* stream) {
     if (!ctx || !plan) return cf_set_error(ctx, CF_EINVAL, "cf_step_run: null");
     if (sig_mode != CF_SIGS_OWN && sig_mode != CF_SIGS_COMPAT) return cf_set_error(ctx, CF_EINVAL, "cf_step_run: bad sig_mode");
-    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_step_run: no item graph uploaded");
+    if (!has_graph(ctx)) return cf_set_error(ctx, CF_ESTATE, "cf_step_run: no item graph uploaded");
     CF_TRY(set_device(ctx));
     return cf_launch_step(ctx, plan, d_item_off, d_items, d_ratings, d_evec_off, d_m, d_sigs, d_evals, d_evecs,
                           sig_mode, d_mse, d_kk, d_pred, (hipStream_t)stream);
@@ -439,7 +378,7 @@ int cf_predict_precomp_sel(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_o
         return cf_set_error(ctx, CF_EINVAL, "cf_predict_precomp: null argument");
     if (sig_mode != CF_SIGS_OWN && sig_mode != CF_SIGS_COMPAT)
         return cf_set_error(ctx, CF_EINVAL, "cf_predict_precomp: bad sig_mode");
-    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_predict_precomp: no item graph uploaded");
+    if (!has_graph(ctx)) return cf_set_error(ctx, CF_ESTATE, "cf_predict_precomp: no item graph uploaded");
     CF_TRY(set_device(ctx));
     const uint64_t n_entries = item_off[n_users];
     uint64_t n_evec = 0;
@@ -599,10 +538,8 @@ int cf_item_cosine(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64
             e = hipMemcpy(w_out, dW, (size_t)n_items * n_items * sizeof(float), hipMemcpyDeviceToHost);
         if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("knn2 run: ") + hipGetErrorString(e));
     }
-    if (rc == CF_OK && adopt_as_graph) {
-        if (ctx->d_graph) (void)hipFree(ctx->d_graph);
-        ctx->d_graph = dW;
-        ctx->n_items = n_items;
+    if (rc == CF_OK && adopt_as_graph) {   // in the context's upload layout (cf_graph.hip)
+        rc = cf_adopt_dense_graph(ctx, n_items, dW);
         dW = nullptr;
     }
     if (dW) (void)hipFree(dW);
@@ -614,7 +551,7 @@ int cf_knn_predict(cf_ctx* ctx, uint32_t n_users, const uint64_t* user_off, cons
                    const float* ratings, double* pred, float* movie_mse, uint32_t* movie_count) {
     if (!ctx || !user_off || !movie_mse || (user_off[n_users] && (!items || !ratings)))
         return cf_set_error(ctx, CF_EINVAL, "cf_knn_predict: null argument");
-    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_knn_predict: no item graph uploaded");
+    if (!has_graph(ctx)) return cf_set_error(ctx, CF_ESTATE, "cf_knn_predict: no item graph uploaded");
     CF_TRY(set_device(ctx));
     const uint64_t n = user_off[n_users];
     for (uint64_t e = 0; e < n; ++e)

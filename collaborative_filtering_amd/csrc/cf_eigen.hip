@@ -86,7 +86,7 @@ struct EigenArgs {
     uint32_t first;
     const uint64_t* item_off;
     const uint32_t* items;
-    const float* graph;
+    GraphDev graph;
     uint64_t n_items;
     const uint64_t* evec_off;
     int32_t* m_out;
@@ -227,8 +227,8 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT)) void eigen_kernel(Ei
     // kLocal: W(i, j) = w(item_i -> item_j) if > 0.1 (graph_loader, local_calc.cpp:113);
     // column 0 mirrors row 0: W(i, 0) = w(movie -> item_i) (:331-333); W(0, 0) = 0.
     for (int i = wave; i < k; i += NW) {
-        const float* row = a.graph + (size_t)s_item[i] * a.n_items;
-        const float* row0 = a.graph + (size_t)s_item[0] * a.n_items;
+        const GraphRow row = a.graph.row(s_item[i]);
+        const GraphRow row0 = a.graph.row(s_item[0]);
         for (int j = lane; j < k; j += 64) {
             float w = row[s_item[j]];
             if (mode == kLocal) {
@@ -670,7 +670,7 @@ int cf_launch_local_eigen(cf_ctx* ctx, const cf_plan* movie_plan, const uint64_t
     args.order = movie_plan->d_order;
     args.item_off = d_item_off;
     args.items = d_items;
-    args.graph = ctx->d_graph;
+    args.graph = graph_dev(ctx);
     args.n_items = ctx->n_items;
     args.evec_off = d_evec_off;
     args.m_out = d_n_out;
@@ -736,7 +736,7 @@ int cf_launch_eigen_flagged(cf_ctx* ctx, const cf_plan* plan, int emax, uint32_t
     args.first = first;
     args.item_off = d_item_off;
     args.items = d_items;
-    args.graph = ctx->d_graph;
+    args.graph = graph_dev(ctx);
     args.n_items = ctx->n_items;
     args.evec_off = d_evec_off;
     args.m_out = d_m;
@@ -768,7 +768,7 @@ int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off
     args.order = plan->d_order;
     args.item_off = d_item_off;
     args.items = d_items;
-    args.graph = ctx->d_graph;
+    args.graph = graph_dev(ctx);
     args.n_items = ctx->n_items;
     args.evec_off = d_evec_off;
     args.m_out = d_m;

@@ -49,7 +49,7 @@ struct SpillArgs {
     uint32_t count;
     const uint64_t* item_off;
     const uint32_t* items;
-    const float* graph;
+    GraphDev graph;
     uint64_t n_items;
     const uint64_t* evec_off;
     int32_t* m_out;
@@ -213,8 +213,8 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         // > 0.1, column 0 mirrors row 0 (W(i, 0) = w(movie -> item_i), W(0, 0) = 0), and no
         // 0 -> 1 degree rule.
         for (int i = wave; i < n; i += SP_W) {
-            const float* grow = a.graph + (size_t)a.items[base + i] * a.n_items;
-            const float* grow0 = a.graph + (size_t)a.items[base] * a.n_items;
+            const GraphRow grow = a.graph.row(a.items[base + i]);
+            const GraphRow grow0 = a.graph.row(a.items[base]);
             double ds = 0.0;
             for (int j = lane; j < n; j += 64) {
                 float w = grow[a.items[base + j]];
@@ -960,7 +960,7 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     a.count = b.count;
     a.item_off = d_item_off;
     a.items = d_items;
-    a.graph = ctx->d_graph;
+    a.graph = graph_dev(ctx);
     a.n_items = ctx->n_items;
     a.evec_off = d_evec_off;
     a.m_out = d_m;

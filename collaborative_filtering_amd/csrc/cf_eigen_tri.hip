@@ -43,7 +43,7 @@ struct TriArgs {
     uint32_t count;
     const uint64_t* item_off;
     const uint32_t* items;
-    const float* graph;
+    GraphDev graph;
     uint64_t n_items;
     const uint64_t* evec_off;
     int32_t* m_out;
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(TA_T) void tri_reduce_kernel(TriArgs a) {
     for (int i = tid; i < n; i += TA_T) s_item[i] = a.items[base + i];
     __syncthreads();
     for (int i = wave; i < n; i += TA_W) {
-        const float* grow = a.graph + (size_t)s_item[i] * a.n_items;
+        const GraphRow grow = a.graph.row(s_item[i]);
         for (int j = lane; j < n; j += 64) A[i * LD + j] = grow[s_item[j]];
     }
     __syncthreads();
@@ -823,7 +823,7 @@ int cf_launch_eigen_tri(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item
     a.order = plan->d_order;
     a.item_off = d_item_off;
     a.items = d_items;
-    a.graph = ctx->d_graph;
+    a.graph = graph_dev(ctx);
     a.n_items = ctx->n_items;
     a.evec_off = d_evec_off;
     a.m_out = d_m;

@@ -10,12 +10,52 @@
 
 #include "cf_abi.h"
 
+// The resident item graph as the kernels see it: dense n x n fp32 row-major (direct
+// indexing), or CSR (row_ptr, columns ascending per row, weights) for catalogues whose dense
+// matrix does not fit, looked up by a binary search of the row.  Every kernel reads the graph
+// through row(a)[b] = w(a -> b), 0 where there is no edge; both layouts give the same floats.
+struct GraphRow {
+    const float* dense;    // this row of the dense matrix, or null
+    const uint32_t* col;   // CSR: the row's columns (ascending) and weights
+    const float* w;
+    uint32_t len;
+    __device__ __forceinline__ float operator[](uint32_t b) const {
+        if (dense) return dense[b];
+        uint32_t lo = 0, hi = len;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (col[mid] < b) lo = mid + 1;
+            else hi = mid;
+        }
+        return (lo < len && col[lo] == b) ? w[lo] : 0.0f;
+    }
+};
+struct GraphDev {
+    const float* dense = nullptr;   // dense layout
+    uint64_t n = 0;
+    const uint64_t* rp = nullptr;   // CSR layout
+    const uint32_t* col = nullptr;
+    const float* w = nullptr;
+    __device__ __forceinline__ GraphRow row(uint32_t a) const {
+        if (dense) return GraphRow{dense + (size_t)a * n, nullptr, nullptr, 0};
+        const uint64_t b = rp[a];
+        return GraphRow{nullptr, col + b, w + b, (uint32_t)(rp[a + 1] - b)};
+    }
+};
+
 struct cf_ctx {
     int device = 0;
     std::string last_error;
-    // Item graph, dense fp32 n_items x n_items row-major, HBM-resident.
+    // Item graph, HBM-resident: dense fp32 n_items x n_items row-major (d_graph), or CSR
+    // (d_grp / d_gcol / d_gw, graph_layout == CF_GRAPH_CSR).
     float* d_graph = nullptr;
     uint32_t n_items = 0;
+    int graph_layout = CF_GRAPH_DENSE;   // layout of the next upload (cf_set_graph_layout)
+    bool graph_csr = false;              // layout of the resident graph
+    uint64_t* d_grp = nullptr;
+    uint32_t* d_gcol = nullptr;
+    float* d_gw = nullptr;
+    uint64_t g_nnz = 0;
     // Jacobi controls
     float tol_scale = 1.0f;
     int max_sweeps = 30;
@@ -117,6 +157,20 @@ struct cf_plan {
 };
 
 int cf_set_error(cf_ctx* ctx, int code, const std::string& msg);
+
+inline bool has_graph(const cf_ctx* ctx) { return ctx->d_graph || ctx->graph_csr; }
+inline GraphDev graph_dev(const cf_ctx* ctx) {
+    GraphDev g;
+    g.n = ctx->n_items;
+    if (ctx->graph_csr) {
+        g.rp = ctx->d_grp;
+        g.col = ctx->d_gcol;
+        g.w = ctx->d_gw;
+    } else {
+        g.dense = ctx->d_graph;
+    }
+    return g;
+}
 
 #define CF_HIP_CHECK(ctx, expr)                                                          \
     do {                                                                                 \
@@ -229,6 +283,12 @@ int cf_launch_knn2(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64
 int cf_launch_knn3(cf_ctx* ctx, uint32_t n_users, const uint64_t* d_user_off, const uint32_t* d_items,
                    const float* d_ratings, double* d_pred, unsigned long long* d_sq, double* d_sq_real,
                    unsigned int* d_cnt, hipStream_t stream);
+
+// cf_graph.hip: a device dense matrix as CSR (new buffers), and a device dense matrix
+// installed as the context's graph in its upload layout (adopted, or compacted and freed).
+int cf_dense_to_csr(cf_ctx* ctx, uint32_t n, const float* d_dense, uint64_t** d_rp, uint32_t** d_col, float** d_w,
+                    uint64_t* nnz, hipStream_t stream);
+int cf_adopt_dense_graph(cf_ctx* ctx, uint32_t n, float* d_dense);
 
 int cf_launch_dense_scatter(cf_ctx* ctx, uint32_t n_items, const uint64_t* d_row_ptr,
                             const uint32_t* d_col, const float* d_w, float* d_dense,

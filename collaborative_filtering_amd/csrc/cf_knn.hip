@@ -369,7 +369,7 @@ struct Knn3Args {
     const uint64_t* user_off;
     const uint32_t* items;     // test items of each user (compact ids)
     const float* ratings;      // test ratings
-    const float* graph;        // dense out_fin_ weights (as parsed floats)
+    GraphDev graph;        // dense out_fin_ weights (as parsed floats)
     uint64_t n_items;
     double* pred;              // per test rating, 0 when no neighbour (ratings_knn default)
     unsigned long long* sq_err;  // per movie: sum of tmp^2 (integer-valued for integer ratings)
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(256) void knn3_kernel(Knn3Args a) {
     const int k = (int)(a.user_off[u + 1] - base);
     for (int r = threadIdx.x; r < k; r += blockDim.x) {
         const uint32_t m = a.items[base + r];
-        const float* wrow = a.graph + (size_t)m * a.n_items;
+        const GraphRow wrow = a.graph.row(m);
         double sw = 0.0, swr = 0.0;
         for (int j = 0; j < k; ++j) {
             const float w = wrow[a.items[base + j]];
@@ -584,7 +584,7 @@ int cf_launch_knn3(cf_ctx* ctx, uint32_t n_users, const uint64_t* d_user_off, co
     a.user_off = d_user_off;
     a.items = d_items;
     a.ratings = d_ratings;
-    a.graph = ctx->d_graph;
+    a.graph = graph_dev(ctx);
     a.n_items = ctx->n_items;
     a.pred = d_pred;
     a.sq_err = d_sq;

@@ -167,7 +167,7 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
                              int32_t* kk, double* pred, float* wlim, int32_t* lim) {
     if (!ctx || (n_movies && (!movie_off || !movie_items)) || !test_off || !mse || !kk)
         return cf_set_error(ctx, CF_EINVAL, "cf_local_calc: null argument");
-    if (!ctx->d_graph) return cf_set_error(ctx, CF_ESTATE, "cf_local_calc: no item graph uploaded");
+    if (!has_graph(ctx)) return cf_set_error(ctx, CF_ESTATE, "cf_local_calc: no item graph uploaded");
     CF_TRY(set_device(ctx));
     const uint32_t n_items = ctx->n_items;
     const uint64_t n_test = test_off[n_items];

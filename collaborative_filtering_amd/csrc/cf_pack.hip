@@ -198,7 +198,7 @@ int cf_eigen_batch_multi(cf_ctx* const* ctxs, int n_dev, uint32_t n_users, const
         return cf_set_error(root, CF_EINVAL, "cf_eigen_batch_multi: null argument");
     for (int d = 0; d < n_dev; ++d) {
         if (!ctxs[d]) return cf_set_error(root, CF_EINVAL, "cf_eigen_batch_multi: null context");
-        if (!ctxs[d]->d_graph) return cf_set_error(root, CF_ESTATE, "cf_eigen_batch_multi: a context has no graph");
+        if (!has_graph(ctxs[d])) return cf_set_error(root, CF_ESTATE, "cf_eigen_batch_multi: a context has no graph");
     }
     std::vector<uint32_t> split(n_dev + 1);
     cost_split(n_users, item_off, n_dev, split.data());

@@ -95,7 +95,7 @@ struct PredArgs {
     const T* evecs;
     const T* sigtab;
     int sig_mode;
-    const float* graph;
+    GraphDev graph;
     uint64_t n_items;
     float* mse;
     int32_t* kk;
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
             float gv[kMaskRows][3];
 #pragma unroll
             for (int x = 0; x < kMaskRows; ++x) {
-                const float* nrow = a.graph + (size_t)s_item[min(r0 + x, k - 1)] * a.n_items;
+                const GraphRow nrow = a.graph.row(s_item[min(r0 + x, k - 1)]);
 #pragma unroll
                 for (int t = 0; t < 3; ++t) gv[x][t] = nrow[s_item[min(64 * t + lane, k - 1)]];
             }
@@ -1091,7 +1091,7 @@ __global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_rating_kern
         for (int si = 0; si < nslow; ++si) {
             const int r = s_slow[si] & 0xffff;
             // connected set C: the user's items that are out-neighbours of movie r (:254-265)
-            const float* nrow = a.graph + (size_t)s_item[r] * a.n_items;
+            const GraphRow nrow = a.graph.row(s_item[r]);
             const bool conn = tid < k && (double)nrow[s_item[tid < k ? tid : 0]] > 0.1;
             const int c = block_compact(conn, tid, s_conn, s_cnt);
             const int nc = block_compact(tid < k && !conn, tid, s_nconn, s_cnt);
@@ -1327,7 +1327,7 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
     args.evecs = d_evecs;
     args.sigtab = d_sigtab;
     args.sig_mode = sig_mode;
-    args.graph = ctx->d_graph;
+    args.graph = graph_dev(ctx);
     args.n_items = ctx->n_items;
     args.mse = d_mse;
     args.kk = d_kk;
@@ -1458,7 +1458,7 @@ int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
     args.evecs = d_evecs;
     args.sigtab = d_sigs;
     args.sig_mode = sig_mode;
-    args.graph = ctx->d_graph;
+    args.graph = graph_dev(ctx);
     args.n_items = ctx->n_items;
     args.mse = d_mse;
     args.kk = d_kk;

@@ -64,7 +64,7 @@ struct SpArgs {
     const T* evecs;
     const T* sigtab;
     int sig_mode;
-    const float* graph;
+    GraphDev graph;
     uint64_t n_items;
     float* mse;
     int32_t* kk;
@@ -424,7 +424,7 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
         SP_STAMP(-1);
 
         // connected set C (:254-265); Cbar = the rest, the movie's own row r included
-        const float* nrow = a.graph + (size_t)a.items[base + r] * a.n_items;
+        const GraphRow nrow = a.graph.row(a.items[base + r]);
         for (int i = tid; i < k; i += kT) s_rat[i] = a.ratings[base + i];
         const int c = compact(k, [&](int i) { return (double)nrow[a.items[base + i]] > 0.1; }, s_conn, s_tmp);
         const int nc = compact(k, [&](int i) { return !((double)nrow[a.items[base + i]] > 0.1); }, s_ncon, s_tmp);
@@ -755,7 +755,7 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
     a.evecs = d_evecs;
     a.sigtab = d_sigtab;
     a.sig_mode = sig_mode;
-    a.graph = ctx->d_graph;
+    a.graph = graph_dev(ctx);
     a.n_items = ctx->n_items;
     a.mse = d_mse;
     a.kk = d_kk;

@@ -1,7 +1,9 @@
 // knn2 -- drop-in for knn2.cpp (a10): cosine item weights on the out_edg_ edges from
 // the out_rat_ train maps; writes out_fin_ "a b w" for w > 0.01 (knn2.cpp:151-164).
-// The weights come from cf_item_cosine (int8 / fp32 MFMA over all item pairs); the
-// writer keeps exactly the out_edg_ edges, in out_edg_ order per source.
+// The weights come from cf_item_cosine_edges (int8 / fp32 MFMA over all item pairs, compacted
+// on the device to the w > 0.01 edge list); the writer keeps exactly the out_edg_ edges, in
+// out_edg_ order per source.
+#include <algorithm>
 #include <cstdio>
 
 #include "cf_cli.hpp"
@@ -38,10 +40,22 @@ int main(int argc, char** argv) {
             r[p] = (float)ur.second;
         }
     const uint32_t n = items.size();
-    std::vector<float> W((size_t)n * n);
+    // knn2 as the compacted edge list (cf_item_cosine_edges): the dense similarity matrix is
+    // compacted on the device, only the w > 0.01 edges come back (targets ascending per source)
+    std::vector<uint64_t> eoff((size_t)n + 1);
+    std::vector<uint32_t> ecol;
+    std::vector<float> ew;
+    uint64_t n_edges = 0;
     cf_ctx* ctx = cfcli::open_device();
-    cfcli::check(ctx, cf_item_cosine(ctx, users.size(), n, off.data(), it.data(), r.data(), 0.01f, 5, 0, W.data()),
-                 "cf_item_cosine");
+    int rc = cf_item_cosine_edges(ctx, users.size(), n, off.data(), it.data(), r.data(), 0.01f, 5, 0, eoff.data(),
+                                  nullptr, nullptr, 0, &n_edges);
+    if (rc == CF_ERANGE && n_edges > 0) {   // sized by the first call
+        ecol.resize(n_edges);
+        ew.resize(n_edges);
+        rc = cf_item_cosine_edges(ctx, users.size(), n, off.data(), it.data(), r.data(), 0.01f, 5, 0, eoff.data(),
+                                  ecol.data(), ew.data(), n_edges, &n_edges);
+    }
+    cfcli::check(ctx, rc, "cf_item_cosine_edges");
     {
         double acc = 0.0;
         int exact = 0, path = 0;
@@ -55,10 +69,17 @@ int main(int argc, char** argv) {
                          acc);
     }
     cf_destroy(ctx);
+    // w(a, b) of an out_edg_ pair: a binary search of a's edge list (0 when absent)
+    const auto weight = [&](uint32_t a, uint32_t b) -> float {
+        const uint32_t* lo = ecol.data() + eoff[a];
+        const uint32_t* hi = ecol.data() + eoff[a + 1];
+        const uint32_t* p = std::lower_bound(lo, hi, b);
+        return (p != hi && *p == b) ? ew[(size_t)(p - ecol.data())] : 0.0f;
+    };
     cfio::ShardWriter fin(".", "out_fin", nshards);
     size_t written = 0;
     for (auto& e : edges) {
-        const float w = W[(size_t)items.at[e.first] * n + items.at[e.second]];
+        const float w = weight(items.at[e.first], items.at[e.second]);
         if (!(w > 0.0f)) continue;
         std::string& out = fin.shard(e.first);
         cfio::append_u(out, e.first);

@@ -95,14 +95,26 @@ int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out16);
 
 /* ---- item graph (out_fin_) ---------------------------------------------------
  * Directed weighted graph exactly as parsed: w(a,b) and w(b,a) are independent.
- * Stored on the device as a dense n_items x n_items fp32 matrix (HBM-resident). */
+ * HBM-resident in one of two layouts (cf_set_graph_layout, applies to the next upload):
+ *   CF_GRAPH_DENSE (default) n_items x n_items fp32, direct indexing (the reference's own
+ *                  dense `weights`, precompute_local_threads.cpp:255; ~250k items per GPU);
+ *   CF_GRAPH_CSR   row pointers (u64), ascending columns (u32), weights (f32); every lookup
+ *                  is a binary search of the row (the GraphLab out-edge lists,
+ *                  local_calc_precomp.cpp:122-136): catalogues whose dense matrix does not fit.
+ * Every kernel reads the same floats from either layout, so results are bit-identical.
+ * A duplicate (a, b) keeps its LAST weight in input order (precompute_local_threads.cpp:284). */
+#define CF_GRAPH_DENSE 0
+#define CF_GRAPH_CSR 1
+int cf_set_graph_layout(cf_ctx* ctx, int layout);
+/* Layout, size and (CSR) stored edges of the resident graph. */
+int cf_graph_info(const cf_ctx* ctx, int* layout, uint32_t* n_items, uint64_t* nnz);
 int cf_item_graph_upload(cf_ctx* ctx, uint32_t n_items, const uint64_t* row_ptr,
                          const uint32_t* col, const float* w);
 /* w_dense: n_items*n_items row-major; on_device != 0 means w_dense is a device
  * pointer that the context adopts by copy. */
 int cf_item_graph_upload_dense(cf_ctx* ctx, uint32_t n_items, const float* w_dense,
                                int on_device);
-/* Device pointer of the resident dense graph (for *_run callers), or NULL. */
+/* Device pointer of the resident dense graph (for *_run callers), or NULL (none, or CSR). */
 const float* cf_item_graph_device(const cf_ctx* ctx, uint32_t* n_items);
 
 /* ---- user batch plan -----------------------------------------------------------
@@ -234,6 +246,15 @@ int cf_step_timing(cf_ctx* ctx, float* eigen_ms, float* total_ms);
 int cf_item_cosine(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64_t* user_off,
                    const uint32_t* item, const float* rating, float w_min, int cnt_min,
                    int adopt_as_graph, float* w_out);
+/* knn2 with the reference's output form: the compacted edge list "a b w" for w > w_min
+ * (knn2.cpp:151-164), as CSR over compact source ids: edge_off[n_items + 1], targets ascending
+ * in edge_col / edge_w (capacity edge_cap).  The dense similarity matrix is compacted on the
+ * device; only the edges cross PCIe.  *n_edges = the edge count; edge_cap too small gives
+ * CF_ERANGE with edge_off and *n_edges filled (retry with edge_cap = *n_edges).
+ * adopt_as_graph != 0 installs the result as the context's item graph (its layout). */
+int cf_item_cosine_edges(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64_t* user_off,
+                         const uint32_t* item, const float* rating, float w_min, int cnt_min, int adopt_as_graph,
+                         uint64_t* edge_off, uint32_t* edge_col, float* edge_w, uint64_t edge_cap, uint64_t* n_edges);
 int cf_item_cosine_run(cf_ctx* ctx, uint32_t n_users, uint32_t n_items,
                        const uint64_t* d_user_off, const uint32_t* d_item, const float* d_rating,
                        int integer_ratings, float w_min, int cnt_min, float* d_w_out,

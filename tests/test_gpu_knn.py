@@ -3,6 +3,7 @@
 import numpy as np
 import pytest
 
+import cases
 import oracle_ref as orc
 
 pytestmark = pytest.mark.gpu
@@ -139,3 +140,83 @@ def test_knn3_matches_oracle(gpu_ctx):
     assert np.allclose(pred_g[order], pred_o, rtol=1e-12, atol=1e-12)
     assert np.array_equal(mse_g, mse_o)
     assert np.array_equal(cnt_g, np.diff(mo))
+
+
+def test_csr_graph_bit_identical_to_dense(gpu_ctx):
+    """The CSR graph layout (cf_set_graph_layout(CSR), for catalogues whose dense matrix does
+    not fit): eigen blocks, predictions, local_calc and knn3 from a CSR-resident graph are the
+    same bits as from the dense one.  The CSR input carries duplicates (the last one wins,
+    precompute_local_threads.cpp:284) and zero weights, in unsorted row order."""
+    from collaborative_filtering_amd.api import CF_SIGS_COMPAT, Context
+
+    rng = np.random.default_rng(12)
+    n = 240
+    W = cases.item_graph(n, 0.5, seed=13)
+    # CSR input per row: its edges in shuffled order, five of them preceded by a stale duplicate
+    # (the later, correct one wins), and one explicit zero weight on a missing edge
+    rows, cols, ws = [], [], []
+    for a in range(n):
+        nz = np.nonzero(W[a])[0]
+        ent = [(int(b), np.float32(W[a, b])) for b in rng.permutation(nz)]
+        for b in rng.choice(nz, size=min(5, len(nz)), replace=False):
+            pos = next(i for i, e in enumerate(ent) if e[0] == b)
+            ent.insert(int(rng.integers(0, pos + 1)), (int(b), np.float32(0.77)))
+        zero = np.nonzero(W[a] == 0)[0]
+        if len(zero):
+            ent.insert(int(rng.integers(0, len(ent) + 1)), (int(rng.choice(zero)), np.float32(0.0)))
+        rows.append(len(ent))
+        cols += [b for b, _ in ent]
+        ws += [w for _, w in ent]
+    rp = np.concatenate([[0], np.cumsum(rows)]).astype(np.uint64)
+    ks = list(rng.integers(2, 190, size=60)) + [1, 192, 200, 260 - 40]
+    off, items = cases.user_items(n, ks, seed=14)
+    rat = cases.ratings_for(len(items), 15)
+    gpu_ctx.set_graph_layout("dense")
+    gpu_ctx.upload_graph_dense(W)
+    ref = gpu_ctx.eigen_batch(off, items)
+    ev64, U64, sg64 = ref.evals.astype(np.float64), ref.evecs.astype(np.float64), ref.sigs.astype(np.float64)
+    p_ref = gpu_ctx.predict_precomp(off, items, rat, ref.m, ev64, ref.evec_off, U64, sg64, sig_mode=CF_SIGS_COMPAT)
+    k_ref = gpu_ctx.knn_predict(off, items, rat)
+    with Context(0) as c:
+        c.set_graph_layout("csr")
+        c.upload_graph_csr(n, rp, np.array(cols, np.uint32), np.array(ws, np.float32))
+        assert c.graph_info()[0] == "csr" and c.graph_info()[2] == int(np.count_nonzero(W))
+        got = c.eigen_batch(off, items)
+        assert np.array_equal(got.m, ref.m)
+        assert np.array_equal(got.sigs, ref.sigs)
+        assert np.array_equal(got.evals, ref.evals)
+        assert np.array_equal(got.evecs, ref.evecs)
+        p = c.predict_precomp(off, items, rat, ref.m, ev64, ref.evec_off, U64, sg64, sig_mode=CF_SIGS_COMPAT)
+        assert np.array_equal(p[1], p_ref[1]) and np.array_equal(p[0], p_ref[0], equal_nan=True)
+        kg = c.knn_predict(off, items, rat)
+        assert np.array_equal(kg[0], k_ref[0]) and np.array_equal(kg[1], k_ref[1])
+
+
+def test_knn2_edge_list_matches_dense_and_adopts_as_csr(gpu_ctx):
+    """cf_item_cosine_edges: the compacted edge list equals the nonzeros of the dense knn2
+    matrix row by row (targets ascending, w > 0.01, cnt > 5, knn2.cpp:142-159), and adopted as a
+    CSR graph it gives the eigen blocks of the dense-adopted one bit for bit."""
+    from collaborative_filtering_amd.api import Context
+
+    n_items, n_users = 300, 4000
+    rng = np.random.default_rng(16)
+    k = rng.integers(5, 60, size=n_users)
+    off = np.concatenate([[0], np.cumsum(k)]).astype(np.uint64)
+    items = np.concatenate([np.sort(rng.choice(n_items, size=int(x), replace=False)) for x in k]).astype(np.uint32)
+    rats = rng.integers(1, 6, size=len(items)).astype(np.float32)
+    W = gpu_ctx.item_cosine(n_items, off, items, rats)
+    eoff, col, w = gpu_ctx.item_cosine_edges(n_items, off, items, rats)
+    nz_r, nz_c = np.nonzero(W)
+    assert len(col) == len(nz_c) > 1000
+    assert np.array_equal(np.diff(eoff.astype(np.int64)), np.bincount(nz_r, minlength=n_items))
+    assert np.array_equal(col, nz_c.astype(np.uint32)) and np.array_equal(w, W[nz_r, nz_c])
+    ku = list(rng.integers(2, 150, size=40))
+    uoff, uitems = cases.user_items(n_items, ku, seed=17)
+    with Context(0) as a, Context(0) as b:
+        a.item_cosine(n_items, off, items, rats, adopt=True, want_matrix=False)
+        b.set_graph_layout("csr")
+        b.item_cosine_edges(n_items, off, items, rats, adopt=True)
+        assert b.graph_info()[0] == "csr" and b.graph_info()[2] == len(col)
+        ra, rb = a.eigen_batch(uoff, uitems), b.eigen_batch(uoff, uitems)
+        assert np.array_equal(ra.m, rb.m) and np.array_equal(ra.evecs, rb.evecs)
+        assert np.array_equal(ra.sigs, rb.sigs) and np.array_equal(ra.evals, rb.evals)
