@@ -76,6 +76,8 @@ def parse():
                    help="BASELINE config 5 sample (N=1, rank 0): power-law k mix through the LDS + spill paths")
     p.add_argument("--c5-users", type=int, default=1000)
     p.add_argument("--c5-kmax", type=int, default=5000, help="cap of the config-5 degrees (SURVEY 8d: 5000)")
+    p.add_argument("--c5-predict-kmax", type=int, default=3072,
+                   help="predict the C5 sample's groups up to this k (the per-rating systems grow as k^3)")
     return p.parse_args()
 
 
@@ -711,10 +713,13 @@ def c5_leg(args, ctx, dev, torch, W):
                        f"{n_items} items (config-4 knn2 graph), seed {seed}"}
     stream = torch.cuda.current_stream(dev)
     total_ms = total_pms = 0.0
-    for name, sel in (("lds", k <= CF_MAX_K), ("spill", k > CF_MAX_K)):
+    n_pred = 0
+    groups = (("lds", k <= CF_MAX_K), ("spill", (k > CF_MAX_K) & (k <= 3072)), ("spill_big", k > 3072))
+    for name, sel in groups:
         ks = k[sel]
         if len(ks) == 0:
             continue
+        print(f"[c5] {name}: {len(ks)} users, k {int(ks.min())}..{int(ks.max())}", file=sys.stderr, flush=True)
         o = np.zeros(len(ks) + 1, dtype=np.uint64)
         o[1:] = np.cumsum(ks.astype(np.uint64))
         it = np.concatenate([items[int(off[u]):int(off[u + 1])] for u in np.nonzero(sel)[0]])
@@ -733,6 +738,16 @@ def c5_leg(args, ctx, dev, torch, W):
         e1.synchronize()
         ms = e0.elapsed_time(e1)
         total_ms += ms
+        print(f"[c5] {name}: eigen {ms:.1f} ms", file=sys.stderr, flush=True)
+        if int(ks.max()) > args.c5_predict_kmax:   # the per-rating systems grow as k^3
+            kf = ks.astype(np.float64)
+            out[name] = {"users": int(len(ks)), "k_mean": float(kf.mean()), "ms": ms, "users_per_s": len(ks) / ms * 1e3,
+                         "GFLOPs_9k3": float(np.sum(9 * kf ** 3)) / ms / 1e6, "m_mean": float(d_m.float().mean().item()),
+                         "predict": f"skipped (k > --c5-predict-kmax {args.c5_predict_kmax})"}
+            plan.close()
+            del d_x
+            torch.cuda.empty_cache()
+            continue
         d_mse = torch.zeros(len(it), dtype=torch.float32, device=dev)
         d_kk = torch.zeros(len(it), dtype=torch.int32, device=dev)
         p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -743,6 +758,8 @@ def c5_leg(args, ctx, dev, torch, W):
         p1.synchronize()
         pms = p0.elapsed_time(p1)
         total_pms += pms
+        n_pred += len(it)
+        print(f"[c5] {name}: predict {pms:.1f} ms ({len(it)} ratings)", file=sys.stderr, flush=True)
         kf = ks.astype(np.float64)
         out[name] = {"users": int(len(ks)), "k_mean": float(kf.mean()), "ms": ms,
                      "users_per_s": len(ks) / ms * 1e3,
@@ -757,7 +774,8 @@ def c5_leg(args, ctx, dev, torch, W):
     out["users_per_s"] = args.c5_users / total_ms * 1e3
     out["ms"] = total_ms
     out["predict_ms"] = total_pms
-    out["ratings_per_s"] = int(k.sum()) / total_pms * 1e3
+    out["ratings_per_s"] = n_pred / total_pms * 1e3 if total_pms else None
+    out["predicted_ratings"] = n_pred
     return out
 
 
