@@ -569,22 +569,62 @@ void write_eigen_file(const std::string& path, bool append, int n_threads, bool 
                       const float* sigs, const float* evals, const uint64_t* eoff, const float* evecs) {
     std::ofstream f(path, std::ofstream::binary | (append ? std::ofstream::app : std::ofstream::trunc));
     if (!f) throw std::runtime_error("cannot open " + path);
-    if (binary) {   // "CFEIGEN1", n, then per record uid k m movies[k] sigs[k] evals[m] evecs[k*m]
+    if (binary) {
+        // "CFEIGEN1", n, then per record uid k m movies[k] sigs[k] evals[m] evecs[k*m]: every
+        // record's offset is known from (k, m) up front, so threads pwrite() user ranges in place
+        std::vector<uint64_t> at((size_t)n_users + 1, sizeof(kEigenMagic) + sizeof(uint64_t));
+        for (uint32_t u = 0; u < n_users; ++u) {
+            const uint64_t k = off[u + 1] - off[u], mm = (uint64_t)std::max(m[u], 0);
+            at[u + 1] = at[u] + 4 * (3 + 2 * k + mm + k * mm);
+        }
         const uint64_t n = n_users;
         f.write(kEigenMagic, sizeof(kEigenMagic));
         f.write(reinterpret_cast<const char*>(&n), sizeof(n));
-        std::vector<float> ev;
-        for (uint32_t u = 0; u < n_users; ++u) {
-            const uint32_t k = (uint32_t)(off[u + 1] - off[u]), mm = (uint32_t)m[u];
-            const uint32_t hdr[3] = {uid[u], k, mm};
-            f.write(reinterpret_cast<const char*>(hdr), sizeof(hdr));
-            f.write(reinterpret_cast<const char*>(movies + off[u]), sizeof(uint32_t) * k);
-            f.write(reinterpret_cast<const char*>(sigs + off[u]), sizeof(float) * k);
-            ev.assign(mm, 0.0f);   // entries past k (k == 1 padding) are 0, as in the text form
-            for (uint32_t j = 0; j < mm && j < k; ++j) ev[j] = evals[off[u] + j];
-            f.write(reinterpret_cast<const char*>(ev.data()), sizeof(float) * mm);
-            f.write(reinterpret_cast<const char*>(evecs + eoff[u]), sizeof(float) * (size_t)k * mm);
-        }
+        f.close();
+        const int wfd = ::open(path.c_str(), O_WRONLY);
+        if (wfd < 0) throw std::runtime_error("cannot open " + path);
+        const uint64_t base = append ? (uint64_t)::lseek(wfd, 0, SEEK_END) - at[0] : 0;
+        const int T = (int)std::min<uint32_t>((uint32_t)resolve_threads(n_threads), std::max<uint32_t>(n_users, 1));
+        std::atomic<bool> failed{false};
+        parallel_for(T, [&](int t) {
+            const uint32_t u0 = (uint32_t)((uint64_t)n_users * t / T), u1 = (uint32_t)((uint64_t)n_users * (t + 1) / T);
+            std::vector<char> buf;
+            for (uint32_t c0 = u0; c0 < u1;) {   // ~8 MB pieces
+                uint32_t c1 = c0;
+                while (c1 < u1 && (c1 == c0 || at[c1 + 1] - at[c0] < (8u << 20))) ++c1;
+                buf.resize(at[c1] - at[c0]);
+                char* p = buf.data();
+                for (uint32_t u = c0; u < c1; ++u) {
+                    const uint32_t k = (uint32_t)(off[u + 1] - off[u]), mm = (uint32_t)std::max(m[u], 0);
+                    const uint32_t hdr[3] = {uid[u], k, mm};
+                    std::memcpy(p, hdr, sizeof(hdr));
+                    p += sizeof(hdr);
+                    std::memcpy(p, movies + off[u], 4ull * k);
+                    p += 4ull * k;
+                    std::memcpy(p, sigs + off[u], 4ull * k);
+                    p += 4ull * k;
+                    for (uint32_t j = 0; j < mm; ++j) {   // entries past k (k == 1 padding) are 0
+                        const float v = j < k ? evals[off[u] + j] : 0.0f;
+                        std::memcpy(p, &v, 4);
+                        p += 4;
+                    }
+                    std::memcpy(p, evecs + eoff[u], 4ull * k * mm);
+                    p += 4ull * k * mm;
+                }
+                size_t done = 0;
+                while (done < buf.size()) {
+                    const ssize_t w = ::pwrite(wfd, buf.data() + done, buf.size() - done, (off_t)(base + at[c0] + done));
+                    if (w <= 0) {
+                        failed = true;
+                        break;
+                    }
+                    done += (size_t)w;
+                }
+                c0 = c1;
+            }
+        });
+        ::close(wfd);
+        if (failed) throw std::runtime_error("write failed: " + path);
         return;
     }
     // text: chunks of users formatted in parallel; chunk c lands at the sum of the sizes of
