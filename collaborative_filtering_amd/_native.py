@@ -63,6 +63,12 @@ SIGNATURES = {
     "cf_predict_precomp_multi": (c_int, [c_void_p, c_int, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p]),
+    "cf_predict_precomp_sel_f32": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_void_p,
+                                       c_void_p, c_void_p]),
+    "cf_predict_precomp_multi_f32": (c_int, [c_void_p, c_int, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p]),
     "cf_step_run": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "cf_step_timing": (c_int, [c_void_p, c_void_p, c_void_p]),
@@ -114,7 +120,11 @@ def load() -> ctypes.CDLL:
         raise NativeError(f"{LIB_PATH} not built; run `make` or __graft_entry__.build()")
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if os.environ.get("CF_MI355X_LIB"):   # an older variant build (A/B runs): skip
+                continue
+            raise NativeError(f"{LIB_PATH} does not export {name}")
         fn.restype = res
         fn.argtypes = args
     _lib = lib

@@ -216,24 +216,34 @@ class Context:
     # -- neigh_program::apply (local_calc_precomp.cpp:217-380) --------------------
     def predict_precomp(self, item_off, items, ratings, m, evals, evec_off, evecs, sigtab,
                         sig_mode=CF_SIGS_COMPAT, want_pred=False):
-        """All arrays host numpy; evals/evecs/sigtab float64 (parsed out_eigen_)."""
+        """All arrays host numpy; evals/sigtab float64 (parsed out_eigen_).  evecs float64 (text
+        out_eigen_), or float32 (the binary form's blocks: cf_predict_precomp_sel_f32, same results
+        as the widened blocks)."""
         item_off = np.ascontiguousarray(item_off, dtype=np.uint64)
         items = np.ascontiguousarray(items, dtype=np.uint32)
         ratings = np.ascontiguousarray(ratings, dtype=np.float32)
         m = np.ascontiguousarray(m, dtype=np.int32)
         evals = np.ascontiguousarray(evals, dtype=np.float64)
         evec_off = np.ascontiguousarray(evec_off, dtype=np.uint64)
-        evecs = np.ascontiguousarray(evecs, dtype=np.float64)
+        f32 = np.asarray(evecs).dtype == np.float32
+        evecs = np.ascontiguousarray(evecs, dtype=np.float32 if f32 else np.float64)
         sigtab = np.ascontiguousarray(sigtab, dtype=np.float64)
         n_users = len(item_off) - 1
         n = int(item_off[-1])
         mse = np.zeros(n, dtype=np.float32)
         kk = np.zeros(n, dtype=np.int32)
         pred = np.zeros(n, dtype=np.float64) if want_pred else None
-        self._chk(self.lib.cf_predict_precomp(self.h, n_users, ptr(item_off), ptr(items), ptr(ratings), ptr(m),
-                                              ptr(evals), ptr(evec_off), ptr(evecs), ptr(sigtab), len(sigtab),
-                                              int(sig_mode), ptr(mse), ptr(kk), ptr(pred)),
-                  "cf_predict_precomp")
+        if f32:
+            self._chk(self.lib.cf_predict_precomp_sel_f32(self.h, n_users, ptr(item_off), ptr(items), ptr(ratings),
+                                                          ptr(m), ptr(evals), ptr(evec_off), ptr(evecs), ptr(sigtab),
+                                                          len(sigtab), int(sig_mode), None, ptr(mse), ptr(kk),
+                                                          ptr(pred)),
+                      "cf_predict_precomp_sel_f32")
+        else:
+            self._chk(self.lib.cf_predict_precomp(self.h, n_users, ptr(item_off), ptr(items), ptr(ratings), ptr(m),
+                                                  ptr(evals), ptr(evec_off), ptr(evecs), ptr(sigtab), len(sigtab),
+                                                  int(sig_mode), ptr(mse), ptr(kk), ptr(pred)),
+                      "cf_predict_precomp")
         return (mse, kk, pred) if want_pred else (mse, kk)
 
     # -- weights_calc (knn2.cpp:127-164) -------------------------------------------
@@ -440,7 +450,8 @@ def predict_precomp_multi(ctxs, item_off, items, ratings, m, evals, evec_off, ev
     m = np.ascontiguousarray(m, dtype=np.int32)
     evals = np.ascontiguousarray(evals, dtype=np.float64)
     evec_off = np.ascontiguousarray(evec_off, dtype=np.uint64)
-    evecs = np.ascontiguousarray(evecs, dtype=np.float64)
+    f32 = np.asarray(evecs).dtype == np.float32   # binary out_eigen_ blocks: the _f32 entry point
+    evecs = np.ascontiguousarray(evecs, dtype=np.float32 if f32 else np.float64)
     sigtab = np.ascontiguousarray(sigtab, dtype=np.float64)
     sel = None if row_sel is None else np.ascontiguousarray(row_sel, dtype=np.uint8)
     n_users = len(item_off) - 1
@@ -450,10 +461,10 @@ def predict_precomp_multi(ctxs, item_off, items, ratings, m, evals, evec_off, ev
     pred = np.zeros(n, dtype=np.float64) if want_pred else None
     split = np.zeros(len(ctxs) + 1, dtype=np.uint32)
     arr = (c_void_p * len(ctxs))(*[c.h for c in ctxs])
-    rc = lib.cf_predict_precomp_multi(arr, len(ctxs), n_users, ptr(item_off), ptr(items), ptr(ratings), ptr(m),
-                                      ptr(evals), ptr(evec_off), ptr(evecs), ptr(sigtab), len(sigtab), int(sig_mode),
-                                      ptr(sel), ptr(mse), ptr(kk), ptr(pred), ptr(split))
-    _check(lib, ctxs[0].h, rc, "cf_predict_precomp_multi")
+    fn = lib.cf_predict_precomp_multi_f32 if f32 else lib.cf_predict_precomp_multi
+    rc = fn(arr, len(ctxs), n_users, ptr(item_off), ptr(items), ptr(ratings), ptr(m), ptr(evals), ptr(evec_off),
+            ptr(evecs), ptr(sigtab), len(sigtab), int(sig_mode), ptr(sel), ptr(mse), ptr(kk), ptr(pred), ptr(split))
+    _check(lib, ctxs[0].h, rc, "cf_predict_precomp_multi" + ("_f32" if f32 else ""))
     out = (mse, kk, pred) if want_pred else (mse, kk)
     return out + (split.astype(np.int64),)
 

@@ -8,6 +8,8 @@
 #include <cstring>
 #include <new>
 
+#include <type_traits>
+
 #include "cf_internal.h"
 
 int cf_set_error(cf_ctx* ctx, int code, const std::string& msg) {
@@ -370,10 +372,17 @@ int cf_predict_precomp(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, 
                                   sigtab_len, sig_mode, nullptr, mse, kk, pred);
 }
 
-int cf_predict_precomp_sel(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, const uint32_t* items,
-                           const float* ratings, const int32_t* m, const double* evals, const uint64_t* evec_off,
-                           const double* evecs, const double* sigtab, uint64_t sigtab_len, int sig_mode,
-                           const uint8_t* row_sel, float* mse, int32_t* kk, double* pred) {
+}  // extern "C"
+
+namespace {
+// EV = double (text out_eigen_: decimal values) or float (binary out_eigen_ / device blocks):
+// the kernels widen fp32 blocks to fp64 on load, so a float block gives the same predictions
+// as the same values passed widened
+template <typename EV>
+int predict_precomp_impl(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, const uint32_t* items,
+                         const float* ratings, const int32_t* m, const double* evals, const uint64_t* evec_off,
+                         const EV* evecs, const double* sigtab, uint64_t sigtab_len, int sig_mode,
+                         const uint8_t* row_sel, float* mse, int32_t* kk, double* pred) {
     if (!ctx || !item_off || !items || !ratings || !m || !evals || !evec_off || !evecs || !sigtab || !mse || !kk)
         return cf_set_error(ctx, CF_EINVAL, "cf_predict_precomp: null argument");
     if (sig_mode != CF_SIGS_OWN && sig_mode != CF_SIGS_COMPAT)
@@ -396,14 +405,14 @@ int cf_predict_precomp_sel(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_o
         if (items[e] >= ctx->n_items) return cf_set_error(ctx, CF_EINVAL, "item index outside the graph");
     cf_plan* plan = nullptr;
     CF_TRY(cf_plan_create(ctx, n_users, item_off, &plan));
-    DevBuf doff, ditems, drat, dm, deval, deoff, devec, dsig, dmse, dkk, dpred, dsel;
+    DevBuf doff, ditems, drat, dm, deval, deoff, devec, dsig, dmse, dkk, dpred, dsel, deval32, dsig32;
     int rc = dev_alloc(ctx, doff, sizeof(uint64_t) * (n_users + 1));
     if (rc == CF_OK) rc = dev_alloc(ctx, ditems, sizeof(uint32_t) * n_entries);
     if (rc == CF_OK) rc = dev_alloc(ctx, drat, sizeof(float) * n_entries);
     if (rc == CF_OK) rc = dev_alloc(ctx, dm, sizeof(int32_t) * std::max<uint32_t>(n_users, 1));
     if (rc == CF_OK) rc = dev_alloc(ctx, deval, sizeof(double) * n_entries);
     if (rc == CF_OK) rc = dev_alloc(ctx, deoff, sizeof(uint64_t) * std::max<uint32_t>(n_users, 1));
-    if (rc == CF_OK) rc = dev_alloc(ctx, devec, sizeof(double) * n_evec);
+    if (rc == CF_OK) rc = dev_alloc(ctx, devec, sizeof(EV) * n_evec);
     if (rc == CF_OK) rc = dev_alloc(ctx, dsig, sizeof(double) * sigtab_len);
     if (rc == CF_OK) rc = dev_alloc(ctx, dmse, sizeof(float) * n_entries);
     if (rc == CF_OK) rc = dev_alloc(ctx, dkk, sizeof(int32_t) * n_entries);
@@ -420,7 +429,7 @@ int cf_predict_precomp_sel(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_o
         h2d(dm.p, m, sizeof(int32_t) * n_users);
         h2d(deval.p, evals, sizeof(double) * n_entries);
         h2d(deoff.p, evec_off, sizeof(uint64_t) * n_users);
-        h2d(devec.p, evecs, sizeof(double) * n_evec);
+        h2d(devec.p, evecs, sizeof(EV) * n_evec);
         h2d(dsig.p, sigtab, sizeof(double) * sigtab_len);
         if (row_sel) {
             h2d(dsel.p, row_sel, n_entries);
@@ -431,12 +440,32 @@ int cf_predict_precomp_sel(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_o
         }
         if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("predict H2D: ") + hipGetErrorString(e));
     }
-    if (rc == CF_OK)
-        rc = cf_launch_predict<double>(ctx, plan, (const uint64_t*)doff.p, (const uint32_t*)ditems.p,
-                                       (const float*)drat.p, (const int32_t*)dm.p, (const double*)deval.p,
-                                       (const uint64_t*)deoff.p, (const double*)devec.p, (const double*)dsig.p,
-                                       sig_mode, (float*)dmse.p, (int32_t*)dkk.p, (double*)dpred.p,
-                                       (const uint8_t*)dsel.p, nullptr);
+    if (rc == CF_OK) {
+        if constexpr (std::is_same<EV, double>::value) {
+            rc = cf_launch_predict<double>(ctx, plan, (const uint64_t*)doff.p, (const uint32_t*)ditems.p,
+                                           (const float*)drat.p, (const int32_t*)dm.p, (const double*)deval.p,
+                                           (const uint64_t*)deoff.p, (const double*)devec.p, (const double*)dsig.p,
+                                           sig_mode, (float*)dmse.p, (int32_t*)dkk.p, (double*)dpred.p,
+                                           (const uint8_t*)dsel.p, nullptr);
+        } else {
+            // the fp32 launch takes fp32 evals / sigs: the binary file's values, narrowed back exactly
+            std::vector<float> ev32(n_entries), sg32(sigtab_len);
+            for (uint64_t i = 0; i < n_entries; ++i) ev32[i] = (float)evals[i];
+            for (uint64_t i = 0; i < sigtab_len; ++i) sg32[i] = (float)sigtab[i];
+            rc = dev_alloc(ctx, deval32, sizeof(float) * std::max<uint64_t>(n_entries, 1));
+            if (rc == CF_OK) rc = dev_alloc(ctx, dsig32, sizeof(float) * std::max<uint64_t>(sigtab_len, 1));
+            if (rc == CF_OK && n_entries) e = hipMemcpy(deval32.p, ev32.data(), sizeof(float) * n_entries, hipMemcpyHostToDevice);
+            if (rc == CF_OK && e == hipSuccess && sigtab_len)
+                e = hipMemcpy(dsig32.p, sg32.data(), sizeof(float) * sigtab_len, hipMemcpyHostToDevice);
+            if (rc == CF_OK && e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("predict H2D: ") + hipGetErrorString(e));
+            if (rc == CF_OK)
+                rc = cf_launch_predict<float>(ctx, plan, (const uint64_t*)doff.p, (const uint32_t*)ditems.p,
+                                              (const float*)drat.p, (const int32_t*)dm.p, (const float*)deval32.p,
+                                              (const uint64_t*)deoff.p, (const float*)devec.p, (const float*)dsig32.p,
+                                              sig_mode, (float*)dmse.p, (int32_t*)dkk.p, (double*)dpred.p,
+                                              (const uint8_t*)dsel.p, nullptr);
+        }
+    }
     if (rc == CF_OK) {
         e = hipDeviceSynchronize();
         if (e == hipSuccess && n_entries) e = hipMemcpy(mse, dmse.p, sizeof(float) * n_entries, hipMemcpyDeviceToHost);
@@ -447,6 +476,25 @@ int cf_predict_precomp_sel(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_o
     }
     cf_plan_destroy(plan);
     return rc;
+}
+}  // namespace
+
+extern "C" {
+
+int cf_predict_precomp_sel(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, const uint32_t* items,
+                           const float* ratings, const int32_t* m, const double* evals, const uint64_t* evec_off,
+                           const double* evecs, const double* sigtab, uint64_t sigtab_len, int sig_mode,
+                           const uint8_t* row_sel, float* mse, int32_t* kk, double* pred) {
+    return predict_precomp_impl<double>(ctx, n_users, item_off, items, ratings, m, evals, evec_off, evecs, sigtab,
+                                        sigtab_len, sig_mode, row_sel, mse, kk, pred);
+}
+
+int cf_predict_precomp_sel_f32(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, const uint32_t* items,
+                               const float* ratings, const int32_t* m, const double* evals, const uint64_t* evec_off,
+                               const float* evecs, const double* sigtab, uint64_t sigtab_len, int sig_mode,
+                               const uint8_t* row_sel, float* mse, int32_t* kk, double* pred) {
+    return predict_precomp_impl<float>(ctx, n_users, item_off, items, ratings, m, evals, evec_off, evecs, sigtab,
+                                       sigtab_len, sig_mode, row_sel, mse, kk, pred);
 }
 
 // ---- knn2: weights_calc over transform_edges (knn2.cpp:127-164) ---------------------

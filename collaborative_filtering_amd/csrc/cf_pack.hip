@@ -92,6 +92,55 @@ void cost_split(uint32_t n_users, const uint64_t* item_off, int n_parts, uint32_
 
 }  // namespace
 
+namespace {
+template <typename EV, typename SEL>
+int predict_precomp_multi_impl(SEL sel, cf_ctx* const* ctxs, int n_dev, uint32_t n_users, const uint64_t* item_off,
+                               const uint32_t* items, const float* ratings, const int32_t* m, const double* evals,
+                               const uint64_t* evec_off, const EV* evecs, const double* sigtab,
+                               uint64_t sigtab_len, int sig_mode, const uint8_t* row_sel, float* mse, int32_t* kk,
+                               double* pred, uint32_t* split_out) {
+    if (!ctxs || n_dev <= 0 || !ctxs[0]) return CF_EINVAL;
+    cf_ctx* root = ctxs[0];
+    if (!item_off || !items || !ratings || !m || !evals || !evec_off || !evecs || !sigtab || !mse || !kk)
+        return cf_set_error(root, CF_EINVAL, "cf_predict_precomp_multi: null argument");
+    if (sig_mode != CF_SIGS_OWN && sig_mode != CF_SIGS_COMPAT)
+        return cf_set_error(root, CF_EINVAL, "cf_predict_precomp_multi: bad sig_mode");
+    if (sig_mode == CF_SIGS_OWN && sigtab_len < item_off[n_users])
+        return cf_set_error(root, CF_EINVAL, "cf_predict_precomp_multi: sig table shorter than item_off[n_users]");
+    for (int d = 0; d < n_dev; ++d)
+        if (!ctxs[d]) return cf_set_error(root, CF_EINVAL, "cf_predict_precomp_multi: null context");
+    std::vector<uint32_t> split(n_dev + 1);
+    cost_split(n_users, item_off, n_dev, split.data());
+    if (split_out) std::copy(split.begin(), split.end(), split_out);
+    std::vector<int> rcs(n_dev, CF_OK);
+    std::vector<std::thread> pool;
+    for (int d = 0; d < n_dev; ++d)
+        pool.emplace_back([&, d]() {
+            const uint32_t u0 = split[d], nu = split[d + 1] - split[d];
+            if (nu == 0) return;
+            const uint64_t e0 = item_off[u0], ne = item_off[u0 + nu] - e0;
+            // the part's eigenvector blocks start at its smallest offset; offsets re-based on it
+            uint64_t lo = UINT64_MAX;
+            std::vector<uint64_t> off(nu + 1), eoff(nu);
+            for (uint32_t u = 0; u < nu; ++u) lo = std::min(lo, evec_off[u0 + u]);
+            for (uint32_t u = 0; u <= nu; ++u) off[u] = item_off[u0 + u] - e0;
+            for (uint32_t u = 0; u < nu; ++u) eoff[u] = evec_off[u0 + u] - lo;
+            const bool compat = sig_mode == CF_SIGS_COMPAT;
+            rcs[d] = sel(ctxs[d], nu, off.data(), items + e0, ratings + e0, m + u0, evals + e0,
+                                            eoff.data(), evecs + lo, compat ? sigtab : sigtab + e0,
+                                            compat ? sigtab_len : ne, sig_mode, row_sel ? row_sel + e0 : nullptr,
+                                            mse + e0, kk + e0, pred ? pred + e0 : nullptr);
+        });
+    for (auto& t : pool) t.join();
+    for (int d = 0; d < n_dev; ++d)
+        if (rcs[d] != CF_OK)
+            return cf_set_error(root, rcs[d], "device part " + std::to_string(d) + ": " + ctxs[d]->last_error);
+    (void)hipSetDevice(root->device);
+    return CF_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int cf_cost_split(uint32_t n_users, const uint64_t* item_off, int n_parts, uint32_t* split) {
@@ -309,44 +358,19 @@ int cf_predict_precomp_multi(cf_ctx* const* ctxs, int n_dev, uint32_t n_users, c
                              const uint64_t* evec_off, const double* evecs, const double* sigtab,
                              uint64_t sigtab_len, int sig_mode, const uint8_t* row_sel, float* mse, int32_t* kk,
                              double* pred, uint32_t* split_out) {
-    if (!ctxs || n_dev <= 0 || !ctxs[0]) return CF_EINVAL;
-    cf_ctx* root = ctxs[0];
-    if (!item_off || !items || !ratings || !m || !evals || !evec_off || !evecs || !sigtab || !mse || !kk)
-        return cf_set_error(root, CF_EINVAL, "cf_predict_precomp_multi: null argument");
-    if (sig_mode != CF_SIGS_OWN && sig_mode != CF_SIGS_COMPAT)
-        return cf_set_error(root, CF_EINVAL, "cf_predict_precomp_multi: bad sig_mode");
-    if (sig_mode == CF_SIGS_OWN && sigtab_len < item_off[n_users])
-        return cf_set_error(root, CF_EINVAL, "cf_predict_precomp_multi: sig table shorter than item_off[n_users]");
-    for (int d = 0; d < n_dev; ++d)
-        if (!ctxs[d]) return cf_set_error(root, CF_EINVAL, "cf_predict_precomp_multi: null context");
-    std::vector<uint32_t> split(n_dev + 1);
-    cost_split(n_users, item_off, n_dev, split.data());
-    if (split_out) std::copy(split.begin(), split.end(), split_out);
-    std::vector<int> rcs(n_dev, CF_OK);
-    std::vector<std::thread> pool;
-    for (int d = 0; d < n_dev; ++d)
-        pool.emplace_back([&, d]() {
-            const uint32_t u0 = split[d], nu = split[d + 1] - split[d];
-            if (nu == 0) return;
-            const uint64_t e0 = item_off[u0], ne = item_off[u0 + nu] - e0;
-            // the part's eigenvector blocks start at its smallest offset; offsets re-based on it
-            uint64_t lo = UINT64_MAX;
-            std::vector<uint64_t> off(nu + 1), eoff(nu);
-            for (uint32_t u = 0; u < nu; ++u) lo = std::min(lo, evec_off[u0 + u]);
-            for (uint32_t u = 0; u <= nu; ++u) off[u] = item_off[u0 + u] - e0;
-            for (uint32_t u = 0; u < nu; ++u) eoff[u] = evec_off[u0 + u] - lo;
-            const bool compat = sig_mode == CF_SIGS_COMPAT;
-            rcs[d] = cf_predict_precomp_sel(ctxs[d], nu, off.data(), items + e0, ratings + e0, m + u0, evals + e0,
-                                            eoff.data(), evecs + lo, compat ? sigtab : sigtab + e0,
-                                            compat ? sigtab_len : ne, sig_mode, row_sel ? row_sel + e0 : nullptr,
-                                            mse + e0, kk + e0, pred ? pred + e0 : nullptr);
-        });
-    for (auto& t : pool) t.join();
-    for (int d = 0; d < n_dev; ++d)
-        if (rcs[d] != CF_OK)
-            return cf_set_error(root, rcs[d], "device part " + std::to_string(d) + ": " + ctxs[d]->last_error);
-    (void)hipSetDevice(root->device);
-    return CF_OK;
+    return predict_precomp_multi_impl<double>(cf_predict_precomp_sel, ctxs, n_dev, n_users, item_off, items, ratings, m,
+                                              evals, evec_off, evecs, sigtab, sigtab_len, sig_mode, row_sel, mse, kk,
+                                              pred, split_out);
+}
+
+int cf_predict_precomp_multi_f32(cf_ctx* const* ctxs, int n_dev, uint32_t n_users, const uint64_t* item_off,
+                                 const uint32_t* items, const float* ratings, const int32_t* m, const double* evals,
+                                 const uint64_t* evec_off, const float* evecs, const double* sigtab,
+                                 uint64_t sigtab_len, int sig_mode, const uint8_t* row_sel, float* mse, int32_t* kk,
+                                 double* pred, uint32_t* split_out) {
+    return predict_precomp_multi_impl<float>(cf_predict_precomp_sel_f32, ctxs, n_dev, n_users, item_off, items, ratings,
+                                             m, evals, evec_off, evecs, sigtab, sigtab_len, sig_mode, row_sel, mse, kk,
+                                             pred, split_out);
 }
 
 }  // extern "C"

@@ -79,11 +79,20 @@ int main(int argc, char** argv) {
             evals[off[u] + j] = j < nm ? recs.evals[recs.eval_off[u] + j] : 0.0;
         }
     }
+    // text records carry fp64 blocks, the binary form its fp32 blocks as they are (the _f32 entry
+    // points: same predictions as the widened values)
+    const bool f32 = recs.binary;
     std::vector<double> evecs_pad;
+    std::vector<float> evecs_pad32;
     const double* evecs_p = recs.evecs.data();
+    const float* evecs_p32 = recs.evecs_f32.data();
     if (recs.evecs.empty()) {
         evecs_pad.assign(1, 0.0);
         evecs_p = evecs_pad.data();
+    }
+    if (recs.evecs_f32.empty()) {
+        evecs_pad32.assign(1, 0.0f);
+        evecs_p32 = evecs_pad32.data();
     }
     // movie vertices sampled like rand() % 100 < pct in apply (:221), BEFORE prediction:
     // only the rows of sampled movies are predicted (cf_predict_precomp_sel)
@@ -116,7 +125,12 @@ int main(int argc, char** argv) {
     if (n_dev == 1) {
         cf_ctx* ctx = cfcli::open_device();
         cfcli::upload_edges(ctx, items, edges);
-        if (n_users)
+        if (n_users && f32)
+            cfcli::check(ctx, cf_predict_precomp_sel_f32(ctx, n_users, off.data(), its.data(), rats.data(), m.data(),
+                                                         evals.data(), eoff.data(), evecs_p32, tab, tab_len, mode,
+                                                         rsel, mse.data(), kk.data(), nullptr),
+                         "cf_predict_precomp_sel_f32");
+        else if (n_users)
             cfcli::check(ctx, cf_predict_precomp_sel(ctx, n_users, off.data(), its.data(), rats.data(), m.data(),
                                                      evals.data(), eoff.data(), evecs_p, tab, tab_len, mode,
                                                      rsel, mse.data(), kk.data(), nullptr),
@@ -133,7 +147,13 @@ int main(int argc, char** argv) {
             cfcli::upload_edges(ctxs[d], items, edges);
         }
         std::vector<uint32_t> split(n_dev + 1);
-        if (n_users)
+        if (n_users && f32)
+            cfcli::check(ctxs[0], cf_predict_precomp_multi_f32(ctxs.data(), n_dev, n_users, off.data(), its.data(),
+                                                               rats.data(), m.data(), evals.data(), eoff.data(),
+                                                               evecs_p32, tab, tab_len, mode, rsel, mse.data(),
+                                                               kk.data(), nullptr, split.data()),
+                         "cf_predict_precomp_multi_f32");
+        else if (n_users)
             cfcli::check(ctxs[0], cf_predict_precomp_multi(ctxs.data(), n_dev, n_users, off.data(), its.data(),
                                                            rats.data(), m.data(), evals.data(), eoff.data(),
                                                            evecs_p, tab, tab_len, mode, rsel, mse.data(),

@@ -389,7 +389,9 @@ void parallel_for(int n, F&& f) {
 struct Mapped {
     const char* p = nullptr;
     size_t n = 0;
-    explicit Mapped(const std::string& path) {
+    // populate: fault the whole file in at map time (one kernel thread); otherwise the parsing
+    // threads fault their own ranges in parallel
+    explicit Mapped(const std::string& path, bool populate = true) {
         const int fd = ::open(path.c_str(), O_RDONLY);
         if (fd < 0) throw std::runtime_error("cannot open " + path);
         struct stat st;
@@ -399,7 +401,7 @@ struct Mapped {
         }
         n = (size_t)st.st_size;
         if (n) {
-            void* v = mmap(nullptr, n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+            void* v = mmap(nullptr, n, PROT_READ, MAP_PRIVATE | (populate ? MAP_POPULATE : 0), fd, 0);
             if (v == MAP_FAILED) {
                 ::close(fd);
                 throw std::runtime_error("cannot map " + path);
@@ -429,7 +431,8 @@ void flat_resize(EigenFlat& F, const std::vector<uint32_t>& k) {
     F.movies.resize(F.off.back());
     F.sigs.resize(F.off.back());
     F.evals.resize(F.eval_off.back());
-    F.evecs.resize(F.evec_off.back());
+    if (F.binary) F.evecs_f32.resize(F.evec_off.back());
+    else F.evecs.resize(F.evec_off.back());
 }
 
 void load_flat_binary(const Mapped& f, const std::string& path, int T, EigenFlat& F) {
@@ -458,10 +461,22 @@ void load_flat_binary(const Mapped& f, const std::string& path, int T, EigenFlat
         need(sizeof(hdr) + body);
         pos += sizeof(hdr) + body;
     }
+    F.binary = true;
     flat_resize(F, k);
+    if (n == 0) return;
+    // record ranges of about equal bytes per thread; the fp32 blocks are copied as they are
+    // (the predictor's fp32 entry widens them on the device, exactly)
+    std::vector<size_t> cut(T + 1, n);
+    cut[0] = 0;
+    {
+        const size_t total = pos - at.front() + 12, per = total / T + 1;
+        size_t t = 1;
+        for (size_t r = 0; r < n && t < (size_t)T; ++r)
+            if (at[r] - at[0] >= per * t) cut[t++] = r;
+        for (; t < (size_t)T; ++t) cut[t] = n;
+    }
     parallel_for(T, [&](int t) {
-        const size_t r0 = n * t / T, r1 = n * (t + 1) / T;
-        for (size_t r = r0; r < r1; ++r) {
+        for (size_t r = cut[t]; r < cut[t + 1]; ++r) {
             const char* q = f.p + at[r];
             const size_t kk = k[r], mm = (size_t)F.m[r];
             std::memcpy(F.movies.data() + F.off[r], q, 4 * kk);
@@ -476,7 +491,7 @@ void load_flat_binary(const Mapped& f, const std::string& path, int T, EigenFlat
             };
             widen(F.sigs.data() + F.off[r], kk);
             widen(F.evals.data() + F.eval_off[r], mm);
-            widen(F.evecs.data() + F.evec_off[r], kk * mm);
+            std::memcpy(F.evecs_f32.data() + F.evec_off[r], q, 4 * kk * mm);
         }
     });
 }
@@ -549,10 +564,16 @@ void load_flat_text(const Mapped& f, const std::string& path, int T, EigenFlat& 
 }  // namespace
 
 EigenFlat load_eigen_flat(const std::string& path, int n_threads) {
-    Mapped f(path);
     EigenFlat F;
     const int T = resolve_threads(n_threads);
-    if (f.n >= sizeof(kEigenMagic) && std::memcmp(f.p, kEigenMagic, sizeof(kEigenMagic)) == 0)
+    bool binary = false;
+    {
+        std::ifstream h(path, std::ifstream::binary);
+        char magic[sizeof(kEigenMagic)] = {};
+        binary = h.read(magic, sizeof(magic)) && std::memcmp(magic, kEigenMagic, sizeof(kEigenMagic)) == 0;
+    }
+    Mapped f(path, !binary);   // the binary form is faulted in by its copying threads
+    if (binary)
         load_flat_binary(f, path, T, F);
     else
         load_flat_text(f, path, T, F);
@@ -715,7 +736,8 @@ extern "C" int64_t cfh_load_eigen(const char* path, int n_threads, double* flat,
             for (uint64_t i = F.off[r]; i < F.off[r + 1]; ++i) put(F.movies[i]);
             for (uint64_t i = F.off[r]; i < F.off[r + 1]; ++i) put(F.sigs[i]);
             for (uint64_t i = F.eval_off[r]; i < F.eval_off[r + 1]; ++i) put(F.evals[i]);
-            for (uint64_t i = F.evec_off[r]; i < F.evec_off[r + 1]; ++i) put(F.evecs[i]);
+            for (uint64_t i = F.evec_off[r]; i < F.evec_off[r + 1]; ++i)
+                put(F.binary ? (double)F.evecs_f32[i] : F.evecs[i]);
         }
         if (flat && pos > cap) return -2;
         return (int64_t)F.size();

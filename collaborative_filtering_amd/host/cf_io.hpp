@@ -115,7 +115,9 @@ struct EigenFlat {
     std::vector<uint64_t> eval_off;   // n + 1, prefix of m
     RawVec<double> evals;
     std::vector<uint64_t> evec_off;   // n + 1, prefix of k * m
-    RawVec<double> evecs;
+    RawVec<double> evecs;             // text form (decimal %g values parse to double, :454-476)
+    RawVec<float> evecs_f32;          // binary form: the file's fp32 blocks, copied as they are
+    bool binary = false;              // evecs_f32 holds the blocks (else evecs)
     size_t size() const { return user.size(); }
 };
 EigenFlat load_eigen_flat(const std::string& path, int n_threads = 0);

@@ -212,6 +212,21 @@ int cf_predict_precomp_multi(cf_ctx* const* ctxs, int n_dev, uint32_t n_users, c
                              const uint64_t* evec_off, const double* evecs, const double* sigtab,
                              uint64_t sigtab_len, int sig_mode, const uint8_t* row_sel, float* mse, int32_t* kk,
                              double* pred, uint32_t* split_out);
+/* The same two entry points with fp32 eigenvector blocks: the binary out_eigen_ stores fp32
+ * values, and keeping them fp32 halves the host copy and the upload.  evals and sigtab are
+ * taken as fp32 values (the binary file's own; they are narrowed back exactly).  The kernels
+ * widen every value to fp64 on load, so results equal the fp64 entry points' on the widened
+ * arrays bit for bit. */
+int cf_predict_precomp_sel_f32(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off,
+                               const uint32_t* items, const float* ratings, const int32_t* m,
+                               const double* evals, const uint64_t* evec_off, const float* evecs,
+                               const double* sigtab, uint64_t sigtab_len, int sig_mode,
+                               const uint8_t* row_sel, float* mse, int32_t* kk, double* pred);
+int cf_predict_precomp_multi_f32(cf_ctx* const* ctxs, int n_dev, uint32_t n_users, const uint64_t* item_off,
+                                 const uint32_t* items, const float* ratings, const int32_t* m, const double* evals,
+                                 const uint64_t* evec_off, const float* evecs, const double* sigtab,
+                                 uint64_t sigtab_len, int sig_mode, const uint8_t* row_sel, float* mse, int32_t* kk,
+                                 double* pred, uint32_t* split_out);
 int cf_predict_run_f64(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
                        const uint32_t* d_items, const float* d_ratings, const int32_t* d_m,
                        const double* d_evals, const uint64_t* d_evec_off,

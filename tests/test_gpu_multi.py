@@ -144,6 +144,37 @@ def test_predict_precomp_multi_bit_identical(gpu_ctx):
         assert np.array_equal(mse, ref[0], equal_nan=True)
 
 
+def test_predict_precomp_f32_blocks_bit_identical(gpu_ctx):
+    """The binary out_eigen_ keeps its fp32 blocks (cf_predict_precomp_sel_f32 /
+    cf_predict_precomp_multi_f32): predictions equal the fp64 entry points' on the widened
+    blocks bit for bit, one context and two (compat mode, C2 subsample)."""
+    from collaborative_filtering_amd.api import CF_SIGS_COMPAT, Context, predict_precomp_multi
+
+    d_W, off, items, rat = _c2_subsample(1200, seed=23)
+    gpu_ctx.upload_graph_dense(d_W)
+    res = gpu_ctx.eigen_batch(off, items)
+    evals = res.evals.astype(np.float64)
+    sig = res.sigs.astype(np.float64)
+    ref = gpu_ctx.predict_precomp(off, items, rat, res.m, evals, res.evec_off, res.evecs.astype(np.float64), sig,
+                                  sig_mode=CF_SIGS_COMPAT)
+    assert np.sum(ref[1] > 0) > 800
+    e32 = np.ascontiguousarray(res.evecs, dtype=np.float32)
+    one = gpu_ctx.predict_precomp(off, items, rat, res.m, evals, res.evec_off, e32, sig, sig_mode=CF_SIGS_COMPAT)
+    assert np.array_equal(one[1], ref[1])
+    assert np.array_equal(one[0], ref[0], equal_nan=True)
+    ctxs = [Context(0) for _ in range(2)]
+    try:
+        for c in ctxs:
+            c.upload_graph_dense(d_W)
+        mse, kk, _ = predict_precomp_multi(ctxs, off, items, rat, res.m, evals, res.evec_off, e32, sig,
+                                           sig_mode=CF_SIGS_COMPAT)
+    finally:
+        for c in ctxs:
+            c.close()
+    assert np.array_equal(kk, ref[1])
+    assert np.array_equal(mse, ref[0], equal_nan=True)
+
+
 def test_bench_ranks_equal_single_rank(gpu_ctx):
     """bench.py's N>1 step on world = 2 and 3 ranks emulated by contexts on GPU 0: each rank's
     Workload (its cost_split range of the global set, the compat table rebuilt from the global
