@@ -1,4 +1,4 @@
-# A/B of eigen variants: tools/gpu_eigen_ab.sh <users> <kfix> <variant names...> (main = the in-tree lib)
+# A/B of eigen variants: tools/ab/gpu_eigen_ab.sh <users> <kfix> <variant names...> (main = the in-tree lib)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out

@@ -1,4 +1,4 @@
-# fused-step correctness + A/B: tools/gpu_fused_ab.sh <tag>
+# fused-step correctness + A/B: tools/ab/gpu_fused_ab.sh <tag>
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out

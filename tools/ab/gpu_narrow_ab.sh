@@ -1,5 +1,5 @@
 # A/B of the narrow bucket-12 eigen layout (CF_EIGEN_NARROW=0/1) on k = 180 and the C2 mix,
-# then the eigen parity tests with the narrow layout on: tools/gpu_narrow_ab.sh
+# then the eigen parity tests with the narrow layout on: tools/ab/gpu_narrow_ab.sh
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
