@@ -78,6 +78,9 @@ def parse():
     p.add_argument("--c5-kmax", type=int, default=5000, help="cap of the config-5 degrees (SURVEY 8d: 5000)")
     p.add_argument("--c5-predict-kmax", type=int, default=3072,
                    help="predict the C5 sample's groups up to this k (the per-rating systems grow as k^3)")
+    p.add_argument("--eigen-method", choices=["jacobi", "tridiag"],
+                   default=os.environ.get("CF_EIGEN_METHOD", "jacobi"),
+                   help="k <= 192 eigensolver of the timed step (cf_set_eigen_method)")
     return p.parse_args()
 
 
@@ -281,6 +284,7 @@ def main():
     d_W, W_host, gstats = train_graph(Context, dev_index, dev, torch, cfg["seed"], cfg["train_users"], cfg["items"],
                                       keep_host=want_cpu)
     ctx = Context(dev_index)
+    ctx.set_eigen_method(args.eigen_method)
     wl = Workload(args, cfg, rank, world, dev, torch, ctx, d_W.view(cfg["items"], cfg["items"]))
     del d_W
     torch.cuda.empty_cache()
@@ -460,6 +464,7 @@ def main():
             "parallelism": f"user range split x{world} (cost_split on sum k^3)" + (
                 f", ranks on devices {devices}" if devices else ""),
             "graph": gstats,
+            "eigen_method": args.eigen_method,
         },
         "predicted_ratings_per_s": n_pred_total / step_s,
         "stages": {
