@@ -294,23 +294,31 @@ def main():
 
     gather_state = {}
 
-    def gather():
-        """Packed records of every rank to rank 0 (per-peer RCCL p2p, one group)."""
+    def gather(kind):
+        """Both record kinds of every rank to rank 0 (per-peer RCCL p2p): kind "eigen" = the
+        packed eigen records (out_eigen_), started right after the pack so the transfer runs
+        beside the predictor; kind "pred" = the prediction rows (out_res_: mse, kk), as the
+        reference saves out_res_ from every rank (local_calc_precomp.cpp:576).  Rank 0 receives
+        into preallocated outputs (no concatenation).  Returns the outstanding works."""
         from collaborative_filtering_amd.multi import exchange_counts, gather_to_rank0
 
         if "counts" not in gather_state:   # sizes are fixed for the workload: exchanged once
             coll_dev = dev if backend == "nccl" else torch.device("cpu")
             gather_state["n_packed"] = int(wl.d_poff[-1].item())
-            gather_state["counts"] = exchange_counts([wl.n_users, wl.n_entries, wl.n_entries,
-                                                      gather_state["n_packed"], wl.n_entries, wl.n_entries],
-                                                     device=coll_dev)
-        # both record kinds: the eigen records (out_eigen_) and the prediction rows (out_res_:
-        # mse, kk), as the reference saves out_res_ from every rank (local_calc_precomp.cpp:576)
-        parts = [wl.d_m[:wl.n_users], wl.d_sigs[:wl.n_entries], wl.d_evals[:wl.n_entries],
-                 wl.d_packed[:gather_state["n_packed"]], wl.d_mse[:wl.n_entries], wl.d_kk[:wl.n_entries]]
+            cnt = exchange_counts([wl.n_users, wl.n_entries, wl.n_entries, gather_state["n_packed"], wl.n_entries,
+                                   wl.n_entries], device=coll_dev)
+            gather_state["counts"] = {"eigen": cnt[:, :4], "pred": cnt[:, 4:]}
+        if kind == "eigen":
+            parts = [wl.d_m[:wl.n_users], wl.d_sigs[:wl.n_entries], wl.d_evals[:wl.n_entries],
+                     wl.d_packed[:gather_state["n_packed"]]]
+        else:
+            parts = [wl.d_mse[:wl.n_entries], wl.d_kk[:wl.n_entries]]
         if backend != "nccl":
             parts = [p_.cpu() for p_ in parts]
-        return gather_to_rank0(parts, gather_state["counts"])
+        res, works = gather_to_rank0(parts, gather_state["counts"][kind], out=gather_state.get(kind), async_op=True)
+        if res is not None:
+            gather_state[kind] = res   # rank 0 reuses its receive buffers every step
+        return works
 
     n_ev = 4
     evs = []
@@ -334,11 +342,14 @@ def main():
             wl.pack(sp)
             if record:
                 e[1].record(stream)
+            works = gather("eigen") if world > 1 else []   # beside the predictor
             wl.predict(sp)
             if record:
                 e[2].record(stream)
-        if world > 1:
-            gather()
+            if world > 1:
+                works += gather("pred")
+                for w in works:
+                    w.wait()
         if record:
             e[3].record(stream)
             evs.append(e)

@@ -51,12 +51,17 @@ def local_slice(item_off: np.ndarray, lo: int, hi: int):
     return (item_off[lo:hi + 1] - np.uint64(b)).astype(np.uint64), b, e
 
 
-def gather_to_rank0(tensors, counts_per_rank, group=None):
+def gather_to_rank0(tensors, counts_per_rank, group=None, out=None, async_op=False):
     """Variable-size gather of 1-D tensors to rank 0 with per-peer p2p (one group).
 
     tensors: this rank's list of 1-D tensors (same dtypes on every rank).
     counts_per_rank: [world][len(tensors)] element counts (every rank knows them).
-    Returns, on rank 0, the list of concatenations in rank order; None elsewhere.
+    out (rank 0, optional): preallocated 1-D outputs of the total sizes; each peer's part is
+    received straight into its slice (rank order), rank 0's own part copied in -- no
+    concatenation pass.  Returns, on rank 0, the list of outputs; None elsewhere.
+    async_op: return (result, works) without waiting; the caller waits on the works (for
+    RCCL the wait orders the current stream after the transfers, so the gather of one part
+    can run beside later kernels).
     """
     import torch
     import torch.distributed as dist
@@ -64,25 +69,33 @@ def gather_to_rank0(tensors, counts_per_rank, group=None):
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     if rank != 0:
         ops = [dist.P2POp(dist.isend, t.contiguous(), 0, group) for t in tensors if t.numel()]
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
+        works = dist.batch_isend_irecv(ops) if ops else []
+        if async_op:
+            return None, works
+        for w in works:
+            w.wait()
         return None
-    bufs = [[None] * len(tensors) for _ in range(world)]
+    counts = np.asarray(counts_per_rank, dtype=np.int64)
+    if out is None:
+        out = [torch.empty(int(counts[:, i].sum()), dtype=t.dtype, device=t.device) for i, t in enumerate(tensors)]
     ops = []
-    for r in range(world):
-        for i, t in enumerate(tensors):
-            n = int(counts_per_rank[r][i])
+    for i, t in enumerate(tensors):
+        lo = 0
+        for r in range(world):
+            n = int(counts[r][i])
+            view = out[i][lo:lo + n]
             if r == 0:
-                bufs[r][i] = t
-                continue
-            bufs[r][i] = torch.empty(n, dtype=t.dtype, device=t.device)
-            if n:
-                ops.append(dist.P2POp(dist.irecv, bufs[r][i], r, group))
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
-    return [torch.cat([bufs[r][i] for r in range(world)]) for i in range(len(tensors))]
+                if n:
+                    view.copy_(t[:n])
+            elif n:
+                ops.append(dist.P2POp(dist.irecv, view, r, group))
+            lo += n
+    works = dist.batch_isend_irecv(ops) if ops else []
+    if async_op:
+        return out, works
+    for w in works:
+        w.wait()
+    return out
 
 
 def exchange_counts(local_counts, device=None):
