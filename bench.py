@@ -787,6 +787,30 @@ def c5_leg(args, ctx, dev, torch, W):
         plan.close()
         del d_x
         torch.cuda.empty_cache()
+    # the whole sample in ONE eigen call, as bin/precompute_local runs it: the spill bucket's k
+    # ranges launch with slots sized per range, the k > 3072 range on its own stream beside the
+    # smaller ranges and the LDS buckets
+    print(f"[c5] all: one eigen call over {len(k)} users", file=sys.stderr, flush=True)
+    eo, ne = evec_offsets(off)
+    d_o, d_i, d_e = T(off.view(np.int64)), T(items.view(np.int32)), T(eo.view(np.int64))
+    d_m = torch.zeros(len(k), dtype=torch.int32, device=dev)
+    d_s = torch.zeros(len(items), dtype=torch.float32, device=dev)
+    d_v = torch.zeros(len(items), dtype=torch.float32, device=dev)
+    d_x = torch.zeros(ne, dtype=torch.float32, device=dev)
+    plan = ctx.plan(off)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    plan.eigen_run(d_o, d_i, d_e, d_m, d_s, d_v, d_x, stream=stream.cuda_stream)
+    e1.record(stream)
+    e1.synchronize()
+    all_ms = e0.elapsed_time(e1)
+    print(f"[c5] all: eigen {all_ms:.1f} ms", file=sys.stderr, flush=True)
+    out["one_call"] = {"eigen_ms": all_ms, "users_per_s": len(k) / all_ms * 1e3,
+                       "note": "every user in one cf_eigen_run (the drop-in precompute_local's batch); the "
+                               "per-group times above run each group alone"}
+    plan.close()
+    del d_x
+    torch.cuda.empty_cache()
     out["users_per_s"] = args.c5_users / total_ms * 1e3
     out["ms"] = total_ms
     out["predict_ms"] = total_pms

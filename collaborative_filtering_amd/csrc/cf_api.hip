@@ -95,6 +95,9 @@ void cf_destroy(cf_ctx* ctx) {
     for (hipEvent_t& e : ctx->prep_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->d_spill) (void)hipFree(ctx->d_spill);
+    for (hipEvent_t& e : ctx->spill_side_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->spill_side) (void)hipStreamDestroy(ctx->spill_side);
     if (ctx->d_pspill) (void)hipFree(ctx->d_pspill);
     if (ctx->pspill_meta_ev) {
         (void)hipEventSynchronize(ctx->pspill_meta_ev);

@@ -618,8 +618,10 @@ int launch_buckets_on(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStrea
             loc.test_user = args.test_user;
             loc.test_rating = args.test_rating;
             loc.wlim = args.wlim;
+            // overlap: its k > 3072 range keeps running on the spill side stream while the LDS
+            // buckets start; launch_all_buckets joins it with the aux streams
             rc = cf_launch_eigen_spill(ctx, plan, b, args.item_off, args.items, args.evec_off, args.m_out, args.sigs,
-                                       args.evals, args.evecs, stream, &loc);
+                                       args.evals, args.evecs, stream, &loc, overlap);
             if (rc != CF_OK) return rc;
             if (overlap) {   // LDS buckets start after the spill solver (it fills every CU)
                 CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[0], stream));
@@ -654,7 +656,9 @@ int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStre
     // join on every path: buckets already queued on the aux streams must order before the
     // caller's stream releases or reuses their outputs, also when a later launch failed
     if (overlap) {
-        const int rj = eigen_join(ctx, caller);
+        int rj = eigen_join(ctx, caller);
+        const int rs = cf_spill_join(ctx, caller);
+        if (rj == CF_OK) rj = rs;
         if (rc == CF_OK) return rj;
     }
     return rc;

@@ -32,6 +32,8 @@
 // ~ (#rotations) x 6k flops over one Z pass per 16 iterations, back-transform 2k^3; see
 // DESIGN.md 3.6.
 
+#include <vector>
+
 #include "cf_internal.h"
 
 namespace {
@@ -923,29 +925,67 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
 
 }  // namespace
 
+// The spill bucket (users sorted by k, largest first) in two k ranges, each launch with slots
+// sized for its own largest k, so a few k = 5000 users (400 MB slots) no longer cap the number
+// of workgroups for the many smaller ones: (3072, 5000] in the BIG layout on ctx->spill_side,
+// beside (192, 3072] on `stream`.  The workspace is split between the two.
 int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, const uint64_t* d_item_off,
                           const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs,
-                          float* d_evals, float* d_evecs, hipStream_t stream, const cf_spill_local* loc) {
+                          float* d_evals, float* d_evecs, hipStream_t stream, const cf_spill_local* loc,
+                          bool defer_join) {
     if (b.count == 0) return CF_OK;
+    if (b.kmax > (uint32_t)CF_SPILL_MAX_K) return cf_set_error(ctx, CF_ERANGE, "spill eigen: k above CF_SPILL_MAX_K");
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    const bool big = b.kmax > (uint32_t)SP_NL;
-    if (b.kmax > (uint32_t)CF_SPILL_MAX_K) return cf_set_error(ctx, CF_ERANGE, "spill eigen: k above CF_SPILL_MAX_K");
-    const uint64_t base_stride =
-        2ull * b.kmax * b.kmax + (uint64_t)SP_NB * b.kmax + 4ull * SP_QB * (b.kmax + 2 * SP_QB + 4) + 64;
-    const uint64_t stride = base_stride + (big ? 3ull * CF_SPILL_MAX_K : 0ull);
-    const uint64_t slot_bytes = stride * sizeof(double);
-    // workspace cap: a fifth of the free HBM (>= 24 GB), fewer resident users beyond it
+    // k ranges over the bucket's plan positions (k non-increasing)
+    struct Range {
+        uint32_t first, count, kmax;
+        bool big;
+    };
+    std::vector<Range> rs;
+    {
+        // (finer ranges run one after the other lost more to each range's tail than their
+        // smaller slots gained: 4.88 vs 4.12 s on the config-5 sample's k <= 3072 users)
+        const uint32_t cuts[2] = {(uint32_t)SP_NL, 0u};
+        uint32_t j = b.first;
+        const uint32_t end = b.first + b.count;
+        auto kof = [&](uint32_t pos) {
+            const uint32_t u = plan->h_order[pos];
+            return (uint32_t)(plan->h_item_off[u + 1] - plan->h_item_off[u]);
+        };
+        for (int c = 0; c < 2 && j < end; ++c) {
+            const uint32_t j0 = j;
+            while (j < end && kof(j) > cuts[c]) ++j;
+            if (j > j0) rs.push_back({j0, j - j0, kof(j0), c == 0});
+        }
+        if (j < end) rs.push_back({j, end - j, kof(j), false});   // (degenerate: k <= 0)
+    }
+    auto base_stride = [](uint64_t kmax) {
+        return 2ull * kmax * kmax + (uint64_t)SP_NB * kmax + 4ull * SP_QB * (kmax + 2 * SP_QB + 4) + 64;
+    };
+    auto stride_of = [&](const Range& r) { return base_stride(r.kmax) + (r.big ? 3ull * CF_SPILL_MAX_K : 0ull); };
+    // workspace cap: a fifth of the free HBM (>= 24 GB); the BIG range gets up to half of it
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
     const uint64_t budget = std::max<uint64_t>(24ull << 30, (uint64_t)free_b / 5);
-    uint32_t grid = std::min<uint32_t>(b.count, (uint32_t)n_cu);
-    grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(grid, budget / slot_bytes));
-    const size_t need = (size_t)grid * slot_bytes + 256;
+    const bool has_big = !rs.empty() && rs.front().big;
+    const bool has_rest = rs.size() > (has_big ? 1u : 0u);
+    std::vector<uint32_t> grid(rs.size());
+    uint64_t big_bytes = 0, rest_bytes = 0;
+    for (size_t i = 0; i < rs.size(); ++i) {
+        const uint64_t slot = stride_of(rs[i]) * sizeof(double);
+        const uint64_t share = rs[i].big ? (has_rest ? budget / 2 : budget) : (has_big ? budget / 2 : budget);
+        uint32_t g = std::min<uint32_t>(rs[i].count, (uint32_t)n_cu);
+        g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, share / slot));
+        grid[i] = g;
+        if (rs[i].big) big_bytes = (uint64_t)g * slot;
+        else rest_bytes = std::max<uint64_t>(rest_bytes, (uint64_t)g * slot);
+    }
+    const size_t need = 256 + big_bytes + rest_bytes;
     if (need > ctx->spill_bytes) {
-        if (ctx->d_spill && ctx->spill_debug) {   // keep the diagnostic counters across the regrowth
-            CF_HIP_CHECK(ctx, hipStreamSynchronize(stream));
-        }
+        // the previous launches on either stream may still read the old workspace
+        CF_HIP_CHECK(ctx, hipStreamSynchronize(stream));
+        if (ctx->spill_side) CF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->spill_side));
         if (ctx->d_spill) (void)hipFree(ctx->d_spill);
         ctx->d_spill = nullptr;
         ctx->spill_bytes = 0;
@@ -954,10 +994,13 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
         ctx->spill_bytes = need;
         CF_HIP_CHECK(ctx, hipMemsetAsync(ctx->d_spill, 0, 256, stream));
     }
+    if (has_big && !ctx->spill_side) {
+        CF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->spill_side, hipStreamNonBlocking));
+        for (hipEvent_t& e : ctx->spill_side_ev) CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    char* ws = static_cast<char*>(ctx->d_spill);
     SpillArgs a{};
     a.order = plan->d_order;
-    a.first = b.first;
-    a.count = b.count;
     a.item_off = d_item_off;
     a.items = d_items;
     a.graph = graph_dev(ctx);
@@ -967,25 +1010,47 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     a.sigs = d_sigs;
     a.evals = d_evals;
     a.evecs = d_evecs;
-    a.counter = reinterpret_cast<unsigned int*>(ctx->d_spill);
-    a.work = reinterpret_cast<double*>(static_cast<char*>(ctx->d_spill) + 256);
-    a.work_stride = stride;
-    a.big_off = base_stride;
     if (loc) a.loc = *loc;
-    a.phase = ctx->spill_debug ? reinterpret_cast<unsigned long long*>(static_cast<char*>(ctx->d_spill) + 64) : nullptr;
-    CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), stream));
-    if (big) {
-        const size_t lds = sizeof(SpillSmemT<CF_SPILL_MAX_K, true>);
-        CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_spill_kernel<CF_SPILL_MAX_K, true>,
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((eigen_spill_kernel<CF_SPILL_MAX_K, true>), dim3(grid), dim3(SP_T), lds, stream, a);
-    } else {
-        const size_t lds = sizeof(SpillSmemT<SP_NL, false>);
-        CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_spill_kernel<SP_NL, false>,
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((eigen_spill_kernel<SP_NL, false>), dim3(grid), dim3(SP_T), lds, stream, a);
+    a.phase = ctx->spill_debug ? reinterpret_cast<unsigned long long*>(ws + 64) : nullptr;
+    for (size_t i = 0; i < rs.size(); ++i) {
+        const Range& r = rs[i];
+        hipStream_t st = r.big ? ctx->spill_side : stream;
+        if (r.big) {   // the side stream starts where `stream` is
+            CF_HIP_CHECK(ctx, hipEventRecord(ctx->spill_side_ev[0], stream));
+            CF_HIP_CHECK(ctx, hipStreamWaitEvent(st, ctx->spill_side_ev[0], 0));
+        }
+        a.first = r.first;
+        a.count = r.count;
+        a.counter = reinterpret_cast<unsigned int*>(ws) + (r.big ? 0 : 1);   // one claim counter per stream
+        a.work = reinterpret_cast<double*>(ws + 256 + (r.big ? 0 : big_bytes));
+        a.work_stride = stride_of(r);
+        a.big_off = base_stride(r.kmax);
+        CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
+        if (r.big) {
+            const size_t lds = sizeof(SpillSmemT<CF_SPILL_MAX_K, true>);
+            CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_spill_kernel<CF_SPILL_MAX_K, true>,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL((eigen_spill_kernel<CF_SPILL_MAX_K, true>), dim3(grid[i]), dim3(SP_T), lds, st, a);
+        } else {
+            const size_t lds = sizeof(SpillSmemT<SP_NL, false>);
+            CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_spill_kernel<SP_NL, false>,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL((eigen_spill_kernel<SP_NL, false>), dim3(grid[i]), dim3(SP_T), lds, st, a);
+        }
+        CF_HIP_CHECK(ctx, hipGetLastError());
+        if (r.big) {
+            CF_HIP_CHECK(ctx, hipEventRecord(ctx->spill_side_ev[1], st));
+            ctx->spill_side_pending = true;
+        }
     }
-    CF_HIP_CHECK(ctx, hipGetLastError());
+    if (!defer_join) return cf_spill_join(ctx, stream);
+    return CF_OK;
+}
+
+int cf_spill_join(cf_ctx* ctx, hipStream_t stream) {
+    if (!ctx->spill_side_pending) return CF_OK;
+    CF_HIP_CHECK(ctx, hipStreamWaitEvent(stream, ctx->spill_side_ev[1], 0));
+    ctx->spill_side_pending = false;
     return CF_OK;
 }
 

@@ -73,6 +73,11 @@ struct cf_ctx {
     void* d_spill = nullptr;
     size_t spill_bytes = 0;
     bool spill_debug = false;   // cf_debug_spill: phase counters in the workspace header
+    // the spill bucket's k > 3072 range runs on its own stream beside the smaller ranges:
+    // fork / done events; spill_side_pending = its done event still has to be joined
+    hipStream_t spill_side = nullptr;
+    hipEvent_t spill_side_ev[2] = {};
+    bool spill_side_pending = false;
     // predictor spill-path workspace (per-user Q / Gbar slots, per-workgroup LDL^T), grown on demand.
     void* d_pspill = nullptr;
     size_t pspill_bytes = 0;
@@ -232,9 +237,13 @@ struct cf_spill_local {
     const float* test_rating;
     float* wlim;                   // mode 2 output per pair
 };
+// defer_join: the k > 3072 range's stream is left running (ctx->spill_side_pending); the caller
+// joins it with cf_spill_join before the results are read.  Otherwise it is joined into `stream`.
 int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, const uint64_t* d_item_off,
                           const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs,
-                          float* d_evals, float* d_evecs, hipStream_t stream, const cf_spill_local* loc = nullptr);
+                          float* d_evals, float* d_evecs, hipStream_t stream, const cf_spill_local* loc = nullptr,
+                          bool defer_join = false);
+int cf_spill_join(cf_ctx* ctx, hipStream_t stream);
 // a8 predictor for (movie, test user) pairs of units with n > CF_MAX_K (cf_predict_spill.hip).
 int cf_launch_local_predict_spill(cf_ctx* ctx, uint32_t n_pairs, int nmax, const uint32_t* d_pair_movie,
                                   const uint32_t* d_pair_user, const uint64_t* d_pair_out, const uint64_t* d_item_off,
