@@ -64,7 +64,17 @@ struct SpillArgs {
     unsigned int* counter;   // next spill user (zeroed before the launch)
     unsigned long long* phase;   // 8 counters (cf_debug_spill), summed by thread 0
     cf_spill_local loc;      // a8 modes (loc.mode = 0: compute_eigens of a user)
+    // staged multi-CU path (BIG users of compute_eigens, see spill_mc_*): 0 = the whole user
+    // here; 1 = assembly only, sig to the slot; 2 = resume after the multi-CU
+    // tridiagonalisation (d, e, sig from the slot).  In stages 1 and 2 the slot is the
+    // user's (claim index), not the workgroup's.
+    int mc_stage;
 };
+
+// Staged slots: after rc / rs / tau (big_off + 3 NL) the tridiagonal d, e, the sigs and the
+// panel's dot products xv, xw.
+constexpr uint64_t MC_D = 3ull * CF_SPILL_MAX_K, MC_E = 4ull * CF_SPILL_MAX_K, MC_SIG = 5ull * CF_SPILL_MAX_K,
+                   MC_XV = 6ull * CF_SPILL_MAX_K, MC_XW = 6ull * CF_SPILL_MAX_K + 32, MC_EXTRA = 6ull * CF_SPILL_MAX_K + 64;
 
 // LDS of one workgroup.  NL = the largest k of the launch's layout.  Up to SP_NL (3072) the
 // per-row vectors rc / rs / tau live in LDS too; a BIG launch (SP_NL < k <= CF_SPILL_MAX_K)
@@ -123,11 +133,11 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     SpillSmemT<NL, BIG>& S = *reinterpret_cast<SpillSmemT<NL, BIG>*>(smem_raw);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    double* M = a.work + (size_t)blockIdx.x * a.work_stride;
+    double* M = a.mc_stage ? nullptr : a.work + (size_t)blockIdx.x * a.work_stride;
     // per-row vectors and the staging tiles (see SpillSmemT)
-    double* const rc = BIG ? M + a.big_off : S.rc;
-    double* const rs = BIG ? M + a.big_off + NL : S.rs;
-    double* const tau = BIG ? M + a.big_off + 2 * NL : S.tau;
+    double* rc = BIG && M ? M + a.big_off : S.rc;
+    double* rs = BIG && M ? M + a.big_off + NL : S.rs;
+    double* tau = BIG && M ? M + a.big_off + 2 * NL : S.tau;
     double* const stage = BIG ? S.stage : S.rc;
     const double eps = 2.220446049250313e-16;   // 2^-52 (tql2)
 
@@ -137,6 +147,14 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         const int idx = S.flag[0];
         __syncthreads();
         if (idx >= (int)a.count) break;   // uniform: every wave leaves together
+        if (a.mc_stage) {
+            M = a.work + (size_t)idx * a.work_stride;
+            if (BIG) {
+                rc = M + a.big_off;
+                rs = M + a.big_off + NL;
+                tau = M + a.big_off + 2 * NL;
+            }
+        }
         const int mode = a.loc.mode;
         const uint32_t unit = a.order[a.first + idx];
         const uint32_t u = mode == 2 ? a.loc.pair_movie[unit] : unit;   // the unit whose items index the graph
@@ -189,7 +207,16 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         unsigned long long t0 = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull, t1 = 0, t2 = 0, t3 = 0, tgen = 0;
         unsigned long long n_iter = 0;
 
-        if (mode == 2) {
+        if (a.mc_stage == 2) {
+            // resume: d, e, sig from the slot (the multi-CU tridiagonalisation left them there)
+            const double* mc = M + a.big_off;
+            for (int i = tid; i < n; i += SP_T) {
+                S.d[i] = mc[MC_D + i];
+                S.e[i] = mc[MC_E + i];
+                S.sig[i] = (float)mc[MC_SIG + i];
+            }
+            __syncthreads();
+        } else if (mode == 2) {
             // ---- 1s. A = L2_h L2_h^T (h x h, fp64 sums of the stored fp32 L2 rows, :425-435)
             const float* L2m = a.loc.l2 + a.loc.l2_off[u];
             const int npk = n * (n + 1) / 2;
@@ -253,6 +280,11 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         __syncthreads();
         }   // mode != 2
 
+        if (a.mc_stage == 1) {   // assembly only: sig to the slot, the next user
+            for (int i = tid; i < n; i += SP_T) M[a.big_off + MC_SIG + i] = (double)S.sig[i];
+            __syncthreads();
+            continue;
+        }
         if (tid == 0) t1 = __builtin_amdgcn_s_memtime();
         // ---- 2. blocked Householder tridiagonalisation (LAPACK dsytrd/dlatrd, lower) ---------
         // Panels of SP_NB columns.  Inside a panel, column j is brought up to date with the
@@ -265,7 +297,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         // workspace traffic is ~8 B per element-step instead of tred2's ~24 B.
         // v_j is stored in M(j+1:n, j); A = Q T Q^T with Q = H_0 H_1 ... H_{n-2},
         // T = tridiag(d, e) with e[j] = T(j+1, j).
-        for (int p = 0; p < n - 1; p += SP_NB) {
+        for (int p = 0; p < (a.mc_stage == 2 ? 0 : n - 1); p += SP_NB) {   // stage 2: done by spill_mc_*
             const int jb = min(SP_NB, n - 1 - p);
             for (int jj = 0; jj < jb; ++jj) {
                 const int j = p + jj;
@@ -453,7 +485,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 __syncthreads();
             }
         }
-        if (tid == 0) {
+        if (tid == 0 && a.mc_stage != 2) {
             S.d[n - 1] = M[(size_t)(n - 1) * n + (n - 1)];
             S.e[n - 1] = 0.0;
         }
@@ -923,7 +955,323 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
     }
 }
 
+// ---- multi-CU tridiagonalisation of the BIG users (k > SP_NL), all of a launch at once ----------
+// The single-workgroup solver spends ~54% of a k = 4000 user in the tridiagonalisation, and its
+// per-reflector symmetric matrix-vector product reads the whole trailing matrix from HBM through
+// ONE CU.  Here the same blocked algorithm (dlatrd panels of SP_NB, the stage-2 code of
+// eigen_spill_kernel) runs as a sequence of launches over every BIG user of the batch: per
+// reflector j, spill_mc_col (one workgroup per user: the column update, the reflector, the
+// panel dot products), spill_mc_symv (G workgroups per user, each a block of the trailing rows)
+// and spill_mc_fin (one per user: the panel corrections, w); per panel, spill_mc_trail (G2 per
+// user, column blocks of the rank-2 SP_NB update).  Kernel boundaries order the steps, so no
+// workgroup waits on another.  The QL and back-transform then resume in eigen_spill_kernel
+// (mc_stage 2) from the slot's d, e, tau and the reflectors stored in M.
+struct McArgs {
+    const uint32_t* order;
+    uint32_t first;
+    uint32_t count;
+    const uint64_t* item_off;
+    double* work;
+    uint64_t stride;     // doubles per user slot
+    uint64_t big_off;    // rc (v), rs (y), tau, then MC_* (d, e, sig, xv, xw)
+    int G;               // workgroups per user of spill_mc_symv / spill_mc_trail
+};
+
+__device__ __forceinline__ int mc_n(const McArgs& a, uint32_t u) {
+    const uint32_t unit = a.order[a.first + u];
+    return (int)(a.item_off[unit + 1] - a.item_off[unit]);
+}
+
+// column j of the panel at p: bring it up to date with the panel's earlier reflectors, form
+// its reflector (v in M(j+1:n, j) and rc, tau, d, e), and the panel dot products xv, xw
+__global__ __launch_bounds__(SP_T) void spill_mc_col(McArgs a, int j, int p) {
+    __shared__ double vj[SP_NB], wj[SP_NB], red[SP_W + 4];
+    const uint32_t u = blockIdx.x;
+    const int n = mc_n(a, u);
+    if (j >= n - 1) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, jj = j - p;
+    double* M = a.work + (size_t)u * a.stride;
+    double* Wp = M + 2 * (size_t)n * n;
+    double* rc = M + a.big_off;
+    double* tau = rc + 2 * CF_SPILL_MAX_K;
+    double* mc = M + a.big_off;
+    double* colj = M + (size_t)j * n;
+    if (jj > 0) {
+        if (tid < jj) {
+            vj[tid] = M[(size_t)(p + tid) * n + j];
+            wj[tid] = Wp[(size_t)tid * n + j];
+        }
+        __syncthreads();
+        for (int r = j + tid; r < n; r += SP_T) {
+            double acc = colj[r];
+            for (int t = 0; t < jj; ++t) acc -= M[(size_t)(p + t) * n + r] * wj[t] + Wp[(size_t)t * n + r] * vj[t];
+            colj[r] = acc;
+        }
+        __syncthreads();
+    }
+    const double alpha = colj[j + 1];
+    const double ajj = colj[j];
+    double part = 0.0;
+    for (int r = j + 2 + tid; r < n; r += SP_T) {
+        const double x = colj[r];
+        part += x * x;
+    }
+    const double sigma = block_sum(part, red);
+    double tj = 0.0, beta = alpha, scal = 0.0;
+    if (sigma != 0.0) {
+        beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+        tj = (beta - alpha) / beta;
+        scal = 1.0 / (alpha - beta);
+    }
+    if (tid == 0) {
+        mc[MC_D + j] = ajj;
+        mc[MC_E + j] = beta;
+        tau[j] = tj;
+    }
+    for (int r = j + 1 + tid; r < n; r += SP_T) {
+        const double vr = (r == j + 1) ? 1.0 : colj[r] * scal;
+        rc[r] = vr;
+        colj[r] = vr;
+    }
+    __syncthreads();
+    if (tj == 0.0) return;
+    // x_v[t] = W(:,t).v and x_w[t] = V(:,t).v over rows j+1..n-1, one wave per dot
+    const int r0 = j + 1;
+    for (int q = wave; q < 2 * jj; q += SP_W) {
+        const int t = q >> 1;
+        const double* src = (q & 1) ? M + (size_t)(p + t) * n : Wp + (size_t)t * n;
+        double sdot = 0.0;
+        for (int r = r0 + lane; r < n; r += 64) sdot += src[r] * rc[r];
+        sdot = wave_sum(sdot);
+        if (lane == 0) mc[((q & 1) ? MC_XW : MC_XV) + t] = sdot;
+    }
+}
+
+// y = A(r0:n, r0:n) v on G workgroups per user: workgroup g takes row blocks g, g + G, ... of
+// 64 rows; its four waves split the columns, partial sums combined in LDS in a fixed order
+constexpr int MC_SYMV_T = 256;
+__global__ __launch_bounds__(MC_SYMV_T) void spill_mc_symv(McArgs a, int j) {
+    __shared__ double vs[CF_SPILL_MAX_K];
+    __shared__ double part[MC_SYMV_T / 64][64];
+    const uint32_t u = blockIdx.x / a.G;
+    const int g = blockIdx.x % a.G;
+    const int n = mc_n(a, u);
+    if (j >= n - 1) return;
+    double* M = a.work + (size_t)u * a.stride;
+    const double* rc = M + a.big_off;
+    double* rs = M + a.big_off + CF_SPILL_MAX_K;
+    const double tj = rc[2 * CF_SPILL_MAX_K + j];
+    if (tj == 0.0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int NWV = MC_SYMV_T / 64;
+    const int r0 = j + 1;
+    const int nrb = (n - r0 + 63) >> 6;
+    if (g >= nrb) return;   // uniform
+    for (int c = r0 + tid; c < n; c += MC_SYMV_T) vs[c] = rc[c];
+    __syncthreads();
+    const int cols = n - r0, seg = (cols + NWV - 1) / NWV;
+    const int c_lo = r0 + wave * seg, c_hi = min(n, c_lo + seg);
+    for (int rb = g; rb < nrb; rb += a.G) {
+        const int r = r0 + rb * 64 + lane;
+        double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+        if (r < n) {
+            const double* mr = M + r;
+            int c = c_lo;
+            for (; c + 16 <= c_hi; c += 16) {
+                double x[16];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) x[t] = mr[(size_t)(c + t) * n];
+#pragma unroll
+                for (int t = 0; t < 16; t += 4) {
+                    p0 += x[t] * vs[c + t];
+                    p1 += x[t + 1] * vs[c + t + 1];
+                    p2 += x[t + 2] * vs[c + t + 2];
+                    p3 += x[t + 3] * vs[c + t + 3];
+                }
+            }
+            for (; c < c_hi; ++c) p0 += mr[(size_t)c * n] * vs[c];
+        }
+        part[wave][lane] = (p0 + p1) + (p2 + p3);
+        __syncthreads();
+        if (wave == 0 && r < n) {
+            double y = 0.0;
+#pragma unroll
+            for (int w = 0; w < NWV; ++w) y += part[w][lane];
+            rs[r] = y;
+        }
+        __syncthreads();
+    }
+}
+
+// w_jj = tau (y - V xv - W xw) - tau/2 ((...) . v) v into W(:, jj) (0 above row j+1)
+__global__ __launch_bounds__(SP_T) void spill_mc_fin(McArgs a, int j, int p) {
+    __shared__ double xv[SP_NB], xw[SP_NB], red[SP_W + 4];
+    const uint32_t u = blockIdx.x;
+    const int n = mc_n(a, u);
+    if (j >= n - 1) return;
+    const int tid = threadIdx.x, jj = j - p;
+    double* M = a.work + (size_t)u * a.stride;
+    double* Wp = M + 2 * (size_t)n * n;
+    const double* rc = M + a.big_off;
+    double* rs = M + a.big_off + CF_SPILL_MAX_K;
+    const double* mc = M + a.big_off;
+    const double tj = rc[2 * CF_SPILL_MAX_K + j];
+    const int r0 = j + 1;
+    if (tj == 0.0) {
+        for (int r = tid; r < n; r += SP_T) Wp[(size_t)jj * n + r] = 0.0;
+        return;
+    }
+    if (tid < jj) {
+        xv[tid] = mc[MC_XV + tid];
+        xw[tid] = mc[MC_XW + tid];
+    }
+    __syncthreads();
+    double yv = 0.0;
+    for (int r = r0 + tid; r < n; r += SP_T) {
+        double y = rs[r];
+        for (int t = 0; t < jj; ++t) y -= M[(size_t)(p + t) * n + r] * xv[t] + Wp[(size_t)t * n + r] * xw[t];
+        y *= tj;
+        rs[r] = y;
+        yv += y * rc[r];
+    }
+    const double a2 = -0.5 * tj * block_sum(yv, red);
+    for (int r = tid; r < n; r += SP_T) Wp[(size_t)jj * n + r] = r >= r0 ? rs[r] + a2 * rc[r] : 0.0;
+}
+
+// trailing update A(q:n, q:n) -= V W^T + W V^T after the panel at p, q = p + jb: G workgroups
+// per user, each a range of SP_CC-column chunks; lane per row with that row's V and W entries
+// in registers, each column's entries broadcast from LDS (the stage-2 code of eigen_spill_kernel)
+__global__ __launch_bounds__(SP_T) void spill_mc_trail(McArgs a, int p) {
+    __shared__ double stg[SP_CC * 2 * SP_NB];
+    const uint32_t u = blockIdx.x / a.G;
+    const int g = blockIdx.x % a.G;
+    const int n = mc_n(a, u);
+    if (p >= n - 1) return;
+    const int jb = min(SP_NB, n - 1 - p);
+    const int q = p + jb, mq = n - q;
+    if (mq <= 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double* M = a.work + (size_t)u * a.stride;
+    const double* Wp = M + 2 * (size_t)n * n;
+    const int nchunk = (mq + SP_CC - 1) / SP_CC;
+    const int per = (nchunk + a.G - 1) / a.G;
+    const int ch_lo = g * per, ch_hi = min(nchunk, ch_lo + per);
+    if (ch_lo >= ch_hi) return;   // uniform
+    const int nrb = (mq + 63) >> 6;
+    for (int pass = 0; pass < nrb; pass += SP_W) {
+        const int rb = pass + wave;
+        const int r = q + rb * 64 + lane;
+        const bool act = rb < nrb && r < n;
+        double vr[SP_NB], wr[SP_NB];
+#pragma unroll
+        for (int t = 0; t < SP_NB; ++t) {
+            vr[t] = (act && t < jb) ? M[(size_t)(p + t) * n + r] : 0.0;
+            wr[t] = (act && t < jb) ? Wp[(size_t)t * n + r] : 0.0;
+        }
+        for (int ch = ch_lo; ch < ch_hi; ++ch) {
+            const int c0 = q + ch * SP_CC;
+            const int cn = min(SP_CC, n - c0);
+            __syncthreads();
+            for (int idx = tid; idx < SP_CC * 2 * SP_NB; idx += SP_T) {
+                const int cc = idx / (2 * SP_NB), t2 = idx - cc * (2 * SP_NB);
+                const int t = t2 & (SP_NB - 1);
+                double v = 0.0;
+                if (cc < cn && t < jb) v = t2 < SP_NB ? M[(size_t)(p + t) * n + c0 + cc] : Wp[(size_t)t * n + c0 + cc];
+                stg[idx] = v;
+            }
+            __syncthreads();
+            if (!act) continue;
+            double* mp = M + (size_t)c0 * n + r;
+            double cur[8];
+#pragma unroll
+            for (int u8 = 0; u8 < 8; ++u8) cur[u8] = u8 < cn ? mp[(size_t)u8 * n] : 0.0;
+            for (int cc = 0; cc < cn; cc += 8) {
+                double nxt[8];
+#pragma unroll
+                for (int u8 = 0; u8 < 8; ++u8) nxt[u8] = cc + 8 + u8 < cn ? mp[(size_t)(cc + 8 + u8) * n] : 0.0;
+#pragma unroll
+                for (int u8 = 0; u8 < 8; ++u8) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    const double* sv = stg + (cc + u8) * 2 * SP_NB;
+                    double acc0 = cur[u8], acc1 = 0.0;
+#pragma unroll
+                    for (int t = 0; t < SP_NB; t += 2) {
+                        if ((t & 7) == 0) __builtin_amdgcn_sched_barrier(0);
+                        acc0 -= vr[t] * sv[SP_NB + t] + wr[t] * sv[t];
+                        acc1 -= vr[t + 1] * sv[SP_NB + t + 1] + wr[t + 1] * sv[t + 1];
+                    }
+                    if (cc + u8 < cn) mp[(size_t)(cc + u8) * n] = acc0 + acc1;
+                }
+#pragma unroll
+                for (int u8 = 0; u8 < 8; ++u8) cur[u8] = nxt[u8];
+            }
+        }
+    }
+}
+
+// the last diagonal element and e[n-1] = 0
+__global__ void spill_mc_end(McArgs a) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= a.count) return;
+    const int n = mc_n(a, u);
+    double* M = a.work + (size_t)u * a.stride;
+    double* mc = M + a.big_off;
+    mc[MC_D + n - 1] = M[(size_t)(n - 1) * n + (n - 1)];
+    mc[MC_E + n - 1] = 0.0;
+}
+
 }  // namespace
+
+// Staged multi-CU path for BIG users [first, first + count) (plan positions, k non-increasing),
+// `slots` users at a time: stage 1 (assembly) on eigen_spill_kernel, the tridiagonalisation on
+// the spill_mc_* launches, stage 2 (QL, back-transform, output) on eigen_spill_kernel.
+static int spill_mc_launch(cf_ctx* ctx, const cf_plan* plan, SpillArgs a, uint32_t first, uint32_t count,
+                           uint32_t slots, uint32_t n_cu, hipStream_t st) {
+    const size_t lds = sizeof(SpillSmemT<CF_SPILL_MAX_K, true>);
+    CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_spill_kernel<CF_SPILL_MAX_K, true>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    for (uint32_t w0 = 0; w0 < count; w0 += slots) {
+        const uint32_t cnt = std::min(slots, count - w0);
+        a.first = first + w0;
+        a.count = cnt;
+        const uint32_t grid = std::min(cnt, n_cu);
+        a.mc_stage = 1;
+        CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
+        hipLaunchKernelGGL((eigen_spill_kernel<CF_SPILL_MAX_K, true>), dim3(grid), dim3(SP_T), lds, st, a);
+        CF_HIP_CHECK(ctx, hipGetLastError());
+        McArgs m{};
+        m.order = a.order;
+        m.first = a.first;
+        m.count = cnt;
+        m.item_off = a.item_off;
+        m.work = a.work;
+        m.stride = a.work_stride;
+        m.big_off = a.big_off;
+        // the largest k of this wave (plan order: the wave's first user)
+        const uint32_t unit0 = plan->h_order[a.first];
+        const uint32_t kmax = (uint32_t)(plan->h_item_off[unit0 + 1] - plan->h_item_off[unit0]);
+        // ~4 workgroups per CU over the batch for the memory-bound products, at least 64 rows each
+        m.G = (int)std::max<uint32_t>(1, std::min<uint32_t>((4 * n_cu + cnt - 1) / cnt, (kmax + 63) / 64));
+        for (int p = 0; p < (int)kmax - 1; p += SP_NB) {
+            const int jbmax = std::min(SP_NB, (int)kmax - 1 - p);
+            for (int jj = 0; jj < jbmax; ++jj) {
+                const int j = p + jj;
+                hipLaunchKernelGGL(spill_mc_col, dim3(cnt), dim3(SP_T), 0, st, m, j, p);
+                hipLaunchKernelGGL(spill_mc_symv, dim3(cnt * m.G), dim3(MC_SYMV_T), 0, st, m, j);
+                hipLaunchKernelGGL(spill_mc_fin, dim3(cnt), dim3(SP_T), 0, st, m, j, p);
+            }
+            hipLaunchKernelGGL(spill_mc_trail, dim3(cnt * m.G), dim3(SP_T), 0, st, m, p);
+            CF_HIP_CHECK(ctx, hipGetLastError());
+        }
+        hipLaunchKernelGGL(spill_mc_end, dim3((cnt + 63) / 64), dim3(64), 0, st, m);
+        CF_HIP_CHECK(ctx, hipGetLastError());
+        a.mc_stage = 2;
+        CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
+        hipLaunchKernelGGL((eigen_spill_kernel<CF_SPILL_MAX_K, true>), dim3(grid), dim3(SP_T), lds, st, a);
+        CF_HIP_CHECK(ctx, hipGetLastError());
+    }
+    return CF_OK;
+}
 
 // The spill bucket (users sorted by k, largest first) in two k ranges, each launch with slots
 // sized for its own largest k, so a few k = 5000 users (400 MB slots) no longer cap the number
@@ -963,7 +1311,16 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     auto base_stride = [](uint64_t kmax) {
         return 2ull * kmax * kmax + (uint64_t)SP_NB * kmax + 4ull * SP_QB * (kmax + 2 * SP_QB + 4) + 64;
     };
-    auto stride_of = [&](const Range& r) { return base_stride(r.kmax) + (r.big ? 3ull * CF_SPILL_MAX_K : 0ull); };
+    // BIG users of compute_eigens take the staged multi-CU path (CF_SPILL_MC=0: the
+    // single-workgroup kernel); their slots carry d, e, sig and the panel dot products too
+    static const bool mc_env = [] {
+        const char* e = getenv("CF_SPILL_MC");
+        return !(e && e[0] == '0');
+    }();
+    const bool mc_on = mc_env && (!loc || loc->mode == 0);
+    auto stride_of = [&](const Range& r) {
+        return base_stride(r.kmax) + (r.big ? (mc_on ? MC_EXTRA : 3ull * CF_SPILL_MAX_K) : 0ull);
+    };
     // workspace cap: a fifth of the free HBM (>= 24 GB); the BIG range gets up to half of it
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
@@ -975,7 +1332,8 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     for (size_t i = 0; i < rs.size(); ++i) {
         const uint64_t slot = stride_of(rs[i]) * sizeof(double);
         const uint64_t share = rs[i].big ? (has_rest ? budget / 2 : budget) : (has_big ? budget / 2 : budget);
-        uint32_t g = std::min<uint32_t>(rs[i].count, (uint32_t)n_cu);
+        // staged BIG users hold one slot each for the whole launch (in waves if the share is short)
+        uint32_t g = std::min<uint32_t>(rs[i].count, rs[i].big && mc_on ? rs[i].count : (uint32_t)n_cu);
         g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, share / slot));
         grid[i] = g;
         if (rs[i].big) big_bytes = (uint64_t)g * slot;
@@ -1025,13 +1383,16 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
         a.work = reinterpret_cast<double*>(ws + 256 + (r.big ? 0 : big_bytes));
         a.work_stride = stride_of(r);
         a.big_off = base_stride(r.kmax);
-        CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
-        if (r.big) {
+        if (r.big && mc_on) {
+            CF_TRY(spill_mc_launch(ctx, plan, a, r.first, r.count, grid[i], (uint32_t)n_cu, st));
+        } else if (r.big) {
+            CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
             const size_t lds = sizeof(SpillSmemT<CF_SPILL_MAX_K, true>);
             CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_spill_kernel<CF_SPILL_MAX_K, true>,
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             hipLaunchKernelGGL((eigen_spill_kernel<CF_SPILL_MAX_K, true>), dim3(grid[i]), dim3(SP_T), lds, st, a);
         } else {
+            CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
             const size_t lds = sizeof(SpillSmemT<SP_NL, false>);
             CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_spill_kernel<SP_NL, false>,
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
