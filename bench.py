@@ -74,7 +74,9 @@ def parse():
     p.add_argument("--knn2-reps", type=int, default=3)
     p.add_argument("--c5", choices=["auto", "off", "only"], default="auto",
                    help="BASELINE config 5 sample (N=1, rank 0): power-law k mix through the LDS + spill paths")
-    p.add_argument("--c5-users", type=int, default=1000)
+    p.add_argument("--c5-users", type=int, default=1000, help="config-5 sample of the per-path legs (eigen + predict)")
+    p.add_argument("--c5-onecall-users", type=int, default=10000,
+                   help="config-5 sample of the one-call eigen leg (every user in one cf_eigen_run)")
     p.add_argument("--c5-kmax", type=int, default=5000, help="cap of the config-5 degrees (SURVEY 8d: 5000)")
     p.add_argument("--c5-predict-kmax", type=int, default=3072,
                    help="predict the C5 sample's groups up to this k (the per-rating systems grow as k^3)")
@@ -787,10 +789,16 @@ def c5_leg(args, ctx, dev, torch, W):
         plan.close()
         del d_x
         torch.cuda.empty_cache()
-    # the whole sample in ONE eigen call, as bin/precompute_local runs it: the spill bucket's k
-    # ranges launch with slots sized per range, the k > 3072 range on its own stream beside the
-    # smaller ranges and the LDS buckets
-    print(f"[c5] all: one eigen call over {len(k)} users", file=sys.stderr, flush=True)
+    # a larger sample of the same generator in ONE eigen call, as bin/precompute_local runs it:
+    # the spill bucket's k ranges launch with slots sized per range, the k > 3072 range on its
+    # own stream (staged multi-CU solver) beside the smaller ranges and the LDS buckets
+    n1 = max(args.c5_onecall_users, 1)
+    if n1 != args.c5_users:
+        del off, items, ratings
+        k = synth.degrees(seed + 1, n1, k_median=100.0, sigma=sigma, kmin=20, kmax=min(args.c5_kmax, CF_SPILL_MAX_K))
+        off, items, _ = synth.user_items(seed + 1, k, n_items, threads=16)
+    print(f"[c5] all: one eigen call over {len(k)} users ({int(np.sum(k > CF_MAX_K))} spill, "
+          f"{int(np.sum(k > 3072))} with k > 3072)", file=sys.stderr, flush=True)
     eo, ne = evec_offsets(off)
     d_o, d_i, d_e = T(off.view(np.int64)), T(items.view(np.int32)), T(eo.view(np.int64))
     d_m = torch.zeros(len(k), dtype=torch.int32, device=dev)
@@ -805,13 +813,21 @@ def c5_leg(args, ctx, dev, torch, W):
     e1.synchronize()
     all_ms = e0.elapsed_time(e1)
     print(f"[c5] all: eigen {all_ms:.1f} ms", file=sys.stderr, flush=True)
-    out["one_call"] = {"eigen_ms": all_ms, "users_per_s": len(k) / all_ms * 1e3,
+    kf = k.astype(np.float64)
+    out["one_call"] = {"users": int(len(k)), "seed": seed + 1 if n1 != args.c5_users else seed,
+                       "spill_users": int(np.sum(k > CF_MAX_K)), "big_users": int(np.sum(k > 3072)),
+                       "k_p95": int(np.percentile(k, 95)), "k_max": int(k.max()),
+                       "eigen_ms": all_ms, "users_per_s": len(k) / all_ms * 1e3,
+                       "GFLOPs_9k3": float(np.sum(9 * kf ** 3)) / all_ms / 1e6,
+                       "m_mean": float(d_m.float().mean().item()),
                        "note": "every user in one cf_eigen_run (the drop-in precompute_local's batch); the "
-                               "per-group times above run each group alone"}
+                               "per-group legs above run each group of the smaller sample alone"}
     plan.close()
     del d_x
     torch.cuda.empty_cache()
-    out["users_per_s"] = args.c5_users / total_ms * 1e3
+    out["users_per_s"] = out["one_call"]["users_per_s"]
+    out["users_per_s_note"] = "eigen stage, one_call sample"
+    out["groups_users_per_s"] = args.c5_users / total_ms * 1e3
     out["ms"] = total_ms
     out["predict_ms"] = total_pms
     out["ratings_per_s"] = n_pred / total_pms * 1e3 if total_pms else None

@@ -65,16 +65,26 @@ struct SpillArgs {
     unsigned long long* phase;   // 8 counters (cf_debug_spill), summed by thread 0
     cf_spill_local loc;      // a8 modes (loc.mode = 0: compute_eigens of a user)
     // staged multi-CU path (BIG users of compute_eigens, see spill_mc_*): 0 = the whole user
-    // here; 1 = assembly only, sig to the slot; 2 = resume after the multi-CU
-    // tridiagonalisation (d, e, sig from the slot).  In stages 1 and 2 the slot is the
-    // user's (claim index), not the workgroup's.
+    // here; 1 = assembly only, sig to the slot; 2 = QL on a block of Z's rows (d, e from the
+    // slot after the multi-CU tridiagonalisation; part 0 stores the eigenvalues); 3 = Z to
+    // row-major; 4 = back-transform and output of a block of Z's columns.  In stages >= 1 the
+    // slot is the user's, not the workgroup's, and a claim is (user, part), mc_parts parts
+    // per user.
     int mc_stage;
+    int mc_parts;
 };
 
-// Staged slots: after rc / rs / tau (big_off + 3 NL) the tridiagonal d, e, the sigs and the
-// panel's dot products xv, xw.
+// Staged slots: after rc / rs / tau (big_off + 3 NL) the tridiagonal d, e, the sigs, the
+// eigenvalues (QL's d), the panel's dot products xv, xw, then one QL coefficient buffer per
+// row part (each part runs its own generator).
 constexpr uint64_t MC_D = 3ull * CF_SPILL_MAX_K, MC_E = 4ull * CF_SPILL_MAX_K, MC_SIG = 5ull * CF_SPILL_MAX_K,
-                   MC_XV = 6ull * CF_SPILL_MAX_K, MC_XW = 6ull * CF_SPILL_MAX_K + 32, MC_EXTRA = 6ull * CF_SPILL_MAX_K + 64;
+                   MC_DF = 6ull * CF_SPILL_MAX_K, MC_XV = 7ull * CF_SPILL_MAX_K, MC_XW = 7ull * CF_SPILL_MAX_K + 32,
+                   MC_GBUF = 7ull * CF_SPILL_MAX_K + 64;
+constexpr int MC_QL_ROWS = 2 * (SP_T - 64);        // rows of one QL part, at least: one applier pass
+constexpr int MC_BT_COLS = SP_T;                   // columns of one back-transform part, at least
+constexpr int MC_QL_PARTS_MAX = (CF_SPILL_MAX_K + MC_QL_ROWS - 1) / MC_QL_ROWS;
+constexpr uint64_t MC_GSZ = 4ull * SP_QB * (CF_SPILL_MAX_K + 2 * SP_QB + 4);   // doubles per buffer
+constexpr uint64_t MC_EXTRA = MC_GBUF + (uint64_t)MC_QL_PARTS_MAX * MC_GSZ;
 
 // LDS of one workgroup.  NL = the largest k of the launch's layout.  Up to SP_NL (3072) the
 // per-row vectors rc / rs / tau live in LDS too; a BIG launch (SP_NL < k <= CF_SPILL_MAX_K)
@@ -146,9 +156,12 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         __syncthreads();
         const int idx = S.flag[0];
         __syncthreads();
-        if (idx >= (int)a.count) break;   // uniform: every wave leaves together
-        if (a.mc_stage) {
-            M = a.work + (size_t)idx * a.work_stride;
+        const int st = a.mc_stage;
+        const int P = st ? a.mc_parts : 1;
+        if (idx >= (int)a.count * P) break;   // uniform: every wave leaves together
+        const int ui = idx / P, part = idx - ui * P;
+        if (st) {
+            M = a.work + (size_t)ui * a.work_stride;
             if (BIG) {
                 rc = M + a.big_off;
                 rs = M + a.big_off + NL;
@@ -156,7 +169,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             }
         }
         const int mode = a.loc.mode;
-        const uint32_t unit = a.order[a.first + idx];
+        const uint32_t unit = a.order[a.first + ui];
         const uint32_t u = mode == 2 ? a.loc.pair_movie[unit] : unit;   // the unit whose items index the graph
         const uint64_t base = a.item_off[u];
         const int nrows = (int)(a.item_off[u + 1] - base);
@@ -205,13 +218,14 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         double* Zb = M + (size_t)n * n;          // tridiagonal eigenvectors Z (column-major, then rows)
         double* Wp = Zb + (size_t)n * n;         // [SP_NB][n] panel W of the tridiagonalisation
         unsigned long long t0 = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull, t1 = 0, t2 = 0, t3 = 0, tgen = 0;
-        unsigned long long n_iter = 0;
+        unsigned long long n_iter = 0, n_rot = 0;
 
-        if (a.mc_stage == 2) {
-            // resume: d, e, sig from the slot (the multi-CU tridiagonalisation left them there)
+        if (st >= 2) {
+            // resume: d, e from the slot (the multi-CU tridiagonalisation left them there) for
+            // QL, the eigenvalues and sigs for the output
             const double* mc = M + a.big_off;
             for (int i = tid; i < n; i += SP_T) {
-                S.d[i] = mc[MC_D + i];
+                S.d[i] = mc[(st == 4 ? MC_DF : MC_D) + i];
                 S.e[i] = mc[MC_E + i];
                 S.sig[i] = (float)mc[MC_SIG + i];
             }
@@ -297,7 +311,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         // workspace traffic is ~8 B per element-step instead of tred2's ~24 B.
         // v_j is stored in M(j+1:n, j); A = Q T Q^T with Q = H_0 H_1 ... H_{n-2},
         // T = tridiag(d, e) with e[j] = T(j+1, j).
-        for (int p = 0; p < (a.mc_stage == 2 ? 0 : n - 1); p += SP_NB) {   // stage 2: done by spill_mc_*
+        for (int p = 0; p < (st >= 2 ? 0 : n - 1); p += SP_NB) {   // stages >= 2: done by spill_mc_*
             const int jb = min(SP_NB, n - 1 - p);
             for (int jj = 0; jj < jb; ++jj) {
                 const int j = p + jj;
@@ -485,7 +499,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 __syncthreads();
             }
         }
-        if (tid == 0 && a.mc_stage != 2) {
+        if (tid == 0 && st < 2) {
             S.d[n - 1] = M[(size_t)(n - 1) * n + (n - 1)];
             S.e[n - 1] = 0.0;
         }
@@ -529,10 +543,20 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             __syncthreads();
             continue;
         }
+        // rows of Z this workgroup runs QL on (stage 2: the P-th part, 64-row aligned; the QL
+        // recurrence is replicated, the rotations touch rows independently)
+        const int part_len = ((n + P - 1) / P + 63) & ~63;
+        const int row_lo = st == 2 ? min(n, part * part_len) : 0;
+        const int row_hi = st == 2 ? min(n, row_lo + part_len) : n;
+        if (st == 0 || (st == 2 && row_lo < row_hi)) {
         // Z = I: tql2 accumulates the tridiagonal eigenvectors, Q is applied afterwards
-        for (size_t idx = tid; idx < (size_t)n * n; idx += SP_T) Zb[idx] = 0.0;
-        __syncthreads();
-        for (int i = tid; i < n; i += SP_T) Zb[(size_t)i * n + i] = 1.0;
+        {
+            const int w = row_hi - row_lo;
+            for (size_t idx = tid; idx < (size_t)n * w; idx += SP_T) {
+                const int c = (int)(idx / w), r = row_lo + (int)(idx - (size_t)c * w);
+                Zb[(size_t)c * n + r] = r == c ? 1.0 : 0.0;
+            }
+        }
         __syncthreads();
         if (tid == 0) t2 = __builtin_amdgcn_s_memtime();
 
@@ -554,7 +578,8 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             constexpr int OFF = QB + 4;
             static_assert(QB == 16, "applier: 64 lanes = 4 steps x 16 stages");
             const int gld = n + 2 * QB + 4;                 // rows -OFF .. n+QB-1
-            double2* Gbuf = reinterpret_cast<double2*>(Wp + (size_t)SP_NB * n);   // [2][gld][QB]
+            double2* Gbuf = reinterpret_cast<double2*>(st == 2 ? M + a.big_off + MC_GBUF + (size_t)part * MC_GSZ
+                                                               : Wp + (size_t)SP_NB * n);   // [2][gld][QB]
             int* seq_l = S.perm;                            // [2][QB]  (perm is free until 4c)
             int* seq_m = S.perm + 2 * QB;                   // [2][QB]
             int* bflag = S.perm + 4 * QB;                   // [2] nseq, [2] generator done
@@ -606,7 +631,10 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     }
                     const int l = gl, m = gm;
                     ++giter;
-                    if (lane == 0) ++n_iter;
+                    if (lane == 0) {
+                        ++n_iter;
+                        n_rot += (unsigned long long)(m - l);
+                    }
                     double hsh = 0.0;
                     if (lane == 0) {
                         const double g0 = S.d[l];
@@ -620,57 +648,92 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     hsh = __shfl(hsh, 0);
                     for (int i = l + 2 + lane; i < n; i += 64) S.d[i] -= hsh;
                     gf += hsh;
-                    int conv = 0;
-                    if (lane == 0) {
-                        const double dl1 = S.d[l + 1];
-                        double p = S.d[m];
-                        double c = 1.0, c2 = 1.0, c3 = 1.0, sn = 0.0, s2 = 0.0;
-                        const double el1 = S.e[l + 1];
-                        double2* gt = G + (ptrdiff_t)(OFF - nseq) * QB + nseq;
-                        double ei = S.e[m - 1], di = S.d[m - 1];
-                        for (int i = m - 1; i >= l; --i) {
-                            // prefetch the next position's (e, d), unconditionally (index
-                            // clamped) so the loop body has no branch and the LDS wait lands
-                            // at the end of the chain instead of its start
-                            const int ip = max(i - 1, 0);
-                            const double ein = S.e[ip];
-                            const double din = S.d[ip];
-                            c3 = c2;
-                            c2 = c;
-                            s2 = sn;
-                            const double g = c * ei;
-                            const double h = c * p;
+                    // the bulge chase, in two phases per 64 positions.  (A) the serial
+                    // chain alone, on wave-uniform values: p and 1/r of each rotation, with
+                    // e_i^2 and d_i broadcast from a per-lane block by v_readlane and the
+                    // two results kept in the position's lane by v_cndmask -- ~24 VALU per
+                    // rotation, no memory access.  (B) every output of the 64 rotations
+                    // (c, s, e and d one place down) at once, lane t = rotation t.  The
+                    // chain never reads a position it has written (writes go to i + 1).
+                    // tools/probes/fp64_chain_probe.hip: 167 cycles per rotation against
+                    // 272 for the one-phase loop (whose stores and extra VALU sat in the
+                    // chain's issue stream).
+                    const double dl1 = S.d[l + 1];
+                    const double el1 = S.e[l + 1];
+                    double p = S.d[m];
+                    double c = 1.0;
+                    // c of the last three rotations and s of the last two (QL's c, c2, c3,
+                    // s, s2 at the end of the chase)
+                    double hc1 = 1.0, hc2 = 1.0, hc3 = 1.0, hs1 = 0.0, hs2 = 0.0;
+                    for (int ib = m - 1; ib >= l; ib -= 64) {
+                        const int cnt = min(64, ib - l + 1);
+                        const int pos = ib - lane;
+                        double eL = lane < cnt ? S.e[pos] : 0.0;
+                        double dL = lane < cnt ? S.d[pos] : 0.0;
+                        // a register redefinition: the loads are waited for here, once
+                        asm volatile("" : "+v"(eL), "+v"(dL));
+                        const double e2L = eL * eL;
+                        double pT = 0.0, iT = 0.0;   // lane t: p entering rotation t, its 1/r
+                        for (int t = 0; t < cnt; ++t) {
+                            const double ei2 = bcast_lane(e2L, t);
+                            const double di = bcast_lane(dL, t);
                             // r = hypot(p, e_i); |p|, |e_i| <= ||T|| here, so the plain form
                             // neither overflows nor underflows.  1/r = rsq(x2) refined by two
-                            // Newton steps (the serial chain is ~11 dependent operations; r
-                            // itself is off the chain)
-                            const double x2 = fma(p, p, ei * ei);
+                            // Newton steps (inv += inv (1/2 - x2/2 inv^2); 0.5 is an inline
+                            // constant).  p' = c' d_i - s' c e_i = (p d_i - c e_i^2) / r.
+                            const double x2 = fma(p, p, ei2);
+                            const double tt = fma(p, di, -(c * ei2));
                             double inv = __builtin_amdgcn_rsq(x2);
                             const double hx = 0.5 * x2;
-                            inv = inv * fma(-hx, inv * inv, 1.5);
-                            inv = inv * fma(-hx, inv * inv, 1.5);
-                            const double r = x2 * inv;
-                            S.e[i + 1] = sn * r;
-                            sn = ei * inv;
+                            inv = fma(inv, fma(-hx, inv * inv, 0.5), inv);
+                            inv = fma(inv, fma(-hx, inv * inv, 0.5), inv);
+                            const bool mine = lane == t;
+                            pT = mine ? p : pT;
+                            iT = mine ? inv : iT;
                             c = p * inv;
-                            p = c * di - sn * g;
-                            S.d[i + 1] = h + sn * (c * g + sn * di);
-                            gt[(size_t)i * QB] = make_double2(c, sn);
-                            ei = ein;
-                            di = din;
+                            p = inv * tt;
                         }
-                        p = -sn * s2 * c3 * el1 * S.e[l] / dl1;
-                        S.e[l] = sn * p;
+                        // (B) lane t < cnt: rotation t at position i = ib - t
+                        const double cT = pT * iT, sT = eL * iT;
+                        const double rT = fma(pT, pT, e2L) * iT;
+                        double cP = __shfl_up(cT, 1), sP = __shfl_up(sT, 1);   // rotation t - 1
+                        if (lane == 0) {
+                            cP = hc1;
+                            sP = hs1;
+                        }
+                        const double g = cP * eL;
+                        const double en = sP * rT;
+                        const double dn = cP * pT + sT * (cT * g + sT * dL);
+                        if (lane < cnt) {
+                            S.e[pos + 1] = en;
+                            S.d[pos + 1] = dn;
+                            G[(size_t)(pos - nseq + OFF) * QB + nseq] = make_double2(cT, sT);
+                        }
+                        const double b1 = __shfl(cT, cnt - 1), b2 = __shfl(cT, max(cnt - 2, 0)),
+                                     b3 = __shfl(cT, max(cnt - 3, 0));
+                        const double q1 = __shfl(sT, cnt - 1), q2 = __shfl(sT, max(cnt - 2, 0));
+                        const double o1 = hc1, o2 = hc2, os1 = hs1;
+                        hc1 = b1;
+                        hc2 = cnt >= 2 ? b2 : o1;
+                        hc3 = cnt >= 3 ? b3 : (cnt == 2 ? o1 : o2);
+                        hs1 = q1;
+                        hs2 = cnt >= 2 ? q2 : os1;
+                    }
+                    const double sn = hs1;
+                    p = -sn * hs2 * hc3 * el1 * S.e[l] / dl1;
+                    c = hc1;
+                    const double e_l = sn * p;
+                    const int conv = !(fabs(e_l) > eps * gtst1 && giter < 60);
+                    if (lane == 0) {
+                        S.e[l] = e_l;
                         S.d[l] = c * p;
                         seq_l[buf * QB + nseq] = l;
                         seq_m[buf * QB + nseq] = m;
-                        conv = !(fabs(S.e[l]) > eps * gtst1 && giter < 60);
                         if (conv) {
                             S.d[l] += gf;
                             S.e[l] = 0.0;
                         }
                     }
-                    conv = __shfl(conv, 0);
                     ++nseq;
                     if (conv) {
                         ++gl;
@@ -708,20 +771,20 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                         Mx = max(Mx, seq_m[buf * QB + t]);
                     }
                     const double2* G = Gbuf + (size_t)buf * QB * gld;
-                    for (int rbase = 0; rbase < n; rbase += 2 * NA) {
+                    for (int rbase = row_lo; rbase < row_hi; rbase += 2 * NA) {
                         // every lane stays active (the coefficient pairs are read from all
-                        // 64 lanes); rows past n alias row 0 and do not store
+                        // 64 lanes); rows past row_hi alias row_lo and do not store
                         const int r0 = rbase + ta, r1 = r0 + NA;
-                        if (rbase + (wave - 1) * 64 >= n) continue;   // the whole wave is past n
-                        const bool a0 = r0 < n, a1 = r1 < n;
+                        if (rbase + (wave - 1) * 64 >= row_hi) continue;   // the whole wave is past the rows
+                        const bool a0 = r0 < row_hi, a1 = r1 < row_hi;
                         double c0[QB], c1[QB];
 #pragma unroll
                         for (int t = 0; t < QB; ++t) {
                             c0[t] = 0.0;
                             c1[t] = 0.0;
                         }
-                        double* z0 = Zb + (a0 ? r0 : 0);
-                        double* z1 = Zb + (a1 ? r1 : 0);
+                        double* z0 = Zb + (a0 ? r0 : row_lo);
+                        double* z1 = Zb + (a1 ? r1 : row_lo);
                         // four steps per iteration: one coalesced load brings the 4 x 16
                         // coefficient pairs (lane 16u + t: step u, stage t), v_readlane puts
                         // each pair in SGPRs for the FMAs; the next four columns of both rows
@@ -768,9 +831,23 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 __syncthreads();
             }
         }
+        }   // st == 0 || st == 2
         const unsigned long long t4 = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
+        if (st == 2) {   // the eigenvalues (every part computed the same d) to the slot
+            if (part == 0) {
+                for (int i = tid; i < n; i += SP_T) M[a.big_off + MC_DF + i] = S.d[i];
+                if (a.phase && tid == 0) {
+                    atomicAdd(&a.phase[4], t4 - t3);
+                    atomicAdd(&a.phase[5], tgen);
+                    atomicAdd(&a.phase[6], n_iter);
+                    atomicAdd(&a.phase[1], n_rot);   // staged path: slot 1 (assembly) holds the rotation count
+                }
+            }
+            __syncthreads();
+            continue;
+        }
         // ---- 4a. Z to row-major (in place, 32 x 32 tile pairs through LDS) ------------------
-        {
+        if (st == 0 || st == 3) {
             double* buf = stage;   // two 32 x 33 tiles
             const int nt = (n + 31) >> 5;
             for (int I = 0; I < nt; ++I) {
@@ -791,6 +868,11 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 }
             }
         }
+        if (st == 3) continue;
+        // columns of Z this workgroup back-transforms and writes (stage 4: the P-th part)
+        const int col_lo = st == 4 ? min(n, part * part_len) : 0;
+        const int col_hi = st == 4 ? min(n, col_lo + part_len) : n;
+        if (col_lo >= col_hi) continue;   // uniform
         // ---- 4b. eigenvectors of A = Q Z: compact-WY panels applied last to first --------------
         // P_b = H_p ... H_{p+jb-1} = I - V T V^T (dlarft forward/columnwise), Z(p+1:n, :) -=
         // V (T (V^T Z)).  Lane per column of the row-major Z; V rows staged in LDS and read as
@@ -827,9 +909,9 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     __syncthreads();
                 }
                 const int r_lo = p + 1;
-                for (int cbase = 0; cbase < n; cbase += SP_W * 64) {
+                for (int cbase = col_lo; cbase < col_hi; cbase += SP_W * 64) {
                     const int c = cbase + wave * 64 + lane;
-                    const bool cact = c < n;
+                    const bool cact = c < col_hi;
                     double x[SP_NB];
 #pragma unroll
                     for (int t = 0; t < SP_NB; ++t) x[t] = 0.0;
@@ -894,6 +976,9 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             }
         }
         // ---- 4c. order, sign, lim, output --------------------------------------------------
+        // (stage 4: every part ranks all eigenvalues; the sign and the output are its columns',
+        // with each column's rank kept in the slot's rc)
+        int* rank_of = st == 4 ? reinterpret_cast<int*>(rc) : nullptr;
         for (int j = tid; j < n; j += SP_T) {
             const double lj = S.d[j];
             int rank = 0;
@@ -902,10 +987,11 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 rank += (li < lj) || (li == lj && i < j);
             }
             S.perm[rank] = j;
+            if (rank_of) rank_of[j] = rank;
         }
-        for (int cb = wave * 64; cb < n; cb += SP_W * 64) {
+        for (int cb = col_lo + wave * 64; cb < col_hi; cb += SP_W * 64) {
             const int c = cb + lane;
-            if (c < n) {
+            if (c < col_hi) {
                 double s0 = 0.0, s1 = 0.0;
                 int r = 0;
                 for (; r + 2 <= n; r += 2) {
@@ -932,9 +1018,25 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         }
         __syncthreads();
         const int mm = S.flag[3];
-        if (mode == 0)
-            for (int i = tid; i < n; i += SP_T) a.sigs[base + i] = (float)((double)S.sig[i] + 0.01);
-        for (int r = tid; r < mm; r += SP_T) a.evals[base + r] = (float)S.d[S.perm[r]];
+        if (part == 0) {
+            if (mode == 0)
+                for (int i = tid; i < n; i += SP_T) a.sigs[base + i] = (float)((double)S.sig[i] + 0.01);
+            for (int r = tid; r < mm; r += SP_T) a.evals[base + r] = (float)S.d[S.perm[r]];
+        }
+        if (st == 4) {
+            const int w = col_hi - col_lo;
+            for (size_t idx = tid; idx < (size_t)n * w; idx += SP_T) {
+                const int i = (int)(idx / w), j = col_lo + (int)(idx - (size_t)i * w);
+                const int r = rank_of[j];
+                if (r < mm) Wt[(size_t)i * mm + r] = (float)(Zb[(size_t)i * n + j] * rs[j]);
+            }
+            __syncthreads();
+            if (a.phase && tid == 0 && part == 0) {
+                atomicAdd(&a.phase[0], 1ull);
+                atomicAdd(&a.phase[7], __builtin_amdgcn_s_memtime() - t4);
+            }
+            continue;
+        }
         for (size_t idx = tid; idx < (size_t)n * mm; idx += SP_T) {
             const int i = (int)(idx / mm), r = (int)(idx - (size_t)i * mm);
             const int j = S.perm[r];
@@ -1224,7 +1326,9 @@ __global__ void spill_mc_end(McArgs a) {
 
 // Staged multi-CU path for BIG users [first, first + count) (plan positions, k non-increasing),
 // `slots` users at a time: stage 1 (assembly) on eigen_spill_kernel, the tridiagonalisation on
-// the spill_mc_* launches, stage 2 (QL, back-transform, output) on eigen_spill_kernel.
+// the spill_mc_* launches, then eigen_spill_kernel again for QL (stage 2, MC_QL_ROWS-row parts,
+// each with its own copy of the serial generator), Z to row-major (stage 3) and the
+// back-transform + output (stage 4, MC_BT_COLS-column parts).
 static int spill_mc_launch(cf_ctx* ctx, const cf_plan* plan, SpillArgs a, uint32_t first, uint32_t count,
                            uint32_t slots, uint32_t n_cu, hipStream_t st) {
     const size_t lds = sizeof(SpillSmemT<CF_SPILL_MAX_K, true>);
@@ -1236,6 +1340,7 @@ static int spill_mc_launch(cf_ctx* ctx, const cf_plan* plan, SpillArgs a, uint32
         a.count = cnt;
         const uint32_t grid = std::min(cnt, n_cu);
         a.mc_stage = 1;
+        a.mc_parts = 1;
         CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
         hipLaunchKernelGGL((eigen_spill_kernel<CF_SPILL_MAX_K, true>), dim3(grid), dim3(SP_T), lds, st, a);
         CF_HIP_CHECK(ctx, hipGetLastError());
@@ -1265,10 +1370,20 @@ static int spill_mc_launch(cf_ctx* ctx, const cf_plan* plan, SpillArgs a, uint32
         }
         hipLaunchKernelGGL(spill_mc_end, dim3((cnt + 63) / 64), dim3(64), 0, st, m);
         CF_HIP_CHECK(ctx, hipGetLastError());
-        a.mc_stage = 2;
-        CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
-        hipLaunchKernelGGL((eigen_spill_kernel<CF_SPILL_MAX_K, true>), dim3(grid), dim3(SP_T), lds, st, a);
-        CF_HIP_CHECK(ctx, hipGetLastError());
+        // QL on row parts, Z to row-major, back-transform + output on column parts: only as
+        // many parts as fill the CUs (each QL part repeats the serial generator, so a batch
+        // that fills the GPU on its own users runs one part per user)
+        const uint32_t fill = (n_cu + cnt - 1) / cnt;
+        const int parts[3] = {(int)std::min<uint32_t>(fill, (kmax + MC_QL_ROWS - 1) / MC_QL_ROWS), 1,
+                              (int)std::min<uint32_t>(fill, (kmax + MC_BT_COLS - 1) / MC_BT_COLS)};
+        for (int s = 0; s < 3; ++s) {
+            a.mc_stage = 2 + s;
+            a.mc_parts = parts[s];
+            const uint32_t g = std::min<uint32_t>(cnt * (uint32_t)parts[s], n_cu);
+            CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
+            hipLaunchKernelGGL((eigen_spill_kernel<CF_SPILL_MAX_K, true>), dim3(g), dim3(SP_T), lds, st, a);
+            CF_HIP_CHECK(ctx, hipGetLastError());
+        }
     }
     return CF_OK;
 }
@@ -1369,6 +1484,7 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     a.evals = d_evals;
     a.evecs = d_evecs;
     if (loc) a.loc = *loc;
+    a.mc_parts = 1;
     a.phase = ctx->spill_debug ? reinterpret_cast<unsigned long long*>(ws + 64) : nullptr;
     for (size_t i = 0; i < rs.size(); ++i) {
         const Range& r = rs[i];

@@ -10,3 +10,6 @@ if [ "${2:-tests}" = tests ]; then
 fi
 timeout -k 10 500 python3 -u bench.py --c5 only > $out/c5_mc.json 2> $out/c5_mc.err || { echo rc=$?; tail -5 $out/c5_mc.err; exit 1; }
 grep -v amdgpu $out/c5_mc.err
+# per-phase cycles (cf_debug_spill) at k = 4000 / 5000
+timeout -k 10 300 python3 -u tools/probe_spill.py 4000:24 5000:8 > $out/probe.log 2>&1 || { echo probe_rc=$?; tail -5 $out/probe.log; exit 1; }
+grep -v amdgpu $out/probe.log
