@@ -85,6 +85,11 @@ constexpr int MC_BT_COLS = SP_T;                   // columns of one back-transf
 constexpr int MC_QL_PARTS_MAX = (CF_SPILL_MAX_K + MC_QL_ROWS - 1) / MC_QL_ROWS;
 constexpr uint64_t MC_GSZ = 4ull * SP_QB * (CF_SPILL_MAX_K + 2 * SP_QB + 4);   // doubles per buffer
 constexpr uint64_t MC_EXTRA = MC_GBUF + (uint64_t)MC_QL_PARTS_MAX * MC_GSZ;
+// the symv's transposed partials z_g (G <= MC_GMAX rows of CF_SPILL_MAX_K) share the QL buffers'
+// space: the tridiagonalisation is over before QL starts
+constexpr int MC_GMAX = (CF_SPILL_MAX_K + 63) / 64;
+constexpr uint64_t MC_Z = MC_GBUF;
+static_assert((uint64_t)MC_GMAX * CF_SPILL_MAX_K <= (uint64_t)MC_QL_PARTS_MAX * MC_GSZ, "symv partials fit");
 
 // LDS of one workgroup.  NL = the largest k of the launch's layout.  Up to SP_NL (3072) the
 // per-row vectors rc / rs / tau live in LDS too; a BIG launch (SP_NL < k <= CF_SPILL_MAX_K)
@@ -1149,12 +1154,22 @@ __global__ __launch_bounds__(SP_T) void spill_mc_col(McArgs a, int j, int p) {
     }
 }
 
-// y = A(r0:n, r0:n) v on G workgroups per user: workgroup g takes row blocks g, g + G, ... of
-// 64 rows; its four waves split the columns, partial sums combined in LDS in a fixed order
+// y = A(r0:n, r0:n) v on G workgroups per user, each 64 x 64 tile of the lower triangle read
+// once (the matrix is symmetric; spill_mc_trail keeps only the lower triangle and a 64-wide band
+// above the diagonal up to date).  Tiles are anchored at r0.  Workgroup g takes the row-block
+// pairs {k, nrb - 1 - k}, k = g, g + G, ... (nrb + 1 tiles a pair: balanced); wave w of it the
+// column blocks C = w, w + 4, ... <= R.  A tile (R, C) adds
+// A_RC v_C to the rows' partial y_R (lane = row, column-major loads coalesce) and, below the
+// diagonal, A_RC^T v_R to the workgroup's partial z_g over C's columns (the 64 x 16 products of
+// a slab transposed through the wave's LDS scratch, four 16-row sums per column).  z_g lives in
+// the slot; a column block always belongs to the same wave of g, so its z entries are updated
+// by one lane in ascending R: deterministic.  spill_mc_fin forms y = y_R + sum_g z_g in order.
 constexpr int MC_SYMV_T = 256;
+constexpr int MC_TQ = 16 * 65;   // a wave's slab transposition scratch: 16 columns x 64 rows (+1 pad)
 __global__ __launch_bounds__(MC_SYMV_T) void spill_mc_symv(McArgs a, int j) {
     __shared__ double vs[CF_SPILL_MAX_K];
     __shared__ double part[MC_SYMV_T / 64][64];
+    __shared__ double tq[MC_SYMV_T / 64][MC_TQ];
     const uint32_t u = blockIdx.x / a.G;
     const int g = blockIdx.x % a.G;
     const int n = mc_n(a, u);
@@ -1168,34 +1183,56 @@ __global__ __launch_bounds__(MC_SYMV_T) void spill_mc_symv(McArgs a, int j) {
     constexpr int NWV = MC_SYMV_T / 64;
     const int r0 = j + 1;
     const int nrb = (n - r0 + 63) >> 6;
-    if (g >= nrb) return;   // uniform
+    const int npair = (nrb + 1) >> 1;
+    if (g >= npair) return;   // uniform; spill_mc_fin sums z over g < min(G, npair)
+    double* z = M + a.big_off + MC_Z + (size_t)g * CF_SPILL_MAX_K;
     for (int c = r0 + tid; c < n; c += MC_SYMV_T) vs[c] = rc[c];
+    // z_g = 0 on this wave's column blocks, by the lanes that update them below
+    for (int C = wave; C < nrb; C += NWV)
+        for (int s16 = 0; s16 < 64; s16 += 16) {
+            const int c = r0 + C * 64 + s16 + lane;
+            if (lane < 16 && c < n) z[c] = 0.0;
+        }
     __syncthreads();
-    const int cols = n - r0, seg = (cols + NWV - 1) / NWV;
-    const int c_lo = r0 + wave * seg, c_hi = min(n, c_lo + seg);
-    for (int rb = g; rb < nrb; rb += a.G) {
-        const int r = r0 + rb * 64 + lane;
-        double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-        if (r < n) {
-            const double* mr = M + r;
-            int c = c_lo;
-            for (; c + 16 <= c_hi; c += 16) {
+    double* q = tq[wave];
+    const int ci = lane & 15, qq = lane >> 4;
+    for (int it = 0; it < 2 * ((npair - g + a.G - 1) / a.G); ++it) {
+        const int k = g + (it >> 1) * a.G;
+        const int R = (it & 1) ? nrb - 1 - k : k;
+        if ((it & 1) && R == k) continue;   // the middle block of an odd count (uniform)
+        const int r = r0 + R * 64 + lane;
+        const bool ract = r < n;
+        const double vr = ract ? vs[r] : 0.0;
+        double y0 = 0.0, y1 = 0.0;
+        for (int C = wave; C <= R; C += NWV) {
+            const int cb0 = r0 + C * 64;
+            const int cw = min(64, n - cb0);
+            for (int s16 = 0; s16 < cw; s16 += 16) {
+                const int c0 = cb0 + s16;
                 double x[16];
+                const double* mp = M + (size_t)c0 * n + r;
 #pragma unroll
-                for (int t = 0; t < 16; ++t) x[t] = mr[(size_t)(c + t) * n];
+                for (int t = 0; t < 16; ++t) x[t] = (ract && s16 + t < cw) ? mp[(size_t)t * n] : 0.0;
 #pragma unroll
-                for (int t = 0; t < 16; t += 4) {
-                    p0 += x[t] * vs[c + t];
-                    p1 += x[t + 1] * vs[c + t + 1];
-                    p2 += x[t + 2] * vs[c + t + 2];
-                    p3 += x[t + 3] * vs[c + t + 3];
+                for (int t = 0; t < 16; t += 2) {
+                    y0 = fma(x[t], s16 + t < cw ? vs[c0 + t] : 0.0, y0);
+                    y1 = fma(x[t + 1], s16 + t + 1 < cw ? vs[c0 + t + 1] : 0.0, y1);
+                }
+                if (C < R) {
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) q[t * 65 + lane] = x[t] * vr;
+                    double sacc = 0.0;
+#pragma unroll
+                    for (int rr = 0; rr < 16; ++rr) sacc += q[ci * 65 + qq * 16 + rr];
+                    sacc += __shfl_xor(sacc, 16);
+                    sacc += __shfl_xor(sacc, 32);
+                    if (qq == 0 && s16 + ci < cw) z[c0 + ci] += sacc;
                 }
             }
-            for (; c < c_hi; ++c) p0 += mr[(size_t)c * n] * vs[c];
         }
-        part[wave][lane] = (p0 + p1) + (p2 + p3);
+        part[wave][lane] = y0 + y1;
         __syncthreads();
-        if (wave == 0 && r < n) {
+        if (wave == 0 && ract) {
             double y = 0.0;
 #pragma unroll
             for (int w = 0; w < NWV; ++w) y += part[w][lane];
@@ -1228,9 +1265,13 @@ __global__ __launch_bounds__(SP_T) void spill_mc_fin(McArgs a, int j, int p) {
         xw[tid] = mc[MC_XW + tid];
     }
     __syncthreads();
+    // y = the row-block partials + the transposed partials z_g of spill_mc_symv, in order
+    const int gz = min(a.G, (((n - r0 + 63) >> 6) + 1) >> 1);
+    const double* z = mc + MC_Z;
     double yv = 0.0;
     for (int r = r0 + tid; r < n; r += SP_T) {
         double y = rs[r];
+        for (int g = 0; g < gz; ++g) y += z[(size_t)g * CF_SPILL_MAX_K + r];
         for (int t = 0; t < jj; ++t) y -= M[(size_t)(p + t) * n + r] * xv[t] + Wp[(size_t)t * n + r] * xw[t];
         y *= tj;
         rs[r] = y;
@@ -1240,9 +1281,11 @@ __global__ __launch_bounds__(SP_T) void spill_mc_fin(McArgs a, int j, int p) {
     for (int r = tid; r < n; r += SP_T) Wp[(size_t)jj * n + r] = r >= r0 ? rs[r] + a2 * rc[r] : 0.0;
 }
 
-// trailing update A(q:n, q:n) -= V W^T + W V^T after the panel at p, q = p + jb: G workgroups
-// per user, each a range of SP_CC-column chunks; lane per row with that row's V and W entries
-// in registers, each column's entries broadcast from LDS (the stage-2 code of eigen_spill_kernel)
+// trailing update A(q:n, q:n) -= V W^T + W V^T after the panel at p, q = p + jb, on the lower
+// triangle and a band of at least 64 above the diagonal (what spill_mc_symv reads): G
+// workgroups per user, workgroup g the SP_CC-column chunks g, g + G, ... (interleaved, so the
+// triangle's work is balanced); lane per row with that row's V and W entries in registers, each
+// column's entries broadcast from LDS (the stage-2 code of eigen_spill_kernel)
 __global__ __launch_bounds__(SP_T) void spill_mc_trail(McArgs a, int p) {
     __shared__ double stg[SP_CC * 2 * SP_NB];
     const uint32_t u = blockIdx.x / a.G;
@@ -1256,21 +1299,23 @@ __global__ __launch_bounds__(SP_T) void spill_mc_trail(McArgs a, int p) {
     double* M = a.work + (size_t)u * a.stride;
     const double* Wp = M + 2 * (size_t)n * n;
     const int nchunk = (mq + SP_CC - 1) / SP_CC;
-    const int per = (nchunk + a.G - 1) / a.G;
-    const int ch_lo = g * per, ch_hi = min(nchunk, ch_lo + per);
-    if (ch_lo >= ch_hi) return;   // uniform
+    if (g >= nchunk) return;   // uniform
     const int nrb = (mq + 63) >> 6;
-    for (int pass = 0; pass < nrb; pass += SP_W) {
+    // row block rb (rows q + 64 rb ..) is updated in chunk ch iff its last row is >= the
+    // chunk's first column - 64, i.e. ch * SP_CC <= 64 rb + 127
+    const int rb_first = max(0, (g * SP_CC - 127 + 63) / 64);   // first row block any chunk of g needs
+    for (int pass = (rb_first / SP_W) * SP_W; pass < nrb; pass += SP_W) {
         const int rb = pass + wave;
         const int r = q + rb * 64 + lane;
         const bool act = rb < nrb && r < n;
+        const int ch_top = (min(pass + SP_W - 1, nrb - 1) * 64 + 127) / SP_CC;   // the pass's last chunk
         double vr[SP_NB], wr[SP_NB];
 #pragma unroll
         for (int t = 0; t < SP_NB; ++t) {
             vr[t] = (act && t < jb) ? M[(size_t)(p + t) * n + r] : 0.0;
             wr[t] = (act && t < jb) ? Wp[(size_t)t * n + r] : 0.0;
         }
-        for (int ch = ch_lo; ch < ch_hi; ++ch) {
+        for (int ch = g; ch < nchunk && ch <= ch_top; ch += a.G) {
             const int c0 = q + ch * SP_CC;
             const int cn = min(SP_CC, n - c0);
             __syncthreads();
@@ -1282,7 +1327,7 @@ __global__ __launch_bounds__(SP_T) void spill_mc_trail(McArgs a, int p) {
                 stg[idx] = v;
             }
             __syncthreads();
-            if (!act) continue;
+            if (!act || ch * SP_CC > rb * 64 + 127) continue;
             double* mp = M + (size_t)c0 * n + r;
             double cur[8];
 #pragma unroll
@@ -1371,9 +1416,10 @@ static int spill_mc_launch(cf_ctx* ctx, const cf_plan* plan, SpillArgs a, uint32
         hipLaunchKernelGGL(spill_mc_end, dim3((cnt + 63) / 64), dim3(64), 0, st, m);
         CF_HIP_CHECK(ctx, hipGetLastError());
         // QL on row parts, Z to row-major, back-transform + output on column parts: only as
-        // many parts as fill the CUs (each QL part repeats the serial generator, so a batch
-        // that fills the GPU on its own users runs one part per user)
-        const uint32_t fill = (n_cu + cnt - 1) / cnt;
+        // many parts as fit the CUs in one round (each QL part repeats the serial generator, so
+        // a batch that fills the GPU on its own users runs one part per user, and a second
+        // round of parts would double the stage)
+        const uint32_t fill = std::max<uint32_t>(1, n_cu / cnt);   // every part in the first round
         const int parts[3] = {(int)std::min<uint32_t>(fill, (kmax + MC_QL_ROWS - 1) / MC_QL_ROWS), 1,
                               (int)std::min<uint32_t>(fill, (kmax + MC_BT_COLS - 1) / MC_BT_COLS)};
         for (int s = 0; s < 3; ++s) {
