@@ -1009,15 +1009,17 @@ def knn2_leg(args, ctx, dev, torch):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ref as orc
 
+        threads, _ = host_threads()
         rng = np.random.default_rng(3)
         cal = rng.choice(n_items, size=2, replace=False).astype(np.int32)
         t = time.perf_counter()
         orc.knn2_rows(off.astype(np.int64), items.astype(np.int32), rats.astype(np.float64), n_items, cal)
         per = (time.perf_counter() - t) / 2
-        n_rows = int(max(2, min(200, args.cpu_seconds * 0.5 / max(per, 1e-3))))
+        n_rows = int(max(2, min(200 * threads, threads * args.cpu_seconds * 0.5 / max(per, 1e-3))))
         rows = np.sort(rng.choice(n_items, size=n_rows, replace=False)).astype(np.int32)
         t = time.perf_counter()
-        Wr = orc.knn2_rows(off.astype(np.int64), items.astype(np.int32), rats.astype(np.float64), n_items, rows)
+        Wr = orc.knn2_rows(off.astype(np.int64), items.astype(np.int32), rats.astype(np.float64), n_items, rows,
+                           threads=threads)
         cpu_s = time.perf_counter() - t
         Wg = W_s[torch.from_numpy(rows.astype(np.int64)).to(dev)].cpu().numpy()
         out["parity_rows_bit_exact"] = bool(np.array_equal(Wg, Wr))
@@ -1025,10 +1027,11 @@ def knn2_leg(args, ctx, dev, torch):
         out["cpu_baseline"] = {
             "value": n_rows * (I - 1) / cpu_s,
             "unit": "item-pair similarities/s",
-            "cores": 1,
+            "cores": threads,
             "kind": "port",
             "sample": f"{n_rows} random rows x {n_items} items of the same workload, oracle weights_calc "
-                      f"(sorted-list intersection per pair, float accumulators as knn2.cpp:127-146), 1 thread",
+                      f"(sorted-list intersection per pair, float accumulators as knn2.cpp:127-146), rows over "
+                      f"{threads} threads (the item maps are built once, serially, inside the timed call)",
         }
     del d_W
     torch.cuda.empty_cache()

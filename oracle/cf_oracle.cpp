@@ -674,17 +674,31 @@ int cfo_knn2(int n_users, const int64_t* user_off, const int32_t* item, const do
 
 // The same for the rows listed in rows[0..n_rows) only (CPU-baseline sample of bench.py):
 // W_out is n_rows x n_items.
+// n_threads > 1: rows are handed out to that many std::threads (each row's values are the
+// same computation, so the output does not depend on the thread count).
+int cfo_knn2_rows_mt(int n_users, const int64_t* user_off, const int32_t* item, const double* rating,
+                     int n_items, int n_rows, const int32_t* rows, float* W_out, int n_threads) {
+    const Knn2Maps maps = knn2_maps(n_users, user_off, item, rating, n_items);
+    std::atomic<int> next{0};
+    auto work = [&]() {
+        for (int i = next++; i < n_rows; i = next++) {
+            const int a = rows[i];
+            for (int b = 0; b < n_items; ++b) {
+                int num_rat = 0;
+                W_out[(size_t)i * n_items + b] = a != b ? knn2_pair(maps[a], maps[b], num_rat) : 0.0f;
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < n_threads; ++t) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+    return 0;
+}
+
 int cfo_knn2_rows(int n_users, const int64_t* user_off, const int32_t* item, const double* rating,
                   int n_items, int n_rows, const int32_t* rows, float* W_out) {
-    const Knn2Maps maps = knn2_maps(n_users, user_off, item, rating, n_items);
-    for (int i = 0; i < n_rows; ++i) {
-        const int a = rows[i];
-        for (int b = 0; b < n_items; ++b) {
-            int num_rat = 0;
-            W_out[(size_t)i * n_items + b] = a != b ? knn2_pair(maps[a], maps[b], num_rat) : 0.0f;
-        }
-    }
-    return 0;
+    return cfo_knn2_rows_mt(n_users, user_off, item, rating, n_items, n_rows, rows, W_out, 1);
 }
 
 // a11: knn_program gather/apply + error_vertex_data (knn3.cpp:185-256).

@@ -37,6 +37,7 @@ def lib():
                                         vp]
         L.cfo_knn2.argtypes = [ci, vp, vp, vp, ci, vp, vp]
         L.cfo_knn2_rows.argtypes = [ci, vp, vp, vp, ci, ci, vp, vp]
+        L.cfo_knn2_rows_mt.argtypes = [ci, vp, vp, vp, ci, ci, vp, vp, ci]
         L.cfo_knn3.argtypes = [ci, vp, vp, vp, vp, vp, vp]
         L.cfo_local_graph.argtypes = [ci, ci, vp, vp, ctypes.c_int64, vp]
         L.cfo_local_graph.restype = ci
@@ -152,14 +153,16 @@ def knn2(user_off, item, rating, n_items):
     return W, C
 
 
-def knn2_rows(user_off, item, rating, n_items, rows):
-    """weights_calc for the listed rows only: float32 (len(rows), n_items)."""
+def knn2_rows(user_off, item, rating, n_items, rows, threads=1):
+    """weights_calc for the listed rows only: float32 (len(rows), n_items); rows spread over
+    `threads` host threads (same values for any count)."""
     user_off = np.ascontiguousarray(user_off, dtype=np.int64)
     item = np.ascontiguousarray(item, dtype=np.int32)
     rating = np.ascontiguousarray(rating, dtype=np.float64)
     rows = np.ascontiguousarray(rows, dtype=np.int32)
     W = np.zeros((len(rows), n_items), dtype=np.float32)
-    lib().cfo_knn2_rows(len(user_off) - 1, _p(user_off), _p(item), _p(rating), n_items, len(rows), _p(rows), _p(W))
+    lib().cfo_knn2_rows_mt(len(user_off) - 1, _p(user_off), _p(item), _p(rating), n_items, len(rows), _p(rows), _p(W),
+                           int(threads))
     return W
 
 

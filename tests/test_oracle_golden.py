@@ -109,6 +109,11 @@ def test_knn2_matches_golden():
     Wg = np.where(z["W"] > 0.01, z["W"], 0.0).astype(np.float32)
     assert np.array_equal(W, Wg)            # bit-exact: integer ratings, exact float sums
     assert np.array_equal(W, W.T)           # both directions agree
+    # the bench CPU baseline's row sampler, one thread and several, gives the same rows
+    rows = np.array([0, 3, n_items - 1], dtype=np.int32)
+    for t in (1, 4):
+        Wr = orc.knn2_rows(np.array(off), np.array(items), np.array(rats), n_items, rows, threads=t)
+        assert np.array_equal(Wr, W[rows])
 
 
 def test_knn3_hand_computed():
