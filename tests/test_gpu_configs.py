@@ -28,6 +28,8 @@ against the reference binaries themselves.
 from __future__ import annotations
 
 import os
+import subprocess
+import sys
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -460,5 +462,30 @@ def test_c5_tail_k_up_to_5000(gpu_ctx, c4_graph):
         good, ill, badp = predict_check(run, [0], max_rows=6, seed=10)
         _report("C5 k=2000", good, ill, 6)
         assert not badp, badp
+    finally:
+        run.free()
+
+
+def test_spill_big_single_workgroup(gpu_ctx, c4_graph):
+    """The BIG layout (k > 3072) on one workgroup per user -- the path local_calc's units with
+    n > 3072 take, and compute_eigens' with CF_SPILL_MC=0 -- next to the staged multi-CU solver
+    the default run uses: the same size-independent properties at k = 3100 and 3400.  The
+    switch is read once per process, so the test re-runs itself in a child with it set."""
+    if os.environ.get("CF_SPILL_MC") != "0":
+        env = dict(os.environ, CF_SPILL_MC="0")
+        p = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                            f"{os.path.abspath(__file__)}::test_spill_big_single_workgroup"],
+                           env=env, capture_output=True, text=True, timeout=900)
+        assert p.returncode == 0, p.stdout[-4000:] + p.stderr[-2000:]
+        return
+    from collaborative_filtering_amd import synth, workloads as wlm
+
+    ks = np.array([3100, 3400], dtype=np.uint32)
+    off, items, rat = synth.user_items(wlm.CONFIGS["c5"]["seed"] + 11, ks, 50_000, threads=THREADS)
+    run = FusedRun(gpu_ctx, c4_graph[0], 50_000, off, items, rat)
+    try:
+        assert np.all(run.m >= 2) and np.all(run.m <= ks)
+        bad = eigen_properties(run, [0, 1])
+        assert not bad, bad
     finally:
         run.free()
