@@ -24,7 +24,9 @@
 //                          a_r = (P y)_r - P_{r,Cbar} y_Cbar,  b = (P y)_Cbar - P_{Cbar,Cbar} y_Cbar
 //                        (Woodbury on U_CS^T U_CS = I - Q_CbarS^T Q_CbarS in the Q basis),
 //                        (P y)_a = Q_aS (g - mean h)_S; every entry is a gather from the
-//                        per-user tables (columns [lim, Lu) subtracted when lim < Lu).  Ratings this form does not take --
+//                        per-user tables (columns [lim, Lu) subtracted when lim < Lu).  For
+//                        c < lim (K singular) the minimum-norm least-squares prediction
+//                        P_{r,C} P_CC^-1 y_C from the c x c block of P instead.  Ratings this form does not take --
 //                        a column dropped by the filter, no basis, c = 0, or a pivot of K
 //                        below kPivMin while c >= lim -- solve the rating's own bordered
 //                        Gram matrix M = U_CS^T U_CS (complement form Gbar_SS -
@@ -453,6 +455,65 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
             if (!fast && a.phase && tid == 0) pc[10] += 1;
         }
         SP_STAMP(1);
+        if (fast && c < lim) {
+            // Underdetermined (c < lim): K = I - P_CbarCbar is singular (rank <= k - lim < nc)
+            // and U_CS^T U_CS too.  The prediction is the minimum-norm least-squares one, as
+            // the G-mode of cf_predict.hip returns it for k <= 192:
+            //   pred - mean = P_{r,C} P_CC^-1 y_C,  P_CC = Q_CS Q_CS^T  (c x c),
+            // the projector's block on the connected rows (full rank when U_CS has full row
+            // rank; the same value as -w_r^T G^-1 h in the complement coordinates).  Its size
+            // is c, which is small exactly when K-mode's nc is large.
+            const size_t need = (size_t)(c + 2) * (c + 3) / 2;
+            double* A = need <= (size_t)kLdsA ? s_la : fa;
+            const auto pent = [&](int ia, int ib) {   // P over S = [0, lim)
+                double v = Pm[(size_t)ia * k + ib];
+                const double* xa = Q + (size_t)ia * Lu;
+                const double* xb = Q + (size_t)ib * Lu;
+                for (int j = lim; j < Lu; ++j) v = fma(-xa[j], xb[j], v);
+                return v;
+            };
+            const int ne = c * (c + 1) / 2;
+            for (int e = tid; e < ne + 2 * c; e += kT) {
+                if (e < ne) {
+                    int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+                    while (ra * (ra + 1) / 2 > e) --ra;
+                    while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
+                    A[e] = pent(s_conn[ra], s_conn[e - ra * (ra + 1) / 2]);
+                } else if (e < ne + c) {
+                    const int j = e - ne;
+                    A[tri(c, j)] = pent(r, s_conn[j]);
+                } else {
+                    const int j = e - ne - c;
+                    A[tri(c + 1, j)] = (double)s_rat[s_conn[j]] - mu;
+                }
+            }
+            __syncthreads();
+            SP_STAMP(2);
+            ldlt_bordered_wide(A, c, c + 2, sA, sB);
+            if (wave == 0) {
+                double dot = 0.0;
+                for (int j = lane; j < c; j += 64) dot = fma(A[tri(c, j)] * A[tri(c + 1, j)], A[tri(j, j)], dot);
+                dot = wsum(dot);
+                if (lane == 0) s_misc[2] = dot;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                double pred = mu + s_misc[2];
+                if (pred > 5) pred = 5;
+                if (pred < 1) pred = 1;
+                const double d = (double)s_rat[r] - pred;
+                a.mse[base + r] = (float)(d * d);
+                a.kk[base + r] = c;
+                if (a.pred) a.pred[base + r] = pred;
+                if (a.phase) {
+                    pc[6] += 1;
+                    pc[8] += c;
+                }
+            }
+            __syncthreads();
+            SP_STAMP(4);
+            continue;
+        }
         if (fast) {
             const int np = nc + 1;   // rows Cbar..., then r
             const size_t need = (size_t)(nc + 2) * (nc + 3) / 2;

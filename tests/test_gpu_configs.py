@@ -181,6 +181,40 @@ def eigen_properties(run: FusedRun, users, res_tol=1e-4):
         return [r for r in ex.map(one, users) if r]
 
 
+def pinv_prediction(U, ev, w_lim, Wu, rat, r, k, max_d_lds=32):
+    """The minimum-norm least-squares prediction of an underdetermined row (c < lim), which
+    the fast paths return (cf_predict.hip's G-mode for k <= 192, the spill predictor's
+    projector block for k > 192): clamp(mean + P_rC P_CC^-1 y_C), P the
+    orthogonal projector on U[:, :lim] (basis-free).  None when the row takes the dense path
+    (a column dropped by the zero-column filter, r connected to itself, or for k <= 192 a
+    system larger than max_d_lds rows, safely below the launch's nmax) or P_CC is worse than
+    cond 1e6.  Returns (prediction, cond(P_CC))."""
+    m = len(ev)
+    lim = m
+    for j in range(m):
+        if ev[j] > w_lim:
+            lim = j
+            break
+    lim = min(max(lim, 2), m)
+    C = np.nonzero(Wu[r].astype(np.float64) > 0.1)[0]
+    c = len(C)
+    if c == 0 or c >= lim or Wu[r, r] > 0.1:
+        return None
+    if k <= 192 and k - lim > max_d_lds:
+        return None
+    if not np.all(np.any(U[C, :lim] >= 1e-4, axis=0)):
+        return None
+    Qn, _ = np.linalg.qr(U[:, :lim])
+    P = Qn @ Qn.T
+    Pcc = P[np.ix_(C, C)]
+    cond = float(np.linalg.cond(Pcc))
+    if not cond <= 1e6:
+        return None
+    mu = float(np.mean(rat[C]))
+    pred = mu + float(P[r, C] @ np.linalg.solve(Pcc, rat[C] - mu))
+    return min(max(pred, 1.0), 5.0), cond
+
+
 def predict_check(run: FusedRun, users, max_rows=None, seed=0, ill_stats=None):
     """Stage-wise a7 parity on the device's own fp32 blocks.  Returns (good, ill, bad).
 
@@ -208,7 +242,8 @@ def predict_check(run: FusedRun, users, max_rows=None, seed=0, ill_stats=None):
                                                rows=rows)
         good = ill = 0
         bad = []
-        st = {"ill": 0, "oracle_nan": 0, "oracle_at_bound": 0, "device_at_bound": 0, "both_at_same_bound": 0}
+        st = {"ill": 0, "oracle_nan": 0, "oracle_at_bound": 0, "device_at_bound": 0, "both_at_same_bound": 0,
+              "pinv_pinned": 0, "pinv_max_err": 0.0}
         for t, r in enumerate(rows):
             g = b + int(r)
             if run.kk[g] != kk_o[t]:
@@ -231,6 +266,14 @@ def predict_check(run: FusedRun, users, max_rows=None, seed=0, ill_stats=None):
                 pg, po = float(run.pred[g]), float(pred_o[t])
                 if not (np.isfinite(run.mse[g]) and 1.0 <= pg <= 5.0):
                     bad.append((u, int(r), "rank-deficient row not finite / not clamped", float(run.mse[g]), pg))
+                pin = pinv_prediction(U, ev, float(tab[r]), Wu, rat.astype(np.float64), int(r), k)
+                if pin is not None:
+                    want, pcond = pin
+                    err = abs(pg - want)
+                    st["pinv_pinned"] += 1
+                    st["pinv_max_err"] = max(st["pinv_max_err"], err)
+                    if err > 1e-9 * max(1.0, pcond) * max(1.0, abs(want)):
+                        bad.append((u, int(r), "rank-deficient row != min-norm LS prediction", pg, want, pcond))
                 st["ill"] += 1
                 st["oracle_nan"] += int(np.isnan(mse_o[t]))
                 ob, gb = po in (1.0, 5.0), pg in (1.0, 5.0)
@@ -244,7 +287,7 @@ def predict_check(run: FusedRun, users, max_rows=None, seed=0, ill_stats=None):
     if ill_stats is not None:
         for r in res:
             for key, v in r[3].items():
-                ill_stats[key] = ill_stats.get(key, 0) + v
+                ill_stats[key] = max(ill_stats.get(key, 0.0), v) if key == "pinv_max_err" else ill_stats.get(key, 0) + v
     return sum(r[0] for r in res), sum(r[1] for r in res), [b for r in res for b in r[2]]
 
 
