@@ -88,6 +88,7 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
     if (ctx->d_phase) (void)hipFree(ctx->d_phase);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    if (ctx->d_pred_next) (void)hipFree(ctx->d_pred_next);
     if (ctx->d_knn) (void)hipFree(ctx->d_knn);
     if (ctx->d_knn_acc) (void)hipFree(ctx->d_knn_acc);
     if (ctx->d_knn_part) (void)hipFree(ctx->d_knn_part);

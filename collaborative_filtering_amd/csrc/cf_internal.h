@@ -66,6 +66,8 @@ struct cf_ctx {
     // Device scratch owned by the context (predictor per-block U^T U), grown on demand.
     void* d_scratch = nullptr;
     size_t scratch_bytes = 0;
+    // fused predictor: one user counter per predictor stream (zeroed before each launch)
+    uint32_t* d_pred_next = nullptr;
     // knn2 rating planes (R, S, B), grown on demand.
     void* d_knn = nullptr;
     size_t knn_bytes = 0;

@@ -337,9 +337,11 @@ __device__ void wave_gram(int nt, int inner, LOAD load, double* E) {
 #define CF_PRED_MASK_ROWS 8
 #endif
 constexpr int kMaskRows = CF_PRED_MASK_ROWS;   // graph rows gathered per wave at once
+// One user (position uo of the plan's order) into `slot`: the body of pred_basis_kernel and
+// the first half of pred_fused_kernel.
 template <typename T>
-__global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel(PredArgs<T> a, uint32_t first, uint32_t count) {
-    extern __shared__ double dsm[];
+__device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, double* slot, double* dsm,
+                                           unsigned long long (&ph_acc)[8], unsigned long long& ph_t) {
     const int lmax = a.lmax;
     double* A = dsm;                                       // block_gemm staging
     double* s_misc = A + kStageElems;                      // [1] sum of the user's ratings
@@ -357,13 +359,10 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long ph_t = 0;
 
-    for (uint32_t ub = blockIdx.x; ub < count; ub += gridDim.x) {
-        double* slot = a.slots + (size_t)ub * a.so.stride;
+    {
         double* Gb = slot + a.so.gb;
-        const uint32_t u = a.order[first + ub];
+        const uint32_t u = a.order[uo];
         const uint64_t base = a.item_off[u];
         const int k = (int)(a.item_off[u + 1] - base);
         const int m = a.m[u];
@@ -609,7 +608,9 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
                         xi[j] = dj > 0.0 ? xi[j] / sqrt(dj) : 0.0;
                     }
                 }
-                if (__syncthreads_or(fail) && tid == 0) s_cnt[9] = 1;
+                // a plain flag store, not __syncthreads_or: that one needs 256 B of static LDS,
+                // which would push the fused kernel's LDS past two workgroups per CU
+                if (fail) s_cnt[9] = 1;
                 __syncthreads();
             }
 #ifdef CF_PRED_BASIS_PROBE   // diagnostics: slot 7 = complement build, slot 6 = joint steps
@@ -704,7 +705,16 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
             }
         }
     }
-    if (a.phase_cycles && tid == 0)
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel(PredArgs<T> a, uint32_t first, uint32_t count) {
+    extern __shared__ double dsm[];
+    unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long ph_t = 0;
+    for (uint32_t ub = blockIdx.x; ub < count; ub += gridDim.x)
+        basis_user(a, first + ub, a.slots + (size_t)ub * a.so.stride, dsm, ph_acc, ph_t);
+    if (a.phase_cycles && threadIdx.x == 0)
         for (int ph = 0; ph < 8; ++ph) atomicAdd(&a.phase_cycles[ph], ph_acc[ph]);
 }
 
@@ -719,9 +729,11 @@ constexpr size_t kRatingLds = 163840 / CF_PRED_RATING_OCC;
 #endif
 constexpr int kLdlPw = CF_PRED_LDL_PW;
 static_assert(kLdlPw == 4 || kLdlPw == 8, "panel width: one or two MFMA k-steps");
+// Every rating of one user (position uo of the plan's order) from `slot`: the body of
+// pred_rating_kernel and the second half of pred_fused_kernel.
 template <typename T>
-__global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_rating_kernel(PredArgs<T> a, uint32_t first, uint32_t count) {
-    extern __shared__ double dsm[];
+__device__ __forceinline__ void rating_user(const PredArgs<T> a, uint32_t uo, double* slot, double* dsm,
+                                            unsigned long long (&ph_acc)[8], unsigned long long& ph_t) {
     const int lmax = a.lmax;
     // A: the factorisation region: the per-wave fast-path scratch, then (dense path) the
     //    packed lower triangle of the bordered matrix [[M, .], [t^T, .], [v^T, .]].
@@ -747,14 +759,11 @@ __global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_rating_kern
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long ph_t = 0;
 
-    for (uint32_t ub = blockIdx.x; ub < count; ub += gridDim.x) {
-        double* slot = a.slots + (size_t)ub * a.so.stride;
+    {
         const double* Gb = slot + a.so.gb;
         double* AP = slot + a.so.ap;
-        const uint32_t u = a.order[first + ub];
+        const uint32_t u = a.order[uo];
         const uint64_t base = a.item_off[u];
         const int k = (int)(a.item_off[u + 1] - base);
         const int m = a.m[u];
@@ -1239,10 +1248,65 @@ __global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_rating_kern
         }
         PHASE_STAMP(3);
     }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_rating_kernel(PredArgs<T> a, uint32_t first, uint32_t count) {
+    extern __shared__ double dsm[];
+    unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long ph_t = 0;
+    for (uint32_t ub = blockIdx.x; ub < count; ub += gridDim.x)
+        rating_user(a, first + ub, a.slots + (size_t)ub * a.so.stride, dsm, ph_acc, ph_t);
     // slots 0-7 (thread 0 of the block); 8-15 are added per rating / user by lane 0 of
     // every wave
-    if (a.phase_cycles && tid == 0)
+    if (a.phase_cycles && threadIdx.x == 0)
         for (int ph = 0; ph < 8; ++ph) atomicAdd(&a.phase_cycles[ph], ph_acc[ph]);
+}
+
+// ---- fused: basis then ratings of one user in the same workgroup, users claimed from a
+// device counter; a workgroup reuses ONE slot for all its users, so the slot set is one
+// slot per resident workgroup (~0.2-0.5 GB, within the 256 MiB Infinity Cache for k <~ 120)
+// and the rating half reads the basis it has just written instead of a chunk of 8192 slots
+// written a whole launch earlier.  Same arithmetic per user as the two kernels.  Measured
+// slower on C4 (1.80 vs 1.66 s): the rating half is latency-bound on its dependent chains,
+// not on where the slot lives, so it is an A/B option (CF_PRED_FUSED=1), not the default.
+// The fused kernel calls the two halves as real functions: each keeps the register
+// allocation of its own kernel instead of one allocation over both bodies (inlined, the
+// fused body spilled 684 B per lane against 444 / 176).
+#ifdef CF_PRED_FUSED_INLINE
+#define CF_PRED_CALL __forceinline__
+#else
+#define CF_PRED_CALL __noinline__
+#endif
+template <typename T>
+__device__ CF_PRED_CALL void basis_user_call(const PredArgs<T> a, uint32_t uo, double* slot, double* dsm,
+                                             unsigned long long (&ph_acc)[8], unsigned long long& ph_t) {
+    basis_user(a, uo, slot, dsm, ph_acc, ph_t);
+}
+template <typename T>
+__device__ CF_PRED_CALL void rating_user_call(const PredArgs<T> a, uint32_t uo, double* slot, double* dsm,
+                                              unsigned long long (&ph_acc)[8], unsigned long long& ph_t) {
+    rating_user(a, uo, slot, dsm, ph_acc, ph_t);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_fused_kernel(PredArgs<T> a, uint32_t first, uint32_t count,
+                                                                                  uint32_t* next) {
+    extern __shared__ double dsm[];
+    unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long ph_t = 0;
+    double* slot = a.slots + (size_t)blockIdx.x * a.so.stride;
+    uint32_t* s_claim = reinterpret_cast<uint32_t*>(dsm);   // free between users (both halves open with a barrier)
+    for (;;) {
+        if (threadIdx.x == 0) s_claim[0] = atomicAdd(next, 1u);
+        __syncthreads();
+        const uint32_t ub = s_claim[0];
+        if (ub >= count) break;   // uniform: every thread read the same claim
+        basis_user_call(a, first + ub, slot, dsm, ph_acc, ph_t);
+        __syncthreads();
+        rating_user_call(a, first + ub, slot, dsm, ph_acc, ph_t);
+        __syncthreads();
+    }
 }
 
 // Chunks of up to kChunk users per (basis, rating) launch pair; each user of a chunk owns a
@@ -1307,6 +1371,30 @@ int setup_bucket(cf_ctx* ctx, PredArgs<T>& args, int lmax, size_t& rating_lds) {
     return CF_OK;
 }
 
+// CF_PRED_FUSED=1 selects the fused persistent kernel; default: the two-kernel chunked path
+// (C4 predict 1660 ms against 1803-1813 ms fused, profiles/r03/pred_fused_rejected/).
+inline bool pred_fused_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("CF_PRED_FUSED");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+// Fused launch of a bucket: dynamic LDS = the larger of the two halves, grid = the
+// workgroups resident at once (capped by the launch bounds the slot set was sized for).
+template <typename T>
+int fused_geometry(cf_ctx* ctx, size_t rating_lds, uint32_t grid_cap, uint32_t& grid, size_t& lds) {
+    lds = std::max(rating_lds, basis_lds());
+    CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)pred_fused_kernel<T>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int per_cu = 0, cus = 0;
+    CF_HIP_CHECK(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pred_fused_kernel<T>, kThreads, lds));
+    CF_HIP_CHECK(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    grid = std::min<uint32_t>(grid_cap, (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus));
+    return CF_OK;
+}
+
 }  // namespace
 
 template <typename T>
@@ -1337,12 +1425,23 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
     // Slots for one chunk of the largest LDS bucket, per stream; the chunks of every bucket
     // alternate between two context-owned streams (fork/join by events with the caller's
     // stream) so one chunk's tail overlaps the next.  Diagnostics keep one stream.
+    const bool overlap = !ctx->d_phase;
+    // fused (CF_PRED_FUSED=1): one slot per resident workgroup; the phase diagnostics keep the two kernels
+    const bool fused = overlap && pred_fused_enabled();
+    uint32_t fused_max = 0;
+    if (fused) {
+        int cus = 0;
+        CF_HIP_CHECK(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        fused_max = (uint32_t)std::max(1, cus) * CF_PRED_RATING_OCC;   // launch-bounds residency
+        if (!ctx->d_pred_next)
+            CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_pred_next, 32 * sizeof(uint32_t) * cf_ctx::kAuxStreams));
+    }
+    const uint32_t users_per_launch = fused ? fused_max : kChunk;
     size_t need = 0;
     for (const cf_bucket& b : plan->buckets)
         if (b.count && b.emax != kSpillBucket)
-            need = std::max(need, (size_t)std::min(b.count, kChunk) *
+            need = std::max(need, (size_t)std::min(b.count, users_per_launch) *
                                       slot_layout(std::max<int>(2, 16 * b.emax)).stride * sizeof(double));
-    const bool overlap = !ctx->d_phase;
     const size_t copies = overlap ? cf_ctx::kAuxStreams : 1;
     if (need * copies > ctx->scratch_bytes) {
         if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
@@ -1379,6 +1478,28 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
         size_t rating_lds = 0;
         rc = setup_bucket<T>(ctx, args, std::max<int>(2, 16 * b.emax), rating_lds);
         if (rc != CF_OK) break;
+        if (fused) {   // the whole bucket in one persistent launch, users claimed largest-k first
+            uint32_t grid = 0;
+            size_t lds = 0;
+            rc = fused_geometry<T>(ctx, rating_lds, fused_max, grid, lds);
+            if (rc != CF_OK) break;
+            grid = std::min(grid, b.count);
+            const int si = nb++ % cf_ctx::kAuxStreams;
+            hipStream_t st = ctx->aux_stream[si];
+            args.slots = reinterpret_cast<double*>(static_cast<char*>(ctx->d_scratch) + si * need);
+            if ((size_t)grid * args.so.stride * sizeof(double) > need) {
+                rc = cf_set_error(ctx, CF_EINVAL, "predict scratch undersized");
+                break;
+            }
+            uint32_t* next = ctx->d_pred_next + 32 * si;
+            if (hipMemsetAsync(next, 0, sizeof(uint32_t), st) != hipSuccess) {
+                rc = cf_set_error(ctx, CF_EHIP, "predict counter reset failed");
+                break;
+            }
+            hipLaunchKernelGGL(pred_fused_kernel<T>, dim3(grid), dim3(kThreads), lds, st, args, b.first, b.count, next);
+            if (hipGetLastError() != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, "predict launch failed");
+            continue;
+        }
         for (uint32_t c0 = 0; c0 < b.count && rc == CF_OK; c0 += kChunk) {
             const uint32_t cnt = std::min(kChunk, b.count - c0);
             const int si = overlap ? (nb++ % cf_ctx::kAuxStreams) : 0;

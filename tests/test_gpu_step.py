@@ -78,3 +78,20 @@ def test_pipeline_is_deterministic(gpu_ctx):
         for key in r:
             assert np.array_equal(r[key].view(np.uint8), runs[0][key].view(np.uint8)), key
     plan.close()
+
+
+def test_fused_predictor_equals_two_kernel_path():
+    """pred_fused_kernel (CF_PRED_FUSED=1: basis and ratings of a user in one persistent
+    workgroup, one slot per resident workgroup) writes the same bits as the default chunked
+    two-kernel path: with the switch set, cf_predict_run takes the fused kernel while
+    cf_step_run keeps the two kernels, so test_step_run_equals_sequential compares them
+    bitwise.  The switch is read once per process, hence the child."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, CF_PRED_FUSED="1")
+    p = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-m", "gpu",
+                        f"{os.path.abspath(__file__)}::test_step_run_equals_sequential"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout[-4000:] + p.stderr[-2000:]
+    assert "2 passed" in p.stdout, p.stdout[-2000:]
