@@ -1312,7 +1312,17 @@ __global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_fused_kerne
 // Chunks of up to kChunk users per (basis, rating) launch pair; each user of a chunk owns a
 // slot (SlotOff) holding Gbar, X, Q1 (the basis's second buffer), the packed triangle AP and
 // the per-row arrays, ~1 MB at lmax = 192.
-constexpr uint32_t kChunk = 8192;
+constexpr uint32_t kChunkDefault = 32768;   // C4 predict: 2048 / 4096 / 8192 / 16384 / 32768 users
+                                            // -> 1712 / 1668 / 1658 / 1649 / 1640 ms (profiles/r03/pred_chunk_ab/)
+// CF_PRED_CHUNK overrides the users per launch pair (A/B runs); read once per process.
+inline uint32_t pred_chunk() {
+    static const uint32_t c = [] {
+        const char* e = std::getenv("CF_PRED_CHUNK");
+        const long v = e ? std::atol(e) : 0;
+        return v >= 256 && v <= (1 << 20) ? (uint32_t)v : kChunkDefault;
+    }();
+    return c;
+}
 inline int fast_tri(int n) { return (n + 2) * (n + 3) / 2; }
 inline SlotOff slot_layout(int lmax) {
     SlotOff so{};
@@ -1332,6 +1342,25 @@ inline SlotOff slot_layout(int lmax) {
     so.pmask = (int)o; o += 3 * (size_t)lmax;                 // u64 per cell
     so.stride = (o + 15) & ~(size_t)15;                      // 128-byte aligned slots
     return so;
+}
+// Slot bytes of one launch pair of up to `users` users, over the plan's LDS buckets.
+inline size_t chunk_slot_bytes(const cf_plan* plan, uint32_t users) {
+    size_t need = 0;
+    for (const cf_bucket& b : plan->buckets)
+        if (b.count && b.emax != kSpillBucket)
+            need = std::max(need, (size_t)std::min(b.count, users) *
+                                      slot_layout(std::max<int>(2, 16 * b.emax)).stride * sizeof(double));
+    return need;
+}
+// Users per launch pair: pred_chunk(), halved while its slot copies would take more than a
+// third of the HBM left (the context's own scratch counted as free), down to 2048.
+inline uint32_t fit_chunk(cf_ctx* ctx, const cf_plan* plan, size_t copies) {
+    uint32_t chunk = pred_chunk();
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return std::min<uint32_t>(chunk, 8192);
+    const size_t budget = (free_b + ctx->scratch_bytes) / 3;
+    while (chunk > 2048 && chunk_slot_bytes(plan, chunk) * copies > budget) chunk /= 2;
+    return chunk;
 }
 inline size_t basis_lds() {
     return sizeof(double) * (kStageElems + 4) + CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 3 * sizeof(int)) +
@@ -1436,13 +1465,9 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
         if (!ctx->d_pred_next)
             CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_pred_next, 32 * sizeof(uint32_t) * cf_ctx::kAuxStreams));
     }
-    const uint32_t users_per_launch = fused ? fused_max : kChunk;
-    size_t need = 0;
-    for (const cf_bucket& b : plan->buckets)
-        if (b.count && b.emax != kSpillBucket)
-            need = std::max(need, (size_t)std::min(b.count, users_per_launch) *
-                                      slot_layout(std::max<int>(2, 16 * b.emax)).stride * sizeof(double));
     const size_t copies = overlap ? cf_ctx::kAuxStreams : 1;
+    const uint32_t kChunk = fused ? 0 : fit_chunk(ctx, plan, copies);
+    const size_t need = chunk_slot_bytes(plan, fused ? fused_max : kChunk);
     if (need * copies > ctx->scratch_bytes) {
         if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
         ctx->d_scratch = nullptr;
@@ -1584,11 +1609,8 @@ int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
     args.mse = d_mse;
     args.kk = d_kk;
     args.pred = d_pred;
-    size_t need = 0;
-    for (const cf_bucket& b : plan->buckets)
-        if (b.count && b.emax != kSpillBucket)
-            need = std::max(need, (size_t)std::min(b.count, kChunk) *
-                                      slot_layout(std::max<int>(2, 16 * b.emax)).stride * sizeof(double));
+    const uint32_t kChunk = fit_chunk(ctx, plan, 2);
+    const size_t need = chunk_slot_bytes(plan, kChunk);
     if (need * 2 > ctx->scratch_bytes) {
         if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
         ctx->d_scratch = nullptr;
