@@ -169,6 +169,99 @@ __device__ void tile_gemm(int M, int N, FA ldA, FB ldB, FK kend, FW want, FO out
     __syncthreads();
 }
 
+// C -= A B on the lower triangle of the output (tile_gemm's staging and MFMA layout), with the
+// tile's C values loaded before its K loop so their latency hides behind the products instead
+// of a load-then-store at the end.  cptr(i, j) = the address of C(i, j), used for j <= i only.
+template <bool A_LFAST, bool B_LFAST, class FA, class FB, class FC>
+__device__ void tile_gemm_sub(int M, int N, int K, FA ldA, FB ldB, FC cptr, double* sA, double* sB) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wr = (tid >> 6) >> 1, wc = (tid >> 6) & 1;
+    const int ti = (M + 63) >> 6, tj = (N + 63) >> 6;
+    for (int t = 0; t < ti * tj; ++t) {
+        const int i0 = (t / tj) << 6, j0 = (t % tj) << 6;
+        if (j0 > i0) continue;   // strictly above the diagonal tiles
+        f64x4 acc[2][2];
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
+        double ra[4], rb[4];
+        auto fetch = [&](int l0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int e = tid + q * kT;
+                const int ii = A_LFAST ? (e >> 4) : (e & 63), la = A_LFAST ? (e & 15) : (e >> 6);
+                const int jj = B_LFAST ? (e >> 4) : (e & 63), lb = B_LFAST ? (e & 15) : (e >> 6);
+                ra[q] = ldA(min(i0 + ii, M - 1), min(l0 + la, K - 1));
+                rb[q] = ldB(min(l0 + lb, K - 1), min(j0 + jj, N - 1));
+            }
+        };
+        if (K > 0) fetch(0);
+        double cv[2][2][4];
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int gi = i0 + 32 * wr + 16 * x + (lane >> 4) + 4 * q;
+                    const int gj = j0 + 32 * wc + 16 * y + (lane & 15);
+                    cv[x][y][q] = (gi < M && gj < N && gj <= gi) ? *cptr(gi, gj) : 0.0;
+                }
+        for (int l0 = 0; l0 < K; l0 += 16) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int e = tid + q * kT;
+                const int ii = A_LFAST ? (e >> 4) : (e & 63), la = A_LFAST ? (e & 15) : (e >> 6);
+                const int jj = B_LFAST ? (e >> 4) : (e & 63), lb = B_LFAST ? (e & 15) : (e >> 6);
+                sA[la * kSt + ii] = (i0 + ii < M && l0 + la < K) ? ra[q] : 0.0;
+                sB[lb * kSt + jj] = (j0 + jj < N && l0 + lb < K) ? rb[q] : 0.0;
+            }
+            __syncthreads();
+            if (l0 + 16 < K) fetch(l0 + 16);
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                const int row = (4 * ks + (lane >> 4)) * kSt + (lane & 15);
+                double av[2], bv[2];
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {
+                    av[x] = sA[row + 32 * wr + 16 * x];
+                    bv[x] = sB[row + 32 * wc + 16 * x];
+                }
+#pragma unroll
+                for (int x = 0; x < 2; ++x)
+#pragma unroll
+                    for (int y = 0; y < 2; ++y)
+                        acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
+            }
+            __syncthreads();   // the chunk is consumed before the next one is staged
+        }
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int gi = i0 + 32 * wr + 16 * x + (lane >> 4) + 4 * q;
+                    const int gj = j0 + 32 * wc + 16 * y + (lane & 15);
+                    if (gi < M && gj < N && gj <= gi) *cptr(gi, gj) = cv[x][y][q] - acc[x][y][q];
+                }
+    }
+    __syncthreads();
+}
+
+// Fill the packed lower triangle of n rows, A[tri(ra, cb)] = f(ra, cb): wave w takes rows
+// w, w + kW, ..., its lanes the columns of a row (contiguous in A; no per-element inversion
+// of the triangular index).  Does not synchronise.
+template <class F>
+__device__ void fill_tri_rows(double* A, int n, F f) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int ra = wave; ra < n; ra += kW) {
+        double* Arow = A + tri(ra, 0);
+        for (int cb = lane; cb <= ra; cb += 64) Arow[cb] = f(ra, cb);
+    }
+}
+
 // Block-wide ordered compaction over [0, n): out[] receives the indices with f(i) set,
 // ascending; returns the count.  s_tmp: kW ints.
 template <class F>
@@ -193,25 +286,65 @@ __device__ int compact(int n, F f, int* out, int* s_tmp) {
     return total;
 }
 
-// LDL^T of the packed bordered matrix (as ldlt_bordered) in panels of 64 columns: each
-// panel is factored by ldlt_bordered_range (rank-16 updates inside it), then the columns
-// right of it take one rank-64 update A22 -= L21 D1 L21^T as LDS-tiled products -- the
-// trailing matrix (L2/HBM-resident for large systems) is read and written once per 64
-// columns instead of once per 16.
-__device__ void ldlt_bordered_wide(double* A, int L, int nrows, double* sA, double* sB) {
-    for (int k0 = 0; k0 < L; k0 += 64) {
-        const int k1 = min(L, k0 + 64);
-        ldlt_bordered_range<kT>(A, L, nrows, k0, k1);
-        if (k1 < L)
-            tile_gemm<true, true>(
-                nrows - k1, L - k1,
-                [=](int i, int l) { return A[tri(k1 + i, k0 + l)] * A[tri(k0 + l, k0 + l)]; },
-                [=](int l, int j) { return A[tri(k1 + j, k0 + l)]; }, [=](int) { return k1 - k0; },
-                [](int i0, int j0) { return j0 <= i0; },
-                [=](int i, int j, double v) {
-                    if (j <= i) A[tri(k1 + i, k1 + j)] -= v;
-                },
-                sA, sB);
+// A[i][j] -= sum_{l in [d0, d1)} A[i][l] D_l A[j][l] over rows [c0, nrows), columns [c0, c1)
+// (lower triangle), on the matrix cores: the rank-(d1 - d0) update of factored columns
+// [d0, d1) into the packed lower triangle.
+__device__ void ldlt_rank_update(double* A, int nrows, int d0, int d1, int c0, int c1, double* sA, double* sB) {
+#ifdef CF_SPILL_LDL_NOPRELOAD
+    tile_gemm<true, true>(
+        nrows - c0, c1 - c0, [=](int i, int l) { return A[tri(c0 + i, d0 + l)] * A[tri(d0 + l, d0 + l)]; },
+        [=](int l, int j) { return A[tri(c0 + j, d0 + l)]; }, [=](int) { return d1 - d0; },
+        [](int i0, int j0) { return j0 <= i0; },
+        [=](int i, int j, double v) {
+            if (j <= i) A[tri(c0 + i, c0 + j)] -= v;
+        },
+        sA, sB);
+#else
+    tile_gemm_sub<true, true>(
+        nrows - c0, c1 - c0, d1 - d0, [=](int i, int l) { return A[tri(c0 + i, d0 + l)] * A[tri(d0 + l, d0 + l)]; },
+        [=](int l, int j) { return A[tri(c0 + j, d0 + l)]; }, [=](int i, int j) { return A + tri(c0 + i, c0 + j); },
+        sA, sB);
+#endif
+}
+
+// LDL^T of the packed bordered matrix (as ldlt_bordered) in panels of kWidePanel columns,
+// three levels: inside a panel, 64-column sub-panels; inside those, 16-column blocks factored
+// by ldlt_bordered_range (diagonal block + row solves); every level updates the rest of its
+// enclosing range on the matrix cores (ldlt_rank_update, C tile loaded ahead of the products)
+// -- the trailing matrix (L2/HBM-resident for large systems) is read and written once per
+// kWidePanel columns.  Measured on the C5 sample's 292 spill users, 185k ratings
+// (profiles/r03/spill_ldl_panel/, tools/probe_pspill_c5.py): one level of 64 / 128 / 32
+// columns 6.56 / 6.41 / 7.79 s (at 128 the VALU panel took 42% of the LDL^T cycles); two
+// levels 128 without / with the C preload 5.92 / 5.51 s; 64 / 256 / 512 with it 5.75 / 5.44 /
+// 5.50 s; three levels at 256: 5.27 s.
+// tsplit (diagnostics, thread 0's s_memtime, or null): [0] += panel cycles, [1] += trailing.
+#ifndef CF_SPILL_LDL_PANEL
+#define CF_SPILL_LDL_PANEL 256
+#endif
+constexpr int kWidePanel = CF_SPILL_LDL_PANEL;   // columns per trailing update (a multiple of 64)
+static_assert(kWidePanel % 64 == 0, "panels are whole 64-column sub-panels");
+__device__ void ldlt_bordered_wide(double* A, int L, int nrows, double* sA, double* sB,
+                                   unsigned long long* tsplit = nullptr) {
+    for (int k0 = 0; k0 < L; k0 += kWidePanel) {
+        const int k1 = min(L, k0 + kWidePanel);
+        const unsigned long long t0 = tsplit ? __builtin_amdgcn_s_memtime() : 0ull;
+        for (int p0 = k0; p0 < k1; p0 += 64) {
+            const int p1 = min(k1, p0 + 64);
+#ifndef CF_SPILL_LDL_TWO_LEVEL   // third level: 16-column blocks, the rest of the sub-panel on the matrix cores
+            for (int q0 = p0; q0 < p1; q0 += 16) {
+                const int q1 = min(p1, q0 + 16);
+                ldlt_bordered_range<kT>(A, L, nrows, q0, q1);
+                if (q1 < p1) ldlt_rank_update(A, nrows, q0, q1, q1, p1, sA, sB);
+            }
+#else
+            ldlt_bordered_range<kT>(A, L, nrows, p0, p1);
+#endif
+            if (p1 < k1) ldlt_rank_update(A, nrows, p0, p1, p1, k1, sA, sB);
+        }
+        const unsigned long long t1 = tsplit ? __builtin_amdgcn_s_memtime() : 0ull;
+        if (tsplit && threadIdx.x == 0) tsplit[0] += t1 - t0;
+        if (k1 < L) ldlt_rank_update(A, nrows, k0, k1, k1, L, sA, sB);
+        if (tsplit && threadIdx.x == 0) tsplit[1] += __builtin_amdgcn_s_memtime() - t1;
     }
 }
 
@@ -375,7 +508,7 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
     // {0 sets + mean, 1 column filter, 2 P entries, 3 b and K, 4 Woodbury LDL^T, 5 dense
     // path}, counts {6 Woodbury, 7 dense, 8 sum nc (Woodbury), 9 np > 64,
     // 10 dense by dropped column, 11 dense by pivot}.
-    unsigned long long pc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long pc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // 12, 13: wide LDL^T panel / trailing
     unsigned long long pt = 0;
 #define SP_STAMP(ph)                                                        \
     if (a.phase && tid == 0) {                                              \
@@ -472,24 +605,14 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
                 for (int j = lim; j < Lu; ++j) v = fma(-xa[j], xb[j], v);
                 return v;
             };
-            const int ne = c * (c + 1) / 2;
-            for (int e = tid; e < ne + 2 * c; e += kT) {
-                if (e < ne) {
-                    int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-                    while (ra * (ra + 1) / 2 > e) --ra;
-                    while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
-                    A[e] = pent(s_conn[ra], s_conn[e - ra * (ra + 1) / 2]);
-                } else if (e < ne + c) {
-                    const int j = e - ne;
-                    A[tri(c, j)] = pent(r, s_conn[j]);
-                } else {
-                    const int j = e - ne - c;
-                    A[tri(c + 1, j)] = (double)s_rat[s_conn[j]] - mu;
-                }
+            fill_tri_rows(A, c, [&](int ra, int cb) { return pent(s_conn[ra], s_conn[cb]); });
+            for (int e = tid; e < 2 * c; e += kT) {
+                if (e < c) A[tri(c, e)] = pent(r, s_conn[e]);
+                else A[tri(c + 1, e - c)] = (double)s_rat[s_conn[e - c]] - mu;
             }
             __syncthreads();
             SP_STAMP(2);
-            ldlt_bordered_wide(A, c, c + 2, sA, sB);
+            ldlt_bordered_wide(A, c, c + 2, sA, sB, a.phase ? pc + 12 : nullptr);
             if (wave == 0) {
                 double dot = 0.0;
                 for (int j = lane; j < c; j += 64) dot = fma(A[tri(c, j)] * A[tri(c + 1, j)], A[tri(j, j)], dot);
@@ -521,26 +644,20 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
             const auto rowid = [&](int q) { return q < np - 1 ? s_ncon[q] : r; };
             // E = P_S over rows [Cbar, r] into packed rows 0..nc, (P y)_a into row nc + 1:
             // gathers from P and PG/PH, less the (usually empty) tail of columns [lim, Lu)
-            const int ne = np * (np + 1) / 2;
-            for (int e = tid; e < ne + np; e += kT) {
-                double v;
-                if (e < ne) {
-                    int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-                    while (ra * (ra + 1) / 2 > e) --ra;
-                    while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
-                    const int ia = rowid(ra), ib = rowid(e - ra * (ra + 1) / 2);
-                    v = Pm[(size_t)ia * k + ib];
-                    const double* xa = Q + (size_t)ia * Lu;
-                    const double* xb = Q + (size_t)ib * Lu;
-                    for (int j = lim; j < Lu; ++j) v = fma(-xa[j], xb[j], v);
-                    A[e] = v;
-                } else {
-                    const int ia = rowid(e - ne);
-                    v = pgv[ia] - mu * pgv[k + ia];
-                    const double* xa = Q + (size_t)ia * Lu;
-                    for (int j = lim; j < Lu; ++j) v = fma(-xa[j], gvec[j] - mu * hvec[j], v);
-                    A[tri(np, e - ne)] = v;
-                }
+            fill_tri_rows(A, np, [&](int ra, int cb) {
+                const int ia = rowid(ra), ib = rowid(cb);
+                double v = Pm[(size_t)ia * k + ib];
+                const double* xa = Q + (size_t)ia * Lu;
+                const double* xb = Q + (size_t)ib * Lu;
+                for (int j = lim; j < Lu; ++j) v = fma(-xa[j], xb[j], v);
+                return v;
+            });
+            for (int pa = tid; pa < np; pa += kT) {
+                const int ia = rowid(pa);
+                double v = pgv[ia] - mu * pgv[k + ia];
+                const double* xa = Q + (size_t)ia * Lu;
+                for (int j = lim; j < Lu; ++j) v = fma(-xa[j], gvec[j] - mu * hvec[j], v);
+                A[tri(np, pa)] = v;
             }
             __syncthreads();
             SP_STAMP(2);
@@ -558,15 +675,10 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
             }
             __syncthreads();
             // K = I - P_CbarCbar
-            for (int e = tid; e < nc * (nc + 1) / 2; e += kT) {
-                int ra = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-                while (ra * (ra + 1) / 2 > e) --ra;
-                while ((ra + 1) * (ra + 2) / 2 <= e) ++ra;
-                A[e] = (e == tri(ra, ra) ? 1.0 : 0.0) - A[e];
-            }
+            fill_tri_rows(A, nc, [&](int ra, int cb) { return (cb == ra ? 1.0 : 0.0) - A[tri(ra, cb)]; });
             __syncthreads();
             SP_STAMP(3);
-            ldlt_bordered_wide(A, nc, nc + 2, sA, sB);
+            ldlt_bordered_wide(A, nc, nc + 2, sA, sB, a.phase ? pc + 12 : nullptr);
             if (wave == 0) {
                 double minpiv = 1.0, dot = 0.0;
                 for (int j = lane; j < nc; j += 64) {
@@ -662,7 +774,7 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
         if (a.phase && tid == 0) pc[7] += 1;
     }
     if (a.phase && tid == 0)
-        for (int x = 0; x < 12; ++x) atomicAdd(&a.phase[x], pc[x]);
+        for (int x = 0; x < 14; ++x) atomicAdd(&a.phase[x], pc[x]);
 #undef SP_STAMP
 }
 
