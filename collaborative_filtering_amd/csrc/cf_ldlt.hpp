@@ -27,7 +27,8 @@ constexpr int kNB = 16;   // default LDL^T panel width
 // ldlt_bordered_range factors only the columns [k0, k1) (all rows below them, trailing
 // updates confined to columns < k1): a caller blocking the factorisation in wider panels
 // applies the update of columns >= k1 itself.  ldlt_bordered = the full range.
-template <int kThreads, int NB = kNB>
+// TAG: distinct instantiations for callers compiled to different register budgets
+template <int kThreads, int NB = kNB, int TAG = 0>
 __device__ void ldlt_bordered_range(double* A, int L, int nrows, int k0, int k1) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;

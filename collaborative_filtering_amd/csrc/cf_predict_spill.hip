@@ -79,6 +79,7 @@ struct SpArgs {
     double* fa;              // per workgroup factorisation region
     size_t fa_d;
     unsigned int* counter;   // work-item counter of the predict kernel
+    uint32_t w0, w1;         // predict launch: the chunk's work items [w0, w1)
     unsigned long long* phase;   // diagnostics (cf_debug_phases) or null: see spill_predict_kernel
 };
 
@@ -289,6 +290,8 @@ __device__ int compact(int n, F f, int* out, int* s_tmp) {
 // A[i][j] -= sum_{l in [d0, d1)} A[i][l] D_l A[j][l] over rows [c0, nrows), columns [c0, c1)
 // (lower triangle), on the matrix cores: the rank-(d1 - d0) update of factored columns
 // [d0, d1) into the packed lower triangle.
+// OCC: the calling kernel's occupancy, so each gets its own copy compiled to its register budget
+template <int OCC = 1>
 __device__ void ldlt_rank_update(double* A, int nrows, int d0, int d1, int c0, int c1, double* sA, double* sB) {
 #ifdef CF_SPILL_LDL_NOPRELOAD
     tile_gemm<true, true>(
@@ -323,6 +326,7 @@ __device__ void ldlt_rank_update(double* A, int nrows, int d0, int d1, int c0, i
 #endif
 constexpr int kWidePanel = CF_SPILL_LDL_PANEL;   // columns per trailing update (a multiple of 64)
 static_assert(kWidePanel % 64 == 0, "panels are whole 64-column sub-panels");
+template <int OCC = 1>
 __device__ void ldlt_bordered_wide(double* A, int L, int nrows, double* sA, double* sB,
                                    unsigned long long* tsplit = nullptr) {
     for (int k0 = 0; k0 < L; k0 += kWidePanel) {
@@ -333,17 +337,17 @@ __device__ void ldlt_bordered_wide(double* A, int L, int nrows, double* sA, doub
 #ifndef CF_SPILL_LDL_TWO_LEVEL   // third level: 16-column blocks, the rest of the sub-panel on the matrix cores
             for (int q0 = p0; q0 < p1; q0 += 16) {
                 const int q1 = min(p1, q0 + 16);
-                ldlt_bordered_range<kT>(A, L, nrows, q0, q1);
-                if (q1 < p1) ldlt_rank_update(A, nrows, q0, q1, q1, p1, sA, sB);
+                ldlt_bordered_range<kT, kNB, OCC>(A, L, nrows, q0, q1);
+                if (q1 < p1) ldlt_rank_update<OCC>(A, nrows, q0, q1, q1, p1, sA, sB);
             }
 #else
-            ldlt_bordered_range<kT>(A, L, nrows, p0, p1);
+            ldlt_bordered_range<kT, kNB, OCC>(A, L, nrows, p0, p1);
 #endif
-            if (p1 < k1) ldlt_rank_update(A, nrows, p0, p1, p1, k1, sA, sB);
+            if (p1 < k1) ldlt_rank_update<OCC>(A, nrows, p0, p1, p1, k1, sA, sB);
         }
         const unsigned long long t1 = tsplit ? __builtin_amdgcn_s_memtime() : 0ull;
         if (tsplit && threadIdx.x == 0) tsplit[0] += t1 - t0;
-        if (k1 < L) ldlt_rank_update(A, nrows, k0, k1, k1, L, sA, sB);
+        if (k1 < L) ldlt_rank_update<OCC>(A, nrows, k0, k1, k1, L, sA, sB);
         if (tsplit && threadIdx.x == 0) tsplit[1] += __builtin_amdgcn_s_memtime() - t1;
     }
 }
@@ -489,21 +493,25 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
 }
 
 // ---- per-rating predictions --------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
+// CAP: the largest k the per-row LDS arrays hold; OCC: workgroups per CU.  Users with
+// k <= kSmallCap take <kSmallCap, 2> (67 KB of LDS, 256 registers: two ratings per CU overlap
+// their latency-bound phases), larger ones <CF_SPILL_MAX_K, 1> (116 KB, one per CU).
+constexpr int kSmallCap = 2048;
+template <typename T, int CAP, int OCC>
+__global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
     __shared__ double sA[16 * kSt], sB[16 * kSt];   // GEMM staging
     __shared__ double s_la[kLdsA];
-    __shared__ float s_rat[CF_SPILL_MAX_K];
-    __shared__ int s_conn[CF_SPILL_MAX_K];
-    __shared__ int s_ncon[CF_SPILL_MAX_K];
-    __shared__ int s_keep[CF_SPILL_MAX_K];
+    __shared__ float s_rat[CAP];
+    __shared__ int s_conn[CAP];
+    __shared__ int s_ncon[CAP];
+    __shared__ int s_keep[CAP];
     __shared__ double s_misc[4];
     __shared__ int s_tmp[kW];
     __shared__ unsigned int s_item;
     __shared__ unsigned int s_slot;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     double* fa = a.fa + (size_t)blockIdx.x * a.fa_d;
-    const uint64_t total = a.roff[a.nu];   // one work item per (slot, row)
+    const uint64_t total = a.w1;   // one work item per (slot, row); this launch's are [w0, w1)
     // Diagnostic counters (thread 0, s_memtime; no effect on outputs): cycles of
     // {0 sets + mean, 1 column filter, 2 P entries, 3 b and K, 4 Woodbury LDL^T, 5 dense
     // path}, counts {6 Woodbury, 7 dense, 8 sum nc (Woodbury), 9 np > 64,
@@ -519,7 +527,7 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
     for (;;) {
         if (tid == 0) {
             // claim an item, and find its slot in the chunk's row prefix (binary search)
-            const uint32_t w = atomicAdd(a.counter, 1u);
+            const uint32_t w = a.w0 + atomicAdd(a.counter, 1u);
             uint32_t lo = 0, hi = a.nu;
             if (w < total)
                 while (hi - lo > 1) {
@@ -612,7 +620,7 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
             }
             __syncthreads();
             SP_STAMP(2);
-            ldlt_bordered_wide(A, c, c + 2, sA, sB, a.phase ? pc + 12 : nullptr);
+            ldlt_bordered_wide<OCC>(A, c, c + 2, sA, sB, a.phase ? pc + 12 : nullptr);
             if (wave == 0) {
                 double dot = 0.0;
                 for (int j = lane; j < c; j += 64) dot = fma(A[tri(c, j)] * A[tri(c + 1, j)], A[tri(j, j)], dot);
@@ -678,7 +686,7 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
             fill_tri_rows(A, nc, [&](int ra, int cb) { return (cb == ra ? 1.0 : 0.0) - A[tri(ra, cb)]; });
             __syncthreads();
             SP_STAMP(3);
-            ldlt_bordered_wide(A, nc, nc + 2, sA, sB, a.phase ? pc + 12 : nullptr);
+            ldlt_bordered_wide<OCC>(A, nc, nc + 2, sA, sB, a.phase ? pc + 12 : nullptr);
             if (wave == 0) {
                 double minpiv = 1.0, dot = 0.0;
                 for (int j = lane; j < nc; j += 64) {
@@ -753,7 +761,7 @@ __global__ __launch_bounds__(kT) void spill_predict_kernel(SpArgs<T> a) {
             A[tri(L + 1, j)] = (double)U[(size_t)r * m + cj];
         }
         __syncthreads();
-        ldlt_bordered_wide(A, L, L + 2, sA, sB);
+        ldlt_bordered_wide<OCC>(A, L, L + 2, sA, sB);
         // pred = v^T M^-1 t + mean = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean (:314-327)
         if (wave == 0) {
             double dot = 0.0;
@@ -1021,13 +1029,36 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
         a.soff = d_meta + c.meta;
         a.sioff = a.soff + (c.nu + 1);
         a.roff = a.sioff + (c.nu + 1);
-        const uint64_t items = meta[c.meta + 2 * (c.nu + 1) + c.nu];
-        CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), stream));
+        const uint64_t* roff_h = meta.data() + c.meta + 2 * (c.nu + 1);
+        const uint64_t items = roff_h[c.nu];
+        // users are largest k first: [0, nb) need the full-capacity kernel, [nb, nu) fit the small one
+        const auto k_of = [&](uint32_t i) {
+            const uint32_t u = plan->h_order[b.first + c.u0 + i];
+            return plan->h_item_off[u + 1] - plan->h_item_off[u];
+        };
+        uint32_t nb = 0;
+        while (nb < c.nu && k_of(nb) > (uint64_t)kSmallCap) ++nb;
+        CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, 256, stream));
         hipLaunchKernelGGL(spill_basis_kernel<T>, dim3(a.nu), dim3(kT), 0, stream, a);
         CF_HIP_CHECK(ctx, hipGetLastError());
-        hipLaunchKernelGGL(spill_predict_kernel<T>, dim3((unsigned)std::min<uint64_t>(blocks, items)), dim3(kT), 0,
-                           stream, a);
-        CF_HIP_CHECK(ctx, hipGetLastError());
+        const uint64_t split = roff_h[nb];
+        if (split > 0) {   // heaviest first, one workgroup per CU
+            SpArgs<T> ab = a;
+            ab.w0 = 0;
+            ab.w1 = (uint32_t)split;
+            hipLaunchKernelGGL((spill_predict_kernel<T, CF_SPILL_MAX_K, 1>),
+                               dim3((unsigned)std::min<uint64_t>(blocks, split)), dim3(kT), 0, stream, ab);
+            CF_HIP_CHECK(ctx, hipGetLastError());
+        }
+        if (items > split) {
+            SpArgs<T> as = a;
+            as.counter = a.counter + 32;   // its own zeroed counter (another 128-byte line)
+            as.w0 = (uint32_t)split;
+            as.w1 = (uint32_t)items;
+            hipLaunchKernelGGL((spill_predict_kernel<T, kSmallCap, 2>),
+                               dim3((unsigned)std::min<uint64_t>(blocks, items - split)), dim3(kT), 0, stream, as);
+            CF_HIP_CHECK(ctx, hipGetLastError());
+        }
     }
     return CF_OK;
 }
