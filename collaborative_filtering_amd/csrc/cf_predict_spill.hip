@@ -494,9 +494,9 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
 
 // ---- per-rating predictions --------------------------------------------------------------
 // CAP: the largest k the per-row LDS arrays hold; OCC: workgroups per CU.  Users with
-// k <= kSmallCap take <kSmallCap, 2> (67 KB of LDS, 256 registers: two ratings per CU overlap
+// k <= kSmallCap take <kSmallCap, 2> (81 KB of LDS, 256 registers: two ratings per CU overlap
 // their latency-bound phases), larger ones <CF_SPILL_MAX_K, 1> (116 KB, one per CU).
-constexpr int kSmallCap = 2048;
+constexpr int kSmallCap = 2816;
 template <typename T, int CAP, int OCC>
 __global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
     __shared__ double sA[16 * kSt], sB[16 * kSt];   // GEMM staging
