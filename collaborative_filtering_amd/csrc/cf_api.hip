@@ -4,6 +4,7 @@
 // copy out; *_run entry points take device pointers and an explicit stream.
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -15,6 +16,15 @@
 int cf_set_error(cf_ctx* ctx, int code, const std::string& msg) {
     if (ctx) ctx->last_error = msg;
     return code;
+}
+
+namespace {
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_ctx_per_device[kMaxDevices];
+}  // namespace
+
+int cf_contexts_on_device(int device) {
+    return (device >= 0 && device < kMaxDevices) ? g_ctx_per_device[device].load() : 1;
 }
 
 namespace {
@@ -32,9 +42,6 @@ __global__ void dense_scatter_kernel(uint32_t n_items, const uint64_t* row_ptr, 
         if (c < n_items) row[c] = w[e];
     }
 }
-
-// RAII device buffer used by the host-pointer wrappers.
-
 
 }  // namespace
 
@@ -66,7 +73,7 @@ int cf_create(int device, cf_ctx** out) {
     *out = nullptr;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CF_EHIP;
-    if (device < 0 || device >= n) return CF_EINVAL;
+    if (device < 0 || device >= n || device >= kMaxDevices) return CF_EINVAL;
     cf_ctx* ctx = new (std::nothrow) cf_ctx();
     if (!ctx) return CF_ENOMEM;
     ctx->device = device;
@@ -74,12 +81,14 @@ int cf_create(int device, cf_ctx** out) {
         delete ctx;
         return CF_EHIP;
     }
+    g_ctx_per_device[device].fetch_add(1);
     *out = ctx;
     return CF_OK;
 }
 
 void cf_destroy(cf_ctx* ctx) {
     if (!ctx) return;
+    g_ctx_per_device[ctx->device].fetch_sub(1);
     (void)hipSetDevice(ctx->device);
     if (ctx->d_graph) (void)hipFree(ctx->d_graph);
     if (ctx->d_grp) (void)hipFree(ctx->d_grp);
@@ -452,11 +461,24 @@ int predict_precomp_impl(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off
                                            sig_mode, (float*)dmse.p, (int32_t*)dkk.p, (double*)dpred.p,
                                            (const uint8_t*)dsel.p, nullptr);
         } else {
-            // the fp32 launch takes fp32 evals / sigs: the binary file's values, narrowed back exactly
+            // the fp32 launch takes fp32 evals / sigs: the binary file's values, narrowed back exactly.
+            // A value fp32 cannot hold (fp64 text parsed next to fp32 blocks) would move lim / w_lim
+            // away from the fp64 path's: rejected rather than silently rounded.
             std::vector<float> ev32(n_entries), sg32(sigtab_len);
-            for (uint64_t i = 0; i < n_entries; ++i) ev32[i] = (float)evals[i];
-            for (uint64_t i = 0; i < sigtab_len; ++i) sg32[i] = (float)sigtab[i];
-            rc = dev_alloc(ctx, deval32, sizeof(float) * std::max<uint64_t>(n_entries, 1));
+            const auto exact = [](double x) { return std::isnan(x) || (double)(float)x == x; };
+            for (uint64_t i = 0; i < n_entries && rc == CF_OK; ++i) {
+                ev32[i] = (float)evals[i];
+                if (!exact(evals[i]))
+                    rc = cf_set_error(ctx, CF_EINVAL, "cf_predict_precomp_sel_f32: evals[" + std::to_string(i) +
+                                                          "] is not an fp32 value (use the fp64 entry point)");
+            }
+            for (uint64_t i = 0; i < sigtab_len && rc == CF_OK; ++i) {
+                sg32[i] = (float)sigtab[i];
+                if (!exact(sigtab[i]))
+                    rc = cf_set_error(ctx, CF_EINVAL, "cf_predict_precomp_sel_f32: sigtab[" + std::to_string(i) +
+                                                          "] is not an fp32 value (use the fp64 entry point)");
+            }
+            if (rc == CF_OK) rc = dev_alloc(ctx, deval32, sizeof(float) * std::max<uint64_t>(n_entries, 1));
             if (rc == CF_OK) rc = dev_alloc(ctx, dsig32, sizeof(float) * std::max<uint64_t>(sigtab_len, 1));
             if (rc == CF_OK && n_entries) e = hipMemcpy(deval32.p, ev32.data(), sizeof(float) * n_entries, hipMemcpyHostToDevice);
             if (rc == CF_OK && e == hipSuccess && sigtab_len)

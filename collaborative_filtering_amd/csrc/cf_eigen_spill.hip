@@ -1482,36 +1482,45 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     auto stride_of = [&](const Range& r) {
         return base_stride(r.kmax) + (r.big ? (mc_on ? MC_EXTRA : 3ull * CF_SPILL_MAX_K) : 0ull);
     };
-    // workspace cap: a fifth of the free HBM (>= 24 GB); the BIG range gets up to half of it
-    size_t free_b = 0, total_b = 0;
-    (void)hipMemGetInfo(&free_b, &total_b);
-    const uint64_t budget = std::max<uint64_t>(24ull << 30, (uint64_t)free_b / 5);
+    // workspace cap: a fifth of this context's share of the free HBM (>= 24 GB, but at most half
+    // the share: cf_hbm_budget); the BIG range gets up to half of it.  A failed allocation
+    // halves the cap (fewer slots: the users run in more waves) down to one slot per range.
+    uint64_t budget = cf_hbm_budget(ctx, ctx->spill_bytes, 0.2, 24ull << 30);
     const bool has_big = !rs.empty() && rs.front().big;
     const bool has_rest = rs.size() > (has_big ? 1u : 0u);
     std::vector<uint32_t> grid(rs.size());
     uint64_t big_bytes = 0, rest_bytes = 0;
-    for (size_t i = 0; i < rs.size(); ++i) {
-        const uint64_t slot = stride_of(rs[i]) * sizeof(double);
-        const uint64_t share = rs[i].big ? (has_rest ? budget / 2 : budget) : (has_big ? budget / 2 : budget);
-        // staged BIG users hold one slot each for the whole launch (in waves if the share is short)
-        uint32_t g = std::min<uint32_t>(rs[i].count, rs[i].big && mc_on ? rs[i].count : (uint32_t)n_cu);
-        g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, share / slot));
-        grid[i] = g;
-        if (rs[i].big) big_bytes = (uint64_t)g * slot;
-        else rest_bytes = std::max<uint64_t>(rest_bytes, (uint64_t)g * slot);
-    }
-    const size_t need = 256 + big_bytes + rest_bytes;
-    if (need > ctx->spill_bytes) {
+    for (;;) {
+        big_bytes = rest_bytes = 0;
+        bool minimal = true;
+        for (size_t i = 0; i < rs.size(); ++i) {
+            const uint64_t slot = stride_of(rs[i]) * sizeof(double);
+            const uint64_t share = rs[i].big ? (has_rest ? budget / 2 : budget) : (has_big ? budget / 2 : budget);
+            // staged BIG users hold one slot each for the whole launch (in waves if the share is short)
+            uint32_t g = std::min<uint32_t>(rs[i].count, rs[i].big && mc_on ? rs[i].count : (uint32_t)n_cu);
+            g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, share / slot));
+            grid[i] = g;
+            minimal = minimal && g == 1;
+            if (rs[i].big) big_bytes = (uint64_t)g * slot;
+            else rest_bytes = std::max<uint64_t>(rest_bytes, (uint64_t)g * slot);
+        }
+        const size_t need = 256 + big_bytes + rest_bytes;
+        if (need <= ctx->spill_bytes) break;
         // the previous launches on either stream may still read the old workspace
         CF_HIP_CHECK(ctx, hipStreamSynchronize(stream));
         if (ctx->spill_side) CF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->spill_side));
         if (ctx->d_spill) (void)hipFree(ctx->d_spill);
         ctx->d_spill = nullptr;
         ctx->spill_bytes = 0;
-        if (hipMalloc(&ctx->d_spill, need) != hipSuccess)
-            return cf_set_error(ctx, CF_ENOMEM, "spill workspace (" + std::to_string(need) + " bytes)");
-        ctx->spill_bytes = need;
-        CF_HIP_CHECK(ctx, hipMemsetAsync(ctx->d_spill, 0, 256, stream));
+        if (hipMalloc(&ctx->d_spill, need) == hipSuccess) {
+            ctx->spill_bytes = need;
+            CF_HIP_CHECK(ctx, hipMemsetAsync(ctx->d_spill, 0, 256, stream));
+            break;
+        }
+        (void)hipGetLastError();
+        ctx->d_spill = nullptr;
+        if (minimal) return cf_set_error(ctx, CF_ENOMEM, "spill workspace (" + std::to_string(need) + " bytes)");
+        budget /= 2;
     }
     if (has_big && !ctx->spill_side) {
         CF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->spill_side, hipStreamNonBlocking));

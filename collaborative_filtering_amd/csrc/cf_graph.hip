@@ -165,6 +165,12 @@ int cf_item_graph_upload(cf_ctx* ctx, uint32_t n_items, const uint64_t* row_ptr,
     if (!ctx || !row_ptr || (row_ptr[n_items] > 0 && (!col || !w)))
         return cf_set_error(ctx, CF_EINVAL, "cf_item_graph_upload: null argument");
     CF_TRY(set_device(ctx));
+    // row_ptr must start at 0 and never decrease: every row range below (the dense scatter's,
+    // the CSR sort's idx.resize(e - b) on a worker thread) trusts it
+    if (row_ptr[0] != 0) return cf_set_error(ctx, CF_EINVAL, "cf_item_graph_upload: row_ptr[0] != 0");
+    for (uint32_t r = 0; r < n_items; ++r)
+        if (row_ptr[r + 1] < row_ptr[r])
+            return cf_set_error(ctx, CF_EINVAL, "cf_item_graph_upload: row_ptr decreases at row " + std::to_string(r));
     const uint64_t nnz = row_ptr[n_items];
     for (uint64_t e = 0; e < nnz; ++e)
         if (col[e] >= n_items) return cf_set_error(ctx, CF_EINVAL, "cf_item_graph_upload: column out of range");

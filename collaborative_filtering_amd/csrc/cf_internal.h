@@ -208,6 +208,21 @@ inline int set_device(cf_ctx* ctx) {
     return CF_OK;
 }
 
+// Live contexts per device (cf_create / cf_destroy): contexts sharing a GPU size their
+// workspaces from the same free-HBM figure, so each takes 1/n of it.
+int cf_contexts_on_device(int device);
+
+// Workspace budget of one context: `frac` of (free HBM + the bytes the caller's own buffer
+// already holds) / (contexts on the device), at least `floor` bytes but never more than half
+// of that share -- a floor above the share would only turn into CF_ENOMEM.
+inline size_t cf_hbm_budget(const cf_ctx* ctx, size_t own_bytes, double frac, size_t floor) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+    const size_t share = (free_b + own_bytes) / (size_t)std::max(1, cf_contexts_on_device(ctx->device));
+    const size_t b = (size_t)((double)share * frac);
+    return std::max(b, std::min(floor, share / 2));
+}
+
 #define CF_TRY(expr)              \
     do {                          \
         int _rc = (expr);         \

@@ -1356,11 +1356,28 @@ inline size_t chunk_slot_bytes(const cf_plan* plan, uint32_t users) {
 // third of the HBM left (the context's own scratch counted as free), down to 2048.
 inline uint32_t fit_chunk(cf_ctx* ctx, const cf_plan* plan, size_t copies) {
     uint32_t chunk = pred_chunk();
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return std::min<uint32_t>(chunk, 8192);
-    const size_t budget = (free_b + ctx->scratch_bytes) / 3;
+    const size_t budget = cf_hbm_budget(ctx, ctx->scratch_bytes, 1.0 / 3.0, 0);   // this context's share
     while (chunk > 2048 && chunk_slot_bytes(plan, chunk) * copies > budget) chunk /= 2;
     return chunk;
+}
+// Grow the context's slot scratch to `copies` chunks of `chunk` users; if the allocation fails
+// (the HBM left is smaller than fit_chunk's estimate) the chunk halves, down to 256 users.
+inline int ensure_slot_scratch(cf_ctx* ctx, const cf_plan* plan, size_t copies, uint32_t& chunk) {
+    for (;;) {
+        const size_t need = chunk_slot_bytes(plan, chunk) * copies;
+        if (need <= ctx->scratch_bytes) return CF_OK;
+        if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+        ctx->d_scratch = nullptr;
+        ctx->scratch_bytes = 0;
+        if (hipMalloc(&ctx->d_scratch, need) == hipSuccess) {
+            ctx->scratch_bytes = need;
+            return CF_OK;
+        }
+        (void)hipGetLastError();
+        ctx->d_scratch = nullptr;
+        if (chunk <= 256) return cf_set_error(ctx, CF_ENOMEM, "predictor slots (" + std::to_string(need) + " bytes)");
+        chunk /= 2;
+    }
 }
 inline size_t basis_lds() {
     return sizeof(double) * (kStageElems + 4) + CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 3 * sizeof(int)) +
@@ -1466,15 +1483,12 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
             CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_pred_next, 32 * sizeof(uint32_t) * cf_ctx::kAuxStreams));
     }
     const size_t copies = overlap ? cf_ctx::kAuxStreams : 1;
-    const uint32_t kChunk = fused ? 0 : fit_chunk(ctx, plan, copies);
-    const size_t need = chunk_slot_bytes(plan, fused ? fused_max : kChunk);
-    if (need * copies > ctx->scratch_bytes) {
-        if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
-        ctx->d_scratch = nullptr;
-        ctx->scratch_bytes = 0;
-        CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_scratch, need * copies));
-        ctx->scratch_bytes = need * copies;
-    }
+    uint32_t kChunk = fused ? fused_max : fit_chunk(ctx, plan, copies);
+    CF_TRY(ensure_slot_scratch(ctx, plan, copies, kChunk));
+    if (fused && kChunk != fused_max)   // one slot per resident workgroup is not negotiable
+        return cf_set_error(ctx, CF_ENOMEM, "fused predictor slots");
+    const size_t need = chunk_slot_bytes(plan, kChunk);   // one copy
+    if (fused) kChunk = 0;
     if (overlap) {
         if (!ctx->aux_stream[0]) {
             for (int i = 0; i < cf_ctx::kAuxStreams; ++i) {
@@ -1609,15 +1623,9 @@ int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
     args.mse = d_mse;
     args.kk = d_kk;
     args.pred = d_pred;
-    const uint32_t kChunk = fit_chunk(ctx, plan, 2);
-    const size_t need = chunk_slot_bytes(plan, kChunk);
-    if (need * 2 > ctx->scratch_bytes) {
-        if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
-        ctx->d_scratch = nullptr;
-        ctx->scratch_bytes = 0;
-        CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_scratch, need * 2));
-        ctx->scratch_bytes = need * 2;
-    }
+    uint32_t kChunk = fit_chunk(ctx, plan, 2);
+    CF_TRY(ensure_slot_scratch(ctx, plan, 2, kChunk));
+    const size_t need = chunk_slot_bytes(plan, kChunk);   // one copy
     // fork every stream from the caller's
     CF_HIP_CHECK(ctx, hipEventRecord(ctx->step_time_ev[0], stream));
     CF_HIP_CHECK(ctx, hipEventRecord(ctx->aux_event[cf_ctx::kAuxStreams], stream));

@@ -35,6 +35,7 @@
 //
 // Output per rating (row r of user u, entry base + r): mse = (float)(r - clamp(pred))^2,
 // kk = |C|, pred (:318-359).
+#include <algorithm>
 #include <cstring>
 
 #include "cf_internal.h"
@@ -946,16 +947,14 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
     // ints.  Every user's slot is sized by its OWN k (4 k^2 + 4 k doubles, 2 k + 4 ints): a
     // config-5 bucket spans k = 193 .. 5000, and kmax-sized slots would hold ~100x fewer users.
     a.fa_d = (size_t)(kmax + 2) * (kmax + 3) / 2;
-    size_t free_b = 0, total_b = 0;
-    CF_HIP_CHECK(ctx, hipMemGetInfo(&free_b, &total_b));
-    const size_t avail = free_b + ctx->pspill_bytes;
-    // slots: as many users per chunk as a third of the free HBM holds (288 GB per GPU: all of
-    // a config-5 shard's spill users at once, so the basis launch fills the chip), >= 8 GB;
-    // factorisation regions: a tenth of it (>= 4 GB), 32 .. 512 persistent workgroups
-    const size_t kSlotBudget = std::max<size_t>((size_t)8 << 30, avail / 3);
-    const size_t kFaBudget = std::max<size_t>((size_t)4 << 30, avail / 10);
-    const int blocks = (int)std::max<size_t>(32, std::min<size_t>(512, kFaBudget / (a.fa_d * 8)));
-    const size_t fa_bytes = (size_t)blocks * a.fa_d * sizeof(double);
+    // slots: as many users per chunk as a third of this context's share of the free HBM holds
+    // (288 GB per GPU: all of a config-5 shard's spill users at once, so the basis launch fills
+    // the chip), >= 8 GB; factorisation regions: a tenth of it (>= 4 GB), 32 .. 512 persistent
+    // workgroups.  The floors never exceed half the share (cf_hbm_budget); if the allocation
+    // still fails (another process or context took the memory meanwhile) both budgets halve
+    // and the chunks are planned again.
+    size_t kSlotBudget = cf_hbm_budget(ctx, ctx->pspill_bytes, 1.0 / 3.0, (size_t)8 << 30);
+    size_t kFaBudget = cf_hbm_budget(ctx, ctx->pspill_bytes, 0.1, (size_t)4 << 30);
     // chunks over the bucket's users (plan order: largest k first), each within the budget
     struct Chunk {
         uint32_t u0, nu;
@@ -963,44 +962,60 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
     };
     std::vector<Chunk> chunks;
     std::vector<uint64_t> meta;
-    size_t ws_max = 0, wsi_max = 0;
-    for (uint32_t u0 = 0; u0 < b.count;) {
-        Chunk c{u0, 0, meta.size()};
-        uint64_t sd = 0, si = 0, rows = 0;
-        std::vector<uint64_t> t_sd{0}, t_si{0}, t_r{0};
-        while (u0 + c.nu < b.count) {
-            const uint32_t u = plan->h_order[b.first + u0 + c.nu];
-            const uint64_t k = plan->h_item_off[u + 1] - plan->h_item_off[u];
-            const uint64_t d = 4 * k * k + 4 * k;
-            if (c.nu > 0 && (sd + d) * sizeof(double) > kSlotBudget) break;
-            sd += d;
-            si += 2 * k + 4;
-            rows += k;
-            t_sd.push_back(sd);
-            t_si.push_back(si);
-            t_r.push_back(rows);
-            ++c.nu;
+    int blocks = 0;
+    size_t fa_bytes = 0, meta_bytes = 0, ws_bytes = 0;
+    for (;;) {
+        blocks = (int)std::max<size_t>(32, std::min<size_t>(512, kFaBudget / (a.fa_d * 8)));
+        fa_bytes = (size_t)blocks * a.fa_d * sizeof(double);
+        chunks.clear();
+        meta.clear();
+        size_t ws_max = 0, wsi_max = 0;
+        for (uint32_t u0 = 0; u0 < b.count;) {
+            Chunk c{u0, 0, meta.size()};
+            uint64_t sd = 0, si = 0, rows = 0;
+            std::vector<uint64_t> t_sd{0}, t_si{0}, t_r{0};
+            while (u0 + c.nu < b.count) {
+                const uint32_t u = plan->h_order[b.first + u0 + c.nu];
+                const uint64_t k = plan->h_item_off[u + 1] - plan->h_item_off[u];
+                const uint64_t d = 4 * k * k + 4 * k;
+                if (c.nu > 0 && (sd + d) * sizeof(double) > kSlotBudget) break;
+                sd += d;
+                si += 2 * k + 4;
+                rows += k;
+                t_sd.push_back(sd);
+                t_si.push_back(si);
+                t_r.push_back(rows);
+                ++c.nu;
+            }
+            meta.insert(meta.end(), t_sd.begin(), t_sd.end());
+            meta.insert(meta.end(), t_si.begin(), t_si.end());
+            meta.insert(meta.end(), t_r.begin(), t_r.end());
+            ws_max = std::max(ws_max, (size_t)sd);
+            wsi_max = std::max(wsi_max, (size_t)si);
+            chunks.push_back(c);
+            u0 += c.nu;
         }
-        meta.insert(meta.end(), t_sd.begin(), t_sd.end());
-        meta.insert(meta.end(), t_si.begin(), t_si.end());
-        meta.insert(meta.end(), t_r.begin(), t_r.end());
-        ws_max = std::max(ws_max, (size_t)sd);
-        wsi_max = std::max(wsi_max, (size_t)si);
-        chunks.push_back(c);
-        u0 += c.nu;
-    }
-    const size_t meta_bytes = ((meta.size() * sizeof(uint64_t) + 255) / 256) * 256;
-    const size_t ws_bytes = ws_max * sizeof(double);
-    const size_t need = 256 + meta_bytes + fa_bytes + ws_bytes + wsi_max * sizeof(int);
-    if (need > ctx->pspill_bytes) {
+        meta_bytes = ((meta.size() * sizeof(uint64_t) + 255) / 256) * 256;
+        ws_bytes = ws_max * sizeof(double);
+        const size_t need = 256 + meta_bytes + fa_bytes + ws_bytes + wsi_max * sizeof(int);
+        if (need <= ctx->pspill_bytes) break;
         if (ctx->d_pspill) {
             CF_HIP_CHECK(ctx, hipStreamSynchronize(stream));   // earlier launches may still read it
             (void)hipFree(ctx->d_pspill);
         }
         ctx->d_pspill = nullptr;
         ctx->pspill_bytes = 0;
-        CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_pspill, need));
-        ctx->pspill_bytes = need;
+        if (hipMalloc(&ctx->d_pspill, need) == hipSuccess) {
+            ctx->pspill_bytes = need;
+            break;
+        }
+        (void)hipGetLastError();
+        ctx->d_pspill = nullptr;
+        // one user per chunk and the fewest regions is the smallest plan there is
+        if (blocks == 32 && std::all_of(chunks.begin(), chunks.end(), [](const Chunk& c) { return c.nu == 1; }))
+            return cf_set_error(ctx, CF_ENOMEM, "spill predictor workspace (" + std::to_string(need) + " bytes)");
+        kSlotBudget /= 2;
+        kFaBudget /= 2;
     }
     char* p = reinterpret_cast<char*>(ctx->d_pspill);
     a.counter = reinterpret_cast<unsigned int*>(p);

@@ -47,9 +47,15 @@ int main(int argc, char** argv) {
     std::vector<float> ew;
     uint64_t n_edges = 0;
     cf_ctx* ctx = cfcli::open_device();
+    // Capacity: every w > 0.01 pair has cnt > 5 co-raters, so it is a co-rated pair and
+    // out_edg_ (written by knn from the same ratings) lists it -- one call computes knn2.
+    // Files from different runs can break that bound: the call then reports the size it
+    // needs (CF_ERANGE) and runs once more.
+    ecol.resize(edges.size());
+    ew.resize(edges.size());
     int rc = cf_item_cosine_edges(ctx, users.size(), n, off.data(), it.data(), r.data(), 0.01f, 5, 0, eoff.data(),
-                                  nullptr, nullptr, 0, &n_edges);
-    if (rc == CF_ERANGE && n_edges > 0) {   // sized by the first call
+                                  ecol.data(), ew.data(), ecol.size(), &n_edges);
+    if (rc == CF_ERANGE && n_edges > ecol.size()) {
         ecol.resize(n_edges);
         ew.resize(n_edges);
         rc = cf_item_cosine_edges(ctx, users.size(), n, off.data(), it.data(), r.data(), 0.01f, 5, 0, eoff.data(),
