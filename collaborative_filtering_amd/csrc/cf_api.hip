@@ -185,6 +185,14 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps) {
     return CF_OK;
 }
 
+int cf_set_eigen_refine(cf_ctx* ctx, int enable, float stop_rel, float delta) {
+    if (!ctx || !(stop_rel > 0.0f) || !(delta >= 0.0f)) return cf_set_error(ctx, CF_EINVAL, "bad refine options");
+    ctx->eigen_refine = enable != 0;
+    ctx->stop_rel = stop_rel;
+    ctx->refine_delta = delta;
+    return CF_OK;
+}
+
 // cf_item_graph_upload / cf_item_graph_upload_dense: cf_graph.hip (dense or CSR layout).
 
 const float* cf_item_graph_device(const cf_ctx* ctx, uint32_t* n_items) {

@@ -42,6 +42,7 @@ constexpr int kGroup = 8;   // lanes per column pair (half a DPP row)
 constexpr float kSigRot2 = CF_EIGEN_SIGROT2;
 
 using f2 = __attribute__((ext_vector_type(2))) float;
+using f4 = __attribute__((ext_vector_type(4))) float;
 // A column read as volatile 8-byte loads: plain loads 64 B apart get fused into
 // ds_read2_b64, which the LDS serves at half the rate of two ds_read_b64 (128 vs 256 B/clk;
 // MI355X_MICROARCH.md, LDS table).  Volatile accesses are never fused.
@@ -95,6 +96,11 @@ struct EigenArgs {
     float* evecs;
     float tol_scale;
     int max_sweeps;
+    // kUser: stop after a sweep with no rotation above stop_rel * sqrt(al be), then one
+    // first-order Gram refinement (section 4b) when refine != 0; else the kSigRot * tol rule
+    int refine;
+    float stop_rel;
+    float refine_delta;
     unsigned long long* stats;
     // kLocal / kSigma
     float* l2;                  // per movie n x n row-major L2 (kLocal writes, kSigma reads)
@@ -140,6 +146,9 @@ struct EigenGeom {
     // == 16 mod 64 where it fits in LDS; the full k <= 192 bucket falls back to NR + 8
     static constexpr int LD = (NC * LD16 + 9 * NR <= 40960 - 4) ? LD16 : NR + 8;
     static constexpr int NT = (NR > 128) ? 1024 : 512;         // 1 pass per step up to NT/8 pairs
+    // waves per SIMD the sweeps fit in (their register peak): held for the whole kernel, so
+    // the refinement's code cannot push a bucket below it (bucket 5: 6 waves = 3 blocks per CU)
+    static constexpr int WPE = EMAX <= 5 ? 6 : 4;   // 3 or 2 blocks of 512 per CU, or 1 of 1024
 
     static constexpr size_t bytes() {
         return sizeof(float) * (size_t)NC * LD     // B
@@ -153,7 +162,7 @@ static_assert(EigenGeom<12, true>::LD % 64 == 16, "narrow bucket-12 layout must 
 static_assert(EigenGeom<12, true>::bytes() <= 163840, "narrow bucket-12 layout exceeds 160 KiB LDS");
 
 template <int EMAX, bool NARROW = false>
-__global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT)) void eigen_kernel(EigenArgs a) {
+__global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NARROW>::WPE)) void eigen_kernel(EigenArgs a) {
     using G = EigenGeom<EMAX, NARROW>;
     constexpr int NR = G::NR;
     constexpr int LD = G::LD;
@@ -301,6 +310,12 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT)) void eigen_kernel(Ei
     const int lig = tid % kGroup;
     const float tol = a.tol_scale * sqrtf((float)k) * 2.384185791015625e-07f;  // sqrt(k) * 2^-22
     const float tol2 = tol * tol;
+    const bool refine = mode == kUser && a.refine && k > 1;
+    // a sweep asks for another one while it made a rotation above this (relative, squared)
+    const float stop2 = refine ? a.stop_rel * a.stop_rel : kSigRot2 * tol2;
+    // close pairs, |mu_q - mu_p| <~ delta: (be - al)^2 <= 2 delta^2 (al + be) (al, be ~ mu^2)
+    const float close2 = refine ? kSigRot2 * tol2 : stop2;
+    const float dclose2 = refine ? 2.0f * a.refine_delta * a.refine_delta : -1.0f;
     // Squared column norms ||b_j||^2 (s_l2d is dead once B is assembled).  A step then
     // needs only the cross product ga = b_p . b_q: the rotated norms follow exactly from
     // (al, be, ga, c, s).  They are recomputed from the columns at every sweep start, and
@@ -403,7 +418,11 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT)) void eigen_kernel(Ei
                             // smaller ones of a sweep leave every pair within tol (their effect
                             // on other pairs is second order) -- the tail sweeps otherwise chase
                             // fp32 rounding noise at the tolerance
-                            if (ga * ga > kSigRot2 * tol2 * (al * be)) s_flag[0] = 1;
+                            // with the refinement: pairs closer than refine_delta in mu, which it
+                            // leaves alone, still converge to kSigRot * tol
+                            const float g2 = ga * ga, ab = al * be, dab = be - al;
+                            if (g2 > stop2 * ab || (g2 > close2 * ab && dab * dab <= dclose2 * (al + be)))
+                                s_flag[0] = 1;
                         }
                         devp = ndp;
                         al = nal;
@@ -439,6 +458,130 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT)) void eigen_kernel(Ei
         atomicAdd(&a.stats[1], 1ull);
         atomicMax(&a.stats[2], (unsigned long long)(sweep + 1));
         if (sweep >= a.max_sweeps) atomicAdd(&a.stats[3], 1ull);
+    }
+
+    // ---- 4b. first-order Gram refinement (kUser) ---------------------------------------
+    // The sweeps stop once no pair rotates by more than stop_rel; what is left is corrected
+    // in one step on the matrix cores.  With B = (A + I) V (V's columns orthogonal, norms
+    // sqrt(1 + dev)), F = B^T B and mu_j = ||b_j|| / sqrt(1 + dev_j), the eigenvectors are
+    // b_j - sum_i b_i K_ij to first order, K_ij = F_ij / (mu_i^2 - mu_j^2) (antisymmetric).
+    // Pairs closer than refine_delta in mu are left to the sweeps (first order breaks down
+    // there, and a pair inside one eigenvalue cluster changes nothing the predictor reads).
+    // V's columns pick up sum_i K_ij^2 of squared norm: dev_j carries it, so the eigenvalues
+    // keep their drift-free form.  Wave J owns column tile J: it forms F(:, J) on
+    // v_mfma_f32_16x16x4_f32 (exact fp32 FMA chains) -- whose accumulator layout is the B
+    // operand layout of the update -- turns it into K(:, J) in registers, and computes
+    // B(:, J) - B K(:, J) for every row tile; the new columns are stored once every wave has
+    // read B.  (no projector escape at the 1e-2 clustering gap, one sweep fewer.)
+    if (refine) {
+        for (int c = g; c < k; c += NG) {   // fresh squared norms and mu^2
+            const f2* bc = reinterpret_cast<const f2*>(B + c * LD);
+            f2 acc = {0.f, 0.f};
+#pragma unroll
+            for (int e = 0; e < E2; ++e) {
+                const f2 x = lds_ld(bc + kGroup * e + lig);
+                acc = __builtin_elementwise_fma(x, x, acc);
+            }
+            const float nc = pair_sum(acc.x + acc.y);
+            if (lig == 0) s_mu[c] = nc / (1.0f + s_dev[c]);
+        }
+        __syncthreads();
+        const int nb = (k + 15) >> 4;
+        const int m16 = lane & 15, kq = lane >> 4;
+        const int j = wave * 16 + m16;   // this lane's column (wave < nb)
+        const bool jv = wave < nb && j < k;
+        constexpr int HB = (EMAX + 1) / 2;   // row tiles per half
+        f4 kv[EMAX];                         // F(:, j), then -K(:, j): the update's B operands
+#pragma unroll
+        for (int I = 0; I < EMAX; ++I) kv[I] = f4{0.f, 0.f, 0.f, 0.f};
+        if (wave < nb) {
+            // F(16 I + 4 kq + r, j) for every row tile I: rows 16 c + 4 kq + {0..3} are the
+            // k-slots of four MFMAs (the same rows on both operands)
+            const f4* pj = reinterpret_cast<const f4*>(B + (jv ? j : 0) * LD + 4 * kq);
+            for (int c = 0; c < nb; ++c) {
+                const f4 y = jv ? pj[4 * c] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int I0 = 0; I0 < EMAX; I0 += 4) {   // four independent accumulators per group
+                    f4 x[4];
+#pragma unroll
+                    for (int g4 = 0; g4 < 4; ++g4) {
+                        const int ci = (I0 + g4) * 16 + m16;
+                        x[g4] = (I0 + g4 < nb && ci < k) ? reinterpret_cast<const f4*>(B + ci * LD + 4 * kq)[4 * c]
+                                                         : f4{0.f, 0.f, 0.f, 0.f};
+                    }
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+#pragma unroll
+                        for (int g4 = 0; g4 < 4; ++g4)
+                            if (I0 + g4 < EMAX && I0 + g4 < nb)
+                                kv[I0 + g4] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[g4][t], y[t], kv[I0 + g4], 0, 0, 0);
+                }
+            }
+            // K(i, j) = F(i, j) / (mu_i^2 - mu_j^2) for i != j, |mu_i - mu_j| > delta; 0 else
+            const float muj2 = jv ? s_mu[j] : 1.0f;
+            const float muj = sqrtf(muj2);
+            const float dlt = a.refine_delta;
+            float ksq = 0.0f;
+#pragma unroll
+            for (int I = 0; I < EMAX; ++I)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = I * 16 + 4 * kq + r;
+                    float kvv = 0.0f;
+                    if (I < nb && jv && i < k && i != j) {
+                        const float mui2 = s_mu[i];
+                        if (fabsf(sqrtf(mui2) - muj) > dlt) kvv = kv[I][r] / (mui2 - muj2);
+                    }
+                    kv[I][r] = -kvv;
+                    ksq = fmaf(kvv, kvv, ksq);
+                }
+            // sum_i K_ij^2 over the four kq quarters (lanes m16 + 16 q): V's column norm growth
+            ksq += __shfl_xor(ksq, 16);
+            ksq += __shfl_xor(ksq, 32);
+            if (kq == 0 && jv) s_dev[j] += ksq;
+        }
+        // out(R) = B(R, j) + sum_i B(R, i) (-K(i, j)), A operand B(16 R + m16, 16 I + 4 kq + t),
+        // in two halves of row tiles: a half's rows are stored after every wave has read them
+        // (barrier), and the next half reads only its own rows
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            f4 out[HB];
+            if (wave < nb) {
+                // HB independent accumulator chains: row tile R = h * HB + q
+#pragma unroll
+                for (int q = 0; q < HB; ++q) {
+                    const int R = h * HB + q;
+                    out[q] = (jv && R < nb) ? *reinterpret_cast<const f4*>(B + j * LD + R * 16 + 4 * kq)
+                                            : f4{0.f, 0.f, 0.f, 0.f};
+                }
+#pragma unroll
+                for (int I = 0; I < EMAX; ++I) {
+                    if (I < nb) {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const int c = I * 16 + 4 * kq + t;
+                            const float* bc = B + c * LD + h * HB * 16 + m16;
+#pragma unroll
+                            for (int q = 0; q < HB; ++q) {
+                                if (h * HB + q < nb) {
+                                    const float av = c < k ? bc[q * 16] : 0.0f;
+                                    out[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, kv[I][t], out[q], 0, 0, 0);
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            __syncthreads();   // every wave has read these rows
+            if (jv) {
+#pragma unroll
+                for (int q = 0; q < HB; ++q) {
+                    const int R = h * HB + q;
+                    if (R < nb) *reinterpret_cast<f4*>(B + j * LD + R * 16 + 4 * kq) = out[q];
+                }
+            }
+        }
+        __syncthreads();
     }
 
     // ---- 5. eigenvalues, ordering, lim, output ----------------------------------------
@@ -749,6 +892,9 @@ int cf_launch_eigen_flagged(cf_ctx* ctx, const cf_plan* plan, int emax, uint32_t
     args.evecs = d_evecs;
     args.tol_scale = ctx->tol_scale;
     args.max_sweeps = ctx->max_sweeps;
+    args.refine = ctx->eigen_refine;
+    args.stop_rel = ctx->stop_rel;
+    args.refine_delta = ctx->refine_delta;
     args.only_flag = flag;
     // units are sorted largest k first within a bucket, so the range's first unit has its kmax
     const uint32_t u0 = plan->h_order[first];
@@ -781,6 +927,9 @@ int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off
     args.evecs = d_evecs;
     args.tol_scale = ctx->tol_scale;
     args.max_sweeps = ctx->max_sweeps;
+    args.refine = ctx->eigen_refine;
+    args.stop_rel = ctx->stop_rel;
+    args.refine_delta = ctx->refine_delta;
     args.stats = ctx->d_stats;
     return launch_all_buckets(ctx, plan, args, stream);
 }

@@ -68,6 +68,12 @@ const char* cf_last_error(const cf_ctx* ctx);
 int cf_set_eigen_method(cf_ctx* ctx, int method);
 /* Jacobi off-diagonal tolerance scale (default 1.0) and sweep cap (default 30). */
 int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
+/* compute_eigens (precompute_local_threads.cpp:164-166) on the LDS Jacobi path: sweeps until
+ * one rotates no pair by more than stop_rel (relative off-diagonal |b_p.b_q| / |b_p||b_q|),
+ * then one first-order Gram refinement on the matrix cores for every pair whose eigenvalues
+ * are more than delta apart.  Defaults: enable 1, stop_rel 3e-4, delta 5e-3.
+ * enable 0 restores the sweeps-only rule (stop after a sweep with no rotation above 16 tol). */
+int cf_set_eigen_refine(cf_ctx* ctx, int enable, float stop_rel, float delta);
 /* Diagnostics: enable != 0 allocates device counters that the eigen kernel fills;
  * out8 (optional) receives and resets {sum of sweeps, users, max sweeps, users that
  * hit the sweep cap, assembly cycles, Jacobi cycles, epilogue cycles, tournament
