@@ -92,7 +92,7 @@ class Context:
     def set_jacobi(self, tol_scale: float = 1.0, max_sweeps: int = 30):
         self._chk(self.lib.cf_set_jacobi(self.h, tol_scale, max_sweeps), "cf_set_jacobi")
 
-    def set_eigen_refine(self, enable: bool = True, stop_rel: float = 3e-4, delta: float = 5e-3):
+    def set_eigen_refine(self, enable: bool = True, stop_rel: float = 1e-3, delta: float = 1e-2):
         """Jacobi sweeps to stop_rel, then the first-order Gram refinement (cf_set_eigen_refine)."""
         self._chk(self.lib.cf_set_eigen_refine(self.h, int(enable), stop_rel, delta), "cf_set_eigen_refine")
 

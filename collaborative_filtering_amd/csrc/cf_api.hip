@@ -77,6 +77,8 @@ int cf_create(int device, cf_ctx** out) {
     cf_ctx* ctx = new (std::nothrow) cf_ctx();
     if (!ctx) return CF_ENOMEM;
     ctx->device = device;
+    if (const char* e = getenv("CF_EIGEN_REFINE")) ctx->eigen_refine = e[0] != '0';   // A/B switches
+    if (const char* e = getenv("CF_EIGEN_CLOSE")) ctx->close_sigrot = (float)atof(e);
     if (hipSetDevice(device) != hipSuccess) {
         delete ctx;
         return CF_EHIP;

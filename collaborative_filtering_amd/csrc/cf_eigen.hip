@@ -101,6 +101,7 @@ struct EigenArgs {
     int refine;
     float stop_rel;
     float refine_delta;
+    float close_sigrot;   // close pairs converge to close_sigrot * tol
     unsigned long long* stats;
     // kLocal / kSigma
     float* l2;                  // per movie n x n row-major L2 (kLocal writes, kSigma reads)
@@ -314,7 +315,7 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
     // a sweep asks for another one while it made a rotation above this (relative, squared)
     const float stop2 = refine ? a.stop_rel * a.stop_rel : kSigRot2 * tol2;
     // close pairs, |mu_q - mu_p| <~ delta: (be - al)^2 <= 2 delta^2 (al + be) (al, be ~ mu^2)
-    const float close2 = refine ? kSigRot2 * tol2 : stop2;
+    const float close2 = refine ? a.close_sigrot * a.close_sigrot * tol2 : stop2;
     const float dclose2 = refine ? 2.0f * a.refine_delta * a.refine_delta : -1.0f;
     // Squared column norms ||b_j||^2 (s_l2d is dead once B is assembled).  A step then
     // needs only the cross product ga = b_p . b_q: the rotated norms follow exactly from
@@ -895,6 +896,7 @@ int cf_launch_eigen_flagged(cf_ctx* ctx, const cf_plan* plan, int emax, uint32_t
     args.refine = ctx->eigen_refine;
     args.stop_rel = ctx->stop_rel;
     args.refine_delta = ctx->refine_delta;
+    args.close_sigrot = ctx->close_sigrot;
     args.only_flag = flag;
     // units are sorted largest k first within a bucket, so the range's first unit has its kmax
     const uint32_t u0 = plan->h_order[first];
@@ -930,6 +932,7 @@ int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off
     args.refine = ctx->eigen_refine;
     args.stop_rel = ctx->stop_rel;
     args.refine_delta = ctx->refine_delta;
+    args.close_sigrot = ctx->close_sigrot;
     args.stats = ctx->d_stats;
     return launch_all_buckets(ctx, plan, args, stream);
 }

@@ -62,8 +62,9 @@ struct cf_ctx {
     // compute_eigens: Jacobi sweeps to stop_rel, then the first-order Gram refinement
     // (cf_set_eigen_refine; refine = 0 keeps the r03 rule: sweeps to 16 * tol)
     int eigen_refine = 1;
-    float stop_rel = 3e-4f;
-    float refine_delta = 5e-3f;
+    float stop_rel = 1e-3f;
+    float refine_delta = 1e-2f;
+    float close_sigrot = 8.0f;    // pairs closer than refine_delta: sweeps to close_sigrot * tol
     // Optional device counters: [0] sum of sweeps, [1] users, [2] max sweeps, [3] capped users.
     unsigned long long* d_stats = nullptr;
     // Optional predictor phase-cycle counters (16 slots), see cf_debug_phases.

@@ -71,7 +71,7 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
 /* compute_eigens (precompute_local_threads.cpp:164-166) on the LDS Jacobi path: sweeps until
  * one rotates no pair by more than stop_rel (relative off-diagonal |b_p.b_q| / |b_p||b_q|),
  * then one first-order Gram refinement on the matrix cores for every pair whose eigenvalues
- * are more than delta apart.  Defaults: enable 1, stop_rel 3e-4, delta 5e-3.
+ * are more than delta apart.  Defaults: enable 1, stop_rel 1e-3, delta 1e-2; pairs closer than delta sweep to 8 tol.
  * enable 0 restores the sweeps-only rule (stop after a sweep with no rotation above 16 tol). */
 int cf_set_eigen_refine(cf_ctx* ctx, int enable, float stop_rel, float delta);
 /* Diagnostics: enable != 0 allocates device counters that the eigen kernel fills;
