@@ -502,9 +502,12 @@ def main():
         "rank_deficient_predictions": {
             "rows": pred_acc["rank_deficient_rows"], "frac": pred_acc["rank_deficient_frac"],
             "c0_rows": pred_acc["c0_rows"],
+            "clamp_bounds": at_bound_stats(wl.off, wl.k, m_h, kk_h, evals_h, sigs_h, wl.ratings, mse_h),
             "note": "rank 0's rows with 0 < c < lim (U_CS^T U_CS singular): the reference's explicit inverse "
                     "returns rounding noise clamped to [1, 5] there, this kernel the minimum-norm least-squares "
-                    "prediction; tests pin kk, finiteness and the clamp range on them, not the value"},
+                    "prediction (tests pin every fast-path row to numpy's min-norm solution and count the "
+                    "block-wide ones); clamp_bounds: the share of them at pred 1 or 5 (cpu_baseline.clamp_bounds "
+                    "has the oracle's share on its sample)"},
     }
 
     # ---- HBM traffic (rank 0, N=1): two rocprofv3 --pmc passes over one child step ------
@@ -528,7 +531,9 @@ def main():
 
     # ---- CPU baseline (rank 0, N=1): the oracle in precompute_local_threads form ---------
     if want_cpu:
-        result["cpu_baseline"] = cpu_baseline(args, wl, W_host)
+        result["cpu_baseline"] = cpu_baseline(args, wl, W_host,
+                                              dev={"m": m_h, "kk": kk_h, "evals": evals_h, "sigs": sigs_h,
+                                                   "mse": mse_h} if world == 1 else None)
     del W_host
 
     # ---- secondary legs (rank 0, N=1; not part of `value`) -----------------------------
@@ -1075,6 +1080,41 @@ def pmc_traffic(args):
     return out
 
 
+def row_lim(off, k, m, evals, sigtab):
+    """lim of every row (local_calc_precomp.cpp:271-279): #(stored eigenvalues of the user <=
+    w_lim), at least 2, at most m, with the compat w_lim of row r = sigtab[r]; one global
+    searchsorted over keys offset by 16 x user (eigenvalues lie in [0, 2], w_lim < 16)."""
+    off = np.asarray(off, dtype=np.int64)
+    k = np.asarray(k, dtype=np.int64)
+    n = int(off[-1])
+    uid = np.repeat(np.arange(len(k)), k)
+    row = np.arange(n) - off[:-1][uid]
+    mu = np.asarray(m, dtype=np.int64)[uid]
+    mu_k = np.minimum(np.asarray(m, dtype=np.int64), k)          # stored eigenvalues per user
+    valid = row < mu_k[uid]
+    ekeys = (uid * 16.0 + np.asarray(evals[:n], dtype=np.float64))[valid]
+    start = np.concatenate([[0], np.cumsum(mu_k)])[:-1]
+    w = np.asarray(sigtab, dtype=np.float64)[row]
+    lim = np.searchsorted(ekeys, uid * 16.0 + w, side="right") - start[uid]
+    return np.minimum(np.maximum(lim, 2), mu).astype(np.float64)
+
+
+def at_bound_stats(off, k, m, kk, evals, sigtab, ratings, mse):
+    """Rank-deficient rows (0 < c < lim) and the share of them whose prediction sits at a clamp
+    bound (pred in {1, 5}: with integer ratings r that is mse == (r-1)^2 or (r-5)^2, bit for
+    bit), next to the same share over the full-rank rows (c >= lim)."""
+    lim = row_lim(off, k, m, evals, sigtab)
+    c = np.asarray(kk, dtype=np.float64)
+    r = np.asarray(ratings, dtype=np.float64)
+    e = np.asarray(mse, dtype=np.float32)
+    bound = (e == np.float32((r - 1.0) ** 2)) | (e == np.float32((r - 5.0) ** 2))
+    rd = (c > 0) & (c < lim)
+    fr = c >= lim
+    return {"rows": int(len(c)), "rank_deficient_rows": int(rd.sum()),
+            "rank_deficient_at_bound_frac": float(bound[rd].mean()) if rd.any() else 0.0,
+            "full_rank_at_bound_frac": float(bound[fr].mean()) if fr.any() else 0.0}
+
+
 def predictor_flops(off, k, m, kk, evals, sigtab):
     """Flop and byte counts of the predict stage (outside the timed region), vectorised.
 
@@ -1089,17 +1129,7 @@ def predictor_flops(off, k, m, kk, evals, sigtab):
     k = np.asarray(k, dtype=np.int64)
     n = int(off[-1])
     uid = np.repeat(np.arange(len(k)), k)
-    row = np.arange(n) - off[:-1][uid]
-    mu = np.asarray(m, dtype=np.int64)[uid]
-    # lim per row = #(stored eigenvalues of the user <= w_lim) (compat table: sigtab[row]), by one
-    # global searchsorted over keys offset by 16 x user (eigenvalues lie in [0, 2], w_lim < 16)
-    mu_k = np.minimum(np.asarray(m, dtype=np.int64), k)          # stored eigenvalues per user
-    valid = row < mu_k[uid]
-    ekeys = (uid * 16.0 + evals[:n].astype(np.float64))[valid]
-    start = np.concatenate([[0], np.cumsum(mu_k)])[:-1]
-    w = sigtab[row].astype(np.float64)
-    lim = np.searchsorted(ekeys, uid * 16.0 + w, side="right") - start[uid]
-    lim = np.minimum(np.maximum(lim, 2), mu).astype(np.float64)
+    lim = row_lim(off, k, m, evals, sigtab)
     c = np.asarray(kk, dtype=np.float64)
     kr = k[uid].astype(np.float64)
     nc = kr - c
@@ -1130,7 +1160,7 @@ def predictor_flops(off, k, m, kk, evals, sigtab):
             "rank_deficient_frac": rdef / max(n, 1), "c0_rows": int(np.sum(c == 0))}
 
 
-def cpu_baseline(args, wl, W):
+def cpu_baseline(args, wl, W, dev=None):
     """The oracle in precompute_local_threads / local_calc_precomp form (fp64, the reference's
     dense LU inverse + 2 GEMMs + Householder/QL eigensolver; neigh_program::apply per rating
     with the explicit-inverse Gram) on a std::thread pool of all the host threads this
@@ -1172,10 +1202,17 @@ def cpu_baseline(args, wl, W):
     per_user = (time.perf_counter() - t) / npu
     npu = int(min(n, max(npu, args.cpu_seconds * 0.4 / max(per_user, 1e-9))))
     t = time.perf_counter()
-    orc.predict_batch(so[:npu + 1], si[:int(so[npu])], sr[:int(so[npu])], m[:npu], evals, eoff[:npu], evecs,
-                      sigs, W, compat=True, n_threads=threads)
+    mse_o, kk_o, _ = orc.predict_batch(so[:npu + 1], si[:int(so[npu])], sr[:int(so[npu])], m[:npu], evals,
+                                       eoff[:npu], evecs, sigs, W, compat=True, n_threads=threads)
     pred_s = time.perf_counter() - t
     n_pred = int(so[npu])
+    ks = np.diff(so[:npu + 1])
+    bound_o = at_bound_stats(so[:npu + 1], ks, m[:npu], kk_o, evals, sigs, sr[:n_pred], mse_o)
+    # the device's rows of the same users (its own eigen records, compat table of the full run)
+    su = users[:npu]
+    rows_d = np.concatenate([np.arange(int(off[u]), int(off[u + 1])) for u in su])
+    bound_d = at_bound_stats(so[:npu + 1], ks, dev["m"][su], dev["kk"][rows_d], dev["evals"][rows_d],
+                             dev["sigs"], ratings[rows_d], dev["mse"][rows_d]) if dev else None
     return {
         "value": n / eig_s,
         "unit": "user-subgraph eigendecomps/s",
@@ -1187,6 +1224,12 @@ def cpu_baseline(args, wl, W):
         "predicted_ratings_per_s": n_pred / pred_s,
         "predict_sample": f"{n_pred} predictions ({npu} users), oracle neigh_program::apply (fp64, explicit "
                           f"PartialPivLU-class inverse per rating, compat w_lim), {threads}-thread pool",
+        "clamp_bounds": {
+            "oracle": bound_o, "device_same_users": bound_d,
+            "note": "rows at a clamp bound (pred 1 or 5) among the rank-deficient rows (0 < c < lim) of the "
+                    "predict sample: the oracle restates the reference's explicit inverse of the singular "
+                    "U_CS^T U_CS (rounding noise, mostly clamped), the device returns the minimum-norm "
+                    "least-squares prediction (DESIGN 3.2, INTEGRATION.md)"},
     }
 
 

@@ -1712,3 +1712,16 @@ template int cf_launch_predict<double>(cf_ctx*, const cf_plan*, const uint64_t*,
                                        const float*, const int32_t*, const double*,
                                        const uint64_t*, const double*, const double*, int, float*,
                                        int32_t*, double*, const uint8_t*, hipStream_t);
+
+// The fast path's largest system (rows min(nc, d)) in a bucket of Gram bound lmax: the nmax
+// setup_bucket derives from the LDS budget.  Ratings with a larger system take the block-wide
+// path; the parity tests use it to tell which rank-deficient rows return the minimum-norm
+// prediction.
+extern "C" int cf_debug_predict_nmax(int lmax) {
+    if (lmax < 2 || lmax > CF_MAX_K) return -1;
+    const size_t lds_fixed = rating_lds_fixed();
+    const auto per_wave = [&](int n) { return fast_tri(n) + 2 * lmax; };
+    int nmax = std::min(kNsysMax, lmax);
+    while (nmax > 8 && sizeof(double) * (size_t)(kWaves * per_wave(nmax)) + lds_fixed > kRatingLds) --nmax;
+    return nmax;
+}

@@ -98,6 +98,10 @@ int cf_debug_tri(cf_ctx* ctx, int enable, uint64_t* out8);
  * completed fast-path ratings with nc <= 4, 5..16 and > 16, and the counts of the first
  * two classes. */
 int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out16);
+/* The predictor's fast-path system bound (rows min(nc, d)) in a k-bucket whose
+ * Gram bound is lmax = 16 ceil(k / 16): ratings above it take the block-wide path.  -1 if
+ * lmax is out of range.  (Test / diagnostics helper.) */
+int cf_debug_predict_nmax(int lmax);
 
 /* ---- item graph (out_fin_) ---------------------------------------------------
  * Directed weighted graph exactly as parsed: w(a,b) and w(b,a) are independent.
