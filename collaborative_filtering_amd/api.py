@@ -172,9 +172,11 @@ class Context:
         self._chk(self.lib.cf_graph_info(self.h, byref(lay), byref(n), ptr(nnz)), "cf_graph_info")
         return ("csr" if lay.value == _native.CF_GRAPH_CSR else "dense"), n.value, int(nnz[0])
 
-    def item_cosine_edges(self, n_items, user_off, items, ratings, w_min=0.01, cnt_min=5, adopt=False):
+    def item_cosine_edges(self, n_items, user_off, items, ratings, w_min=0.01, cnt_min=5, adopt=False, topk=0):
         """knn2 as the compacted edge list (cf_item_cosine_edges): (edge_off[n_items + 1],
-        targets, weights) per source, targets ascending."""
+        targets, weights) per source, targets ascending; topk > 0 keeps the K largest weights
+        per source (cf_set_knn2_topk; ties: lower target ids)."""
+        self._chk(self.lib.cf_set_knn2_topk(self.h, int(topk)), "cf_set_knn2_topk")
         user_off = np.ascontiguousarray(user_off, dtype=np.uint64)
         items = np.ascontiguousarray(items, dtype=np.uint32)
         ratings = np.ascontiguousarray(ratings, dtype=np.float32)

@@ -36,18 +36,95 @@ __global__ __launch_bounds__(kGT) void row_nnz_kernel(uint64_t n, const float* d
     }
 }
 
-__global__ __launch_bounds__(kGT) void row_compact_kernel(uint64_t n, const float* dense, const uint64_t* rp,
-                                                          uint32_t* col, float* w) {
+// Optional top-K per row (cf_set_knn2_topk): the K largest weights of the row, ties at the
+// K-th value broken by ascending column.  One workgroup per row finds the K-th largest key by
+// a 4 x 8-bit radix select over the float bits (the weights are positive, so their bit
+// patterns order like their values); thr[r] = that key, take[r] = how many of the entries
+// equal to it are kept (the first ones in column order), cnt[r] = min(nnz, K).  Rows with at
+// most K entries keep them all (thr 0).
+__global__ __launch_bounds__(kGT) void row_topk_kernel(uint64_t n, const float* dense, uint32_t K, uint32_t* thr,
+                                                       uint32_t* take, uint64_t* cnt) {
+    __shared__ unsigned int s_hist[256];
     __shared__ unsigned int s_c[kGT / 64];
+    __shared__ unsigned int s_sel[2];
+    for (uint64_t r = blockIdx.x; r < n; r += gridDim.x) {
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(dense + r * n);
+        unsigned int c = 0;
+        for (uint64_t j = threadIdx.x; j < n; j += kGT) c += row[j] != 0u && (row[j] << 1) != 0u;
+        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
+        if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = c;
+        __syncthreads();
+        const unsigned int total = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+        __syncthreads();
+        if (total <= K) {
+            if (threadIdx.x == 0) {
+                thr[r] = 0u;
+                take[r] = 0xffffffffu;
+                cnt[r] = total;
+            }
+            continue;
+        }
+        uint32_t prefix = 0, mask = 0, rem = K;   // rem: entries still to take at or below the prefix
+        for (int shift = 24; shift >= 0; shift -= 8) {
+            s_hist[threadIdx.x] = 0u;   // kGT == 256 bins
+            __syncthreads();
+            for (uint64_t j = threadIdx.x; j < n; j += kGT) {
+                const uint32_t key = row[j];
+                if ((key << 1) != 0u && (key & mask) == prefix) atomicAdd(&s_hist[(key >> shift) & 255u], 1u);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                unsigned int above = 0;
+                int b = 255;
+                for (; b > 0; --b) {
+                    if (above + s_hist[b] >= rem) break;
+                    above += s_hist[b];
+                }
+                s_sel[0] = (unsigned int)b;
+                s_sel[1] = above;
+            }
+            __syncthreads();
+            prefix |= s_sel[0] << shift;
+            mask |= 255u << shift;
+            rem -= s_sel[1];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            thr[r] = prefix;
+            take[r] = rem;
+            cnt[r] = K;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kGT) void row_compact_kernel(uint64_t n, const float* dense, const uint64_t* rp,
+                                                          uint32_t* col, float* w, const uint32_t* thr,
+                                                          const uint32_t* take) {
+    __shared__ unsigned int s_c[kGT / 64];
+    __shared__ unsigned int s_t[kGT / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint64_t r = blockIdx.x; r < n; r += gridDim.x) {
         const float* row = dense + r * n;
+        const uint32_t T = thr ? thr[r] : 0u, tk = thr ? take[r] : 0xffffffffu;
         uint64_t pos = rp[r];
+        unsigned int ties = 0;   // entries equal to the threshold seen so far (column order)
         for (uint64_t j0 = 0; j0 < n; j0 += kGT) {
             const uint64_t j = j0 + threadIdx.x;
             const float v = j < n ? row[j] : 0.0f;
+            const uint32_t key = __float_as_uint(v);
             const bool nz = v != 0.0f;
-            const unsigned long long bal = __ballot(nz);
+            const bool tie = nz && thr && key == T;
+            const unsigned long long tb = __ballot(tie);
+            if (lane == 0) s_t[wave] = (unsigned int)__popcll(tb);
+            __syncthreads();
+            unsigned int tbefore = 0, tall = 0;
+            for (int x = 0; x < kGT / 64; ++x) {
+                tbefore += x < wave ? s_t[x] : 0u;
+                tall += s_t[x];
+            }
+            const unsigned int trank = ties + tbefore + (unsigned int)__popcll(tb & ((1ull << lane) - 1ull));
+            const bool keep = nz && (!thr || key > T || (tie && trank < tk));
+            const unsigned long long bal = __ballot(keep);
             if (lane == 0) s_c[wave] = (unsigned int)__popcll(bal);
             __syncthreads();
             unsigned int before = 0, all = 0;
@@ -55,12 +132,13 @@ __global__ __launch_bounds__(kGT) void row_compact_kernel(uint64_t n, const floa
                 before += x < wave ? s_c[x] : 0u;
                 all += s_c[x];
             }
-            if (nz) {
+            if (keep) {
                 const uint64_t o = pos + before + (unsigned int)__popcll(bal & ((1ull << lane) - 1ull));
                 col[o] = (uint32_t)j;
                 w[o] = v;
             }
             pos += all;
+            ties += tall;
             __syncthreads();
         }
     }
@@ -85,15 +163,24 @@ void free_graph(cf_ctx* ctx) {
 // Dense n x n device matrix -> CSR in new device buffers (row pointers through the host: n + 1
 // words).  Synchronous on `stream`.
 int cf_dense_to_csr(cf_ctx* ctx, uint32_t n, const float* d_dense, uint64_t** d_rp, uint32_t** d_col, float** d_w,
-                    uint64_t* nnz, hipStream_t stream) {
+                    uint64_t* nnz, hipStream_t stream, uint32_t topk) {
     *d_rp = nullptr;
     *d_col = nullptr;
     *d_w = nullptr;
     std::vector<uint64_t> rp((size_t)n + 1, 0);
     CF_HIP_CHECK(ctx, hipMalloc(d_rp, sizeof(uint64_t) * ((size_t)n + 1)));
+    DevBuf dthr, dtake;
+    if (topk) {
+        CF_TRY(dev_alloc(ctx, dthr, sizeof(uint32_t) * std::max<uint32_t>(n, 1)));
+        CF_TRY(dev_alloc(ctx, dtake, sizeof(uint32_t) * std::max<uint32_t>(n, 1)));
+    }
     const unsigned grid = (unsigned)std::max<uint32_t>(1, std::min<uint32_t>(n, 65536u));
     if (n) {
-        hipLaunchKernelGGL(row_nnz_kernel, dim3(grid), dim3(kGT), 0, stream, (uint64_t)n, d_dense, *d_rp + 1);
+        if (topk)
+            hipLaunchKernelGGL(row_topk_kernel, dim3(grid), dim3(kGT), 0, stream, (uint64_t)n, d_dense, topk,
+                               (uint32_t*)dthr.p, (uint32_t*)dtake.p, *d_rp + 1);
+        else
+            hipLaunchKernelGGL(row_nnz_kernel, dim3(grid), dim3(kGT), 0, stream, (uint64_t)n, d_dense, *d_rp + 1);
         CF_HIP_CHECK(ctx, hipGetLastError());
         CF_HIP_CHECK(ctx, hipMemcpyAsync(rp.data() + 1, *d_rp + 1, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, stream));
         CF_HIP_CHECK(ctx, hipStreamSynchronize(stream));
@@ -107,7 +194,8 @@ int cf_dense_to_csr(cf_ctx* ctx, uint32_t n, const float* d_dense, uint64_t** d_
         return cf_set_error(ctx, CF_ENOMEM, "CSR graph allocation");
     if (n) {
         hipLaunchKernelGGL(row_compact_kernel, dim3(grid), dim3(kGT), 0, stream, (uint64_t)n, d_dense,
-                           (const uint64_t*)*d_rp, *d_col, *d_w);
+                           (const uint64_t*)*d_rp, *d_col, *d_w, topk ? (const uint32_t*)dthr.p : nullptr,
+                           topk ? (const uint32_t*)dtake.p : nullptr);
         CF_HIP_CHECK(ctx, hipGetLastError());
     }
     CF_HIP_CHECK(ctx, hipStreamSynchronize(stream));
@@ -126,7 +214,7 @@ int cf_adopt_dense_graph(cf_ctx* ctx, uint32_t n, float* d_dense) {
     uint64_t *rp = nullptr, nnz = 0;
     uint32_t* col = nullptr;
     float* w = nullptr;
-    const int rc = cf_dense_to_csr(ctx, n, d_dense, &rp, &col, &w, &nnz, nullptr);
+    const int rc = cf_dense_to_csr(ctx, n, d_dense, &rp, &col, &w, &nnz, nullptr, 0);
     (void)hipFree(d_dense);
     if (rc != CF_OK) {
         if (rp) (void)hipFree(rp);
@@ -315,7 +403,7 @@ int cf_item_cosine_edges(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const 
     uint64_t *rp = nullptr, nnz = 0;
     uint32_t* col = nullptr;
     float* wv = nullptr;
-    if (rc == CF_OK) rc = cf_dense_to_csr(ctx, n_items, dW, &rp, &col, &wv, &nnz, nullptr);
+    if (rc == CF_OK) rc = cf_dense_to_csr(ctx, n_items, dW, &rp, &col, &wv, &nnz, nullptr, ctx->knn2_topk);
     if (rc == CF_OK) {
         *n_edges = nnz;
         e = hipMemcpy(edge_off, rp, sizeof(uint64_t) * ((size_t)n_items + 1), hipMemcpyDeviceToHost);
@@ -339,6 +427,14 @@ int cf_item_cosine_edges(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const 
             col = nullptr;
             wv = nullptr;
         } else {
+            if (ctx->knn2_topk) {   // the dense graph holds the top-K list only
+                e = hipMemset(dW, 0, (size_t)n_items * n_items * sizeof(float));
+                if (e == hipSuccess)
+                    rc = cf_launch_dense_scatter(ctx, n_items, rp, col, wv, dW, nullptr);
+                else
+                    rc = cf_set_error(ctx, CF_EHIP, "top-k dense graph reset");
+                if (rc == CF_OK && hipDeviceSynchronize() != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, "top-k scatter");
+            }
             ctx->d_graph = dW;
             dW = nullptr;
         }
@@ -349,6 +445,12 @@ int cf_item_cosine_edges(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const 
     if (wv) (void)hipFree(wv);
     if (dW) (void)hipFree(dW);
     return rc;
+}
+
+int cf_set_knn2_topk(cf_ctx* ctx, uint32_t topk) {
+    if (!ctx) return CF_EINVAL;
+    ctx->knn2_topk = topk;
+    return CF_OK;
 }
 
 }  // extern "C"

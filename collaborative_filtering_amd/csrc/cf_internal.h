@@ -106,6 +106,7 @@ struct cf_ctx {
     void* d_knn_part = nullptr;
     size_t knn_part_bytes = 0;
     uint32_t knn_chunk_users = 0;
+    uint32_t knn2_topk = 0;   // cf_set_knn2_topk: K largest weights per source in the edge list (0: all)
     int knn_chunks = 0;   // knn2: largest accumulator of the last launch (float bits)
     // data prep (cf_prep.hip): sort / bitmap scratch, grown on demand; events of the last call
     void* d_prep = nullptr;
@@ -319,7 +320,7 @@ int cf_launch_knn3(cf_ctx* ctx, uint32_t n_users, const uint64_t* d_user_off, co
 // cf_graph.hip: a device dense matrix as CSR (new buffers), and a device dense matrix
 // installed as the context's graph in its upload layout (adopted, or compacted and freed).
 int cf_dense_to_csr(cf_ctx* ctx, uint32_t n, const float* d_dense, uint64_t** d_rp, uint32_t** d_col, float** d_w,
-                    uint64_t* nnz, hipStream_t stream);
+                    uint64_t* nnz, hipStream_t stream, uint32_t topk = 0);
 int cf_adopt_dense_graph(cf_ctx* ctx, uint32_t n, float* d_dense);
 
 int cf_launch_dense_scatter(cf_ctx* ctx, uint32_t n_items, const uint64_t* d_row_ptr,

@@ -1,5 +1,6 @@
 // knn2 -- drop-in for knn2.cpp (a10): cosine item weights on the out_edg_ edges from
 // the out_rat_ train maps; writes out_fin_ "a b w" for w > 0.01 (knn2.cpp:151-164).
+// Optional --topk K (off by default): only the K largest weights per source item.
 // The weights come from cf_item_cosine_edges (int8 / fp32 MFMA over all item pairs, compacted
 // on the device to the w > 0.01 edge list); the writer keeps exactly the out_edg_ edges, in
 // out_edg_ order per source.
@@ -10,6 +11,13 @@
 
 int main(int argc, char** argv) {
     const int nshards = std::stoi(cfcli::opt(argc, argv, "nshards", "4"));
+    // --topk K (default 0 = off, the reference's threshold-only neighbourhoods): keep the K
+    // largest weights per source item (ties: lower item ids), cf_set_knn2_topk
+    const long topk = std::stol(cfcli::opt(argc, argv, "topk", "0"));
+    if (topk < 0) {
+        std::fprintf(stderr, "knn2: --topk must be >= 0\n");
+        return 2;
+    }
     cfio::VertexRatings rat = cfio::load_vertex_ratings(".", "out_rat_", false);   // :79-102
     auto edges = cfio::load_adjacency(".", "out_edg_");                            // :104-121
     std::vector<uint32_t> all;
@@ -47,6 +55,7 @@ int main(int argc, char** argv) {
     std::vector<float> ew;
     uint64_t n_edges = 0;
     cf_ctx* ctx = cfcli::open_device();
+    cfcli::check(ctx, cf_set_knn2_topk(ctx, (uint32_t)topk), "cf_set_knn2_topk");
     // Capacity: every w > 0.01 pair has cnt > 5 co-raters, so it is a co-rated pair and
     // out_edg_ (written by knn from the same ratings) lists it -- one call computes knn2.
     // Files from different runs can break that bound: the call then reports the size it

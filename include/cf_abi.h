@@ -280,6 +280,12 @@ int cf_item_cosine(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64
 int cf_item_cosine_edges(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const uint64_t* user_off,
                          const uint32_t* item, const float* rating, float w_min, int cnt_min, int adopt_as_graph,
                          uint64_t* edge_off, uint32_t* edge_col, float* edge_w, uint64_t edge_cap, uint64_t* n_edges);
+/* Optional top-K cap on cf_item_cosine_edges' list (0 = off, the default: the reference has
+ * no top-k, its neighbourhoods are thresholds, knn2.cpp:142,157): per source item only the K
+ * largest weights are returned (ties at the K-th value: the lower target ids), still in
+ * ascending target order; adopt_as_graph installs the capped list.  Selection is a per-row
+ * radix select on the device over the exact weights, so the indices are bit-exact. */
+int cf_set_knn2_topk(cf_ctx* ctx, uint32_t topk);
 int cf_item_cosine_run(cf_ctx* ctx, uint32_t n_users, uint32_t n_items,
                        const uint64_t* d_user_off, const uint32_t* d_item, const float* d_rating,
                        int integer_ratings, float w_min, int cnt_min, float* d_w_out,

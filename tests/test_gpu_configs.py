@@ -498,6 +498,35 @@ def test_c3_knn2_rows_bit_exact(gpu_ctx):
     torch.cuda.empty_cache()
 
 
+def test_c3_knn2_topk_rows_bit_exact(gpu_ctx):
+    """The optional top-K cap (cf_set_knn2_topk, `bin/knn2 --topk`; default off) at full C3 size
+    (20k items x 500k users): the returned lists of Zipf head-to-tail rows equal a numpy argsort
+    of the oracle's weights_calc rows (K largest, ties to the lower id), indices and weights
+    bit-exact."""
+    from collaborative_filtering_amd import workloads as wlm
+    from collaborative_filtering_amd.api import Context
+
+    K = 64
+    kd, off, items, rats = wlm.c3_population(threads=THREADS)
+    n_items = wlm.CONFIGS["c3"]["items"]
+    with Context(0) as kctx:
+        eo, col, w = kctx.item_cosine_edges(n_items, off, items, rats, topk=K)
+    rows = np.array([0, 1, 2, 17, 999, 5000, 12345, 19999], dtype=np.int32)
+    Wr = orc.knn2_rows(off.astype(np.int64), items.astype(np.int32), rats.astype(np.float64), n_items, rows,
+                       threads=THREADS)
+    capped = 0
+    for t, a in enumerate(rows):
+        nz = np.nonzero(Wr[t])[0]
+        order = np.lexsort((nz, -Wr[t, nz].astype(np.float64)))
+        want = np.sort(nz[order[:K]])
+        b, e = int(eo[a]), int(eo[a + 1])
+        assert np.array_equal(col[b:e], want.astype(np.uint32)), a
+        assert np.array_equal(w[b:e], Wr[t, want]), a
+        capped += len(nz) > K
+    assert capped >= 4   # the cap binds on the head rows
+    assert int(eo[-1]) <= K * n_items
+
+
 def test_c5_tail_k_up_to_5000(gpu_ctx, c4_graph):
     """C5 as specified: its lognormal tail reaches the k = 5000 cap.  Users with k = 2000,
     3100, 4000 and 5000 (Zipf items of the 50k C4 graph) through the timed fused path: the

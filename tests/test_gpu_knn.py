@@ -220,3 +220,53 @@ def test_knn2_edge_list_matches_dense_and_adopts_as_csr(gpu_ctx):
         ra, rb = a.eigen_batch(uoff, uitems), b.eigen_batch(uoff, uitems)
         assert np.array_equal(ra.m, rb.m) and np.array_equal(ra.evecs, rb.evecs)
         assert np.array_equal(ra.sigs, rb.sigs) and np.array_equal(ra.evals, rb.evals)
+
+
+def topk_reference(W, K):
+    """Per source row: the K largest nonzero weights (ties at the K-th value: lower ids), as
+    CSR with ascending targets -- what cf_set_knn2_topk asks of the edge list."""
+    off = [0]
+    cols, ws = [], []
+    for a in range(W.shape[0]):
+        nz = np.nonzero(W[a])[0]
+        order = np.lexsort((nz, -W[a, nz].astype(np.float64)))   # weight descending, then id ascending
+        keep = np.sort(nz[order[:K]])
+        cols.append(keep)
+        ws.append(W[a, keep])
+        off.append(off[-1] + len(keep))
+    return np.array(off, np.uint64), np.concatenate(cols).astype(np.uint32), np.concatenate(ws).astype(np.float32)
+
+
+@pytest.mark.parametrize("K", [1, 7, 40])
+def test_knn2_topk_edges_with_ties(gpu_ctx, K):
+    """The optional top-K cap (default off): K largest weights per source, ties broken by the
+    lower target id, bit-exact indices and weights.  Duplicated items make many weights equal,
+    so the K-th value is often tied (the radix select's tie count is exercised)."""
+    n_items = 240
+    off, items, rats = synth_train(3000, n_items // 2, seed=K, zero_frac=0.0)
+    # item j and j + 120 get identical rating columns: every weight appears at least twice
+    k = np.diff(off.astype(np.int64))
+    uo = np.zeros(len(k) + 1, np.uint64)
+    uo[1:] = np.cumsum(2 * k)
+    it2 = np.empty(2 * len(items), np.uint32)
+    rt2 = np.empty(2 * len(items), np.float64)
+    for u in range(len(k)):
+        b, e = int(off[u]), int(off[u + 1])
+        seg = np.argsort(np.concatenate([items[b:e], items[b:e] + n_items // 2]), kind="stable")
+        both_i = np.concatenate([items[b:e], items[b:e] + n_items // 2])[seg]
+        both_r = np.concatenate([rats[b:e], rats[b:e]])[seg]
+        it2[int(uo[u]):int(uo[u + 1])] = both_i
+        rt2[int(uo[u]):int(uo[u + 1])] = both_r
+    Wo, _ = orc.knn2(uo.astype(np.int64), it2.astype(np.int32), rt2, n_items)
+    eo, co, wo = topk_reference(Wo, K)
+    eg, cg, wg = gpu_ctx.item_cosine_edges(n_items, uo, it2, rt2.astype(np.float32), topk=K)
+    try:
+        assert np.array_equal(eg, eo)
+        assert np.array_equal(cg, co)
+        assert np.array_equal(wg, wo)
+        # the cap binds and ties at the cut exist
+        assert int(eo[-1]) < int((Wo > 0).sum())
+    finally:
+        gpu_ctx.item_cosine_edges(n_items, uo, it2, rt2.astype(np.float32), topk=0)   # cap off again
+    e0, c0, w0 = gpu_ctx.item_cosine_edges(n_items, uo, it2, rt2.astype(np.float32))
+    assert int(e0[-1]) == int((Wo > 0).sum())   # default: the full thresholded list
