@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--pmc", choices=["auto", "off"], default="auto",
                    help="N=1: HBM traffic from two rocprofv3 --pmc child passes (FETCH_SIZE, WRITE_SIZE)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)   # one pass, no output
+    p.add_argument("--io", choices=["auto", "off"], default="auto",
+                   help="C4-size out_eigen_ write/parse leg (binary all records, text the first 100k)")
     p.add_argument("--c2", choices=["auto", "off"], default="auto",
                    help="N=1 secondary leg: BASELINE config 2 (100k x 10k) steps and the out_eigen_ text phases")
     p.add_argument("--knn2", choices=["auto", "off", "only"], default="auto",
@@ -537,6 +539,13 @@ def main():
     del W_host
 
     # ---- secondary legs (rank 0, N=1; not part of `value`) -----------------------------
+    if solo and args.io == "auto" and args.config == "c4":
+        # the C4-size out_eigen_ round trip: binary form of all 1M records,
+        # text form of the first 100k (the full text file would be ~128 GB)
+        try:
+            result["config4_eigen_io"] = text_phases(wl, text_users=100_000, label="C4 record set")
+        except OSError as exc:
+            result["config4_eigen_io"] = f"skipped: {exc}"
     if solo and args.c2 == "auto" and args.config != "c2":
         wl.plan.close()
         del wl
@@ -668,8 +677,13 @@ def c2_leg(args, ctx, dev_index, dev, torch):
     return out
 
 
-def text_phases(wl):
+def text_phases(wl, text_users=None, label="whole C2 record set"):
+    """out_eigen_ write + parse phases on the host (compute and text-write timed
+    separately): the text form (cfh_write_eigen = bin/precompute_local's %g writer) on the first
+    `text_users` records (all when None) and the binary form on all of them; cfh_load_eigen =
+    load_precomputed_data of bin/local_calc_precomp.  Download from HBM excluded."""
     import ctypes
+    import shutil
 
     from collaborative_filtering_amd import synth
     from collaborative_filtering_amd._native import ptr
@@ -687,28 +701,40 @@ def text_phases(wl):
     poff = wl.d_poff.cpu().numpy().astype(np.uint64)
     packed = wl.d_packed.cpu().numpy()
     uid = np.arange(wl.n_users, dtype=np.uint32)
-    path = os.path.join("/tmp", f"cf_bench_out_eigen_{os.getpid()}").encode()
-    res = {"threads": threads, "records": wl.n_users}
+    tmpdir = os.environ.get("CF_BENCH_TMP", "/tmp")
+    path = os.path.join(tmpdir, f"cf_bench_out_eigen_{os.getpid()}").encode()
+    res = {"threads": threads, "dir": tmpdir}
     try:
         for fmt, binary in (("text", 0), ("binary", 1)):
+            n_rec = wl.n_users if (binary or text_users is None) else min(wl.n_users, int(text_users))
+            k = np.diff(wl.off[:n_rec + 1].astype(np.int64))
+            mm = m[:n_rec].astype(np.int64)
+            est = int(np.sum(12 + 8 * k + 4 * mm + 4 * k * mm)) * (3 if not binary else 1)
+            free = shutil.disk_usage(tmpdir).free
+            if est > 0.8 * free:
+                res[fmt] = f"skipped: ~{est / 1e9:.1f} GB would not fit the {free / 1e9:.1f} GB free in {tmpdir}"
+                continue
             t = time.perf_counter()
-            rc = L.cfh_write_eigen(path, 0, threads, binary, wl.n_users, ptr(uid), ptr(wl.off), ptr(m),
+            rc = L.cfh_write_eigen(path, 0, threads, binary, n_rec, ptr(uid), ptr(wl.off), ptr(m),
                                    ptr(wl.items), ptr(sigs), ptr(evals), ptr(poff), ptr(packed))
             w_s = time.perf_counter() - t
             size = os.path.getsize(path.decode())
             t = time.perf_counter()
             n = L.cfh_load_eigen(path, threads, None, 0)
             r_s = time.perf_counter() - t
-            res[fmt] = {"write_s": w_s, "parse_s": r_s, "bytes": size, "write_GBps": size / w_s / 1e9,
-                        "parse_GBps": size / r_s / 1e9, "ok": bool(rc == 0 and n == wl.n_users)}
+            res[fmt] = {"records": n_rec, "write_s": w_s, "parse_s": r_s, "bytes": size,
+                        "write_GBps": size / w_s / 1e9, "parse_GBps": size / r_s / 1e9,
+                        "ok": bool(rc == 0 and n == n_rec)}
+            os.remove(path.decode())
     finally:
         try:
             os.remove(path.decode())
         except OSError:
             pass
-    res["note"] = ("whole C2 record set (download excluded): cfh_write_eigen = the out_eigen_ writer of "
-                   "bin/precompute_local (%g via to_chars, records formatted on `threads` threads), cfh_load_eigen = "
-                   "load_precomputed_data of bin/local_calc_precomp (records parsed in parallel); file in /tmp")
+    res["note"] = (f"{label} (download excluded): cfh_write_eigen = the out_eigen_ writer of bin/precompute_local "
+                   "(text: %g via to_chars, records formatted on `threads` threads; binary CFEIGEN1: fp32 blocks, "
+                   "pieces pwrite()n in place), cfh_load_eigen = load_precomputed_data of bin/local_calc_precomp "
+                   "(records parsed in parallel); file in `dir`")
     return res
 
 

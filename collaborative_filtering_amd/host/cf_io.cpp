@@ -605,14 +605,30 @@ void write_eigen_file(const std::string& path, bool append, int n_threads, bool 
         const int wfd = ::open(path.c_str(), O_WRONLY);
         if (wfd < 0) throw std::runtime_error("cannot open " + path);
         const uint64_t base = append ? (uint64_t)::lseek(wfd, 0, SEEK_END) - at[0] : 0;
-        const int T = (int)std::min<uint32_t>((uint32_t)resolve_threads(n_threads), std::max<uint32_t>(n_users, 1));
+        // the file gets its final size first, so the pieces land inside it instead of extending
+        // it out of order; pieces of ~8 MB are claimed in file order by whichever thread is free
+        // (a static split by user count left threads idle on unequal byte ranges)
+        if (::ftruncate(wfd, (off_t)(base + at[n_users])) != 0) {
+            ::close(wfd);
+            throw std::runtime_error("cannot size " + path);
+        }
+        std::vector<uint32_t> piece{0};
+        for (uint32_t u = 0; u < n_users;) {
+            uint32_t c1 = u + 1;
+            while (c1 < n_users && at[c1 + 1] - at[u] < (8u << 20)) ++c1;
+            piece.push_back(c1);
+            u = c1;
+        }
+        const uint32_t n_pieces = (uint32_t)piece.size() - 1;
+        const int T = (int)std::min<uint32_t>((uint32_t)resolve_threads(n_threads), std::max<uint32_t>(n_pieces, 1));
         std::atomic<bool> failed{false};
-        parallel_for(T, [&](int t) {
-            const uint32_t u0 = (uint32_t)((uint64_t)n_users * t / T), u1 = (uint32_t)((uint64_t)n_users * (t + 1) / T);
+        std::atomic<uint32_t> next{0};
+        parallel_for(T, [&](int) {
             std::vector<char> buf;
-            for (uint32_t c0 = u0; c0 < u1;) {   // ~8 MB pieces
-                uint32_t c1 = c0;
-                while (c1 < u1 && (c1 == c0 || at[c1 + 1] - at[c0] < (8u << 20))) ++c1;
+            for (;;) {
+                const uint32_t pc = next.fetch_add(1);
+                if (pc >= n_pieces) break;
+                const uint32_t c0 = piece[pc], c1 = piece[pc + 1];
                 buf.resize(at[c1] - at[c0]);
                 char* p = buf.data();
                 for (uint32_t u = c0; u < c1; ++u) {
@@ -641,7 +657,7 @@ void write_eigen_file(const std::string& path, bool append, int n_threads, bool 
                     }
                     done += (size_t)w;
                 }
-                c0 = c1;
+                if (failed) break;
             }
         });
         ::close(wfd);
