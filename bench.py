@@ -639,7 +639,6 @@ def c2_leg(args, ctx, dev_index, dev, torch):
     a.users = cfg["users"]
     d_W, _, gstats = train_graph(Context, dev_index, dev, torch, cfg["seed"], cfg["train_users"], cfg["items"])
     wl = Workload(a, cfg, 0, 1, dev, torch, ctx, d_W.view(cfg["items"], cfg["items"]))
-    del d_W
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     for _ in range(2):
@@ -673,8 +672,58 @@ def c2_leg(args, ctx, dev_index, dev, torch):
         out["text_io"] = text_phases(wl)
     except OSError as exc:
         out["text_io"] = f"skipped: {exc}"
+    # ---- local_calc (a8) on the same graph: `local_calc --pct 1` ------------------------
+    try:
+        out["local_calc"] = local_calc_leg(ctx, wl, d_W.view(cfg["items"], cfg["items"]), pct=1)
+    except Exception as exc:   # reported, never fatal for the headline
+        out["local_calc"] = f"failed: {exc}"
+    del d_W
     wl.plan.close()
     return out
+
+
+def local_calc_leg(ctx, wl, W, pct=1, seed=2026):
+    """local_calc's engine 2 (local_calc.cpp:262-526, cf_local_calc) as `bin/local_calc --pct P`
+    runs it: movies sampled with probability P %, each movie's unit = [m, out-neighbours with
+    w > 0.1] of the resident knn2 graph, test ratings = the config's user ratings grouped by
+    movie (users ascending).  Host-pointer call (PCIe included)."""
+    n_items = wl.n_items
+    rng = np.random.default_rng(seed)
+    movies = np.nonzero(rng.random(n_items) * 100.0 < pct)[0]
+    # test ratings CSR over movies, users ascending
+    uid = np.repeat(np.arange(wl.n_users, dtype=np.int64), wl.k)
+    mv = wl.items[:wl.n_entries].astype(np.int64)
+    order = np.lexsort((uid, mv))
+    toff = np.zeros(n_items + 1, np.uint64)
+    np.add.at(toff, mv + 1, 1)
+    toff = np.cumsum(toff).astype(np.uint64)
+    tuser = uid[order].astype(np.uint32)
+    trat = wl.ratings[:wl.n_entries][order].astype(np.float32)
+    # units of the sampled movies that have test ratings (the rest write no rows, :269-272)
+    moff, mitems, ns = [0], [], []
+    for m in movies:
+        if toff[m + 1] == toff[m]:
+            continue
+        row = W[int(m)].cpu().numpy()
+        nb = np.nonzero(row.astype(np.float64) > 0.1)[0]
+        nb = nb[nb != m]
+        mitems.append(np.concatenate([[m], nb]).astype(np.uint32))
+        moff.append(moff[-1] + 1 + len(nb))
+        ns.append(1 + len(nb))
+    ns = np.array(ns)
+    moff = np.array(moff, np.uint64)
+    mitems = np.concatenate(mitems) if mitems else np.zeros(0, np.uint32)
+    t = time.perf_counter()
+    mse, kk, pred, wlim, lim = ctx.local_calc(moff, mitems, toff, tuser, trat)
+    dt = time.perf_counter() - t
+    pairs = int(np.sum(kk >= 0))
+    return {"movies_sampled": int(len(movies)), "units": int(len(ns)),
+            "unit_n": {"mean": float(ns.mean()) if len(ns) else 0.0, "max": int(ns.max()) if len(ns) else 0,
+                       "gt_192": int(np.sum(ns > 192)), "ge_5000": int(np.sum(ns >= 5000))},
+            "predictions": pairs, "seconds": dt, "predictions_per_s": pairs / dt if dt > 0 else 0.0,
+            "cf_erange": 0,
+            "note": f"bin/local_calc --pct {pct} on this config's knn2 graph: {len(ns)} movie units, every (movie, "
+                    "test user) pair of them; host-pointer cf_local_calc (PCIe included)"}
 
 
 def text_phases(wl, text_users=None, label="whole C2 record set"):

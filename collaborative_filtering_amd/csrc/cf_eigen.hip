@@ -102,6 +102,7 @@ struct EigenArgs {
     float stop_rel;
     float refine_delta;
     float close_sigrot;   // close pairs converge to close_sigrot * tol
+    int close_only;       // after the far pairs stop: sweeps over the close pairs only
     unsigned long long* stats;
     // kLocal / kSigma
     float* l2;                  // per movie n x n row-major L2 (kLocal writes, kSigma reads)
@@ -317,6 +318,7 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
     // close pairs, |mu_q - mu_p| <~ delta: (be - al)^2 <= 2 delta^2 (al + be) (al, be ~ mu^2)
     const float close2 = refine ? a.close_sigrot * a.close_sigrot * tol2 : stop2;
     const float dclose2 = refine ? 2.0f * a.refine_delta * a.refine_delta : -1.0f;
+    bool close_phase = false;
     // Squared column norms ||b_j||^2 (s_l2d is dead once B is assembled).  A step then
     // needs only the cross product ga = b_p . b_q: the rotated norms follow exactly from
     // (al, be, ga, c, s).  They are recomputed from the columns at every sweep start, and
@@ -376,7 +378,9 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
             f2* const bq0 = reinterpret_cast<f2*>(B + (s0 + f) * LD);
             for (int step = 0; step < FL; ++step) {
                 const int q = s0 + f + ti;
-                if (step < nlive && ti < tv) {
+                // close-only sweeps skip the far pairs before loading the traveling column
+                if (step < nlive && ti < tv &&
+                    !(close_phase && (s_nrm[q] - al) * (s_nrm[q] - al) > dclose2 * (al + s_nrm[q]))) {
                     const float dq = s_dev[q];   // issued with the column loads
                     const float be = s_nrm[q];
                     f2 xq[E2];
@@ -422,7 +426,10 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
                             // with the refinement: pairs closer than refine_delta in mu, which it
                             // leaves alone, still converge to kSigRot * tol
                             const float g2 = ga * ga, ab = al * be, dab = be - al;
-                            if (g2 > stop2 * ab || (g2 > close2 * ab && dab * dab <= dclose2 * (al + be)))
+                            const bool cl = dab * dab <= dclose2 * (al + be);
+                            if (!refine ? g2 > stop2 * ab
+                                        : (close_phase ? cl && g2 > close2 * ab
+                                                       : (!cl && g2 > stop2 * ab) || (!a.close_only && cl && g2 > close2 * ab)))
                                 s_flag[0] = 1;
                         }
                         devp = ndp;
@@ -449,7 +456,13 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
         }
         const int rotated = s_flag[0];
         __syncthreads();
-        if (!rotated) break;
+        if (!rotated) {
+            // refine: once no far pair rotates above stop_rel, sweeps touch only the close pairs
+            // (|mu_q - mu_p| <~ delta: the ones the refinement leaves alone) until they are
+            // within close_sigrot * tol
+            if (!(refine && a.close_only && !close_phase)) break;
+            close_phase = true;
+        }
         if (tid == 0) s_flag[0] = 0;
         __syncthreads();
     }
@@ -897,6 +910,7 @@ int cf_launch_eigen_flagged(cf_ctx* ctx, const cf_plan* plan, int emax, uint32_t
     args.stop_rel = ctx->stop_rel;
     args.refine_delta = ctx->refine_delta;
     args.close_sigrot = ctx->close_sigrot;
+    args.close_only = ctx->close_only;
     args.only_flag = flag;
     // units are sorted largest k first within a bucket, so the range's first unit has its kmax
     const uint32_t u0 = plan->h_order[first];
@@ -933,6 +947,7 @@ int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off
     args.stop_rel = ctx->stop_rel;
     args.refine_delta = ctx->refine_delta;
     args.close_sigrot = ctx->close_sigrot;
+    args.close_only = ctx->close_only;
     args.stats = ctx->d_stats;
     return launch_all_buckets(ctx, plan, args, stream);
 }

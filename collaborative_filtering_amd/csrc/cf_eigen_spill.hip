@@ -1455,7 +1455,15 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     {
         // (finer ranges run one after the other lost more to each range's tail than their
         // smaller slots gained: 4.88 vs 4.12 s on the config-5 sample's k <= 3072 users)
-        const uint32_t cuts[2] = {(uint32_t)SP_NL, 0u};
+        // compute_eigens: users above mc_min (default SP_NL) take the staged multi-CU path in
+        // the BIG layout; CF_SPILL_MC_MIN lowers the cut for A/B
+        static const uint32_t mc_min = [] {
+            const char* e = getenv("CF_SPILL_MC_MIN");
+            const long v = e ? atol(e) : (long)SP_NL;
+            return (uint32_t)std::max<long>(CF_MAX_K, std::min<long>(v, SP_NL));
+        }();
+        const bool user_mode = !loc || loc->mode == 0;
+        const uint32_t cuts[2] = {user_mode ? mc_min : (uint32_t)SP_NL, 0u};
         uint32_t j = b.first;
         const uint32_t end = b.first + b.count;
         auto kof = [&](uint32_t pos) {
