@@ -80,7 +80,7 @@ def parse():
     p.add_argument("--c5-onecall-users", type=int, default=10000,
                    help="config-5 sample of the one-call eigen leg (every user in one cf_eigen_run)")
     p.add_argument("--c5-kmax", type=int, default=5000, help="cap of the config-5 degrees (SURVEY 8d: 5000)")
-    p.add_argument("--c5-predict-kmax", type=int, default=3072,
+    p.add_argument("--c5-predict-kmax", type=int, default=5000,
                    help="predict the C5 sample's groups up to this k (the per-rating systems grow as k^3)")
     p.add_argument("--eigen-method", choices=["jacobi", "tridiag"],
                    default=os.environ.get("CF_EIGEN_METHOD", "jacobi"),
