@@ -96,6 +96,10 @@ class Context:
         """Jacobi sweeps to stop_rel, then the first-order Gram refinement (cf_set_eigen_refine)."""
         self._chk(self.lib.cf_set_eigen_refine(self.h, int(enable), stop_rel, delta), "cf_set_eigen_refine")
 
+    def set_step_masks(self, enable: bool = True):
+        """Eigen runs hand the predictor its complement masks (cf_set_step_masks)."""
+        self._chk(self.lib.cf_set_step_masks(self.h, int(enable)), "cf_set_step_masks")
+
     def debug_stats(self, enable: bool = True, read: bool = False):
         """Jacobi diagnostics (sweeps, per-phase s_memtime cycles) when read."""
         out = np.zeros(8, dtype=np.uint64) if read else None

@@ -79,7 +79,7 @@ int cf_create(int device, cf_ctx** out) {
     ctx->device = device;
     if (const char* e = getenv("CF_EIGEN_REFINE")) ctx->eigen_refine = e[0] != '0';   // A/B switches
     if (const char* e = getenv("CF_EIGEN_CLOSE")) ctx->close_sigrot = (float)atof(e);
-    if (const char* e = getenv("CF_EIGEN_CLOSEONLY")) ctx->close_only = e[0] != '0';
+    if (const char* e = getenv("CF_STEP_MASKS")) ctx->step_masks = e[0] != '0';
     if (hipSetDevice(device) != hipSuccess) {
         delete ctx;
         return CF_EHIP;
@@ -101,6 +101,7 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_phase) (void)hipFree(ctx->d_phase);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_pred_next) (void)hipFree(ctx->d_pred_next);
+    if (ctx->d_cmask) (void)hipFree(ctx->d_cmask);
     if (ctx->d_knn) (void)hipFree(ctx->d_knn);
     if (ctx->d_knn_acc) (void)hipFree(ctx->d_knn_acc);
     if (ctx->d_knn_part) (void)hipFree(ctx->d_knn_part);
@@ -188,6 +189,13 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps) {
     return CF_OK;
 }
 
+int cf_set_step_masks(cf_ctx* ctx, int enable) {
+    if (!ctx) return CF_EINVAL;
+    ctx->step_masks = enable != 0;
+    if (!ctx->step_masks) ctx->cmask_gen = ~0ull;   // the predictor gathers again from now on
+    return CF_OK;
+}
+
 int cf_set_eigen_refine(cf_ctx* ctx, int enable, float stop_rel, float delta) {
     if (!ctx || !(stop_rel > 0.0f) || !(delta >= 0.0f)) return cf_set_error(ctx, CF_EINVAL, "bad refine options");
     ctx->eigen_refine = enable != 0;
@@ -221,6 +229,8 @@ int cf_plan_create(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, cf_p
     CF_TRY(set_device(ctx));
     cf_plan* plan = new (std::nothrow) cf_plan();
     if (!plan) return cf_set_error(ctx, CF_ENOMEM, "plan allocation");
+    static std::atomic<uint64_t> next_plan_id{1};
+    plan->id = next_plan_id++;
     plan->n_users = n_users;
     plan->h_item_off.assign(item_off, item_off + n_users + 1);
     // Bucket by emax = ceil(k/16); within a bucket, largest k first (cost ~ k^3).

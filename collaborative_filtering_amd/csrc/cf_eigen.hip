@@ -102,7 +102,6 @@ struct EigenArgs {
     float stop_rel;
     float refine_delta;
     float close_sigrot;   // close pairs converge to close_sigrot * tol
-    int close_only;       // after the far pairs stop: sweeps over the close pairs only
     unsigned long long* stats;
     // kLocal / kSigma
     float* l2;                  // per movie n x n row-major L2 (kLocal writes, kSigma reads)
@@ -114,6 +113,10 @@ struct EigenArgs {
     const float* test_rating;
     float* wlim;                // kSigma output per pair
     const int* only_flag;       // non-null: run only units j with only_flag[blockIdx.x] != 0
+    // kUser, optional: the predictor's complement masks from the gathered W, 3 words per row at
+    // 3 * item_off[u] (bit i of word 3r + (i >> 6) = !(w(item_r -> item_i) > 0.1), cf_predict.hip)
+    uint64_t* cmask_out;
+    uint64_t cmask_words;       // its extent (users beyond it write none)
 };
 
 // Test rating of `user` for compact item `movie` (0 if absent): binary search of the
@@ -250,6 +253,18 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
         }
     }
     __syncthreads();
+    if (mode == kUser && a.cmask_out && 3 * (base + (uint64_t)k) <= a.cmask_words) {
+        // the predictor's complement masks (local_calc_precomp.cpp:254-265)
+        uint64_t* cm = a.cmask_out + 3 * base;
+        for (int r = wave; r < k; r += NW)
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const int i = 64 * t + lane;
+                const bool out = i < k && !((double)B[bidx(r, min(i, k - 1))] > 0.1);
+                const unsigned long long bal = __ballot(out);
+                if (lane == 0) cm[3 * r + t] = bal;
+            }
+    }
 
     // ---- 2. degrees, D^-1/2, diagonal of L2, sig_min -------------------------------
     for (int i = tid; i < k; i += NT) {
@@ -318,7 +333,6 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
     // close pairs, |mu_q - mu_p| <~ delta: (be - al)^2 <= 2 delta^2 (al + be) (al, be ~ mu^2)
     const float close2 = refine ? a.close_sigrot * a.close_sigrot * tol2 : stop2;
     const float dclose2 = refine ? 2.0f * a.refine_delta * a.refine_delta : -1.0f;
-    bool close_phase = false;
     // Squared column norms ||b_j||^2 (s_l2d is dead once B is assembled).  A step then
     // needs only the cross product ga = b_p . b_q: the rotated norms follow exactly from
     // (al, be, ga, c, s).  They are recomputed from the columns at every sweep start, and
@@ -378,9 +392,7 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
             f2* const bq0 = reinterpret_cast<f2*>(B + (s0 + f) * LD);
             for (int step = 0; step < FL; ++step) {
                 const int q = s0 + f + ti;
-                // close-only sweeps skip the far pairs before loading the traveling column
-                if (step < nlive && ti < tv &&
-                    !(close_phase && (s_nrm[q] - al) * (s_nrm[q] - al) > dclose2 * (al + s_nrm[q]))) {
+                if (step < nlive && ti < tv) {
                     const float dq = s_dev[q];   // issued with the column loads
                     const float be = s_nrm[q];
                     f2 xq[E2];
@@ -426,10 +438,7 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
                             // with the refinement: pairs closer than refine_delta in mu, which it
                             // leaves alone, still converge to kSigRot * tol
                             const float g2 = ga * ga, ab = al * be, dab = be - al;
-                            const bool cl = dab * dab <= dclose2 * (al + be);
-                            if (!refine ? g2 > stop2 * ab
-                                        : (close_phase ? cl && g2 > close2 * ab
-                                                       : (!cl && g2 > stop2 * ab) || (!a.close_only && cl && g2 > close2 * ab)))
+                            if (g2 > stop2 * ab || (g2 > close2 * ab && dab * dab <= dclose2 * (al + be)))
                                 s_flag[0] = 1;
                         }
                         devp = ndp;
@@ -456,13 +465,7 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
         }
         const int rotated = s_flag[0];
         __syncthreads();
-        if (!rotated) {
-            // refine: once no far pair rotates above stop_rel, sweeps touch only the close pairs
-            // (|mu_q - mu_p| <~ delta: the ones the refinement leaves alone) until they are
-            // within close_sigrot * tol
-            if (!(refine && a.close_only && !close_phase)) break;
-            close_phase = true;
-        }
+        if (!rotated) break;
         if (tid == 0) s_flag[0] = 0;
         __syncthreads();
     }
@@ -889,7 +892,7 @@ static int launch_emax(cf_ctx* ctx, int emax, const EigenArgs& args, uint32_t co
 int cf_launch_eigen_flagged(cf_ctx* ctx, const cf_plan* plan, int emax, uint32_t first, uint32_t count,
                             const int* flag, const uint64_t* d_item_off, const uint32_t* d_items,
                             const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals,
-                            float* d_evecs, hipStream_t stream) {
+                            float* d_evecs, hipStream_t stream, uint64_t* d_cmask) {
     if (count == 0) return CF_OK;
     EigenArgs args{};
     args.mode = kUser;
@@ -910,8 +913,9 @@ int cf_launch_eigen_flagged(cf_ctx* ctx, const cf_plan* plan, int emax, uint32_t
     args.stop_rel = ctx->stop_rel;
     args.refine_delta = ctx->refine_delta;
     args.close_sigrot = ctx->close_sigrot;
-    args.close_only = ctx->close_only;
     args.only_flag = flag;
+    args.cmask_out = d_cmask;
+    args.cmask_words = ctx->cmask_bytes / sizeof(uint64_t);
     // units are sorted largest k first within a bucket, so the range's first unit has its kmax
     const uint32_t u0 = plan->h_order[first];
     const uint32_t kmax = (uint32_t)(plan->h_item_off[u0 + 1] - plan->h_item_off[u0]);
@@ -922,6 +926,7 @@ int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off
                     const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m,
                     float* d_sigs, float* d_evals, float* d_evecs, hipStream_t stream) {
     if (ctx->eigen_method == CF_EIGEN_TRIDIAG) {
+        cf_cmask_mark(ctx, plan, d_item_off, d_items, false);
         for (const cf_bucket& b : plan->buckets)
             if (b.emax == kSpillBucket && b.count)
                 CF_TRY(cf_launch_eigen_spill(ctx, plan, b, d_item_off, d_items, d_evec_off, d_m, d_sigs, d_evals,
@@ -947,7 +952,11 @@ int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off
     args.stop_rel = ctx->stop_rel;
     args.refine_delta = ctx->refine_delta;
     args.close_sigrot = ctx->close_sigrot;
-    args.close_only = ctx->close_only;
     args.stats = ctx->d_stats;
-    return launch_all_buckets(ctx, plan, args, stream);
+    args.cmask_out = cf_cmask_buffer(ctx, plan);   // the predictor's complement masks
+    args.cmask_words = ctx->cmask_bytes / sizeof(uint64_t);
+    cf_cmask_mark(ctx, plan, d_item_off, d_items, false);
+    const int rc = launch_all_buckets(ctx, plan, args, stream);
+    cf_cmask_mark(ctx, plan, d_item_off, d_items, rc == CF_OK && args.cmask_out);
+    return rc;
 }

@@ -145,6 +145,7 @@ __global__ __launch_bounds__(kGT) void row_compact_kernel(uint64_t n, const floa
 }
 
 void free_graph(cf_ctx* ctx) {
+    ++ctx->graph_gen;   // complement masks of earlier eigen runs no longer apply
     if (ctx->d_graph) (void)hipFree(ctx->d_graph);
     if (ctx->d_grp) (void)hipFree(ctx->d_grp);
     if (ctx->d_gcol) (void)hipFree(ctx->d_gcol);

@@ -65,7 +65,6 @@ struct cf_ctx {
     float stop_rel = 1e-3f;
     float refine_delta = 1e-2f;
     float close_sigrot = 8.0f;    // pairs closer than refine_delta: sweeps to close_sigrot * tol
-    int close_only = 1;           // ... in sweeps that skip the far pairs once those are done
     // Optional device counters: [0] sum of sweeps, [1] users, [2] max sweeps, [3] capped users.
     unsigned long long* d_stats = nullptr;
     // Optional predictor phase-cycle counters (16 slots), see cf_debug_phases.
@@ -75,6 +74,15 @@ struct cf_ctx {
     size_t scratch_bytes = 0;
     // fused predictor: one user counter per predictor stream (zeroed before each launch)
     uint32_t* d_pred_next = nullptr;
+    // the complement masks the eigen kernel hands to the predictor (24 B per rating), valid for
+    // the plan / item arrays / graph generation of the eigen run that wrote them (cf_cmask_*)
+    void* d_cmask = nullptr;
+    size_t cmask_bytes = 0;
+    uint64_t cmask_plan = 0;                            // cf_plan::id of that run
+    const void* cmask_key[2] = {nullptr, nullptr};      // its item_off, items
+    uint64_t cmask_gen = ~0ull;
+    uint64_t graph_gen = 0;   // bumped by every graph (re)load (free_graph)
+    int step_masks = 1;       // cf_set_step_masks (env CF_STEP_MASKS=0 for A/B runs)
     // knn2 rating planes (R, S, B), grown on demand.
     void* d_knn = nullptr;
     size_t knn_bytes = 0;
@@ -154,6 +162,7 @@ struct cf_tri_group {   // plan-order range sharing one QL-record buffer and one
 };
 
 struct cf_plan {
+    uint64_t id = 0;   // unique per process (cf_plan_create), never reused
     uint32_t n_users = 0;
     uint64_t n_entries = 0;
     // tridiagonal eigen path (cf_eigen_tri.hip): chunks and per-user QL record offsets
@@ -281,11 +290,19 @@ int cf_launch_eigen_tri(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item
                         const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals, float* d_evecs,
                         hipStream_t stream);
 // Jacobi kernel over plan order [first, first + count) of LDS bucket emax, only for users
-// with flag[j - first] != 0 (fallback of the tridiagonal path).
+// with flag[j - first] != 0 (fallback of the tridiagonal path); d_cmask (optional) receives
+// the predictor's complement masks, 3 words per rating at 3 * item_off[u] (the fused step).
 int cf_launch_eigen_flagged(cf_ctx* ctx, const cf_plan* plan, int emax, uint32_t first, uint32_t count,
                             const int* flag, const uint64_t* d_item_off, const uint32_t* d_items,
                             const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals,
-                            float* d_evecs, hipStream_t stream);
+                            float* d_evecs, hipStream_t stream, uint64_t* d_cmask = nullptr);
+// Complement masks of the LDS-bucket users (cf_predict.hip): the buffer an eigen run over `plan`
+// writes (null: disabled by CF_STEP_MASKS=0 or no HBM), marked valid once launched, and looked
+// up by a predictor run over the same plan, item arrays and graph.
+uint64_t* cf_cmask_buffer(cf_ctx* ctx, const cf_plan* plan);
+void cf_cmask_mark(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items, bool valid);
+const uint64_t* cf_cmask_lookup(const cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
+                                const uint32_t* d_items);
 int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
                     const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m,
                     float* d_sigs, float* d_evals, float* d_evecs, hipStream_t stream);

@@ -106,16 +106,43 @@ struct PredArgs {
     int ew;                // doubles of per-wave fast-path scratch (system + y + g)
     int a_elems;           // doubles of the rating kernel's shared factorisation region
     int big_lds;           // 1: the block-wide systems use the LDS region A
+    int tail_basis;        // 1: the last joint step writes only X's columns from Lmin on
+    const uint64_t* cmask_in;   // the eigen kernel's complement masks (fused step), or null
+    uint64_t cmask_words;       // their extent (users beyond it gather the graph)
     double* slots;         // per-user slots of the chunk
     SlotOff so;
 };
 
 
+#ifdef CF_PRED_SHFL_SUM   // A/B: the LDS-permute butterfly (six dependent ds_bpermute pairs)
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
     return v;
 }
+#else
+// lane i's value exchanged with lane perm(i) inside its row of 16 (DPP: no LDS round trip)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double lane_f64(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+// Sum over the wave, the same bits in every lane: a butterfly inside each row of 16 (quad
+// permutes xor 1 and xor 2, then the half-row and row mirrors pair the quads and the halves;
+// each pair adds the same two operands in both lanes), then the four row sums in a fixed order.
+// Called with every lane active.
+__device__ __forceinline__ double wave_sum(double v) {
+    v += dpp_f64<0xB1>(v);    // quad_perm [1, 0, 3, 2]
+    v += dpp_f64<0x4E>(v);    // quad_perm [2, 3, 0, 1]
+    v += dpp_f64<0x141>(v);   // row_half_mirror
+    v += dpp_f64<0x140>(v);   // row_mirror
+    return (lane_f64(v, 0) + lane_f64(v, 16)) + (lane_f64(v, 32) + lane_f64(v, 48));
+}
+#endif
 
 // Block-wide ordered compaction of flags[0..n): writes the indices with flag set to
 // out[] in ascending order and returns their count.  n <= 256.
@@ -370,7 +397,10 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
         const T* ev = a.evals + base;
         __syncthreads();
         PHASE_STAMP(-1);
-        if (tid == 0) s_cnt[5] = 0;
+        if (tid == 0) {
+            s_cnt[5] = 0;
+            s_cnt[10] = CF_MAX_K;
+        }
         for (int j = tid; j < m; j += kThreads) A[j] = (double)ev[j];   // evals staged in A
         __syncthreads();
         for (int i = tid; i < k; i += kThreads) {
@@ -392,6 +422,7 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
             lim = min(max(lim, 2), m);
             s_lim[i] = lim;
             atomicMax(&s_cnt[5], lim);
+            atomicMin(&s_cnt[10], lim);
         }
         if (wave == 0) {
             double sum = 0.0;
@@ -401,8 +432,16 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
         }
         __syncthreads();
         const int Lu = s_cnt[5];
-        // complement masks, kMaskRows graph rows in flight per wave (unconditional clamped
-        // loads, see block_gemm), then nc of every row in s_slow (free until the fast path)
+        // complement masks: from the eigen kernel, which gathered the same graph entries (fused
+        // step), else kMaskRows graph rows in flight per wave (unconditional clamped loads, see
+        // block_gemm); nc of every row in s_slow (free until the fast path)
+        if (a.cmask_in && 3 * (base + (uint64_t)k) <= a.cmask_words) {
+            const uint64_t* cm = a.cmask_in + 3 * base;
+            for (int i = tid; i < 3 * k; i += kThreads) s_cmask[i] = cm[i];
+            __syncthreads();
+            for (int r = tid; r < k; r += kThreads)
+                s_slow[r] = __popcll(s_cmask[3 * r]) + __popcll(s_cmask[3 * r + 1]) + __popcll(s_cmask[3 * r + 2]);
+        } else
         for (int r0 = kMaskRows * wave; r0 < k; r0 += kMaskRows * kWaves) {
             float gv[kMaskRows][3];
 #pragma unroll
@@ -503,6 +542,7 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
         const int ld = lmax;
         double* Xf = Xb;   // the final basis
         int Lx = 0;        // 0: no basis (every rating of the user takes the dense path)
+        int jlo = 0;       // first column of Xf the last joint step wrote (a multiple of 64)
         if (Lq > 0) {
             // the W-failure flag is cleared before the barrier that ends the Q product, so every
             // thread reads it cleared below also when there is no complement (du == 0)
@@ -617,18 +657,25 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
             if (a.phase_cycles && tid == 0) ph_acc[7] += __builtin_amdgcn_s_memtime() - tw0;
             const unsigned long long tj0 = (a.phase_cycles && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
 #endif
-            // joint T steps on X (k columns): X^T X packed in AP, X <- X T (ping-pong Xb/Q1)
+            // joint T steps on X (k columns): X^T X packed in AP, X <- X T (ping-pong Xb/Q1).
+            // The ratings read only the columns [lim, k) of X, lim >= Lmin, and T is upper
+            // triangular, so the last step needs only the column blocks from jlo = Lmin rounded
+            // down to 64 on: the Gram rows i >= jlo (every G(l, j), l <= j, of those columns)
+            // and the product columns j >= jlo.  A step that another one must follow needs the
+            // whole X: its Gram is then redone in full (jlo = 0) before the product.
             double* Xs = Xb;
             double* Xd = Q1;
+            jlo = a.tail_basis ? (min(s_cnt[10], k) & ~63) : 0;
             if (s_cnt[9] == 0) {
                 for (int it = 0; it < 3; ++it) {
                     if (tid == 0) s_cnt[6] = 0;
                     __syncthreads();
                     float dv = 0.0f;
+                    const int glo = jlo;
                     block_gemm<false, false>(
                         k, k, [&](int i, int l) { return Xs[(size_t)l * ld + i]; }, as_double,
                         [&](int l, int j) { return Xs[(size_t)l * ld + j]; }, as_double, [&](int) { return k; },
-                        lower_blocks,
+                        [glo](int i0, int j0) { return j0 <= i0 && i0 >= glo; },
                         [&](int i, int j, double v) {
                             if (j > i) return;
                             AP[tri(i, j)] = v;
@@ -641,10 +688,17 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
                     __syncthreads();
                     const float dev_x = __int_as_float(s_cnt[6]);
                     if (!(dev_x <= (float)kOrthoMax)) break;   // no basis: Lx stays 0
+                    if (glo > 0 && !(dev_x <= kOrthoDone)) {   // another step follows: full Gram
+                        jlo = 0;
+                        --it;
+                        __syncthreads();   // every thread has read dev_x before s_cnt[6] is reset
+                        continue;
+                    }
                     const auto k_end = [&](int j0) { return min(k, j0 + 64); };
                     block_gemm<true, false>(
                         k, k, [&](int i, int l) { return Xs[(size_t)i * ld + l]; }, as_double,
-                        [&](int l, int j) { return AP[tri(max(l, j), min(l, j))]; }, tri_T, k_end, all_blocks,
+                        [&](int l, int j) { return AP[tri(max(l, j), min(l, j))]; }, tri_T, k_end,
+                        [glo](int, int j0) { return j0 >= glo; },
                         [&](int i, int j, double v) { Xd[(size_t)i * ld + j] = v; }, stage);
                     __syncthreads();
                     double* tmp = Xs;
@@ -665,7 +719,7 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
         double* s_gx = slot + a.so.gx;
         double* s_hx = slot + a.so.hx;
         if (Lx > 0)
-            for (int j = tid; j < k; j += kThreads) {
+            for (int j = jlo + tid; j < k; j += kThreads) {
                 double g0 = 0.0, g1 = 0.0, h0 = 0.0, h1 = 0.0;
                 int i = 0;
                 for (; i + 1 < k; i += 2) {
@@ -1427,6 +1481,16 @@ inline bool pred_fused_enabled() {
     return on;
 }
 
+// CF_PRED_TAIL=0 makes the last joint basis step write every column of X (A/B runs); default:
+// only the column blocks the ratings read (from Lmin = min_r lim_r on).
+inline int pred_tail_basis() {
+    static const int on = [] {
+        const char* e = std::getenv("CF_PRED_TAIL");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    return on;
+}
+
 // Fused launch of a bucket: dynamic LDS = the larger of the two halves, grid = the
 // workgroups resident at once (capped by the launch bounds the slot set was sized for).
 template <typename T>
@@ -1467,6 +1531,9 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
     args.kk = d_kk;
     args.pred = d_pred;
     args.phase_cycles = ctx->d_phase;
+    args.tail_basis = pred_tail_basis();
+    args.cmask_in = cf_cmask_lookup(ctx, plan, d_item_off, d_items);
+    args.cmask_words = ctx->cmask_bytes / sizeof(uint64_t);
     int rc = CF_OK;
     // Slots for one chunk of the largest LDS bucket, per stream; the chunks of every bucket
     // alternate between two context-owned streams (fork/join by events with the caller's
@@ -1623,6 +1690,13 @@ int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
     args.mse = d_mse;
     args.kk = d_kk;
     args.pred = d_pred;
+    args.tail_basis = pred_tail_basis();
+    // the eigen kernels hand the predictor its complement masks (24 B per rating); without the
+    // buffer (CF_STEP_MASKS=0, or no HBM for it) the basis kernel gathers the graph itself
+    uint64_t* d_cmask = cf_cmask_buffer(ctx, plan);
+    cf_cmask_mark(ctx, plan, d_item_off, d_items, false);
+    args.cmask_in = d_cmask;
+    args.cmask_words = ctx->cmask_bytes / sizeof(uint64_t);
     uint32_t kChunk = fit_chunk(ctx, plan, 2);
     CF_TRY(ensure_slot_scratch(ctx, plan, 2, kChunk));
     const size_t need = chunk_slot_bytes(plan, kChunk);   // one copy
@@ -1663,7 +1737,7 @@ int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
             continue;
         }
         rc = cf_launch_eigen_flagged(ctx, plan, b.emax, b.first, b.count, nullptr, d_item_off, d_items, d_evec_off,
-                                     d_m, d_sigs, d_evals, d_evecs, est);
+                                     d_m, d_sigs, d_evals, d_evecs, est, d_cmask);
         if (rc != CF_OK) break;
         CF_STEP_CHECK(hipEventRecord(ctx->step_bucket_ev[bi], est));
         size_t rating_lds = 0;
@@ -1701,7 +1775,40 @@ int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
         CF_HIP_CHECK(ctx, hipStreamWaitEvent(stream, ctx->step_sync_ev[1 + i], 0));
     }
     CF_HIP_CHECK(ctx, hipEventRecord(ctx->step_time_ev[2], stream));
+    cf_cmask_mark(ctx, plan, d_item_off, d_items, rc == CF_OK && d_cmask);
     return rc;
+}
+
+uint64_t* cf_cmask_buffer(cf_ctx* ctx, const cf_plan* plan) {
+    if (!ctx->step_masks || !plan->n_users) return nullptr;
+    const size_t mb = 3 * sizeof(uint64_t) * (size_t)plan->h_item_off[plan->n_users];
+    if (mb > ctx->cmask_bytes) {
+        if (ctx->d_cmask) (void)hipFree(ctx->d_cmask);
+        ctx->d_cmask = nullptr;
+        ctx->cmask_bytes = 0;
+        ctx->cmask_gen = ~0ull;
+        if (hipMalloc(&ctx->d_cmask, mb) != hipSuccess) {   // optional: the predictor gathers instead
+            (void)hipGetLastError();
+            ctx->d_cmask = nullptr;
+            return nullptr;
+        }
+        ctx->cmask_bytes = mb;
+    }
+    return static_cast<uint64_t*>(ctx->d_cmask);
+}
+
+void cf_cmask_mark(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items, bool valid) {
+    ctx->cmask_plan = plan->id;
+    ctx->cmask_key[0] = d_item_off;
+    ctx->cmask_key[1] = d_items;
+    ctx->cmask_gen = valid ? ctx->graph_gen : ~0ull;
+}
+
+const uint64_t* cf_cmask_lookup(const cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
+                                const uint32_t* d_items) {
+    const bool hit = ctx->d_cmask && ctx->cmask_gen == ctx->graph_gen && ctx->cmask_plan == plan->id &&
+                     ctx->cmask_key[0] == d_item_off && ctx->cmask_key[1] == d_items;
+    return hit ? static_cast<const uint64_t*>(ctx->d_cmask) : nullptr;
 }
 
 template int cf_launch_predict<float>(cf_ctx*, const cf_plan*, const uint64_t*, const uint32_t*,

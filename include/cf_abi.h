@@ -74,6 +74,14 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
  * are more than delta apart.  Defaults: enable 1, stop_rel 1e-3, delta 1e-2; pairs closer than delta sweep to 8 tol.
  * enable 0 restores the sweeps-only rule (stop after a sweep with no rotation above 16 tol). */
 int cf_set_eigen_refine(cf_ctx* ctx, int enable, float stop_rel, float delta);
+/* Complement-mask handoff (default on): an eigen run over a plan (cf_eigen_run, cf_step_run)
+ * also writes, per rating, the 3 x 64-bit mask of the user's items that are NOT out-neighbours
+ * (w <= 0.1) of that item, from the graph entries it gathers anyway (24 B per rating of HBM,
+ * owned by the context); a later cf_predict_run* over the same plan, the same item arrays and the
+ * same graph reads them instead of re-gathering k^2 graph entries per user.  Outputs are
+ * bit-identical either way.  enable 0 frees nothing but makes every predictor run gather.
+ * Replaces the per-rating neighbour scan of local_calc_precomp.cpp:254-265. */
+int cf_set_step_masks(cf_ctx* ctx, int enable);
 /* Diagnostics: enable != 0 allocates device counters that the eigen kernel fills;
  * out8 (optional) receives and resets {sum of sweeps, users, max sweeps, users that
  * hit the sweep cap, assembly cycles, Jacobi cycles, epilogue cycles, tournament

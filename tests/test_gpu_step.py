@@ -95,3 +95,59 @@ def test_fused_predictor_equals_two_kernel_path():
                        env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stdout[-4000:] + p.stderr[-2000:]
     assert "2 passed" in p.stdout, p.stdout[-2000:]
+
+
+def test_mask_handoff_bit_identical_and_invalidated(gpu_ctx):
+    """The complement masks the eigen kernel hands to the predictor (cf_set_step_masks) give the
+    same bits as the predictor's own graph gather; a graph reload or another item array makes the
+    predictor gather again (a stale mask set would change the connected sets)."""
+    torch = pytest.importorskip("torch")
+    seed, n_items = 2026101503, 1500
+    k = synth.degrees(seed, 3000, k_median=80.0, sigma=0.6, kmin=2, kmax=192)
+    k[[3, 2000]] = [250, 205]          # spill users (no masks on their path)
+    off, items, rats = synth.user_items(seed, k, n_items, threads=8)
+    W = synth.graph_model(seed, n_items, threads=8)
+    dev = torch.device("cuda")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    eoff, ne = evec_offsets(off)
+    n, U = int(off[-1]), len(k)
+    d_off, d_items, d_rat, d_eoff = T(off.view(np.int64)), T(items.view(np.int32)), T(rats), T(eoff.view(np.int64))
+    plan = gpu_ctx.plan(off)
+
+    def run(masks, eigen=True, rec=None):
+        gpu_ctx.set_step_masks(masks)
+        o = {key: rec[key] for key in ("m", "sigs", "evals", "evecs")} if rec else dict(
+            m=torch.zeros(U, dtype=torch.int32, device=dev), sigs=torch.zeros(n, device=dev),
+            evals=torch.zeros(n, device=dev), evecs=torch.zeros(ne, device=dev))
+        if eigen:
+            plan.eigen_run(d_off, d_items, d_eoff, o["m"], o["sigs"], o["evals"], o["evecs"])
+        o["mse"] = torch.zeros(n, device=dev)
+        o["kk"] = torch.zeros(n, dtype=torch.int32, device=dev)
+        o["pred"] = torch.zeros(n, dtype=torch.float64, device=dev)
+        plan.predict_run(d_off, d_items, d_rat, o["m"], o["evals"], d_eoff, o["evecs"], o["sigs"], CF_SIGS_COMPAT,
+                         o["mse"], o["kk"], o["pred"])
+        torch.cuda.synchronize()
+        return o
+
+    def same(x, y):
+        for key in ("mse", "kk", "pred"):
+            a, b = x[key].cpu().numpy(), y[key].cpu().numpy()
+            assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), key
+
+    try:
+        for layout in ("dense", "csr"):
+            gpu_ctx.set_graph_layout(layout)
+            gpu_ctx.upload_graph_dense(W)
+            with_masks = run(True)
+            same(with_masks, run(False, eigen=False, rec=with_masks))
+            # another graph: the masks of the eigen run above must not be used
+            W2 = W.copy()
+            W2[W2 > 0] = np.where(np.random.default_rng(1).random(int((W2 > 0).sum())) < 0.5, 0.05, 0.9)
+            gpu_ctx.upload_graph_dense(W2)
+            gpu_ctx.set_step_masks(True)
+            stale = run(True, eigen=False, rec=with_masks)
+            same(stale, run(False, eigen=False, rec=with_masks))
+    finally:
+        gpu_ctx.set_step_masks(True)
+        gpu_ctx.set_graph_layout("dense")
+        plan.close()

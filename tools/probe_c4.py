@@ -54,6 +54,8 @@ for f, name in ((eig, "eigen"), (pred, "predict")):
     e1.synchronize()
     print(f"{name}: {e0.elapsed_time(e1):.1f} ms for {users} users / {n} ratings", flush=True)
 
+if os.environ.get("PROBE_SAVE"):   # outputs of the timed configuration, for A/B equality checks
+    np.savez(os.environ["PROBE_SAVE"], mse=d["mse"].cpu().numpy(), kk=d["kk"].cpu().numpy())
 ctx.debug_phases(True)
 pred()
 torch.cuda.synchronize()
