@@ -144,6 +144,22 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 #endif
 
+// 1 / d for an LDL^T pivot: v_rcp_f64 and two Newton steps (5 dependent ops; the IEEE
+// division is a ~10-op chain with scale / fixup steps) -- within an ulp or two of 1 / d for
+// the normal pivots the fast path factors (|d| in [1e-300, 1e300]); CF_PRED_IEEE_DIV restores
+// the division (A/B)
+__device__ __forceinline__ double pivot_rcp(double d) {
+#ifdef CF_PRED_IEEE_DIV
+    return 1.0 / d;
+#else
+    double x = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, x, 1.0);
+    x = fma(x, e, x);
+    e = fma(-d, x, 1.0);
+    return fma(x, e, x);
+#endif
+}
+
 // Block-wide ordered compaction of flags[0..n): writes the indices with flag set to
 // out[] in ascending order and returns their count.  n <= 256.
 __device__ int block_compact(bool flag, int idx, int* out, int* s_cnt) {
@@ -1003,7 +1019,7 @@ __device__ __forceinline__ void rating_user(const PredArgs<T> a, uint32_t uo, do
 #pragma unroll
                         for (int s2 = 0; s2 < t; ++s2) d = fma(-Lm[t][s2] * Dv[s2], Lm[t][s2], d);
                         Dv[t] = d;
-                        Di[t] = d != 0.0 ? 1.0 / d : 0.0;   // exact-zero pivot: column skipped
+                        Di[t] = d != 0.0 ? pivot_rcp(d) : 0.0;   // exact-zero pivot: column skipped
                     }
 #pragma unroll
                     for (int t = 0; t < kLdlPw; ++t)

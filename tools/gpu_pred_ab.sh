@@ -12,10 +12,12 @@ run intree CF_NOTHING=1
 run tail0 CF_PRED_TAIL=0
 run shfl CF_MI355X_LIB=$GRAFT_REPO_ROOT/collaborative_filtering_amd/variants/libcf_shfl.so
 run nomask CF_STEP_MASKS=0
+[ -e collaborative_filtering_amd/variants/libcf_ieee.so ] && run ieee CF_MI355X_LIB=$GRAFT_REPO_ROOT/collaborative_filtering_amd/variants/libcf_ieee.so
 python - <<'PY'
 import numpy as np
 a = np.load("gpurun_out/pab_intree.npz")
-for nm in ("tail0", "shfl", "nomask"):
+import os
+for nm in [x for x in ("tail0", "shfl", "nomask", "ieee") if os.path.exists(f"gpurun_out/pab_{x}.npz")]:
     b = np.load(f"gpurun_out/pab_{nm}.npz")
     d = np.abs(a["mse"].astype(np.float64) - b["mse"])
     print(nm, "kk equal", bool((a["kk"] == b["kk"]).all()), "mse bits differ", int((a["mse"].view(np.uint32) != b["mse"].view(np.uint32)).sum()),
