@@ -1455,11 +1455,13 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     {
         // (finer ranges run one after the other lost more to each range's tail than their
         // smaller slots gained: 4.88 vs 4.12 s on the config-5 sample's k <= 3072 users)
-        // compute_eigens: users above mc_min (default SP_NL) take the staged multi-CU path in
-        // the BIG layout; CF_SPILL_MC_MIN lowers the cut for A/B
+        // compute_eigens: users above mc_min take the staged multi-CU path in the BIG layout.
+        // Default 1536: on the config-5 sample's 292 users with 192 < k <= 3072 the spill group
+        // eigen went 4.08 -> 1.24 s (cut 3072 -> 1536; 1024: 1.41 s; profiles/r04/c5_mc_cut/);
+        // CF_SPILL_MC_MIN overrides (A/B)
         static const uint32_t mc_min = [] {
             const char* e = getenv("CF_SPILL_MC_MIN");
-            const long v = e ? atol(e) : (long)SP_NL;
+            const long v = e ? atol(e) : 1536L;
             return (uint32_t)std::max<long>(CF_MAX_K, std::min<long>(v, SP_NL));
         }();
         const bool user_mode = !loc || loc->mode == 0;

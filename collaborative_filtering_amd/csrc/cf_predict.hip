@@ -114,13 +114,6 @@ struct PredArgs {
 };
 
 
-#ifdef CF_PRED_SHFL_SUM   // A/B: the LDS-permute butterfly (six dependent ds_bpermute pairs)
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-    return v;
-}
-#else
 // lane i's value exchanged with lane perm(i) inside its row of 16 (DPP: no LDS round trip)
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
@@ -128,6 +121,23 @@ __device__ __forceinline__ double dpp_f64(double v) {
     const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
     return __hiloint2double(hi, lo);
 }
+// Sum over each row of 16 lanes, the same bits in all 16 (quad permutes xor 1 and xor 2, then
+// the half-row and row mirrors pair the quads and the halves; each pair adds the same two
+// operands in both lanes).  Every lane of the row active.
+__device__ __forceinline__ double row16_sum(double v) {
+    v += dpp_f64<0xB1>(v);    // quad_perm [1, 0, 3, 2]
+    v += dpp_f64<0x4E>(v);    // quad_perm [2, 3, 0, 1]
+    v += dpp_f64<0x141>(v);   // row_half_mirror
+    v += dpp_f64<0x140>(v);   // row_mirror
+    return v;
+}
+#ifdef CF_PRED_SHFL_SUM   // A/B: the LDS-permute butterfly (six dependent ds_bpermute pairs)
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+#else
 __device__ __forceinline__ double lane_f64(double v, int l) {
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
 }
@@ -136,10 +146,7 @@ __device__ __forceinline__ double lane_f64(double v, int l) {
 // each pair adds the same two operands in both lanes), then the four row sums in a fixed order.
 // Called with every lane active.
 __device__ __forceinline__ double wave_sum(double v) {
-    v += dpp_f64<0xB1>(v);    // quad_perm [1, 0, 3, 2]
-    v += dpp_f64<0x4E>(v);    // quad_perm [2, 3, 0, 1]
-    v += dpp_f64<0x141>(v);   // row_half_mirror
-    v += dpp_f64<0x140>(v);   // row_mirror
+    v = row16_sum(v);
     return (lane_f64(v, 0) + lane_f64(v, 16)) + (lane_f64(v, 32) + lane_f64(v, 48));
 }
 #endif
@@ -200,7 +207,11 @@ constexpr int kStageNbuf = 2;                       // chunks alternate buffers:
 #endif
 constexpr int kStageElems = kStageNbuf * kStageBuf;
 using f64x4 = __attribute__((ext_vector_type(4))) double;
-template <bool A_LFAST, bool B_LFAST, class LA, class XA, class LB, class XB, class FK, class FW, class FO>
+// MFMAs of 16 x 16 tiles that hold no output are skipped (wave-uniform): tiles past M or N,
+// and with LOWER (callers that keep only j <= i) tiles wholly above the diagonal -- at k = 107
+// that is 7 x 7 of the 8 x 8 tiles of a k x k product, and 6 of 16 in a diagonal block.
+template <bool A_LFAST, bool B_LFAST, bool LOWER = false, class LA, class XA, class LB, class XB, class FK, class FW,
+          class FO>
 __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK kend, FW want, FO out,
                            double* stage) {
     int tid = threadIdx.x;
@@ -213,6 +224,18 @@ __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK ke
         for (int j0 = 0; j0 < N; j0 += 64) {
             if (!want(i0, j0)) continue;
             const int K = kend(j0);
+            bool live[2][2];
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y) {
+                    const int ti = i0 + 32 * wr + 16 * x, tj = j0 + 32 * wc + 16 * y;
+#ifdef CF_PRED_GEMM_NOSKIP   // A/B: every tile of the block
+                    live[x][y] = ti == ti && tj == tj;
+#else
+                    live[x][y] = ti < M && tj < N && (!LOWER || tj <= ti + 15);
+#endif
+                }
             f64x4 acc[2][2];
 #pragma unroll
             for (int x = 0; x < 2; ++x)
@@ -270,7 +293,8 @@ __device__ void block_gemm(int M, int N, LA loadA, XA xA, LB loadB, XB xB, FK ke
                     for (int x = 0; x < 2; ++x)
 #pragma unroll
                         for (int y = 0; y < 2; ++y)
-                            acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
+                            if (live[x][y])
+                                acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
                 }
             };
             if (K > 0) fetch(0, ra0, rb0);
@@ -398,6 +422,9 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
     // item r with w > 0.1 (:254-265); fast-path rating order (largest nc first)
     uint64_t* s_cmask = reinterpret_cast<uint64_t*>(s_cnt + 12);
     int* s_order = reinterpret_cast<int*>(s_cmask + 3 * CF_MAX_K);
+    // per row: the smallest column j whose rows with U(i, j) >= 1e-4 are this row alone (a
+    // single-complement rating of the row drops j if j < lim); -1 once the row is predicted here
+    int* s_dmin = s_order + CF_MAX_K;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -416,6 +443,7 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
         if (tid == 0) {
             s_cnt[5] = 0;
             s_cnt[10] = CF_MAX_K;
+            s_cnt[11] = CF_MAX_K;   // first column with no U(i, j) >= 1e-4
         }
         for (int j = tid; j < m; j += kThreads) A[j] = (double)ev[j];   // evals staged in A
         __syncthreads();
@@ -437,6 +465,7 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
             }
             lim = min(max(lim, 2), m);
             s_lim[i] = lim;
+            s_dmin[i] = CF_MAX_K;
             atomicMax(&s_cnt[5], lim);
             atomicMin(&s_cnt[10], lim);
         }
@@ -506,7 +535,7 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
         const auto as_double = [](int, int, auto v) { return (double)v; };
         // T(l, j) from a symmetric G: -G(l, j) (l < j), 1.5 - G(j, j) / 2 (l = j), 0 (l > j)
         const auto tri_T = [](int l, int j, double g) { return l < j ? -g : (l == j ? 1.5 - 0.5 * g : 0.0); };
-        block_gemm<false, false>(
+        block_gemm<false, false, true>(
             Lu, Lu, [&](int i, int l) { return U[(size_t)l * m + i]; }, as_double,
             [&](int l, int j) { return U[(size_t)l * m + j]; }, as_double, [&](int) { return k; }, lower_blocks,
             [&](int i, int j, double v) {
@@ -527,7 +556,7 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
         {
             uint64_t* pm_g = reinterpret_cast<uint64_t*>(slot + a.so.pmask);
             for (int j = tid; j < Lu; j += kThreads) {
-                int cnt = 0;
+                int cnt = 0, sole = 0;
 #pragma unroll
                 for (int w = 0; w < 3; ++w) {
                     uint64_t bits = 0;
@@ -542,8 +571,11 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
                     }
                     pm_g[3 * j + w] = bits;
                     cnt += __popcll(bits);
+                    if (bits) sole = 64 * w + __builtin_ctzll(bits);
                 }
                 s_cpos[j] = cnt;
+                if (cnt == 0) atomicMin(&s_cnt[11], j);
+                if (cnt == 1) atomicMin(&s_dmin[sole], j);
             }
         }
         __syncthreads();
@@ -610,7 +642,7 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
                     all_blocks, [&](int i, int j, double v) { Xb[(size_t)i * ld + Lq + j] = omega(i, j) - v; }, stage);
                 __syncthreads();
                 // Y^T Y (du x du, packed lower) -> AP, L D L^T in place
-                block_gemm<false, false>(
+                block_gemm<false, false, true>(
                     du, du, [&](int i, int l) { return Xb[(size_t)l * ld + Lq + i]; }, as_double,
                     [&](int l, int j) { return Xb[(size_t)l * ld + Lq + j]; }, as_double, [&](int) { return k; },
                     lower_blocks, [&](int i, int j, double v) { if (j <= i) AP[tri(i, j)] = v; }, stage);
@@ -688,7 +720,7 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
                     __syncthreads();
                     float dv = 0.0f;
                     const int glo = jlo;
-                    block_gemm<false, false>(
+                    block_gemm<false, false, true>(
                         k, k, [&](int i, int l) { return Xs[(size_t)l * ld + i]; }, as_double,
                         [&](int l, int j) { return Xs[(size_t)l * ld + j]; }, as_double, [&](int) { return k; },
                         [glo](int i0, int j0) { return j0 <= i0 && i0 >= glo; },
@@ -734,6 +766,9 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
         // X^T r and X^T 1, the rating-level arrays and the flags into the slot
         double* s_gx = slot + a.so.gx;
         double* s_hx = slot + a.so.hx;
+        double* gxl = A;                 // LDS copies for the closed form below (staging is idle)
+        double* hxl = A + CF_MAX_K;
+        int* s_list = reinterpret_cast<int*>(A + 2 * CF_MAX_K);
         if (Lx > 0)
             for (int j = jlo + tid; j < k; j += kThreads) {
                 double g0 = 0.0, g1 = 0.0, h0 = 0.0, h1 = 0.0;
@@ -750,10 +785,62 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
                     g0 = fma(x0, (double)s_rat[i], g0);
                     h0 += x0;
                 }
-                s_gx[j] = g0 + g1;
-                s_hx[j] = h0 + h1;
+                s_gx[j] = gxl[j] = g0 + g1;
+                s_hx[j] = hxl[j] = h0 + h1;
             }
         __syncthreads();
+        // ---- single-complement ratings (Cbar = {r}, nc = 1: about a third of C4's) in closed
+        // form here, instead of one rating-kernel wave each.  The fast path's K-mode at n = 1:
+        // K = x.x with x = X[r, lim:k], b = x.g - K y_r (g = (X^T r - mu X^T 1)[lim:k], y_r = r_r -
+        // mu), then its 1 x 1 LDL^T bordered by b and e_r: pred = mu - ((b / K)(1 / K)) K.  A row
+        // whose column filter drops a column (P_j within {r}: s_cnt[11], s_dmin) or whose K is
+        // below kPivMin stays with the rating kernel.  16 lanes per row, DPP row sums.
+        int n_rate = k;   // ratings left to the rating kernel: s_order[0, n_rate)
+#ifdef CF_PRED_NO_CLOSED   // A/B: every rating in the rating kernel
+        if (false) {
+#else
+        if (Lx > 0 && m >= 2 && k >= 2) {
+#endif
+            const int zmin = s_cnt[11];
+            const bool cand = tid < k && s_slow[tid] == 1 && ((s_cmask[3 * tid + (tid >> 6)] >> (tid & 63)) & 1ull) &&
+                              s_lim[tid] < k && s_lim[tid] <= zmin && s_lim[tid] <= s_dmin[tid];
+            const int ncand = block_compact(cand, tid, s_list, s_cnt);
+            const double sum_all = s_misc[1];
+            const int gl = tid & 15;
+            for (int e = tid >> 4; e < ncand; e += kThreads / 16) {
+                const int r = s_list[e];
+                const int lim = s_lim[r];
+                const int d = k - lim;
+                const double rr = (double)s_rat[r];
+                const double mu = (sum_all - rr) / (double)(k - 1);   // mean over C (:311)
+                double kq = 0.0, bg = 0.0;
+                for (int j = gl; j < d; j += 16) {
+                    const double x = Xf[(size_t)r * ld + lim + j];
+                    const double g = gxl[lim + j] - mu * hxl[lim + j];
+                    kq = fma(x, x, kq);
+                    bg = fma(x, g, bg);
+                }
+                kq = row16_sum(kq);
+                bg = row16_sum(bg);
+                if (gl == 0 && kq >= kPivMin) {
+                    if (!a.row_sel || a.row_sel[base + r]) {
+                        const double di = pivot_rcp(kq);
+                        const double ba = fma(-kq, rr - mu, bg);
+                        double pred = mu - ((ba * di) * di) * kq;
+                        if (pred > 5) pred = 5;
+                        if (pred < 1) pred = 1;
+                        const double er = rr - pred;
+                        a.mse[base + r] = (float)(er * er);
+                        a.kk[base + r] = k - 1;
+                        if (a.pred) a.pred[base + r] = pred;
+                    }
+                    s_dmin[r] = -1;
+                }
+            }
+            __syncthreads();
+            const int ord = tid < k ? s_order[tid] : 0;
+            n_rate = block_compact(tid < k && s_dmin[ord] != -1, ord, s_order, s_cnt);
+        }
         PHASE_STAMP(1);
         {
             int* lim_g = reinterpret_cast<int*>(slot + a.so.lim);
@@ -772,6 +859,7 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
                 misc[1] = (double)Lx;
                 misc[2] = (double)Lq;
                 misc[3] = Xf == Q1 ? 1.0 : 0.0;
+                misc[4] = (double)n_rate;
             }
         }
     }
@@ -842,6 +930,7 @@ __device__ __forceinline__ void rating_user(const PredArgs<T> a, uint32_t uo, do
         const int Lx = (int)misc[1];
         const int Lq = (int)misc[2];
         const double* Xf = slot + (misc[3] != 0.0 ? a.so.q1 : a.so.x);
+        const int n_rate = (int)misc[4];   // the rest were predicted by the basis kernel
         const int ld = lmax;
         __syncthreads();
         {
@@ -885,7 +974,7 @@ __device__ __forceinline__ void rating_user(const PredArgs<T> a, uint32_t uo, do
             // diagnostics, summed over this wave's ratings of the user (wave-uniform)
             unsigned long long wacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             int idx = claim();
-            while (idx < k) {
+            while (idx < n_rate) {
                 const int r = s_order[idx];
                 idx = claim();
                 if (a.row_sel && !a.row_sel[base + r]) continue;   // movie not sampled (wave-uniform)
@@ -1404,7 +1493,7 @@ inline SlotOff slot_layout(int lmax) {
     so.ap = (int)o; o += (size_t)(lmax + 2) * (lmax + 3) / 2;
     so.gx = (int)o; o += lmax;
     so.hx = (int)o; o += lmax;
-    so.misc = (int)o; o += 4;
+    so.misc = (int)o; o += 8;
     so.cmask = (int)o; o += 3 * (size_t)lmax;                 // u64 per cell
     so.lim = (int)o; o += (lmax + 1) / 2;                    // ints, two per cell
     so.order = (int)o; o += (lmax + 1) / 2;
@@ -1451,8 +1540,9 @@ inline int ensure_slot_scratch(cf_ctx* ctx, const cf_plan* plan, size_t copies, 
 }
 inline size_t basis_lds() {
     return sizeof(double) * (kStageElems + 4) + CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 3 * sizeof(int)) +
-           12 * sizeof(int) + CF_MAX_K * (3 * sizeof(uint64_t) + sizeof(int));
+           12 * sizeof(int) + CF_MAX_K * (3 * sizeof(uint64_t) + 2 * sizeof(int));   // ..., s_order, s_dmin
 }
+static_assert(2 * CF_MAX_K + CF_MAX_K / 2 <= kStageElems, "closed-form LDS copies exceed the staging area");
 inline size_t rating_lds_fixed() {
     return sizeof(double) * (4 + 2 * CF_MAX_K) +                                      // s_misc, s_gx, s_hx
            CF_MAX_K * (sizeof(uint32_t) + sizeof(float) + 6 * sizeof(int)) + 12 * sizeof(int) +

@@ -2,7 +2,7 @@
 (lognormal k, median 100, sigma ln(15)/1.645, C4 knn2 graph of 50k items), as bench.py's c5 leg
 builds it.
 
-usage: python tools/probe_pspill_c5.py [users=1000]
+usage: python tools/probe_pspill_c5.py [users=1000] [kmin=192] [kmax=3072]   (users with kmin < k <= kmax)
 """
 import ctypes, os, sys, time
 import numpy as np
@@ -12,13 +12,15 @@ from collaborative_filtering_amd import synth, workloads as wlm
 from collaborative_filtering_amd.api import CF_SIGS_OWN, Context, evec_offsets
 
 users = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
+kmin = int(sys.argv[2]) if len(sys.argv) > 2 else 192
+kmax = int(sys.argv[3]) if len(sys.argv) > 3 else 3072
 dev = torch.device("cuda")
 d_W, _, gs = wlm.config_graph("c4", Context, 0, dev, torch)
 n_items = wlm.CONFIGS["c4"]["items"]
 seed = 2026101505
 k0 = synth.degrees(seed, users, k_median=100.0, sigma=float(np.log(15.0) / 1.6449), kmin=20, kmax=5000)
 off0, items0, rat0 = synth.user_items(seed, k0, n_items, threads=16)
-sel = np.nonzero((k0 > 192) & (k0 <= 3072))[0]
+sel = np.nonzero((k0 > kmin) & (k0 <= kmax))[0]
 ks = k0[sel]
 off = np.zeros(len(ks) + 1, np.uint64); off[1:] = np.cumsum(ks.astype(np.uint64))
 items = np.concatenate([items0[int(off0[u]):int(off0[u + 1])] for u in sel])
