@@ -584,15 +584,23 @@ __global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
         SP_STAMP(0);
         bool fast = basis && c > 0;
         if (fast) {
-            // zero-column filter from the complement: column j < lim is dropped iff every
-            // row with U(i, j) >= 1e-4 lies in Cbar
+            // zero-column filter: column j < lim is dropped iff no row of C has U(i, j) >= 1e-4,
+            // i.e. every such row lies in Cbar -- counted over the smaller of the two sets (on
+            // the k > 3072 users c is ~60 against nc ~ k: lim x nc loads per rating were the
+            // whole cost of their prediction)
             bool drop = false;
-            for (int j = tid; j < lim; j += kT)
-                if (cpos[j] <= nc) {
+            const bool via_c = c < nc;
+            for (int j = tid; j < lim; j += kT) {
+                if (via_c) {
+                    bool hit = false;
+                    for (int q = 0; q < c && !hit; ++q) hit = (double)U[(size_t)s_conn[q] * m + j] >= 0.0001;
+                    drop |= !hit;
+                } else if (cpos[j] <= nc) {
                     int hit = 0;
                     for (int q = 0; q < nc; ++q) hit += (double)U[(size_t)s_ncon[q] * m + j] >= 0.0001;
                     drop |= hit == cpos[j];
                 }
+            }
             fast = !__syncthreads_or(drop);
             if (!fast && a.phase && tid == 0) pc[10] += 1;
         }

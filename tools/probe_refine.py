@@ -1,7 +1,7 @@
 """Eigen stage A/B on C4 users: sweeps-only (r03 rule) vs sweeps to stop_rel + Gram refinement.
 Times the eigen pass of a C4 user range, reads the sweep counters, and compares a stratified
 sample with the fp64 oracle (projector escapes at proj_tol 1e-3, eigenvalue / residual errors).
-usage: probe_refine.py [users=125000] [configs: 'off' | 'on:<stop_rel>:<delta>' ...]"""
+usage: probe_refine.py [users=125000] [configs: 'off' | 'on:<stop_rel>:<delta>' | 'tri' ...]"""
 import os
 import sys
 import time
@@ -60,8 +60,11 @@ def run():
 
 
 for c in confs:
+    ctx.set_eigen_method("tridiag" if c == "tri" else "jacobi")
     if c == "off":
         ctx.set_eigen_refine(False)
+    elif c == "tri":   # Householder + QL (cf_set_eigen_method(CF_EIGEN_TRIDIAG)); no sweep counters
+        pass
     else:
         _, sr, dl = c.split(":")
         ctx.set_eigen_refine(True, float(sr), float(dl))
