@@ -36,6 +36,7 @@ SIGNATURES = {
     "cf_set_jacobi": (c_int, [c_void_p, c_float, c_int]),
     "cf_set_eigen_refine": (c_int, [c_void_p, c_int, c_float, c_float]),
     "cf_set_step_masks": (c_int, [c_void_p, c_int]),
+    "cf_set_local_wlim": (c_int, [c_void_p, c_int]),
     "cf_debug_predict_nmax": (c_int, [c_int]),
     "cf_set_knn2_topk": (c_int, [c_void_p, c_uint32]),
     "cf_set_eigen_method": (c_int, [c_void_p, c_int]),

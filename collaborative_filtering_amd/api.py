@@ -96,6 +96,10 @@ class Context:
         """Jacobi sweeps to stop_rel, then the first-order Gram refinement (cf_set_eigen_refine)."""
         self._chk(self.lib.cf_set_eigen_refine(self.h, int(enable), stop_rel, delta), "cf_set_eigen_refine")
 
+    def set_local_wlim(self, bisect: bool = True):
+        """local_calc spill pairs: w_lim by bisection on the movie's B = L2 L2^T (cf_set_local_wlim)."""
+        self._chk(self.lib.cf_set_local_wlim(self.h, int(bisect)), "cf_set_local_wlim")
+
     def set_step_masks(self, enable: bool = True):
         """Eigen runs hand the predictor its complement masks (cf_set_step_masks)."""
         self._chk(self.lib.cf_set_step_masks(self.h, int(enable)), "cf_set_step_masks")

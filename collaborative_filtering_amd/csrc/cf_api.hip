@@ -189,6 +189,12 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps) {
     return CF_OK;
 }
 
+int cf_set_local_wlim(cf_ctx* ctx, int bisect) {
+    if (!ctx) return CF_EINVAL;
+    ctx->local_wlim_bisect = bisect != 0;
+    return CF_OK;
+}
+
 int cf_set_step_masks(cf_ctx* ctx, int enable) {
     if (!ctx) return CF_EINVAL;
     ctx->step_masks = enable != 0;

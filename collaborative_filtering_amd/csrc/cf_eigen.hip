@@ -117,6 +117,7 @@ struct EigenArgs {
     // 3 * item_off[u] (bit i of word 3r + (i >> 6) = !(w(item_r -> item_i) > 0.1), cf_predict.hip)
     uint64_t* cmask_out;
     uint64_t cmask_words;       // its extent (users beyond it write none)
+    const uint8_t* solved;      // kSigma, spill pairs: w_lim already written (local_wlim_kernel)
 };
 
 // Test rating of `user` for compact item `movie` (0 if absent): binary search of the
@@ -778,6 +779,7 @@ int launch_buckets_on(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStrea
             loc.test_user = args.test_user;
             loc.test_rating = args.test_rating;
             loc.wlim = args.wlim;
+            loc.solved = args.solved;
             // overlap: its k > 3072 range keeps running on the spill side stream while the LDS
             // buckets start; launch_all_buckets joins it with the aux streams
             rc = cf_launch_eigen_spill(ctx, plan, b, args.item_off, args.items, args.evec_off, args.m_out, args.sigs,
@@ -851,9 +853,10 @@ int cf_launch_local_sigma(cf_ctx* ctx, const cf_plan* pair_plan, const uint64_t*
                           const uint32_t* d_items, const uint32_t* d_pair_movie,
                           const uint32_t* d_pair_user, const float* d_l2, const uint64_t* d_l2_off,
                           const uint64_t* d_test_off, const uint32_t* d_test_user,
-                          const float* d_test_rating, float* d_wlim, hipStream_t stream) {
+                          const float* d_test_rating, float* d_wlim, hipStream_t stream, const uint8_t* d_solved) {
     EigenArgs args{};
     args.mode = kSigma;
+    args.solved = d_solved;
     args.order = pair_plan->d_order;
     args.item_off = d_item_off;
     args.items = d_items;

@@ -176,6 +176,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         const int mode = a.loc.mode;
         const uint32_t unit = a.order[a.first + ui];
         const uint32_t u = mode == 2 ? a.loc.pair_movie[unit] : unit;   // the unit whose items index the graph
+        if (mode == 2 && a.loc.solved && a.loc.solved[unit]) continue;   // w_lim by bisection already
         const uint64_t base = a.item_off[u];
         const int nrows = (int)(a.item_off[u + 1] - base);
         int n = nrows;
@@ -235,8 +236,10 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 S.sig[i] = (float)mc[MC_SIG + i];
             }
             __syncthreads();
-        } else if (mode == 2) {
-            // ---- 1s. A = L2_h L2_h^T (h x h, fp64 sums of the stored fp32 L2 rows, :425-435)
+        } else if (mode == 2 || mode == 3) {
+            // ---- 1s. A = L2_h L2_h^T (h x h, fp64 sums of the stored fp32 L2 rows, :425-435);
+            // mode 3: every row, B = L2 L2^T of the movie, whose eigenpairs the bisection of
+            // local_wlim_kernel (cf_local.hip) shares across the movie's pairs
             const float* L2m = a.loc.l2 + a.loc.l2_off[u];
             const int npk = n * (n + 1) / 2;
             for (int e = wave; e < npk; e += SP_W) {
@@ -244,8 +247,8 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 while (p * (p + 1) / 2 > e) --p;
                 while ((p + 1) * (p + 2) / 2 <= e) ++p;
                 const int q = e - p * (p + 1) / 2;
-                const float* rp = L2m + (size_t)S.perm[p] * nrows;
-                const float* rq = L2m + (size_t)S.perm[q] * nrows;
+                const float* rp = L2m + (size_t)(mode == 3 ? p : S.perm[p]) * nrows;
+                const float* rq = L2m + (size_t)(mode == 3 ? q : S.perm[q]) * nrows;
                 double acc = 0.0;
                 for (int j = lane; j < nrows; j += 64) acc = fma((double)rp[j], (double)rq[j], acc);
                 acc = wave_sum(acc);
@@ -1017,7 +1020,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             for (lim = 0; lim < n; ++lim)
                 if (S.d[S.perm[lim]] > (double)smm) break;   // (:186-188)
             if (lim < 2) lim = 2;                             // (:190-191)
-            if (mode == 1) lim = n;   // local_calc keeps every eigenpair (es(ll2), local_calc.cpp:378)
+            if (mode == 1 || mode == 3) lim = n;   // local_calc keeps every eigenpair (es(ll2), local_calc.cpp:378)
             S.flag[3] = lim;
             a.m_out[u] = lim;
         }

@@ -83,6 +83,7 @@ struct cf_ctx {
     uint64_t cmask_gen = ~0ull;
     uint64_t graph_gen = 0;   // bumped by every graph (re)load (free_graph)
     int step_masks = 1;       // cf_set_step_masks (env CF_STEP_MASKS=0 for A/B runs)
+    int local_wlim_bisect = 1;   // cf_set_local_wlim: spill pairs' w_lim by bisection (cf_local.hip)
     // knn2 rating planes (R, S, B), grown on demand.
     void* d_knn = nullptr;
     size_t knn_bytes = 0;
@@ -256,12 +257,14 @@ int cf_launch_local_sigma(cf_ctx* ctx, const cf_plan* pair_plan, const uint64_t*
                           const uint32_t* d_items, const uint32_t* d_pair_movie,
                           const uint32_t* d_pair_user, const float* d_l2, const uint64_t* d_l2_off,
                           const uint64_t* d_test_off, const uint32_t* d_test_user,
-                          const float* d_test_rating, float* d_wlim, hipStream_t stream);
+                          const float* d_test_rating, float* d_wlim, hipStream_t stream,
+                          const uint8_t* d_solved = nullptr);
 
 // a8 (local_calc) modes of the spill eigen kernel for units with n > CF_MAX_K.
 struct cf_spill_local {
     int mode;                      // 1: the movie's local graph (all n eigenpairs, L2 kept);
-                                   // 2: w_lim of a (movie, test user) pair (eigenvalue only)
+                                   // 2: w_lim of a (movie, test user) pair (eigenvalue only);
+                                   // 3: all n eigenpairs of B = L2 L2^T of the movie
     float* l2;                     // per movie n x n row-major L2 (mode 1 writes, mode 2 reads)
     const uint64_t* l2_off;
     const uint32_t* pair_movie;    // mode 2: unit -> movie unit, test user
@@ -270,6 +273,7 @@ struct cf_spill_local {
     const uint32_t* test_user;
     const float* test_rating;
     float* wlim;                   // mode 2 output per pair
+    const uint8_t* solved;         // mode 2, optional: pairs whose w_lim is already written
 };
 // defer_join: the k > 3072 range's stream is left running (ctx->spill_side_pending); the caller
 // joins it with cf_spill_join before the results are read.  Otherwise it is joined into `stream`.

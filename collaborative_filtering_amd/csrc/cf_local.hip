@@ -159,6 +159,187 @@ __global__ __launch_bounds__(kThreads) void local_predict_kernel(LocalPredArgs a
     }
 }
 
+// ---- w_lim of the pairs of units with n > CF_MAX_K, shared per movie ---------------------
+// L2_h L2_h^T (:425-435) is the principal submatrix B_hh of B = L2 L2^T with the user's rated
+// rows R deleted.  With B = W Theta W^T (spill eigen mode 3, once per movie) and mu not an
+// eigenvalue, Haynsworth's inertia additivity on B - mu (whose inverse has the R-block
+// F(mu) = W_R (Theta - mu)^-1 W_R^T, the inverse of the Schur complement of B_hh - mu) gives
+//   #{eigenvalues of B_hh below mu} = #{theta_j < mu} - #{negative eigenvalues of F(mu)},
+// and interlacing puts lambda_min(B_hh) in [theta_0, theta_c] (c = |R|).  Bisection on that
+// count -- per step one c x c F (VALU fp64 over W_R staged through LDS 96 columns at a time)
+// and its LDL^T inertia -- replaces the per-pair fp64 Gram + tridiagonalisation of n x n (mode 2
+// of eigen_spill_kernel, ~n^3 per pair): ~40 c^2 n per pair.  One workgroup per pair; pairs with
+// c > kWlimCmax keep mode 2 (solved = 0).
+constexpr int kWlimCmax = 96;
+constexpr int kWlimJc = 96;    // LDS ~75 KB: two workgroups per CU
+constexpr int kWlimIters = 44;
+struct WlimArgs {
+    uint32_t n_pairs;
+    const uint32_t* pair_movie;
+    const uint32_t* pair_user;
+    const uint64_t* item_off;
+    const uint32_t* items;
+    const float* theta;     // per movie unit at item_off: eigenvalues of B, ascending
+    const uint64_t* w_off;  // per movie unit: its n x n eigenvector block, row-major
+    const float* W;
+    const uint64_t* test_off;
+    const uint32_t* test_user;
+    const float* test_rating;
+    float* wlim;
+    uint8_t* solved;
+};
+
+__global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
+    __shared__ float s_W[kWlimCmax * kWlimJc];
+    __shared__ double s_d[kWlimJc];
+    __shared__ double s_F[kWlimCmax * (kWlimCmax + 1) / 2];
+    __shared__ int s_R[kWlimCmax];
+    __shared__ int s_c[kThreads / 64];
+    __shared__ double s_x[2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    LocalPredArgs la{};   // lookup_rating's test arrays
+    la.test_off = a.test_off;
+    la.test_user = a.test_user;
+    la.test_rating = a.test_rating;
+    for (uint32_t p = blockIdx.x; p < a.n_pairs; p += gridDim.x) {
+        const uint32_t v = a.pair_movie[p], user = a.pair_user[p];
+        const uint64_t base = a.item_off[v];
+        const int n = (int)(a.item_off[v + 1] - base);
+        // rated rows, ascending (row 0, the movie itself, counts as unrated: :405-413)
+        int c = 0;
+        for (int b0 = 0; b0 < n; b0 += kThreads) {
+            const int i = b0 + tid;
+            const bool rated = i >= 1 && i < n && lookup_rating(la, a.items[base + i], user) != 0.0f;
+            const unsigned long long bal = __ballot(rated);
+            if (lane == 0) s_c[wave] = __popcll(bal);
+            __syncthreads();
+            int off = c, all = 0;
+            for (int w = 0; w < kThreads / 64; ++w) {
+                if (w < wave) off += s_c[w];
+                all += s_c[w];
+            }
+            const int pos = off + __popcll(bal & ((1ull << lane) - 1ull));
+            if (rated && pos < kWlimCmax) s_R[pos] = i;
+            c += all;
+            __syncthreads();
+        }
+        if (c > kWlimCmax) {   // uniform
+            if (tid == 0) a.solved[p] = 0;
+            continue;
+        }
+        const float* th = a.theta + base;
+        const float* Wv = a.W + a.w_off[v];
+        double lo = (double)th[0], hi = (double)th[min(c, n - 1)];
+        // 4 x 4 micro-tiles of F's lower triangle; with few tiles, several threads split a
+        // tile's columns (segments) and their partial sums meet in LDS
+        const int nb = (c + 3) >> 2, ntile = nb * (nb + 1) / 2;
+        const int nseg = ntile == 0 ? 1 : max(1, min(kThreads / ntile, kWlimJc / 4));
+        const int nwork = ntile * nseg;   // <= 300 (c <= 96): at most two items per thread
+        const int cp = 4 * nb;            // staged rows (zero beyond c)
+        for (int it = 0; it < kWlimIters && c > 0 && hi - lo > 1e-11 * fabs(hi); ++it) {
+            const double mu = 0.5 * (lo + hi);
+            for (int e = tid; e < c * (c + 1) / 2; e += kThreads) s_F[e] = 0.0;
+            double acc[2][16];
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+#pragma unroll
+                for (int x = 0; x < 16; ++x) acc[q][x] = 0.0;
+            for (int j0 = 0; j0 < n; j0 += kWlimJc) {
+                __syncthreads();   // the previous chunk is consumed (and s_F zeroed)
+                for (int e = tid; e < cp * kWlimJc; e += kThreads) {
+                    const int r = e / kWlimJc, jj = e - r * kWlimJc;
+                    s_W[e] = (r < c && j0 + jj < n) ? Wv[(size_t)s_R[r] * n + j0 + jj] : 0.0f;
+                }
+                for (int jj = tid; jj < kWlimJc; jj += kThreads)
+                    s_d[jj] = j0 + jj < n ? 1.0 / ((double)th[j0 + jj] - mu) : 0.0;
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int w = tid + q * kThreads;
+                    if (w >= nwork) continue;
+                    const int t = w / nseg, g = w - t * nseg;
+                    int bi = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+                    while (bi * (bi + 1) / 2 > t) --bi;
+                    while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+                    const int bj = t - bi * (bi + 1) / 2;
+                    const float* ra = s_W + 4 * bi * kWlimJc;
+                    const float* rb = s_W + 4 * bj * kWlimJc;
+                    for (int jj = g; jj < kWlimJc; jj += nseg) {
+                        const double d = s_d[jj];
+                        double xa[4], xb[4];
+#pragma unroll
+                        for (int x = 0; x < 4; ++x) {
+                            xa[x] = (double)ra[x * kWlimJc + jj] * d;
+                            xb[x] = (double)rb[x * kWlimJc + jj];
+                        }
+#pragma unroll
+                        for (int x = 0; x < 4; ++x)
+#pragma unroll
+                            for (int y = 0; y < 4; ++y) acc[q][4 * x + y] = fma(xa[x], xb[y], acc[q][4 * x + y]);
+                    }
+                }
+            }
+            // partial tiles into the packed lower triangle of F
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int w = tid + q * kThreads;
+                if (w >= nwork) continue;
+                const int t = w / nseg;
+                int bi = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+                while (bi * (bi + 1) / 2 > t) --bi;
+                while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+                const int bj = t - bi * (bi + 1) / 2;
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                    for (int y = 0; y < 4; ++y) {
+                        const int ia = 4 * bi + x, ib = 4 * bj + y;
+                        if (ia < c && ib <= ia) atomicAdd(&s_F[tri(ia, ib)], acc[q][4 * x + y]);
+                    }
+            }
+            __syncthreads();
+            // inertia of F: right-looking LDL^T, negative pivots counted (thread 0)
+            int neg = 0;
+            for (int k = 0; k < c; ++k) {
+                const double dk = s_F[tri(k, k)];
+                neg += dk < 0.0;
+                if (dk != 0.0) {
+                    const double rdk = 1.0 / dk;
+                    const int m = c - 1 - k;   // trailing rows k+1 .. c-1
+                    for (int e = tid; e < m * (m + 1) / 2; e += kThreads) {
+                        int ii = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+                        while (ii * (ii + 1) / 2 > e) --ii;
+                        while ((ii + 1) * (ii + 2) / 2 <= e) ++ii;
+                        const int i = k + 1 + ii, j = k + 1 + (e - ii * (ii + 1) / 2);
+                        s_F[tri(i, j)] -= s_F[tri(i, k)] * rdk * s_F[tri(j, k)];
+                    }
+                }
+                __syncthreads();
+            }
+            if (tid == 0) {
+                // #{theta_j < mu} by binary search over the ascending eigenvalues
+                int l = 0, h = n;
+                while (l < h) {
+                    const int md = (l + h) >> 1;
+                    if ((double)th[md] < mu) l = md + 1;
+                    else h = md;
+                }
+                const bool below = l - neg >= 1;   // lambda_min(B_hh) < mu
+                s_x[0] = below ? lo : mu;
+                s_x[1] = below ? mu : hi;
+            }
+            __syncthreads();
+            lo = s_x[0];
+            hi = s_x[1];
+            __syncthreads();
+        }
+        if (tid == 0) {
+            a.wlim[p] = (float)sqrt(fmax(0.5 * (lo + hi), 0.0));   // as mode 2 (:435-436)
+            a.solved[p] = 1;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* movie_off,
@@ -254,7 +435,10 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
     };
     const uint64_t n_entries = movie_off[n_movies];
     DevBuf d_moff, d_mitems, d_sqoff, d_evals, d_evecs, d_l2, d_nout, d_toff, d_tuser, d_trat, d_pm, d_pu,
-        d_po, d_wlim, d_mse, d_kk, d_pred, d_lim;
+        d_po, d_wlim, d_mse, d_kk, d_pred, d_lim, d_theta, d_bvec, d_solved;
+    // spill pairs' w_lim by bisection on the movie's B = L2 L2^T (local_wlim_kernel), unless
+    // cf_set_local_wlim(ctx, 0) keeps the per-pair tridiagonalisation for every one
+    const bool use_bisect = ctx->local_wlim_bisect && n_pairs > n_small;
     auto alloc_copy = [&](DevBuf& b, const void* h, size_t bytes) -> int {
         CF_TRY(dev_alloc(ctx, b, bytes));
         if (h && bytes) CF_HIP_CHECK(ctx, hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice));
@@ -287,11 +471,54 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
                                         static_cast<float*>(d_evecs.p), static_cast<float*>(d_l2.p), sqo,
                                         static_cast<int32_t*>(d_nout.p), 0)))
             break;
+        if (use_bisect) {
+            // the eigenpairs of every large movie's B = L2 L2^T (spill eigen mode 3), then one
+            // bisection per spill pair; the pairs it leaves (c > kWlimCmax) go to mode 2 below
+            if ((rc = alloc_copy(d_theta, nullptr, sizeof(float) * n_entries))) break;
+            if ((rc = alloc_copy(d_bvec, nullptr, sizeof(float) * sq_off[n_movies]))) break;
+            if ((rc = alloc_copy(d_solved, nullptr, n_pairs))) break;
+            CF_HIP_CHECK(ctx, hipMemset(d_solved.p, 0, n_pairs));
+            for (const cf_bucket& b : mplan->buckets) {
+                if (b.emax != kSpillBucket || !b.count) continue;
+                cf_spill_local loc{};
+                loc.mode = 3;
+                loc.l2 = static_cast<float*>(d_l2.p);
+                loc.l2_off = sqo;
+                if ((rc = cf_launch_eigen_spill(ctx, mplan, b, moff, mit, sqo, static_cast<int32_t*>(d_nout.p), nullptr,
+                                                static_cast<float*>(d_theta.p), static_cast<float*>(d_bvec.p), 0,
+                                                &loc)))
+                    break;
+            }
+            if (rc != CF_OK) break;
+            WlimArgs wa{};
+            wa.n_pairs = n_pairs - n_small;
+            wa.pair_movie = static_cast<const uint32_t*>(d_pm.p) + n_small;
+            wa.pair_user = static_cast<const uint32_t*>(d_pu.p) + n_small;
+            wa.item_off = moff;
+            wa.items = mit;
+            wa.theta = static_cast<const float*>(d_theta.p);
+            wa.w_off = sqo;
+            wa.W = static_cast<const float*>(d_bvec.p);
+            wa.test_off = static_cast<const uint64_t*>(d_toff.p);
+            wa.test_user = static_cast<const uint32_t*>(d_tuser.p);
+            wa.test_rating = static_cast<const float*>(d_trat.p);
+            wa.wlim = static_cast<float*>(d_wlim.p) + n_small;
+            wa.solved = static_cast<uint8_t*>(d_solved.p) + n_small;
+            int cus = 0;
+            CF_HIP_CHECK(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+            const uint32_t blocks = std::min<uint32_t>(wa.n_pairs, (uint32_t)std::max(1, cus) * 8u);
+            hipLaunchKernelGGL(local_wlim_kernel, dim3(blocks), dim3(kThreads), 0, 0, wa);
+            if (hipGetLastError() != hipSuccess) {
+                rc = cf_set_error(ctx, CF_EHIP, "local_wlim_kernel launch");
+                break;
+            }
+        }
         if ((rc = cf_launch_local_sigma(ctx, pplan, moff, mit, static_cast<const uint32_t*>(d_pm.p),
                                         static_cast<const uint32_t*>(d_pu.p), static_cast<const float*>(d_l2.p),
                                         sqo, static_cast<const uint64_t*>(d_toff.p),
                                         static_cast<const uint32_t*>(d_tuser.p),
-                                        static_cast<const float*>(d_trat.p), static_cast<float*>(d_wlim.p), 0)))
+                                        static_cast<const float*>(d_trat.p), static_cast<float*>(d_wlim.p), 0,
+                                        use_bisect ? static_cast<const uint8_t*>(d_solved.p) : nullptr)))
             break;
         if (n_pairs > n_small) {
             int nbig = 3;

@@ -138,3 +138,48 @@ def test_local_calc_spill_units(gpu_ctx):
     # many ratings rank-deficient or without a 1e-3 gap at the lim cut)
     assert n_wl > 1000 and n_cmp > 400, (n_wl, n_cmp)
     print(f"spill units: sizes {sorted(sizes)}; w_lim compared {n_wl}, predictions compared {n_cmp}")
+
+
+def _local_inputs(G, test):
+    n_items = G.shape[0]
+    toff = np.zeros(n_items + 1, np.uint64)
+    tuser, trat = [], []
+    for mv in range(n_items):
+        us = sorted(test.get(mv, {}))
+        tuser += us
+        trat += [test[mv][u] for u in us]
+        toff[mv + 1] = toff[mv] + len(us)
+    moff, mitems = [0], []
+    for mv in range(n_items):
+        mitems += [mv] + [j for j in range(n_items) if float(G[mv, j]) > 0.1]
+        moff.append(len(mitems))
+    return np.array(moff), np.array(mitems), toff, np.array(tuser), np.array(trat)
+
+
+def test_local_calc_spill_wlim_bisection(gpu_ctx):
+    """Spill units (n > 192) whose pairs rate few of the unit's rows (c <= 96) take w_lim from
+    the movie's shared B = L2 L2^T eigenpairs by inertia-count bisection (cf_set_local_wlim):
+    the oracle's w_lim to 1e-4 and the predictions as in the other parity tests, and the same
+    w_lim as the per-pair tridiagonalisation of L2_h L2_h^T to 1e-6, every pair of the call."""
+    G, test = build_case(12, n_items=240, n_users=200, p_edge=0.85, p_rate=0.1)
+    try:
+        gpu_ctx.set_local_wlim(True)
+        n_wl, n_cmp, sizes, bad = _run_local_case(gpu_ctx, G, test, check_movies=set(range(24)), spill_gap=1e-3)
+        assert not bad, bad[:10]
+        assert sum(s > 192 for s in sizes) >= 12, sizes
+        assert n_wl > 300, n_wl
+        gpu_ctx.upload_graph_dense(G)
+        args = _local_inputs(G, test)
+        mse_b, kk_b, pred_b, wl_b, lim_b = gpu_ctx.local_calc(*args)
+        gpu_ctx.set_local_wlim(False)
+        mse_t, kk_t, pred_t, wl_t, lim_t = gpu_ctx.local_calc(*args)
+    finally:
+        gpu_ctx.set_local_wlim(True)
+    assert np.array_equal(kk_b, kk_t)
+    ok = kk_b > 0
+    rel = np.abs(wl_b[ok].astype(np.float64) - wl_t[ok]) / np.maximum(1e-3, wl_t[ok])
+    assert rel.max() <= 1e-6, (rel.max(), int(np.argmax(rel)))
+    same_lim = (lim_b == lim_t) & ok
+    assert same_lim.sum() >= 0.99 * ok.sum(), (int(same_lim.sum()), int(ok.sum()))
+    print(f"bisection: {int(ok.sum())} pairs, max rel w_lim diff {rel.max():.2e}, "
+          f"lim equal {int(same_lim.sum())}; oracle: {n_wl} w_lim, {n_cmp} predictions compared")

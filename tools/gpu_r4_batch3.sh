@@ -13,3 +13,5 @@ c5 = d.get("config5", d)
 for g in ("lds", "spill", "spill_big", "one_call"):
     print(g, {k: v for k, v in c5.get(g, {}).items() if isinstance(v, (int, float))})
 PY
+timeout -k 10 600 python -u -m pytest tests/test_gpu_local.py -v -s --timeout 500 --timeout-method thread > gpurun_out/r4_local_$tag.log 2>&1
+echo local_rc=$?; grep -E "PASSED|FAILED|bisection:|spill units:|Error|assert" gpurun_out/r4_local_$tag.log | head -20
