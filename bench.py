@@ -682,7 +682,7 @@ def c2_leg(args, ctx, dev_index, dev, torch):
     return out
 
 
-def local_calc_leg(ctx, wl, W, pct=1, seed=2026):
+def local_calc_leg(ctx, wl, W, pct=1, seed=2026, nmax=4999):
     """local_calc's engine 2 (local_calc.cpp:262-526, cf_local_calc) as `bin/local_calc --pct P`
     runs it: movies sampled with probability P %, each movie's unit = [m, out-neighbours with
     w > 0.1] of the resident knn2 graph, test ratings = the config's user ratings grouped by
@@ -700,13 +700,16 @@ def local_calc_leg(ctx, wl, W, pct=1, seed=2026):
     tuser = uid[order].astype(np.uint32)
     trat = wl.ratings[:wl.n_entries][order].astype(np.float32)
     # units of the sampled movies that have test ratings (the rest write no rows, :269-272)
-    moff, mitems, ns = [0], [], []
+    moff, mitems, ns, over = [0], [], [], []
     for m in movies:
         if toff[m + 1] == toff[m]:
             continue
         row = W[int(m)].cpu().numpy()
         nb = np.nonzero(row.astype(np.float64) > 0.1)[0]
         nb = nb[nb != m]
+        if 1 + len(nb) > nmax:   # CF_ERANGE in cf_local_calc (CF_SPILL_MAX_K): left out, counted
+            over.append(1 + len(nb))
+            continue
         mitems.append(np.concatenate([[m], nb]).astype(np.uint32))
         moff.append(moff[-1] + 1 + len(nb))
         ns.append(1 + len(nb))
@@ -717,11 +720,15 @@ def local_calc_leg(ctx, wl, W, pct=1, seed=2026):
     mse, kk, pred, wlim, lim = ctx.local_calc(moff, mitems, toff, tuser, trat)
     dt = time.perf_counter() - t
     pairs = int(np.sum(kk >= 0))
+    sel = kk > 0
     return {"movies_sampled": int(len(movies)), "units": int(len(ns)),
             "unit_n": {"mean": float(ns.mean()) if len(ns) else 0.0, "max": int(ns.max()) if len(ns) else 0,
-                       "gt_192": int(np.sum(ns > 192)), "ge_5000": int(np.sum(ns >= 5000))},
+                       "gt_192": int(np.sum(ns > 192))},
+            "units_over_cap": {"count": len(over), "n_min": int(min(over)) if over else 0,
+                               "n_max": int(max(over)) if over else 0,
+                               "note": f"units with n > {nmax} (CF_ERANGE in cf_local_calc) left out of the call"},
             "predictions": pairs, "seconds": dt, "predictions_per_s": pairs / dt if dt > 0 else 0.0,
-            "cf_erange": 0,
+            "rank_deficient_frac": float(np.mean(kk[sel] < lim[sel])) if sel.any() else 0.0,
             "note": f"bin/local_calc --pct {pct} on this config's knn2 graph: {len(ns)} movie units, every (movie, "
                     "test user) pair of them; host-pointer cf_local_calc (PCIe included)"}
 

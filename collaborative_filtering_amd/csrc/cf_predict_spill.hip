@@ -879,6 +879,53 @@ __global__ __launch_bounds__(kT) void local_predict_spill_kernel(LocSpArgs a) {
         }
         __syncthreads();
         const double mean = s_misc[0];
+        if (c > 0 && c < L) {
+            // U_CS^T U_CS (L x L) has rank <= c < L: singular, and the reference's explicit
+            // inverse returns rounding noise (:490).  As the predictor does for c < lim, this
+            // returns the minimum-norm least-squares prediction, from the c x c system of the
+            // same rows: pred - mean = (U_CS v_S)^T K^-1 y_C, K = U_CS U_CS^T -- O(c^2 L)
+            // instead of O(L^3) (units of thousands of rows rated by tens)
+            const size_t needc = (size_t)(c + 2) * (c + 3) / 2;
+            double* Ac = needc <= (size_t)kLdsA ? s_la : fa;
+            tile_gemm<true, true>(
+                c, c, [&](int i, int l) { return (double)U[(size_t)s_c[i] * n + l]; },
+                [&](int l, int j) { return (double)U[(size_t)s_c[j] * n + l]; }, [=](int) { return L; },
+                [](int i0, int j0) { return j0 <= i0; },
+                [&](int i, int j, double v) {
+                    if (j <= i) Ac[tri(i, j)] = v;
+                },
+                sA, sB);
+            for (int q = wave; q < c; q += kW) {
+                const float* row = U + (size_t)s_c[q] * n;
+                double t = 0.0;
+                for (int j = lane; j < L; j += 64) t = fma((double)row[j], (double)U[j], t);   // v = row 0
+                t = wsum(t);
+                if (lane == 0) {
+                    Ac[tri(c, q)] = t;
+                    Ac[tri(c + 1, q)] = (double)s_rat[s_c[q]] - mean;
+                }
+            }
+            __syncthreads();
+            ldlt_bordered_wide(Ac, c, c + 2, sA, sB);
+            if (wave == 0) {
+                double dot = 0.0;
+                for (int j = lane; j < c; j += 64) dot = fma(Ac[tri(c, j)] * Ac[tri(c + 1, j)], Ac[tri(j, j)], dot);
+                dot = wsum(dot);
+                if (lane == 0) {
+                    double pred = dot + mean;
+                    if (pred > 5) pred = 5;
+                    if (pred < 1) pred = 1;
+                    const double d = s_misc[1] - pred;
+                    const uint64_t o = a.pair_out[p];
+                    a.mse[o] = (float)(d * d);
+                    a.kk[o] = c;
+                    if (a.pred) a.pred[o] = pred;
+                    if (a.lim_out) a.lim_out[o] = L;
+                }
+            }
+            __syncthreads();
+            continue;
+        }
         const size_t need = (size_t)(L + 2) * (L + 3) / 2;
         double* A = need <= (size_t)kLdsA ? s_la : fa;
         // bordered Gram: A[i][j] = (U_C^T U_C)_ij (j <= i < L), A[L][j] = t_j, A[L+1][j] = v_j
