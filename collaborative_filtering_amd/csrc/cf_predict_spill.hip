@@ -486,10 +486,113 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
             }
         }
     }
+    // ---- complement basis W (k x du, du = k - Lu) of span(Q), for the G-mode of the
+    // rank-deficient ratings (spill_predict_kernel): Y = (I - Q Q^T) Omega for a +-1 test matrix,
+    // W = Y L^-T D^-1/2 from Y^T Y = L D L^T (Cholesky-QR), then W^T r and W^T 1 -- the basis of
+    // cf_predict.hip's G-mode, here beside P.  Regions: W in Gt (ld du), Q^T Omega and the packed
+    // Y^T Y after Gbar's Lu x Lu in Gb, W^T r / W^T 1 after PG / PH.
+    const int du = k - Lu;
+    int gm = 0;
+    if (basis && du > 0 && du <= CF_SPILL_MAX_K) {
+        const double* Q = Qb[cur];
+        double* Wm = Gt;
+        double* QO = Gb + (size_t)Lu * Lu;
+        double* YY = QO + (size_t)Lu * du;
+        __shared__ int s_fail;
+        // Omega(i, j) = +-1 from a hash of the user's content (k and three item ids), i and j
+        const auto mix = [](uint32_t h) {
+            h ^= h >> 16;
+            h *= 0x7FEB352Du;
+            h ^= h >> 15;
+            h *= 0x846CA68Bu;
+            return h ^ (h >> 16);
+        };
+        const uint32_t seed = mix(mix(mix((uint32_t)k * 0x9E3779B1u + 0x7F4A7C15u) ^ a.items[base]) ^
+                                  a.items[base + (k >> 1)]) ^ a.items[base + k - 1];
+        const auto omega = [seed](int i, int j) -> double {
+            uint32_t h = seed ^ ((uint32_t)i * 0x85EBCA6Bu) ^ ((uint32_t)j * 0xC2B2AE35u);
+            h ^= h >> 16;
+            h *= 0x7FEB352Du;
+            h ^= h >> 15;
+            h *= 0x846CA68Bu;
+            h ^= h >> 16;
+            return (h & 1u) ? 1.0 : -1.0;
+        };
+        tile_gemm<false, false>(
+            Lu, du, [=](int i, int l) { return Q[(size_t)l * Lu + i]; }, [=](int l, int j) { return omega(l, j); },
+            [=](int) { return k; }, [](int, int) { return true; },
+            [=](int i, int j, double v) { QO[(size_t)i * du + j] = v; }, sA, sB);
+        tile_gemm<true, false>(
+            k, du, [=](int i, int l) { return Q[(size_t)i * Lu + l]; }, [=](int l, int j) { return QO[(size_t)l * du + j]; },
+            [=](int) { return Lu; }, [](int, int) { return true; },
+            [=](int i, int j, double v) { Wm[(size_t)i * du + j] = omega(i, j) - v; }, sA, sB);
+        tile_gemm<false, false>(
+            du, du, [=](int i, int l) { return Wm[(size_t)l * du + i]; }, [=](int l, int j) { return Wm[(size_t)l * du + j]; },
+            [=](int) { return k; }, [](int i0, int j0) { return j0 <= i0; },
+            [=](int i, int j, double v) {
+                if (j <= i) YY[tri(i, j)] = v;
+            },
+            sA, sB);
+        ldlt_bordered_wide(YY, du, du, sA, sB);
+        if (tid == 0) s_fail = 0;
+        __syncthreads();
+        double dmax = 0.0;
+        for (int j = 0; j < du; ++j) dmax = fmax(dmax, YY[tri(j, j)]);
+        bool fail = false;
+        for (int i = tid; i < k; i += kT) {
+            double* xi = Wm + (size_t)i * du;
+            // forward substitution in 16-column register panels (cf_predict.hip's W solve)
+            for (int p0 = 0; p0 < du; p0 += 16) {
+                const int bw = min(16, du - p0);
+                double acc[16];
+                int rb[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    acc[q] = q < bw ? xi[p0 + q] : 0.0;
+                    rb[q] = tri(p0 + min(q, bw - 1), 0);
+                }
+                for (int t = 0; t < p0; ++t) {
+                    const double xt = xi[t];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) acc[q] = fma(-YY[rb[q] + t], xt, acc[q]);
+                }
+#pragma unroll
+                for (int q = 1; q < 16; ++q)
+#pragma unroll
+                    for (int t = 0; t < q; ++t) acc[q] = fma(-YY[rb[q] + p0 + t], acc[t], acc[q]);
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    if (q < bw) xi[p0 + q] = acc[q];
+            }
+            for (int j = 0; j < du; ++j) {
+                const double dj = YY[tri(j, j)];
+                fail |= !(dj > 1e-12 * dmax);
+                xi[j] = dj > 0.0 ? xi[j] / sqrt(dj) : 0.0;
+            }
+        }
+        if (fail) s_fail = 1;
+        __syncthreads();
+        gm = s_fail == 0;
+        if (gm) {   // W^T r, W^T 1
+            double* gw = gh + 2 * (size_t)Lu + 2 * (size_t)k;
+            for (int j = tid; j < du; j += kT) {
+                double g = 0.0, h = 0.0;
+                for (int i = 0; i < k; ++i) {
+                    const double w = Wm[(size_t)i * du + j];
+                    g = fma(w, (double)a.ratings[base + i], g);
+                    h += w;
+                }
+                gw[j] = g;
+                gw[du + j] = h;
+            }
+        }
+        __syncthreads();
+    }
     if (tid == 0) {
         hdr[0] = Lu;
         hdr[1] = basis;
         hdr[2] = cur;
+        hdr[3] = gm;   // complement basis W ready: G-mode for c < lim
     }
 }
 
@@ -605,6 +708,62 @@ __global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
             if (!fast && a.phase && tid == 0) pc[10] += 1;
         }
         SP_STAMP(1);
+        if (fast && c < lim && hdr[3] && k - lim < c) {
+            // G-mode (cf_predict.hip): in the complement coordinates X = [Q | W] of the user's
+            // basis, B = X[Cbar, lim:k] (nc x d, d = k - lim < c), h = g - B^T y_Cbar with
+            // g = (X^T r - mean X^T 1)[lim:k]:  pred - mean = -w_r^T (B^T B)^-1 h, w_r = X[r, lim:k]
+            // -- the same minimum-norm prediction as P_{r,C} P_CC^-1 y_C below, from a d x d
+            // system instead of c x c (the k > 3072 users: d ~ 600 against c ~ 2000)
+            const int d = k - lim, du = k - Lu;
+            const double* Wm = slot + 3 * kk2;
+            const double* gW = gvec + 2 * Lu + 2 * k;
+            const double* hW = gW + du;
+            const auto X = [&](int i, int col) -> double {
+                return col < Lu ? Q[(size_t)i * Lu + col] : Wm[(size_t)i * du + (col - Lu)];
+            };
+            const size_t need = (size_t)(d + 2) * (d + 3) / 2;
+            double* A = need <= (size_t)kLdsA ? s_la : fa;
+            tile_gemm<false, false>(
+                d, d, [&](int i, int l) { return X(s_ncon[l], lim + i); }, [&](int l, int j) { return X(s_ncon[l], lim + j); },
+                [=](int) { return nc; }, [](int i0, int j0) { return j0 <= i0; },
+                [&](int i, int j, double v) {
+                    if (j <= i) A[tri(i, j)] = v;
+                },
+                sA, sB);
+            for (int j = tid; j < d; j += kT) {
+                const int col = lim + j;
+                double h = col < Lu ? gvec[col] - mu * hvec[col] : gW[col - Lu] - mu * hW[col - Lu];
+                for (int q = 0; q < nc; ++q) h = fma(-X(s_ncon[q], col), (double)s_rat[s_ncon[q]] - mu, h);
+                A[tri(d, j)] = X(r, col);
+                A[tri(d + 1, j)] = h;
+            }
+            __syncthreads();
+            SP_STAMP(2);
+            ldlt_bordered_wide<OCC>(A, d, d + 2, sA, sB, a.phase ? pc + 12 : nullptr);
+            if (wave == 0) {
+                double dot = 0.0;
+                for (int j = lane; j < d; j += 64) dot = fma(A[tri(d, j)] * A[tri(d + 1, j)], A[tri(j, j)], dot);
+                dot = wsum(dot);
+                if (lane == 0) s_misc[2] = dot;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                double pred = mu - s_misc[2];
+                if (pred > 5) pred = 5;
+                if (pred < 1) pred = 1;
+                const double dd = (double)s_rat[r] - pred;
+                a.mse[base + r] = (float)(dd * dd);
+                a.kk[base + r] = c;
+                if (a.pred) a.pred[base + r] = pred;
+                if (a.phase) {
+                    pc[6] += 1;
+                    pc[8] += d;
+                }
+            }
+            __syncthreads();
+            SP_STAMP(4);
+            continue;
+        }
         if (fast && c < lim) {
             // Underdetermined (c < lim): K = I - P_CbarCbar is singular (rank <= k - lim < nc)
             // and U_CS^T U_CS too.  The prediction is the minimum-norm least-squares one, as
