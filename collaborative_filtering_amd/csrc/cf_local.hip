@@ -166,12 +166,13 @@ __global__ __launch_bounds__(kThreads) void local_predict_kernel(LocalPredArgs a
 // F(mu) = W_R (Theta - mu)^-1 W_R^T, the inverse of the Schur complement of B_hh - mu) gives
 //   #{eigenvalues of B_hh below mu} = #{theta_j < mu} - #{negative eigenvalues of F(mu)},
 // and interlacing puts lambda_min(B_hh) in [theta_0, theta_c] (c = |R|).  Bisection on that
-// count -- per step one c x c F (VALU fp64 over W_R staged through LDS 96 columns at a time)
+// count -- per step one c x c F (VALU fp64 over W_R staged through LDS 16 columns at a time)
 // and its LDL^T inertia -- replaces the per-pair fp64 Gram + tridiagonalisation of n x n (mode 2
-// of eigen_spill_kernel, ~n^3 per pair): ~40 c^2 n per pair.  One workgroup per pair; pairs with
+// of eigen_spill_kernel, ~n^3 per pair): ~22 c^2 n per pair.  One workgroup per pair; pairs with
 // c > kWlimCmax keep mode 2 (solved = 0).
-constexpr int kWlimCmax = 96;
-constexpr int kWlimJc = 96;    // LDS ~75 KB: two workgroups per CU
+constexpr int kWlimCmax = 184;   // F packed fp64 in LDS (133 KB): every pair of a k <= 180 user
+constexpr int kWlimJc = 16;      // columns of W_R staged per chunk (LDS 149 KB in all)
+constexpr int kWlimItems = 5;    // 4 x 4 tiles per thread: ceil(1081 / 256) at c = 184
 constexpr int kWlimIters = 44;
 struct WlimArgs {
     uint32_t n_pairs;
@@ -234,14 +235,14 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
         // tile's columns (segments) and their partial sums meet in LDS
         const int nb = (c + 3) >> 2, ntile = nb * (nb + 1) / 2;
         const int nseg = ntile == 0 ? 1 : max(1, min(kThreads / ntile, kWlimJc / 4));
-        const int nwork = ntile * nseg;   // <= 300 (c <= 96): at most two items per thread
+        const int nwork = ntile * nseg;   // <= 1081 (c <= 184): at most kWlimItems per thread
         const int cp = 4 * nb;            // staged rows (zero beyond c)
         for (int it = 0; it < kWlimIters && c > 0 && hi - lo > 1e-11 * fabs(hi); ++it) {
             const double mu = 0.5 * (lo + hi);
             for (int e = tid; e < c * (c + 1) / 2; e += kThreads) s_F[e] = 0.0;
-            double acc[2][16];
+            double acc[kWlimItems][16];
 #pragma unroll
-            for (int q = 0; q < 2; ++q)
+            for (int q = 0; q < kWlimItems; ++q)
 #pragma unroll
                 for (int x = 0; x < 16; ++x) acc[q][x] = 0.0;
             for (int j0 = 0; j0 < n; j0 += kWlimJc) {
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
                     s_d[jj] = j0 + jj < n ? 1.0 / ((double)th[j0 + jj] - mu) : 0.0;
                 __syncthreads();
 #pragma unroll
-                for (int q = 0; q < 2; ++q) {
+                for (int q = 0; q < kWlimItems; ++q) {
                     const int w = tid + q * kThreads;
                     if (w >= nwork) continue;
                     const int t = w / nseg, g = w - t * nseg;
@@ -281,7 +282,7 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
             }
             // partial tiles into the packed lower triangle of F
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
+            for (int q = 0; q < kWlimItems; ++q) {
                 const int w = tid + q * kThreads;
                 if (w >= nwork) continue;
                 const int t = w / nseg;

@@ -83,7 +83,7 @@ int cf_set_eigen_refine(cf_ctx* ctx, int enable, float stop_rel, float delta);
  * Replaces the per-rating neighbour scan of local_calc_precomp.cpp:254-265. */
 int cf_set_step_masks(cf_ctx* ctx, int enable);
 /* cf_local_calc, units with n > CF_MAX_K: bisect != 0 (default) computes the w_lim of a
- * (movie, test user) pair with c <= 96 rated rows from the eigenpairs of the movie's
+ * (movie, test user) pair with c <= 184 rated rows from the eigenpairs of the movie's
  * B = L2 L2^T, shared by all its pairs (Haynsworth inertia count, bisection);
  * bisect 0 tridiagonalises each pair's L2_h L2_h^T as local_calc.cpp:425-436 spells it out.
  * Both return sqrt(lambda_min(L2_h L2_h^T)). */
