@@ -723,20 +723,25 @@ __global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
             };
             const size_t need = (size_t)(d + 2) * (d + 3) / 2;
             double* A = need <= (size_t)kLdsA ? s_la : fa;
+            // one Gram pass over the Cbar rows of [B | y]: B^T B, and B^T y in its last row,
+            // which becomes h = g - B^T y in the packed border row d + 1 (row d: w_r)
+            const auto By = [&](int l, int i) -> double {
+                return i < d ? X(s_ncon[l], lim + i) : (double)s_rat[s_ncon[l]] - mu;
+            };
             tile_gemm<false, false>(
-                d, d, [&](int i, int l) { return X(s_ncon[l], lim + i); }, [&](int l, int j) { return X(s_ncon[l], lim + j); },
+                d + 1, d + 1, [&](int i, int l) { return By(l, i); }, [&](int l, int j) { return By(l, j); },
                 [=](int) { return nc; }, [](int i0, int j0) { return j0 <= i0; },
                 [&](int i, int j, double v) {
-                    if (j <= i) A[tri(i, j)] = v;
+                    if (j > i) return;
+                    if (i < d) {
+                        A[tri(i, j)] = v;
+                    } else if (j < d) {
+                        const int col = lim + j;
+                        A[tri(d + 1, j)] = (col < Lu ? gvec[col] - mu * hvec[col] : gW[col - Lu] - mu * hW[col - Lu]) - v;
+                    }
                 },
                 sA, sB);
-            for (int j = tid; j < d; j += kT) {
-                const int col = lim + j;
-                double h = col < Lu ? gvec[col] - mu * hvec[col] : gW[col - Lu] - mu * hW[col - Lu];
-                for (int q = 0; q < nc; ++q) h = fma(-X(s_ncon[q], col), (double)s_rat[s_ncon[q]] - mu, h);
-                A[tri(d, j)] = X(r, col);
-                A[tri(d + 1, j)] = h;
-            }
+            for (int j = tid; j < d; j += kT) A[tri(d, j)] = X(r, lim + j);
             __syncthreads();
             SP_STAMP(2);
             ldlt_bordered_wide<OCC>(A, d, d + 2, sA, sB, a.phase ? pc + 12 : nullptr);

@@ -578,6 +578,47 @@ def test_c5_tail_k_up_to_5000(gpu_ctx, c4_graph):
         run.free()
 
 
+def test_spill_rank_deficient_rows_pinned(gpu_ctx, c4_graph):
+    """Spill users (k > 192) on the C4 graph through the timed path: their rank-deficient rows
+    (0 < c < lim) return the minimum-norm least-squares prediction -- from the complement basis
+    X = [Q | W] as a d x d system when d = k - lim < c (G-mode), else from the c x c projector
+    block -- pinned to numpy within 1e-9 max(1, cond(P_CC)) on 40 sampled rows per
+    user; the rows that are not pinnable are counted by reason."""
+    from collaborative_filtering_amd import synth, workloads as wlm
+
+    ks = np.array([260, 480, 900], dtype=np.uint32)
+    off, items, rat = synth.user_items(wlm.CONFIGS["c5"]["seed"] + 9, ks, 50_000, threads=THREADS)
+    run = FusedRun(gpu_ctx, c4_graph[0], 50_000, off, items, rat)
+    rng = np.random.default_rng(3)
+    counts, bad, worst = {}, [], 0.0
+    try:
+        for u in range(len(ks)):
+            it, rat_u, Wu, m, sig_u, ev, U = run.user(u)
+            k = len(it)
+            b = int(off[u])
+            tab = run.sigs[:k]   # compat: row i's w_lim is entry i of the concatenated table
+            U64 = U.astype(np.float64)
+            for r in rng.choice(k, size=40, replace=False):
+                r = int(r)
+                want, cond, why = pinv_prediction(U64, ev, float(tab[r]), Wu, rat_u.astype(np.float64), r, k)
+                if want is None:
+                    counts[why] = counts.get(why, 0) + 1
+                    continue
+                lim = min(max(int(np.argmax(ev > tab[r])) if np.any(ev > tab[r]) else m, 2), m)
+                c = int(run.kk[b + r])
+                key = "pinned, g-mode" if k - lim < c else "pinned, projector block"
+                counts[key] = counts.get(key, 0) + 1
+                err = abs(float(run.pred[b + r]) - want)
+                worst = max(worst, err / max(1.0, cond))
+                if err > 1e-9 * max(1.0, cond) * max(1.0, abs(want)):
+                    bad.append((u, r, float(run.pred[b + r]), want, cond, k - lim, c))
+    finally:
+        run.free()
+    print(f"spill rank-deficient rows: {counts}, max err / cond {worst:.2e}", flush=True)
+    assert not bad, bad[:10]
+    assert sum(v for key, v in counts.items() if key.startswith("pinned")) >= 30, counts
+
+
 def test_spill_big_single_workgroup(gpu_ctx, c4_graph):
     """The BIG layout (k > 3072) on one workgroup per user -- the path local_calc's units with
     n > 3072 take, and compute_eigens' with CF_SPILL_MC=0 -- next to the staged multi-CU solver

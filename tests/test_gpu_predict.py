@@ -230,61 +230,3 @@ def test_predict_spill_users_match_oracle(gpu_ctx, density, mode, wlim, min_good
     assert n_good >= min_good, (n_good, n_ill)
     print(f"spill density={density} mode={mode} wlim={wlim} well-conditioned={n_good} ill-conditioned={n_ill}")
 
-
-@pytest.mark.parametrize("density,wlim", [(0.6, None), (0.3, 0.3)])
-def test_predict_spill_rank_deficient_min_norm(gpu_ctx, density, wlim):
-    """Rank-deficient rows (0 < c < lim) of spill users (k > 192) return the minimum-norm
-    least-squares prediction clamp(mean + P_rC P_CC^-1 y_C) (P the projector on U[:, :lim];
-    DESIGN 3.8): from the complement basis X = [Q | W] as a d x d system (G-mode) when
-    d = k - lim < c, else from the c x c block of P.  Both are pinned to numpy within
-    1e-9 max(1, cond(P_CC)) wherever cond(P_CC) <= 1e7 and no column is dropped."""
-    ks = [300, 257, 230, 210, 193]
-    W, off, items, rat, m, sigs, evals, evec_off, evecs, blocks = build_case(density, ks, seed=81, n_items=400)
-    mode = CF_SIGS_COMPAT if wlim is None else CF_SIGS_OWN
-    sigtab = sigs.copy() if wlim is None else np.full_like(sigs, wlim)
-    gpu_ctx.upload_graph_dense(W)
-    mse_g, kk_g, pred_g = gpu_ctx.predict_precomp(off, items, rat, m, evals, evec_off, evecs, sigtab,
-                                                  sig_mode=mode, want_pred=True)
-    counts = {"g-mode": 0, "projector block": 0, "skipped": 0}
-    bad = []
-    worst = 0.0
-    for u in range(len(ks)):
-        b, e = int(off[u]), int(off[u + 1])
-        k = e - b
-        it = items[b:e].astype(np.int64)
-        ev, U = blocks[u]
-        Wu = W[np.ix_(it, it)]
-        tab = sigtab[:k] if mode == CF_SIGS_COMPAT else sigtab[b:e]
-        ru = rat[b:e].astype(np.float64)
-        mu_u = int(m[u])
-        for r in range(k):
-            lim = mu_u
-            for j in range(mu_u):
-                if ev[j] > tab[r]:
-                    lim = j
-                    break
-            lim = min(max(lim, 2), mu_u)
-            C = np.nonzero(Wu[r].astype(np.float64) > 0.1)[0]
-            c = len(C)
-            if c == 0 or c >= lim or Wu[r, r] > 0.1:
-                continue
-            if not np.all(np.any(U[C, :lim] >= 1e-4, axis=0)):
-                counts["skipped"] += 1
-                continue
-            Qn, _ = np.linalg.qr(U[:, :lim])
-            P = Qn @ Qn.T
-            Pcc = P[np.ix_(C, C)]
-            cond = float(np.linalg.cond(Pcc))
-            if not cond <= 1e7:
-                counts["skipped"] += 1
-                continue
-            mu = float(np.mean(ru[C]))
-            want = min(max(mu + float(P[r, C] @ np.linalg.solve(Pcc, ru[C] - mu)), 1.0), 5.0)
-            counts["g-mode" if k - lim < c else "projector block"] += 1
-            err = abs(float(pred_g[b + r]) - want)
-            worst = max(worst, err / max(1.0, cond))
-            if kk_g[b + r] != c or err > 1e-9 * max(1.0, cond) * max(1.0, abs(want)):
-                bad.append((u, r, int(kk_g[b + r]), c, float(pred_g[b + r]), want, cond, k - lim))
-    print(f"spill rank-deficient rows vs min-norm: {counts}, max err / cond {worst:.2e}")
-    assert not bad, bad[:10]
-    assert counts["g-mode"] + counts["projector block"] >= 50, counts
