@@ -237,8 +237,32 @@ class Workload:
                               tab, CF_SIGS_COMPAT, self.d_mse, self.d_kk, stream=sp)
 
 
+_PHASE = ["start"]
+
+
+def phase(name):
+    """Name the bench phase for the stderr heartbeat (and print it there)."""
+    _PHASE[0] = name
+    print(f"[bench] {name}", file=sys.stderr, flush=True)
+
+
+def _heartbeat(t0):
+    # one stderr line every 30 s: long silent phases (graph build, PMC passes, the I/O and
+    # local_calc legs) stay visible to a supervisor that takes a silent process for a hung one
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(30)
+            print(f"[bench] {time.time() - t0:.0f} s: {_PHASE[0]}", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     args = parse()
+    if not args.pmc_child:
+        _heartbeat(time.time())
     import torch
     import torch.distributed as dist
 
@@ -284,6 +308,7 @@ def main():
     want_cpu = solo and not args.no_cpu_baseline
 
     # ---- workload (untimed setup) -------------------------------------------------
+    phase("setup: item graph and workload")
     t_setup = time.time()
     d_W, W_host, gstats = train_graph(Context, dev_index, dev, torch, cfg["seed"], cfg["train_users"], cfg["items"],
                                       keep_host=want_cpu)
@@ -365,6 +390,7 @@ def main():
         torch.cuda.synchronize(dev)
         return
 
+    phase("warmup and timed steps")
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize(dev)
@@ -514,6 +540,7 @@ def main():
 
     # ---- HBM traffic (rank 0, N=1): two rocprofv3 --pmc passes over one child step ------
     if solo and args.pmc == "auto":
+        phase("PMC traffic passes (rocprofv3 children)")
         tr = pmc_traffic(args)
         if tr is not None:
             for key, roof in (("predict", roof_pred), ("eigen", roof_eigen)):
@@ -533,6 +560,7 @@ def main():
 
     # ---- CPU baseline (rank 0, N=1): the oracle in precompute_local_threads form ---------
     if want_cpu:
+        phase("CPU baseline sample")
         result["cpu_baseline"] = cpu_baseline(args, wl, W_host,
                                               dev={"m": m_h, "kk": kk_h, "evals": evals_h, "sigs": sigs_h,
                                                    "mse": mse_h} if world == 1 else None)
@@ -540,6 +568,7 @@ def main():
 
     # ---- secondary legs (rank 0, N=1; not part of `value`) -----------------------------
     if solo and args.io == "auto" and args.config == "c4":
+        phase("C4 out_eigen_ I/O leg")
         # the C4-size out_eigen_ round trip: binary form of all 1M records,
         # text form of the first 100k (the full text file would be ~128 GB)
         try:
@@ -550,14 +579,18 @@ def main():
         wl.plan.close()
         del wl
         torch.cuda.empty_cache()
+        phase("C2 leg (steps, out_eigen_ text, local_calc --pct 1)")
         result["config2"] = c2_leg(args, ctx, dev_index, dev, torch)
     if solo and args.knn2 == "auto":
         torch.cuda.empty_cache()
+        phase("C3 knn2 leg")
         result["knn2"] = knn2_leg(args, ctx, dev, torch)
     if solo and args.prep == "auto":
         torch.cuda.empty_cache()
+        phase("data-prep leg")
         result["prep"] = prep_leg(args, ctx, dev, torch)
     if solo and args.c5 == "auto":
+        phase("C5 leg")
         torch.cuda.empty_cache()
         W, _, _ = train_graph(Context, dev_index, dev, torch, CONFIGS["c4"]["seed"], CONFIGS["c4"]["train_users"],
                               CONFIGS["c4"]["items"])

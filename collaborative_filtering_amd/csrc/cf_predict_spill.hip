@@ -723,21 +723,28 @@ __global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
             };
             const size_t need = (size_t)(d + 2) * (d + 3) / 2;
             double* A = need <= (size_t)kLdsA ? s_la : fa;
-            // one Gram pass over the Cbar rows of [B | y]: B^T B, and B^T y in its last row,
-            // which becomes h = g - B^T y in the packed border row d + 1 (row d: w_r)
+            // one Gram pass over the rows of [X[., lim:k] | y] of the smaller of C and Cbar
+            // (X has orthonormal columns, so X_Cbar^T X_Cbar = I - X_C^T X_C and
+            // h = X_C^T y_C = g - X_Cbar^T y_Cbar): B^T B and, in its last row, h, which goes to
+            // the packed border row d + 1 (row d: w_r).  The subtraction costs ~eps cond(B^T B),
+            // the conditioning of the minimum-norm problem itself.
+            const bool via_c = c < nc;
+            const int nrow = via_c ? c : nc;
+            const int* rows = via_c ? s_conn : s_ncon;
             const auto By = [&](int l, int i) -> double {
-                return i < d ? X(s_ncon[l], lim + i) : (double)s_rat[s_ncon[l]] - mu;
+                return i < d ? X(rows[l], lim + i) : (double)s_rat[rows[l]] - mu;
             };
             tile_gemm<false, false>(
                 d + 1, d + 1, [&](int i, int l) { return By(l, i); }, [&](int l, int j) { return By(l, j); },
-                [=](int) { return nc; }, [](int i0, int j0) { return j0 <= i0; },
+                [=](int) { return nrow; }, [](int i0, int j0) { return j0 <= i0; },
                 [&](int i, int j, double v) {
                     if (j > i) return;
                     if (i < d) {
-                        A[tri(i, j)] = v;
+                        A[tri(i, j)] = via_c ? (i == j ? 1.0 : 0.0) - v : v;
                     } else if (j < d) {
                         const int col = lim + j;
-                        A[tri(d + 1, j)] = (col < Lu ? gvec[col] - mu * hvec[col] : gW[col - Lu] - mu * hW[col - Lu]) - v;
+                        A[tri(d + 1, j)] = via_c ? v
+                                                 : (col < Lu ? gvec[col] - mu * hvec[col] : gW[col - Lu] - mu * hW[col - Lu]) - v;
                     }
                 },
                 sA, sB);
