@@ -1467,8 +1467,10 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
             const long v = e ? atol(e) : 1536L;
             return (uint32_t)std::max<long>(CF_MAX_K, std::min<long>(v, SP_NL));
         }();
-        const bool user_mode = !loc || loc->mode == 0;
-        const uint32_t cuts[2] = {user_mode ? mc_min : (uint32_t)SP_NL, 0u};
+        // every whole-unit mode (a user; local_calc's movie graph and its B = L2 L2^T) may take the
+        // staged multi-CU path; the per-pair w_lim mode (its n is the pair's unrated rows) may not
+        const bool unit_mode = !loc || loc->mode != 2;
+        const uint32_t cuts[2] = {unit_mode ? mc_min : (uint32_t)SP_NL, 0u};
         uint32_t j = b.first;
         const uint32_t end = b.first + b.count;
         auto kof = [&](uint32_t pos) {
@@ -1491,7 +1493,7 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
         const char* e = getenv("CF_SPILL_MC");
         return !(e && e[0] == '0');
     }();
-    const bool mc_on = mc_env && (!loc || loc->mode == 0);
+    const bool mc_on = mc_env && (!loc || loc->mode != 2);
     auto stride_of = [&](const Range& r) {
         return base_stride(r.kmax) + (r.big ? (mc_on ? MC_EXTRA : 3ull * CF_SPILL_MAX_K) : 0ull);
     };

@@ -183,3 +183,64 @@ def test_local_calc_spill_wlim_bisection(gpu_ctx):
     assert same_lim.sum() >= 0.99 * ok.sum(), (int(same_lim.sum()), int(ok.sum()))
     print(f"bisection: {int(ok.sum())} pairs, max rel w_lim diff {rel.max():.2e}, "
           f"lim equal {int(same_lim.sum())}; oracle: {n_wl} w_lim, {n_cmp} predictions compared")
+
+
+def test_local_calc_unit_above_mc_cut(gpu_ctx):
+    """Movies with n > 1536 rows take the staged multi-CU spill solver for both per-movie
+    eigendecompositions (the local graph's, and B = L2 L2^T's for the w_lim bisection): two
+    movies of n ~ 1650 on a dense 1700-item graph; every pair's kk exact and w_lim against
+    LAPACK's smallest eigenvalue of L2_h L2_h^T (numpy eigvalsh; the C++ oracle's tql2 at
+    n = 1650 per pair would take minutes), 1e-4 relative; predictions finite and clamped."""
+    rng = np.random.default_rng(21)
+    n_items = 1700
+    G = rng.random((n_items, n_items)).astype(np.float32)
+    G = ((G + G.T) / 2).astype(np.float32)
+    G[G < 0.03] = 0
+    np.fill_diagonal(G, 0)
+    movies = [3, 900]
+    test = {mv: {} for mv in movies}
+    for u in range(10):   # each test user rates both movies and ~30 other items
+        for mv in movies:
+            test[mv][u] = float(rng.integers(1, 6))
+        for it in rng.choice(n_items, size=30, replace=False):
+            test.setdefault(int(it), {})[u] = float(rng.integers(1, 6))
+    moff, mitems, toff, tuser, trat = [0], [], np.zeros(n_items + 1, np.uint64), [], []
+    for mv in range(n_items):
+        us = sorted(test.get(mv, {}))
+        tuser += us
+        trat += [test[mv][u] for u in us]
+        toff[mv + 1] = toff[mv] + len(us)
+    units = []
+    for mv in movies:
+        nbrs = [j for j in range(n_items) if float(G[mv, j]) > 0.1]
+        units.append((mv, nbrs))
+        mitems += [mv] + nbrs
+        moff.append(len(mitems))
+    gpu_ctx.upload_graph_dense(G)
+    mse, kk, pred, wlim, lim = gpu_ctx.local_calc(np.array(moff), np.array(mitems), toff, np.array(tuser),
+                                                  np.array(trat))
+    bad, n_wl = [], 0
+    for mv, nbrs in units:
+        assert len(nbrs) + 1 > 1536, len(nbrs)
+        W = orc.local_graph(mv, nbrs, G)
+        users, R = orc.local_ratings(mv, nbrs, test)
+        d = W.sum(1)
+        L2 = (np.sqrt(1 / d)[:, None] * (np.diag(d) - W)) * np.sqrt(1 / d)[None, :]
+        b = int(toff[mv])
+        for t, u in enumerate(users):
+            g = b + t
+            h = [i for i in range(len(nbrs) + 1) if i == 0 or R[i, t] == 0]   # unrated rows (:405-413)
+            c = sum(1 for i in range(1, len(nbrs) + 1) if R[i, t] != 0)
+            if kk[g] != c:
+                bad.append((mv, u, "kk", int(kk[g]), c))
+                continue
+            Lh = L2[h]
+            wl = float(np.sqrt(max(np.linalg.eigvalsh(Lh @ Lh.T)[0], 0.0)))
+            n_wl += 1
+            if abs(float(wlim[g]) - wl) > 1e-4 * max(1e-3, wl):
+                bad.append((mv, u, "w_lim", float(wlim[g]), wl))
+            if c > 0 and not (np.isfinite(mse[g]) and 1.0 <= pred[g] <= 5.0):
+                bad.append((mv, u, "pred", float(mse[g]), float(pred[g])))
+    assert not bad, bad[:10]
+    assert n_wl >= 20, n_wl
+    print(f"units above the multi-CU cut: n {[len(nb) + 1 for _, nb in units]}; w_lim compared {n_wl}")
