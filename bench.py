@@ -794,8 +794,11 @@ def text_phases(wl, text_users=None, label="whole C2 record set"):
     path = os.path.join(tmpdir, f"cf_bench_out_eigen_{os.getpid()}").encode()
     res = {"threads": threads, "dir": tmpdir}
     try:
-        for fmt, binary in (("text", 0), ("binary", 1)):
-            n_rec = wl.n_users if (binary or text_users is None) else min(wl.n_users, int(text_users))
+        n_text = wl.n_users if text_users is None else min(wl.n_users, int(text_users))
+        passes = [("text", 0, n_text), ("binary", 1, wl.n_users)]
+        if n_text < wl.n_users:   # the binary form on the text sample too: bytes/s on the same records
+            passes.append(("binary_text_sample", 1, n_text))
+        for fmt, binary, n_rec in passes:
             k = np.diff(wl.off[:n_rec + 1].astype(np.int64))
             mm = m[:n_rec].astype(np.int64)
             est = int(np.sum(12 + 8 * k + 4 * mm + 4 * k * mm)) * (3 if not binary else 1)
