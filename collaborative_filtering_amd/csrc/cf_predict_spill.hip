@@ -103,8 +103,16 @@ __device__ __forceinline__ double wsum(double v) {
 // whole block; ends synchronised.
 using f64x4 = __attribute__((ext_vector_type(4))) double;
 constexpr int kSt = 80;
-template <bool A_LFAST, bool B_LFAST, class FA, class FB, class FK, class FW, class FO>
+// NBUF = 2 (the caller's sA / sB hold two chunks, 2 * 16 * kSt doubles each): two chunks of raw
+// operands in flight in registers and the staged chunks alternating between the buffers, one
+// barrier per chunk (cf_predict.hip's block_gemm scheme: the gathers of a 64-wide row block are
+// ~2k cycles away, a chunk's MFMAs ~1k).  NBUF = 1 keeps the single-buffer LDS footprint for
+// the two-workgroups-per-CU predictor.  LOWER: 16 x 16 tiles wholly above the diagonal skip
+// their MFMAs (the callers keep j <= i only); tiles past M / N always do.
+template <bool A_LFAST, bool B_LFAST, int NBUF = 1, bool LOWER = false, class FA, class FB, class FK, class FW,
+          class FO>
 __device__ void tile_gemm(int M, int N, FA ldA, FB ldB, FK kend, FW want, FO out, double* sA, double* sB) {
+    static_assert(NBUF == 1 || NBUF == 2, "one or two staging buffers");
     const int tid = threadIdx.x, lane = tid & 63;
     const int wr = (tid >> 6) >> 1, wc = (tid >> 6) & 1;
     const int ti = (M + 63) >> 6, tj = (N + 63) >> 6;
@@ -112,13 +120,21 @@ __device__ void tile_gemm(int M, int N, FA ldA, FB ldB, FK kend, FW want, FO out
         const int i0 = (t / tj) << 6, j0 = (t % tj) << 6;
         if (!want(i0, j0)) continue;
         const int K = kend(j0);
+        bool live[2][2];
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) {
+                const int r0 = i0 + 32 * wr + 16 * x, c0 = j0 + 32 * wc + 16 * y;
+                live[x][y] = r0 < M && c0 < N && (!LOWER || c0 <= r0 + 15);
+            }
         f64x4 acc[2][2];
 #pragma unroll
         for (int x = 0; x < 2; ++x)
 #pragma unroll
             for (int y = 0; y < 2; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
-        double ra[4], rb[4];
-        auto fetch = [&](int l0) {
+        double ra0[4], rb0[4], ra1[4], rb1[4];
+        auto fetch = [&](int l0, double (&ra)[4], double (&rb)[4]) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int e = tid + q * kT;
@@ -128,34 +144,63 @@ __device__ void tile_gemm(int M, int N, FA ldA, FB ldB, FK kend, FW want, FO out
                 rb[q] = ldB(min(l0 + lb, K - 1), min(j0 + jj, N - 1));
             }
         };
-        if (K > 0) fetch(0);
-        for (int l0 = 0; l0 < K; l0 += 16) {
+        auto stage = [&](int l0, double (&ra)[4], double (&rb)[4], int b) {
+            double* As = sA + (NBUF - 1) * b * 16 * kSt;
+            double* Bs = sB + (NBUF - 1) * b * 16 * kSt;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int e = tid + q * kT;
                 const int ii = A_LFAST ? (e >> 4) : (e & 63), la = A_LFAST ? (e & 15) : (e >> 6);
                 const int jj = B_LFAST ? (e >> 4) : (e & 63), lb = B_LFAST ? (e & 15) : (e >> 6);
-                sA[la * kSt + ii] = (i0 + ii < M && l0 + la < K) ? ra[q] : 0.0;
-                sB[lb * kSt + jj] = (j0 + jj < N && l0 + lb < K) ? rb[q] : 0.0;
+                As[la * kSt + ii] = (i0 + ii < M && l0 + la < K) ? ra[q] : 0.0;
+                Bs[lb * kSt + jj] = (j0 + jj < N && l0 + lb < K) ? rb[q] : 0.0;
             }
             __syncthreads();
-            if (l0 + 16 < K) fetch(l0 + 16);
+        };
+        auto mma = [&](int b) {
+            const double* As = sA + (NBUF - 1) * b * 16 * kSt;
+            const double* Bs = sB + (NBUF - 1) * b * 16 * kSt;
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
                 const int row = (4 * ks + (lane >> 4)) * kSt + (lane & 15);
                 double av[2], bv[2];
 #pragma unroll
                 for (int x = 0; x < 2; ++x) {
-                    av[x] = sA[row + 32 * wr + 16 * x];
-                    bv[x] = sB[row + 32 * wc + 16 * x];
+                    av[x] = As[row + 32 * wr + 16 * x];
+                    bv[x] = Bs[row + 32 * wc + 16 * x];
                 }
 #pragma unroll
                 for (int x = 0; x < 2; ++x)
 #pragma unroll
                     for (int y = 0; y < 2; ++y)
-                        acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
+                        if (live[x][y])
+                            acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
             }
-            __syncthreads();   // the chunk is consumed before the next one is staged
+        };
+        if (NBUF == 2) {
+            if (K > 0) fetch(0, ra0, rb0);
+            if (K > 16) fetch(16, ra1, rb1);
+            for (int l0 = 0; l0 < K; l0 += 32) {
+                // chunk c goes to buffer c & 1 after the barrier that published chunk c - 1,
+                // which every wave reaches only after its MFMAs on chunk c - 2 (same buffer)
+                stage(l0, ra0, rb0, 0);
+                if (l0 + 32 < K) fetch(l0 + 32, ra0, rb0);
+                mma(0);
+                if (l0 + 16 < K) {
+                    stage(l0 + 16, ra1, rb1, 1);
+                    if (l0 + 48 < K) fetch(l0 + 48, ra1, rb1);
+                    mma(1);
+                }
+            }
+            __syncthreads();   // the next tile restarts at buffer 0, which slower waves may still read
+        } else {
+            if (K > 0) fetch(0, ra0, rb0);
+            for (int l0 = 0; l0 < K; l0 += 16) {
+                stage(l0, ra0, rb0, 0);
+                if (l0 + 16 < K) fetch(l0 + 16, ra0, rb0);
+                mma(0);
+                __syncthreads();   // the chunk is consumed before the next one is staged
+            }
         }
 #pragma unroll
         for (int x = 0; x < 2; ++x)
@@ -356,7 +401,7 @@ __device__ void ldlt_bordered_wide(double* A, int L, int nrows, double* sA, doub
 // ---- per-user tables ---------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
-    __shared__ double sA[16 * kSt], sB[16 * kSt];
+    __shared__ double sA[2 * 16 * kSt], sB[2 * 16 * kSt];   // tile_gemm<.., 2>: two staging buffers
     __shared__ double s_ev[CF_SPILL_MAX_K];
     __shared__ int s_hdr[4];
     __shared__ float s_dev[kW];
@@ -411,7 +456,7 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
         const double* Q = Qb[cur];
         double* G = step == 0 ? Gb : Gt;
         float dev = 0.0f;
-        tile_gemm<false, false>(
+        tile_gemm<false, false, 2>(
             Lu, Lu, [=](int i, int l) { return Q[(size_t)l * Lu + i]; },
             [=](int l, int j) { return Q[(size_t)l * Lu + j]; }, [=](int) { return k; },
             [](int, int) { return true; },
@@ -432,7 +477,7 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
         // Q' = Q T,  T(l, j) = -G(l, j) (l < j), 1.5 - G(j, j)/2 (l = j), 0 (l > j)
         const double* Gr = G;
         double* Qn = Qb[cur ^ 1];
-        tile_gemm<true, false>(
+        tile_gemm<true, false, 2>(
             k, Lu, [=](int i, int l) { return Q[(size_t)i * Lu + l]; },
             [=](int l, int j) {
                 const double gv = Gr[(size_t)l * Lu + j];
@@ -459,7 +504,7 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
         __syncthreads();
         // P = Q Q^T over [0, Lu) (k x k, ld k) into the spare Q buffer; PG = Q g, PH = Q h
         double* P = Qb[cur ^ 1];
-        tile_gemm<true, true>(
+        tile_gemm<true, true, 2, true>(
             k, k, [=](int i, int l) { return Q[(size_t)i * Lu + l]; },
             [=](int l, int j) { return Q[(size_t)j * Lu + l]; }, [=](int) { return Lu; },
             [](int i0, int j0) { return j0 <= i0; },
@@ -518,15 +563,15 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
             h ^= h >> 16;
             return (h & 1u) ? 1.0 : -1.0;
         };
-        tile_gemm<false, false>(
+        tile_gemm<false, false, 2>(
             Lu, du, [=](int i, int l) { return Q[(size_t)l * Lu + i]; }, [=](int l, int j) { return omega(l, j); },
             [=](int) { return k; }, [](int, int) { return true; },
             [=](int i, int j, double v) { QO[(size_t)i * du + j] = v; }, sA, sB);
-        tile_gemm<true, false>(
+        tile_gemm<true, false, 2>(
             k, du, [=](int i, int l) { return Q[(size_t)i * Lu + l]; }, [=](int l, int j) { return QO[(size_t)l * du + j]; },
             [=](int) { return Lu; }, [](int, int) { return true; },
             [=](int i, int j, double v) { Wm[(size_t)i * du + j] = omega(i, j) - v; }, sA, sB);
-        tile_gemm<false, false>(
+        tile_gemm<false, false, 2, true>(
             du, du, [=](int i, int l) { return Wm[(size_t)l * du + i]; }, [=](int l, int j) { return Wm[(size_t)l * du + j]; },
             [=](int) { return k; }, [](int i0, int j0) { return j0 <= i0; },
             [=](int i, int j, double v) {
@@ -603,7 +648,10 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
 constexpr int kSmallCap = 2816;
 template <typename T, int CAP, int OCC>
 __global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
-    __shared__ double sA[16 * kSt], sB[16 * kSt];   // GEMM staging
+    // GEMM staging: two buffers for the one-per-CU instantiation, one where two workgroups
+    // must share a CU (the <kSmallCap, 2> LDS budget)
+    constexpr int kNbuf = CAP > kSmallCap ? 2 : 1;
+    __shared__ double sA[kNbuf * 16 * kSt], sB[kNbuf * 16 * kSt];
     __shared__ double s_la[kLdsA];
     __shared__ float s_rat[CAP];
     __shared__ int s_conn[CAP];
@@ -734,7 +782,7 @@ __global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
             const auto By = [&](int l, int i) -> double {
                 return i < d ? X(rows[l], lim + i) : (double)s_rat[rows[l]] - mu;
             };
-            tile_gemm<false, false>(
+            tile_gemm<false, false, kNbuf, true>(
                 d + 1, d + 1, [&](int i, int l) { return By(l, i); }, [&](int l, int j) { return By(l, j); },
                 [=](int) { return nrow; }, [](int i0, int j0) { return j0 <= i0; },
                 [&](int i, int j, double v) {
@@ -925,7 +973,7 @@ __global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
         const int nrows = use_complement ? nc : c;
         const int* rows = use_complement ? s_ncon : s_conn;
         // A(i, j) = (U_CS^T U_CS)_ij (j <= i < L), A(L, j) = t_j, A(L + 1, j) = v_j
-        tile_gemm<false, false>(
+        tile_gemm<false, false, kNbuf, true>(
             L, L, [&](int i, int l) { return (double)U[(size_t)rows[l] * m + s_keep[i]]; },
             [&](int l, int j) { return (double)U[(size_t)rows[l] * m + s_keep[j]]; },
             [=](int) { return nrows; }, [](int i0, int j0) { return j0 <= i0; },
