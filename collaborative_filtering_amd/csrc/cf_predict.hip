@@ -72,7 +72,9 @@ constexpr double kPivMin = 1e-10;
 constexpr double kOrthoMax = 1e-2;
 constexpr float kOrthoDone = 1e-8f;
 #ifndef CF_PRED_BASIS_OCC
-#define CF_PRED_BASIS_OCC 2    // basis-kernel blocks per CU (registers; its LDS is ~50 KB)
+#define CF_PRED_BASIS_OCC 3    // basis-kernel blocks per CU: LDS ~50 KB each.  3 -> 168 VGPRs with
+                               // spills still beats 2 (256, fewer spills): C4 shard predict 170.4
+                               // -> 161.8 ms; 1 block: 214 ms (profiles/r04/pred_variants_v2, _v3)
 #endif
 
 // Per-user slot of a chunk (basis kernel -> rating kernel), offsets in doubles from the slot
