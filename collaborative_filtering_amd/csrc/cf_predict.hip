@@ -885,7 +885,10 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
 #endif
 constexpr size_t kRatingLds = 163840 / CF_PRED_RATING_OCC;
 #ifndef CF_PRED_LDL_PW
-#define CF_PRED_LDL_PW 4   // fast-path LDL^T panel width (4 or 8): columns per trailing update
+// fast-path LDL^T panel width (4 or 8): columns per trailing update.  8 (two MFMA k-steps per
+// trailing update, half the updates): C4 125k-user shard predict 163.1 -> 159.9 ms, 299 of
+// 13.3M outputs differ by <= 1.3e-5 (rounding order; profiles/r04/pred_variants_v4/)
+#define CF_PRED_LDL_PW 8
 #endif
 constexpr int kLdlPw = CF_PRED_LDL_PW;
 static_assert(kLdlPw == 4 || kLdlPw == 8, "panel width: one or two MFMA k-steps");
