@@ -79,7 +79,7 @@ int cf_create(int device, cf_ctx** out) {
     ctx->device = device;
     if (const char* e = getenv("CF_EIGEN_REFINE")) ctx->eigen_refine = e[0] != '0';   // A/B switches
     if (const char* e = getenv("CF_EIGEN_CLOSE")) ctx->close_sigrot = (float)atof(e);
-    if (const char* e = getenv("CF_EIGEN_SORT")) ctx->eigen_sort = e[0] != '0';
+    if (const char* e = getenv("CF_EIGEN_SORT")) ctx->eigen_sort = atoi(e);   // 0 off, 1 descending, 2 ascending
     if (const char* e = getenv("CF_STEP_MASKS")) ctx->step_masks = e[0] != '0';
     if (hipSetDevice(device) != hipSuccess) {
         delete ctx;

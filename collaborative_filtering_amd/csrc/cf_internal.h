@@ -65,7 +65,7 @@ struct cf_ctx {
     float stop_rel = 1e-3f;
     float refine_delta = 1e-2f;
     float close_sigrot = 8.0f;    // pairs closer than refine_delta: sweeps to close_sigrot * tol
-    int eigen_sort = 1;           // LDS Jacobi: norm-sorted sweeps (CF_EIGEN_SORT=0 for A/B)
+    int eigen_sort = 2;           // LDS Jacobi: norm-sorted sweeps, 2 ascending / 1 descending / 0 off (CF_EIGEN_SORT)
     // Optional device counters: [0] sum of sweeps, [1] users, [2] max sweeps, [3] capped users.
     unsigned long long* d_stats = nullptr;
     // Optional predictor phase-cycle counters (16 slots), see cf_debug_phases.
