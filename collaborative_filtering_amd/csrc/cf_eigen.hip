@@ -102,7 +102,7 @@ struct EigenArgs {
     float stop_rel;
     float refine_delta;
     float close_sigrot;   // close pairs converge to close_sigrot * tol
-    int sort_sweeps;      // reorder the columns by descending norm before every sweep
+    int sort_sweeps;      // reorder the columns by norm before every sweep: 2 ascending, 1 descending, 0 off
     unsigned long long* stats;
     // kLocal / kSigma
     float* l2;                  // per movie n x n row-major L2 (kLocal writes, kSigma reads)
