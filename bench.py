@@ -292,6 +292,9 @@ def main():
         return
     if args.knn2 == "only":
         with Context(dev_index) as kctx:
+            if args.pmc_child:   # one knn2 call for the PMC collector, then exit
+                knn2_workload_call(args, kctx, dev, torch)
+                return
             print(json.dumps(knn2_leg(args, kctx, dev, torch)), flush=True)
         return
     if args.prep == "only":
@@ -396,6 +399,9 @@ def main():
     torch.cuda.synchronize(dev)
 
     # ---- timed region: exactly K steps between barrier+sync pairs --------------------
+    # (per-bucket HIP event pairs on the eigen launch streams, read after the region: the
+    # dominant kernel's in-step duration for the roofline)
+    ctx.eigen_bucket_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -406,6 +412,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    bucket_ms = ctx.eigen_bucket_timing(False, read=True)
     if world > 1:
         coll_dev = dev if backend == "nccl" else torch.device("cpu")
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
@@ -464,7 +471,7 @@ def main():
     else:
         n_pred_total = n_pred_local
     value = wl.U / step_s
-    roof_eigen = eigen_roofline(wl.k, m_h, eig_s, jstats)
+    roof_eigen = eigen_roofline(wl.k, m_h, eig_s, jstats, bucket_ms)
     pred_acc = predictor_flops(wl.off, wl.k, m_h, kk_h, evals_h, sigs_h)
     roof_pred = predict_roofline(pred_acc, pred_s)
     dominant_is_pred = pred_s >= eig_s
@@ -543,6 +550,11 @@ def main():
         phase("PMC traffic passes (rocprofv3 children)")
         tr = pmc_traffic(args)
         if tr is not None:
+            dom = roof_eigen.get("dominant")
+            if dom and dom.get("kernel") == "eigen_kernel<12, true>":
+                f12, w12 = tr["eigen12"]
+                dom["traffic"] = 2.0 * f12 + w12
+                dom["traffic_note"] = "2 x FETCH_SIZE + WRITE_SIZE of the one eigen_kernel<12, true> launch of a child step"
             for key, roof in (("predict", roof_pred), ("eigen", roof_eigen)):
                 fetch, write = tr[key]
                 roof["traffic"] = 2.0 * fetch + write
@@ -603,7 +615,7 @@ def main():
         dist.destroy_process_group()
 
 
-def eigen_roofline(k, m_h, eig_s, jstats):
+def eigen_roofline(k, m_h, eig_s, jstats, bucket_ms=None):
     kf = k.astype(np.float64)
     flops = float(np.sum(9.0 * kf ** 3 + 4.0 * kf ** 2))
     # algorithmic bytes: item ids in, W_u entries (index+weight), sigs/evals/evecs out
@@ -629,7 +641,39 @@ def eigen_roofline(k, m_h, eig_s, jstats):
         "executed_flops_per_stage": exe,
         "executed_TFLOPs": exe / eig_s / 1e12,
         "executed_frac": exe / eig_s / 1e12 / FP32_PEAK_TFLOPS,
+        **({"dominant": eigen_dominant(k, bucket_ms)} if bucket_ms is not None else {}),
     }
+
+
+def eigen_dominant(k, bucket_ms):
+    """The dominant kernel of the eigen stage, eigen_kernel<12, true> (bucket 12: 176 < k <= 192,
+    one launch per step), and every other LDS bucket: algorithmic flops per launch (9k^3 + 4k^2
+    per user) over the launch's duration from cf_eigen_bucket_timing (HIP events on
+    the aux stream it runs on, mean over the timed steps; it co-runs with the other buckets on
+    the second stream, as in a rocprofv3 kernel trace of the step)."""
+    kf = k.astype(np.float64)
+    emax = np.ceil(kf / 16.0).astype(np.int64)
+    rows = []
+    for e in range(1, 13):
+        sel = (emax == e) & (kf <= 192)
+        ms = float(bucket_ms[e])
+        if not sel.any() or ms <= 0:
+            continue
+        fl = float(np.sum(9.0 * kf[sel] ** 3 + 4.0 * kf[sel] ** 2))
+        rows.append({"emax": e, "users": int(sel.sum()), "flops_per_launch": fl, "ms_per_launch": ms,
+                     "achieved_TFLOPs": fl / ms / 1e9, "frac": fl / ms / 1e9 / FP32_PEAK_TFLOPS})
+    dom = max(rows, key=lambda r: r["ms_per_launch"]) if rows else None
+    out = {"kernel": "eigen_kernel<12, true>" if dom and dom["emax"] == 12 else
+                     (f"eigen_kernel<{dom['emax']}>" if dom else None),
+           "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS, "buckets": rows,
+           "note": "per-launch algorithmic flops / the launch's HIP-event duration in the timed steps "
+                   "(mean); the stage-level achieved/frac above divides the whole stage's flops by the "
+                   "stage span (all buckets + the record pack, two streams)"}
+    if dom:
+        out.update({"users": dom["users"], "flops_per_launch": dom["flops_per_launch"],
+                    "ms_per_launch": dom["ms_per_launch"], "achieved": dom["achieved_TFLOPs"],
+                    "frac": dom["frac"]})
+    return out
 
 
 def predict_roofline(acc, pred_s):
@@ -715,7 +759,7 @@ def c2_leg(args, ctx, dev_index, dev, torch):
     return out
 
 
-def local_calc_leg(ctx, wl, W, pct=1, seed=2026, nmax=4999):
+def local_calc_leg(ctx, wl, W, pct=1, seed=2026, nmax=None):
     """local_calc's engine 2 (local_calc.cpp:262-526, cf_local_calc) as `bin/local_calc --pct P`
     runs it: movies sampled with probability P %, each movie's unit = [m, out-neighbours with
     w > 0.1] of the resident knn2 graph, test ratings = the config's user ratings grouped by
@@ -740,7 +784,7 @@ def local_calc_leg(ctx, wl, W, pct=1, seed=2026, nmax=4999):
         row = W[int(m)].cpu().numpy()
         nb = np.nonzero(row.astype(np.float64) > 0.1)[0]
         nb = nb[nb != m]
-        if 1 + len(nb) > nmax:   # CF_ERANGE in cf_local_calc (CF_SPILL_MAX_K): left out, counted
+        if nmax is not None and 1 + len(nb) > nmax:   # an optional cap (none by default): left out, counted
             over.append(1 + len(nb))
             continue
         mitems.append(np.concatenate([[m], nb]).astype(np.uint32))
@@ -756,10 +800,11 @@ def local_calc_leg(ctx, wl, W, pct=1, seed=2026, nmax=4999):
     sel = kk > 0
     return {"movies_sampled": int(len(movies)), "units": int(len(ns)),
             "unit_n": {"mean": float(ns.mean()) if len(ns) else 0.0, "max": int(ns.max()) if len(ns) else 0,
-                       "gt_192": int(np.sum(ns > 192))},
+                       "gt_192": int(np.sum(ns > 192)), "gt_5000": int(np.sum(ns > 5000))},
             "units_over_cap": {"count": len(over), "n_min": int(min(over)) if over else 0,
                                "n_max": int(max(over)) if over else 0,
-                               "note": f"units with n > {nmax} (CF_ERANGE in cf_local_calc) left out of the call"},
+                               "note": "no cap: every sampled unit is in the call" if nmax is None else
+                               f"units with n > {nmax} left out of the call"},
             "predictions": pairs, "seconds": dt, "predictions_per_s": pairs / dt if dt > 0 else 0.0,
             "rank_deficient_frac": float(np.mean(kk[sel] < lim[sel])) if sel.any() else 0.0,
             "note": f"bin/local_calc --pct {pct} on this config's knn2 graph: {len(ns)} movie units, every (movie, "
@@ -1020,18 +1065,25 @@ def prep_leg(args, ctx, dev, torch):
                              "two sorts and the bitmap are several passes over that"},
     }
     if not args.no_cpu_baseline:
-        sys.path.insert(0, ROOT)
-        from oracle import cf_prep_oracle as prep
+        # the oracle's C++ restatement with the reference's containers (a std::map per movie and
+        # role, sorted unique co-rated lists) on every host thread, over the WHOLE rating set, so
+        # its entry counts must equal the GPU's
+        import ctypes
 
-        m = 300_000
+        lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "libcf_oracle.so"))
+        lib.cfo_knn_regroup_mt.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int] * 3 + [ctypes.c_void_p]
+        threads, _ = host_threads()
+        cnt = np.zeros(3, np.uint64)
+        P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
         t = time.perf_counter()
-        prep.knn_regroup(n_items, user[:m], items[:m], rats[:m], validate[:m])
+        lib.cfo_knn_regroup_mt(n, P(user), P(items), P(rats), P(validate), n_items, n_users, threads, P(cnt))
         dt = time.perf_counter() - t
-        out["cpu_baseline"] = {"value": m / dt, "unit": "ratings/s", "cores": 1, "kind": "port",
-                               "sample": f"first {m} ratings, oracle/cf_prep_oracle.knn_regroup (Python maps, "
-                                         "the reference's map semantics), 1 thread"}
-    del d_user, d_movie, d_rat, d_val, tru, teu, trr, ter, edg, d_order
-    torch.cuda.empty_cache()
+        out["cpu_baseline"] = {"value": n / dt, "unit": "ratings/s", "cores": threads, "kind": "port",
+                               "sample": f"all {n} ratings, oracle cfo_knn_regroup_mt (C++: std::map per movie and "
+                                         f"role, last assignment wins; sorted unique co-rated lists), {threads} threads",
+                               "seconds": dt,
+                               "counts_equal_gpu": bool(int(cnt[0]) == n_tr and int(cnt[1]) == n_te and
+                                                        int(cnt[2]) == n_edg)}
     return out
 
 
@@ -1039,6 +1091,22 @@ def ctypes_void(p):
     import ctypes
 
     return ctypes.c_void_p(p or 0)
+
+
+def knn2_workload_call(args, ctx, dev, torch):
+    """The knn2 leg's workload and one cf_item_cosine_run on it (the PMC child's pass)."""
+    from collaborative_filtering_amd import synth
+
+    seed = 2026101503
+    n_items, n_users = args.knn2_items, args.knn2_users
+    kd = synth.degrees(seed, n_users, k_median=89.0, sigma=0.5, kmin=20, kmax=2000)
+    off, items, rats = synth.user_items(seed, kd, n_items, threads=16)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    d_off, d_items, d_rat = T(off.view(np.int64)), T(items.view(np.int32)), T(rats)
+    d_W = torch.empty(n_items * n_items, dtype=torch.float32, device=dev)
+    ctx.item_cosine_run(n_users, n_items, d_off, d_items, d_rat, 1, d_W,
+                        stream=torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
 
 
 def knn2_leg(args, ctx, dev, torch):
@@ -1128,6 +1196,15 @@ def knn2_leg(args, ctx, dev, torch):
                     "cnt=B^T B on the upper triangle); executed counts the 128-item tile and 128-user padding",
         },
     }
+    if args.pmc == "auto" and not args.pmc_child:
+        tr = pmc_traffic(args, knn2=True)
+        if tr is not None:
+            fetch, write = tr["knn2"]
+            out["roofline"].update({
+                "traffic": 2.0 * fetch + write, "traffic_fetch_bytes_raw": fetch, "traffic_write_bytes": write,
+                "traffic_note": "HBM bytes of the one knn2_code_kernel launch of a child call, rocprofv3 --pmc "
+                                "FETCH_SIZE and WRITE_SIZE in separate passes; traffic = 2 x FETCH_SIZE + "
+                                "WRITE_SIZE (MI355X_MICROARCH.md's gfx950 correction)"})
     if not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ref as orc
@@ -1161,10 +1238,11 @@ def knn2_leg(args, ctx, dev, torch):
     return out
 
 
-def pmc_traffic(args):
+def pmc_traffic(args, knn2=False):
     """FETCH_SIZE and WRITE_SIZE (bytes) summed over the predict_kernel and eigen_kernel
     launches of one child step, each counter in its own rocprofv3 run (MI355X_MICROARCH.md:
-    FETCH_SIZE costs 3 TCC slots, WRITE_SIZE 2, so they cannot share a pass)."""
+    FETCH_SIZE costs 3 TCC slots, WRITE_SIZE 2, so they cannot share a pass).  knn2: the
+    knn2_code_kernel launch of one child knn2 call instead."""
     import csv
     import re
     import shutil
@@ -1174,9 +1252,12 @@ def pmc_traffic(args):
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None
-    out = {"predict": [0.0, 0.0], "eigen": [0.0, 0.0]}
+    out = {"predict": [0.0, 0.0], "eigen": [0.0, 0.0], "eigen12": [0.0, 0.0], "knn2": [0.0, 0.0]}
     child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", args.config,
              "--users", str(args.users)]
+    if knn2:
+        child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--knn2", "only", "--knn2-users",
+                 str(args.knn2_users), "--knn2-items", str(args.knn2_items)]
     env = dict(os.environ, TMPDIR="/tmp")
     for slot, counter in enumerate(("FETCH_SIZE", "WRITE_SIZE")):
         d = tempfile.mkdtemp(prefix="cf_pmc_", dir="/tmp")
@@ -1187,10 +1268,16 @@ def pmc_traffic(args):
             path = os.path.join(d, "run_counter_collection.csv")
             for r in csv.DictReader(open(path)):
                 name = r["Kernel_Name"]
+                if knn2:
+                    if re.search(r"knn2_(code|i8|f32)_kernel", name) and r["Counter_Name"] == counter:
+                        out["knn2"][slot] += float(r["Counter_Value"]) * 1024.0
+                    continue
                 key = "predict" if re.search(r"pred_(basis|rating)_kernel<|spill_(basis|predict)_kernel<", name) else \
                       "eigen" if re.search(r"eigen_kernel<", name) else None
                 if key and r["Counter_Name"] == counter:
                     out[key][slot] += float(r["Counter_Value"]) * 1024.0   # the counter is in KiB
+                    if re.search(r"eigen_kernel<12, ?true>", name):   # the dominant kernel alone
+                        out["eigen12"][slot] += float(r["Counter_Value"]) * 1024.0
         except (subprocess.SubprocessError, OSError, KeyError, ValueError):
             return None
         finally:

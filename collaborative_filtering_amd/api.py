@@ -116,6 +116,12 @@ class Context:
                     "jacobi_cyc_per_step": int(out[5]) / max(int(out[7]), 1)}
         return None
 
+    def eigen_bucket_timing(self, enable: bool = True, read: bool = False):
+        """cf_eigen_bucket_timing: per k-bucket device ms of the last eigen run (index = emax)."""
+        out = np.zeros(13, dtype=np.float32) if read else None
+        self._chk(self.lib.cf_eigen_bucket_timing(self.h, int(enable), ptr(out)), "cf_eigen_bucket_timing")
+        return out
+
     def debug_spill(self, enable: bool = True, read: bool = False):
         """Spill-path phase cycles (thread 0 s_memtime sums) when read."""
         out = np.zeros(8, dtype=np.uint64) if read else None

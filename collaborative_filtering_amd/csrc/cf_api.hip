@@ -103,12 +103,17 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_pred_next) (void)hipFree(ctx->d_pred_next);
     if (ctx->d_cmask) (void)hipFree(ctx->d_cmask);
+    if (ctx->d_cmask_fp) (void)hipFree(ctx->d_cmask_fp);
     if (ctx->d_knn) (void)hipFree(ctx->d_knn);
     if (ctx->d_knn_acc) (void)hipFree(ctx->d_knn_acc);
     if (ctx->d_knn_part) (void)hipFree(ctx->d_knn_part);
     if (ctx->d_prep) (void)hipFree(ctx->d_prep);
     for (hipEvent_t& e : ctx->prep_ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& run : ctx->bucket_ev)
+        for (auto& pr : run)
+            for (hipEvent_t& e : pr)
+                if (e) (void)hipEventDestroy(e);
     if (ctx->d_spill) (void)hipFree(ctx->d_spill);
     for (hipEvent_t& e : ctx->spill_side_ev)
         if (e) (void)hipEventDestroy(e);
@@ -231,6 +236,12 @@ uint64_t cf_evec_offsets(uint32_t n_users, const uint64_t* item_off, uint64_t* e
 }
 
 int cf_plan_create(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, cf_plan** out) {
+    return cf_plan_create_cap(ctx, n_users, item_off, CF_SPILL_MAX_K, out);
+}
+
+}  // extern "C"
+
+int cf_plan_create_cap(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, uint64_t kcap, cf_plan** out) {
     if (!ctx || !out || (!item_off && n_users)) return cf_set_error(ctx, CF_EINVAL, "cf_plan_create: null");
     *out = nullptr;
     CF_TRY(set_device(ctx));
@@ -241,15 +252,15 @@ int cf_plan_create(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, cf_p
     plan->n_users = n_users;
     plan->h_item_off.assign(item_off, item_off + n_users + 1);
     // Bucket by emax = ceil(k/16); within a bucket, largest k first (cost ~ k^3).
-    // by[0]: the spill path (CF_MAX_K < k <= CF_SPILL_MAX_K), launched first.
+    // by[0]: the spill path (CF_MAX_K < k <= kcap), launched first.
     std::vector<std::vector<uint32_t>> by(13);
     for (uint32_t u = 0; u < n_users; ++u) {
         const uint64_t k = item_off[u + 1] - item_off[u];
-        if (k > CF_SPILL_MAX_K) {
+        if (k > kcap) {
             delete plan;
             return cf_set_error(ctx, CF_ERANGE,
                                 "user " + std::to_string(u) + " has k=" + std::to_string(k) +
-                                    " items; the eigen path supports k <= " + std::to_string(CF_SPILL_MAX_K));
+                                    " items; the eigen path supports k <= " + std::to_string(kcap));
         }
         by[k == 0 ? 1 : (k > CF_MAX_K ? 0 : (int)((k + 15) / 16))].push_back(u);
         plan->kmax = std::max<uint32_t>(plan->kmax, (uint32_t)k);
@@ -291,6 +302,8 @@ int cf_plan_create(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, cf_p
     *out = plan;
     return CF_OK;
 }
+
+extern "C" {
 
 void cf_plan_destroy(cf_plan* plan) {
     if (!plan) return;

@@ -118,7 +118,10 @@ struct EigenArgs {
     // 3 * item_off[u] (bit i of word 3r + (i >> 6) = !(w(item_r -> item_i) > 0.1), cf_predict.hip)
     uint64_t* cmask_out;
     uint64_t cmask_words;       // its extent (users beyond it write none)
+    uint64_t* cmask_fp;         // per user: cf_items_fp of the items the masks were built from
+    uint32_t cmask_users;
     const uint8_t* solved;      // kSigma, spill pairs: w_lim already written (local_wlim_kernel)
+    int skip_spill;             // kSigma: every spill pair is solved, no spill launch
 };
 
 // Test rating of `user` for compact item `movie` (0 if absent): binary search of the
@@ -255,8 +258,13 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
         }
     }
     __syncthreads();
-    if (mode == kUser && a.cmask_out && 3 * (base + (uint64_t)k) <= a.cmask_words) {
-        // the predictor's complement masks (local_calc_precomp.cpp:254-265)
+    if (mode == kUser && a.cmask_out && 3 * (base + (uint64_t)k) <= a.cmask_words && u < a.cmask_users) {
+        // the predictor's complement masks (local_calc_precomp.cpp:254-265) and the
+        // fingerprint of the item list they belong to
+        if (wave == 0) {
+            const uint64_t fp = cf_items_fp(s_item, k, base, lane);
+            if (lane == 0) a.cmask_fp[u] = fp;
+        }
         uint64_t* cm = a.cmask_out + 3 * base;
         for (int r = wave; r < k; r += NW)
 #pragma unroll
@@ -837,6 +845,7 @@ int launch_buckets_on(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStrea
             }
         }
         int rc;
+        if (b.emax == kSpillBucket && args.skip_spill) continue;
         if (b.emax == kSpillBucket) {
             // n > 192: the fp64 HBM-workspace solver; a8 units in its local-graph / w_lim modes
             cf_spill_local loc{};
@@ -861,6 +870,9 @@ int launch_buckets_on(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStrea
             }
             continue;
         }
+        const bool timed = ctx->bucket_timing && args.mode == kUser && b.emax >= 1 && b.emax <= 12;
+        const int slot = ctx->bucket_run % cf_ctx::kBucketRuns;
+        if (timed) CF_HIP_CHECK(ctx, hipEventRecord(ctx->bucket_ev[slot][b.emax][0], stream));
         switch (b.emax) {
             case 1: rc = launch_bucket<1>(ctx, args, b.count, stream); break;
             case 2: rc = launch_bucket<2>(ctx, args, b.count, stream); break;
@@ -877,7 +889,12 @@ int launch_buckets_on(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStrea
             default: return cf_set_error(ctx, CF_ERANGE, "eigen bucket out of range (k > 192)");
         }
         if (rc != CF_OK) return rc;
+        if (timed) {
+            CF_HIP_CHECK(ctx, hipEventRecord(ctx->bucket_ev[slot][b.emax][1], stream));
+            ctx->bucket_recorded[slot][b.emax] = true;
+        }
     }
+    if (ctx->bucket_timing && args.mode == kUser) ++ctx->bucket_run;
     return CF_OK;
 }
 
@@ -896,6 +913,34 @@ int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStre
     return rc;
 }
 }  // namespace
+
+extern "C" int cf_eigen_bucket_timing(cf_ctx* ctx, int enable, float* ms13) {
+    if (!ctx) return CF_EINVAL;
+    CF_TRY(set_device(ctx));
+    if (enable && !ctx->bucket_ev[0][1][0])
+        for (auto& run : ctx->bucket_ev)
+            for (auto& pr : run)
+                for (hipEvent_t& e : pr) CF_HIP_CHECK(ctx, hipEventCreate(&e));
+    if (ms13) {   // mean over the recorded runs (the last kBucketRuns of them)
+        for (int e = 0; e < 13; ++e) {
+            double sum = 0.0;
+            int cnt = 0;
+            for (int r = 0; r < cf_ctx::kBucketRuns; ++r) {
+                if (!ctx->bucket_recorded[r][e]) continue;
+                float ms = 0.0f;
+                CF_HIP_CHECK(ctx, hipEventSynchronize(ctx->bucket_ev[r][e][1]));
+                CF_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->bucket_ev[r][e][0], ctx->bucket_ev[r][e][1]));
+                sum += ms;
+                ++cnt;
+                ctx->bucket_recorded[r][e] = false;
+            }
+            ms13[e] = cnt ? (float)(sum / cnt) : -1.0f;
+        }
+        ctx->bucket_run = 0;
+    }
+    ctx->bucket_timing = enable != 0;
+    return CF_OK;
+}
 
 int cf_launch_local_eigen(cf_ctx* ctx, const cf_plan* movie_plan, const uint64_t* d_item_off,
                           const uint32_t* d_items, const uint64_t* d_evec_off, float* d_evals,
@@ -924,10 +969,12 @@ int cf_launch_local_sigma(cf_ctx* ctx, const cf_plan* pair_plan, const uint64_t*
                           const uint32_t* d_items, const uint32_t* d_pair_movie,
                           const uint32_t* d_pair_user, const float* d_l2, const uint64_t* d_l2_off,
                           const uint64_t* d_test_off, const uint32_t* d_test_user,
-                          const float* d_test_rating, float* d_wlim, hipStream_t stream, const uint8_t* d_solved) {
+                          const float* d_test_rating, float* d_wlim, hipStream_t stream, const uint8_t* d_solved,
+                          bool skip_spill) {
     EigenArgs args{};
     args.mode = kSigma;
     args.solved = d_solved;
+    args.skip_spill = skip_spill;
     args.order = pair_plan->d_order;
     args.item_off = d_item_off;
     args.items = d_items;
@@ -991,7 +1038,9 @@ int cf_launch_eigen_flagged(cf_ctx* ctx, const cf_plan* plan, int emax, uint32_t
     args.close_sigrot = ctx->close_sigrot;
     args.only_flag = flag;
     args.cmask_out = d_cmask;
-    args.cmask_words = ctx->cmask_bytes / sizeof(uint64_t);
+    args.cmask_words = d_cmask ? ctx->cmask_bytes / sizeof(uint64_t) : 0;
+    args.cmask_fp = d_cmask ? ctx->d_cmask_fp : nullptr;
+    args.cmask_users = d_cmask ? ctx->cmask_users : 0;
     // units are sorted largest k first within a bucket, so the range's first unit has its kmax
     const uint32_t u0 = plan->h_order[first];
     const uint32_t kmax = (uint32_t)(plan->h_item_off[u0 + 1] - plan->h_item_off[u0]);
@@ -1031,7 +1080,9 @@ int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off
     args.close_sigrot = ctx->close_sigrot;
     args.stats = ctx->d_stats;
     args.cmask_out = cf_cmask_buffer(ctx, plan);   // the predictor's complement masks
-    args.cmask_words = ctx->cmask_bytes / sizeof(uint64_t);
+    args.cmask_words = args.cmask_out ? ctx->cmask_bytes / sizeof(uint64_t) : 0;
+    args.cmask_fp = args.cmask_out ? ctx->d_cmask_fp : nullptr;
+    args.cmask_users = args.cmask_out ? ctx->cmask_users : 0;
     cf_cmask_mark(ctx, plan, d_item_off, d_items, false);
     const int rc = launch_all_buckets(ctx, plan, args, stream);
     cf_cmask_mark(ctx, plan, d_item_off, d_items, rc == CF_OK && args.cmask_out);

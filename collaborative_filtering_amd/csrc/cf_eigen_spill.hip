@@ -72,24 +72,39 @@ struct SpillArgs {
     // per user.
     int mc_stage;
     int mc_parts;
+    uint64_t vs;   // BIG / HUGE: stride of the slot's k-long vectors (McLayout), >= the launch's kmax
+    int de_lds;    // HUGE: QL's d / e in the dynamic LDS tail (else in the slot's per-part pair)
 };
 
-// Staged slots: after rc / rs / tau (big_off + 3 NL) the tridiagonal d, e, the sigs, the
-// eigenvalues (QL's d), the panel's dot products xv, xw, then one QL coefficient buffer per
-// row part (each part runs its own generator).
-constexpr uint64_t MC_D = 3ull * CF_SPILL_MAX_K, MC_E = 4ull * CF_SPILL_MAX_K, MC_SIG = 5ull * CF_SPILL_MAX_K,
-                   MC_DF = 6ull * CF_SPILL_MAX_K, MC_XV = 7ull * CF_SPILL_MAX_K, MC_XW = 7ull * CF_SPILL_MAX_K + 32,
-                   MC_GBUF = 7ull * CF_SPILL_MAX_K + 64;
+// Staged slots: after rc / rs / tau (big_off + 3 vs, vs = the launch's vector stride >= its
+// largest k) the tridiagonal d, e, the sigs, the eigenvalues (QL's d), the panel's dot products
+// xv, xw, then one QL coefficient buffer per row part (each part runs its own generator).  HUGE
+// launches (k > CF_SPILL_MAX_K, whose per-row vectors no longer fit in LDS) add a private
+// (d, e) pair per QL part, for parts whose d / e do not fit in LDS either, and the rank / row
+// list `perm`.
 constexpr int MC_QL_ROWS = 2 * (SP_T - 64);        // rows of one QL part, at least: one applier pass
 constexpr int MC_BT_COLS = SP_T;                   // columns of one back-transform part, at least
-constexpr int MC_QL_PARTS_MAX = (CF_SPILL_MAX_K + MC_QL_ROWS - 1) / MC_QL_ROWS;
-constexpr uint64_t MC_GSZ = 4ull * SP_QB * (CF_SPILL_MAX_K + 2 * SP_QB + 4);   // doubles per buffer
-constexpr uint64_t MC_EXTRA = MC_GBUF + (uint64_t)MC_QL_PARTS_MAX * MC_GSZ;
-// the symv's transposed partials z_g (G <= MC_GMAX rows of CF_SPILL_MAX_K) share the QL buffers'
-// space: the tridiagonalisation is over before QL starts
-constexpr int MC_GMAX = (CF_SPILL_MAX_K + 63) / 64;
-constexpr uint64_t MC_Z = MC_GBUF;
-static_assert((uint64_t)MC_GMAX * CF_SPILL_MAX_K <= (uint64_t)MC_QL_PARTS_MAX * MC_GSZ, "symv partials fit");
+struct McLayout {
+    uint64_t vs, d, e, sig, df, xv, xw, gbuf, gsz, parts_max, pde, perm, extra_big, extra_huge;
+    __host__ __device__ explicit McLayout(uint64_t v) : vs(v) {
+        d = 3 * v;
+        e = 4 * v;
+        sig = 5 * v;
+        df = 6 * v;
+        xv = 7 * v;
+        xw = 7 * v + 32;
+        gbuf = 7 * v + 64;
+        gsz = 4ull * SP_QB * (v + 2 * SP_QB + 4);   // doubles per coefficient buffer pair
+        parts_max = (v + MC_QL_ROWS - 1) / MC_QL_ROWS;
+        pde = gbuf + parts_max * gsz;
+        perm = pde + 2 * parts_max * v;
+        extra_big = pde;
+        extra_huge = perm + v;
+    }
+};
+// the symv's transposed partials z_g (G <= ceil(vs / 64) rows of vs) share the QL buffers'
+// space (gbuf): the tridiagonalisation is over before QL starts.  ceil(v/64) v <= ceil(v/896)
+// 64 (v + 36) for every v >= 1, so they fit.
 
 // LDS of one workgroup.  NL = the largest k of the launch's layout.  Up to SP_NL (3072) the
 // per-row vectors rc / rs / tau live in LDS too; a BIG launch (SP_NL < k <= CF_SPILL_MAX_K)
@@ -115,6 +130,30 @@ struct SpillSmemT {
 };
 static_assert(sizeof(SpillSmemT<SP_NL, false>) <= 163840, "spill LDS");
 static_assert(sizeof(SpillSmemT<CF_SPILL_MAX_K, true>) <= 163840, "big spill LDS");
+
+// LDS of a HUGE launch (k > CF_SPILL_MAX_K): every k-long vector lives in the user's slot,
+// except QL's d / e, which take the dynamic tail of the workgroup's LDS when 16 k bytes fit
+// beside the header (k <= ~10,100; the generator's serial chain reads them): then they overlay
+// the staging tiles, which QL does not use.
+struct SpillSmemHugeHdr {
+    double vj[SP_NB], wj[SP_NB], xv[SP_NB], xw[SP_NB];
+    double red[SP_W + 4];
+    int seq[4 * SP_QB + 8];   // the generator's sequence ranges and flags (BIG: in perm)
+    int flag[4];
+};
+struct SpillSmemHugeWork {
+    double stage[SP_STAGE];
+    double vsb[SP_RC * (SP_NB + 1)];   // back-transform V rows (BIG: in e)
+    double part[8 * 64];
+};
+constexpr size_t kHugeHdr = (sizeof(SpillSmemHugeHdr) + 15) & ~(size_t)15;
+constexpr size_t kLdsMax = 163840;
+// dynamic LDS of a HUGE launch of largest k with d / e in LDS (de_lds) or not
+inline size_t huge_lds_bytes(uint64_t kmax, bool de_lds) {
+    return kHugeHdr + std::max<size_t>(sizeof(SpillSmemHugeWork), de_lds ? 16 * kmax : 0);
+}
+// largest k whose d / e fit in a HUGE launch's LDS
+constexpr uint64_t kHugeDeLdsMax = (kLdsMax - kHugeHdr) / 16;
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -143,23 +182,41 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
     return t;
 }
 
-template <int NL, bool BIG>
+template <int NL, bool BIG, bool HUGE = false>
 __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    SpillSmemT<NL, BIG>& S = *reinterpret_cast<SpillSmemT<NL, BIG>*>(smem_raw);
+    // LDS views: SpillSmemT, or (HUGE) the header + the staging work area / the d-e tail
+    using SmT = SpillSmemT<(HUGE ? 1 : NL), (BIG || HUGE)>;
+    SmT& S = *reinterpret_cast<SmT*>(smem_raw);
+    SpillSmemHugeHdr& H = *reinterpret_cast<SpillSmemHugeHdr*>(smem_raw);
+    SpillSmemHugeWork& HW = *reinterpret_cast<SpillSmemHugeWork*>(smem_raw + kHugeHdr);
+    double* const de_tail = reinterpret_cast<double*>(smem_raw + kHugeHdr);
+    int* const s_flag = HUGE ? H.flag : S.flag;
+    double* const s_red = HUGE ? H.red : S.red;
+    double* const s_vj = HUGE ? H.vj : S.vj;
+    double* const s_wj = HUGE ? H.wj : S.wj;
+    double* const s_xv = HUGE ? H.xv : S.xv;
+    double* const s_xw = HUGE ? H.xw : S.xw;
+    double* const s_part = HUGE ? HW.part : S.part;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const McLayout Lo(a.vs);
+    constexpr bool SLOTV = BIG || HUGE;   // rc / rs / tau in the slot
     double* M = a.mc_stage ? nullptr : a.work + (size_t)blockIdx.x * a.work_stride;
     // per-row vectors and the staging tiles (see SpillSmemT)
-    double* rc = BIG && M ? M + a.big_off : S.rc;
-    double* rs = BIG && M ? M + a.big_off + NL : S.rs;
-    double* tau = BIG && M ? M + a.big_off + 2 * NL : S.tau;
-    double* const stage = BIG ? S.stage : S.rc;
+    double* rc = SLOTV && M ? M + a.big_off : S.rc;
+    double* rs = SLOTV && M ? M + a.big_off + Lo.vs : S.rs;
+    double* tau = SLOTV && M ? M + a.big_off + 2 * Lo.vs : S.tau;
+    double* const stage = HUGE ? HW.stage : (BIG ? S.stage : S.rc);
+    // QL's d / e, the rank / row list, the sigs: LDS (SpillSmemT) or the slot (HUGE, set per unit)
+    double* Sd = S.d;
+    double* Se = S.e;
+    int* Sperm = S.perm;
     const double eps = 2.220446049250313e-16;   // 2^-52 (tql2)
 
     for (;;) {
-        if (tid == 0) S.flag[0] = (int)atomicAdd(a.counter, 1u);
+        if (tid == 0) s_flag[0] = (int)atomicAdd(a.counter, 1u);
         __syncthreads();
-        const int idx = S.flag[0];
+        const int idx = s_flag[0];
         __syncthreads();
         const int st = a.mc_stage;
         const int P = st ? a.mc_parts : 1;
@@ -167,10 +224,27 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         const int ui = idx / P, part = idx - ui * P;
         if (st) {
             M = a.work + (size_t)ui * a.work_stride;
-            if (BIG) {
+            if (SLOTV) {
                 rc = M + a.big_off;
-                rs = M + a.big_off + NL;
-                tau = M + a.big_off + 2 * NL;
+                rs = M + a.big_off + Lo.vs;
+                tau = M + a.big_off + 2 * Lo.vs;
+            }
+        }
+        if constexpr (HUGE) {
+            // the per-row vectors of this unit: QL parts take their own (d, e) copy, in the LDS
+            // tail when it fits (de_lds) or in the part's pair of the slot; the back-transform
+            // reads the eigenvalues where part 0 of QL left them; stage 0 (one workgroup per
+            // unit) uses the slot's d / e
+            double* mc = M + a.big_off;
+            Sperm = reinterpret_cast<int*>(mc + Lo.perm);
+            if (st == 2) {
+                Sd = a.de_lds ? de_tail : mc + Lo.pde + 2 * (uint64_t)part * Lo.vs;
+                Se = Sd + Lo.vs;
+            } else if (st == 4) {
+                Sd = mc + Lo.df;
+            } else {
+                Sd = mc + Lo.d;
+                Se = mc + Lo.e;
             }
         }
         const int mode = a.loc.mode;
@@ -182,7 +256,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         int n = nrows;
         if (mode == 2) {
             // w_lim pass (local_calc.cpp:402-436): the unrated rows h of the movie's L2 (row 0,
-            // the movie itself, counts as unrated, :405-413), in row order, into S.perm
+            // the movie itself, counts as unrated, :405-413), in row order, into Sperm
             const uint32_t user = a.loc.pair_user[unit];
             int h = 0;
             for (int b0 = 0; b0 < nrows; b0 += SP_T) {
@@ -205,15 +279,15 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     }
                 }
                 const unsigned long long bal = __ballot(unr);
-                if (lane == 0) S.red[wave] = (double)__popcll(bal);
+                if (lane == 0) s_red[wave] = (double)__popcll(bal);
                 __syncthreads();
                 int off = h, all = 0;
                 for (int w = 0; w < SP_W; ++w) {
-                    const int cw = (int)S.red[w];
+                    const int cw = (int)s_red[w];
                     if (w < wave) off += cw;
                     all += cw;
                 }
-                if (unr) S.perm[off + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+                if (unr) Sperm[off + __popcll(bal & ((1ull << lane) - 1ull))] = i;
                 h += all;
                 __syncthreads();
             }
@@ -225,15 +299,32 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         double* Wp = Zb + (size_t)n * n;         // [SP_NB][n] panel W of the tridiagonalisation
         unsigned long long t0 = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull, t1 = 0, t2 = 0, t3 = 0, tgen = 0;
         unsigned long long n_iter = 0, n_rot = 0;
+        // the sigs of the rows: LDS, or the slot (HUGE)
+        auto sig_set = [&](int i, float v) {
+            if constexpr (HUGE) M[a.big_off + Lo.sig + i] = (double)v;
+            else S.sig[i] = v;
+        };
+        auto sig_get = [&](int i) -> float {
+            if constexpr (HUGE) return (float)M[a.big_off + Lo.sig + i];
+            else return S.sig[i];
+        };
 
         if (st >= 2) {
             // resume: d, e from the slot (the multi-CU tridiagonalisation left them there) for
             // QL, the eigenvalues and sigs for the output
             const double* mc = M + a.big_off;
-            for (int i = tid; i < n; i += SP_T) {
-                S.d[i] = mc[(st == 4 ? MC_DF : MC_D) + i];
-                S.e[i] = mc[MC_E + i];
-                S.sig[i] = (float)mc[MC_SIG + i];
+            if constexpr (HUGE) {
+                if (st == 2)   // this part's own copy (the generator updates it)
+                    for (int i = tid; i < n; i += SP_T) {
+                        Sd[i] = mc[Lo.d + i];
+                        Se[i] = mc[Lo.e + i];
+                    }
+            } else {
+                for (int i = tid; i < n; i += SP_T) {
+                    Sd[i] = mc[(st == 4 ? Lo.df : Lo.d) + i];
+                    Se[i] = mc[Lo.e + i];
+                    S.sig[i] = (float)mc[Lo.sig + i];
+                }
             }
             __syncthreads();
         } else if (mode == 2 || mode == 3) {
@@ -247,8 +338,8 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 while (p * (p + 1) / 2 > e) --p;
                 while ((p + 1) * (p + 2) / 2 <= e) ++p;
                 const int q = e - p * (p + 1) / 2;
-                const float* rp = L2m + (size_t)(mode == 3 ? p : S.perm[p]) * nrows;
-                const float* rq = L2m + (size_t)(mode == 3 ? q : S.perm[q]) * nrows;
+                const float* rp = L2m + (size_t)(mode == 3 ? p : Sperm[p]) * nrows;
+                const float* rq = L2m + (size_t)(mode == 3 ? q : Sperm[q]) * nrows;
                 double acc = 0.0;
                 for (int j = lane; j < nrows; j += 64) acc = fma((double)rp[j], (double)rq[j], acc);
                 acc = wave_sum(acc);
@@ -297,13 +388,14 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 }
             }
             sq = wave_sum(sq);
-            if (lane == 0) S.sig[i] = sqrtf((float)sq);   // (:172-176)
+            if (lane == 0) sig_set(i, sqrtf((float)sq));   // (:172-176)
         }
         __syncthreads();
         }   // mode != 2
 
         if (a.mc_stage == 1) {   // assembly only: sig to the slot, the next user
-            for (int i = tid; i < n; i += SP_T) M[a.big_off + MC_SIG + i] = (double)S.sig[i];
+            if constexpr (!HUGE)   // (HUGE: written there already)
+                for (int i = tid; i < n; i += SP_T) M[a.big_off + Lo.sig + i] = (double)S.sig[i];
             __syncthreads();
             continue;
         }
@@ -326,14 +418,14 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 double* colj = M + (size_t)j * n;
                 if (jj > 0) {
                     if (tid < jj) {
-                        S.vj[tid] = M[(size_t)(p + tid) * n + j];
-                        S.wj[tid] = Wp[(size_t)tid * n + j];
+                        s_vj[tid] = M[(size_t)(p + tid) * n + j];
+                        s_wj[tid] = Wp[(size_t)tid * n + j];
                     }
                     __syncthreads();
                     for (int r = j + tid; r < n; r += SP_T) {
                         double acc = colj[r];
                         for (int t = 0; t < jj; ++t)
-                            acc -= M[(size_t)(p + t) * n + r] * S.wj[t] + Wp[(size_t)t * n + r] * S.vj[t];
+                            acc -= M[(size_t)(p + t) * n + r] * s_wj[t] + Wp[(size_t)t * n + r] * s_vj[t];
                         colj[r] = acc;
                     }
                     __syncthreads();
@@ -346,7 +438,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     const double x = colj[r];
                     part += x * x;
                 }
-                const double sigma = block_sum(part, S.red);   // barriers: alpha read before v is stored
+                const double sigma = block_sum(part, s_red);   // barriers: alpha read before v is stored
                 double tj = 0.0, beta = alpha, scal = 0.0;
                 if (sigma != 0.0) {
                     beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
@@ -354,8 +446,8 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     scal = 1.0 / (alpha - beta);
                 }
                 if (tid == 0) {
-                    S.d[j] = ajj;
-                    S.e[j] = beta;
+                    Sd[j] = ajj;
+                    Se[j] = beta;
                     tau[j] = tj;
                 }
                 for (int r = j + 1 + tid; r < n; r += SP_T) {
@@ -379,9 +471,9 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     s = wave_sum(s);
                     if (lane == 0) {
                         if (q & 1)
-                            S.xw[t] = s;
+                            s_xw[t] = s;
                         else
-                            S.xv[t] = s;
+                            s_xv[t] = s;
                     }
                 }
                 // y = A(r0:n, r0:n) v: a wave per (64-row block, column segment), lane per row
@@ -419,7 +511,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     if (segs == 1) {
                         if (r < n) rs[r] = ps;
                     } else {
-                        S.part[sg * (nrb * 64) + rb * 64 + lane] = ps;
+                        s_part[sg * (nrb * 64) + rb * 64 + lane] = ps;
                     }
                 }
                 __syncthreads();
@@ -430,15 +522,15 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                         y = rs[r];
                     } else {
                         y = 0.0;
-                        for (int sg = 0; sg < segs; ++sg) y += S.part[sg * (nrb * 64) + (r - r0)];
+                        for (int sg = 0; sg < segs; ++sg) y += s_part[sg * (nrb * 64) + (r - r0)];
                     }
                     for (int t = 0; t < jj; ++t)
-                        y -= M[(size_t)(p + t) * n + r] * S.xv[t] + Wp[(size_t)t * n + r] * S.xw[t];
+                        y -= M[(size_t)(p + t) * n + r] * s_xv[t] + Wp[(size_t)t * n + r] * s_xw[t];
                     y *= tj;
                     rs[r] = y;
                     yv += y * rc[r];
                 }
-                const double a2 = -0.5 * tj * block_sum(yv, S.red);
+                const double a2 = -0.5 * tj * block_sum(yv, s_red);
                 for (int r = tid; r < n; r += SP_T) Wp[(size_t)jj * n + r] = r >= r0 ? rs[r] + a2 * rc[r] : 0.0;
                 __syncthreads();
             }
@@ -508,8 +600,8 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             }
         }
         if (tid == 0 && st < 2) {
-            S.d[n - 1] = M[(size_t)(n - 1) * n + (n - 1)];
-            S.e[n - 1] = 0.0;
+            Sd[n - 1] = M[(size_t)(n - 1) * n + (n - 1)];
+            Se[n - 1] = 0.0;
         }
         if (mode == 2) {
             // w_lim = sqrt(lambda_min(L2_h L2_h^T)) (:435-436): the smallest eigenvalue of
@@ -519,9 +611,9 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             if (wave == 0) {
                 double lo = 1e300, hi = -1e300;
                 for (int i = lane; i < n; i += 64) {
-                    const double rad = (i > 0 ? fabs(S.e[i - 1]) : 0.0) + (i < n - 1 ? fabs(S.e[i]) : 0.0);
-                    lo = fmin(lo, S.d[i] - rad);
-                    hi = fmax(hi, S.d[i] + rad);
+                    const double rad = (i > 0 ? fabs(Se[i - 1]) : 0.0) + (i < n - 1 ? fabs(Se[i]) : 0.0);
+                    lo = fmin(lo, Sd[i] - rad);
+                    hi = fmax(hi, Sd[i] + rad);
                 }
                 for (int off = 32; off >= 1; off >>= 1) {
                     lo = fmin(lo, __shfl_xor(lo, off));
@@ -532,8 +624,8 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     int cnt = 0;
                     double q = 1.0;
                     for (int i = 0; i < n; ++i) {
-                        const double ei = i > 0 ? S.e[i - 1] : 0.0;
-                        q = (S.d[i] - x) - (i > 0 ? ei * ei / q : 0.0);
+                        const double ei = i > 0 ? Se[i - 1] : 0.0;
+                        q = (Sd[i] - x) - (i > 0 ? ei * ei / q : 0.0);
                         if (q == 0.0) q = -1e-300;   // x is an eigenvalue of the leading block
                         cnt += q < 0.0;
                     }
@@ -586,11 +678,12 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             constexpr int OFF = QB + 4;
             static_assert(QB == 16, "applier: 64 lanes = 4 steps x 16 stages");
             const int gld = n + 2 * QB + 4;                 // rows -OFF .. n+QB-1
-            double2* Gbuf = reinterpret_cast<double2*>(st == 2 ? M + a.big_off + MC_GBUF + (size_t)part * MC_GSZ
+            double2* Gbuf = reinterpret_cast<double2*>(st == 2 ? M + a.big_off + Lo.gbuf + (size_t)part * Lo.gsz
                                                                : Wp + (size_t)SP_NB * n);   // [2][gld][QB]
-            int* seq_l = S.perm;                            // [2][QB]  (perm is free until 4c)
-            int* seq_m = S.perm + 2 * QB;                   // [2][QB]
-            int* bflag = S.perm + 4 * QB;                   // [2] nseq, [2] generator done
+            int* const seqb = HUGE ? H.seq : Sperm;         // (BIG: perm is free until 4c)
+            int* seq_l = seqb;                              // [2][QB]
+            int* seq_m = seqb + 2 * QB;                     // [2][QB]
+            int* bflag = seqb + 4 * QB;                     // [2] nseq, [2] generator done
             for (size_t idx = tid; idx < (size_t)2 * QB * gld; idx += SP_T) Gbuf[idx] = make_double2(1.0, 0.0);
             if (tid < 2 * QB) {
                 seq_l[tid] = 0;
@@ -612,13 +705,16 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 __threadfence_block();
                 int nseq = 0;
                 while (nseq < QB && gl < n) {
+                    // HUGE with d / e in the slot: the lanes' stores of the previous iteration
+                    // land before this one reads them (LDS accesses of a wave are in order)
+                    if constexpr (HUGE) __threadfence_block();
                     if (gphase == 0) {
-                        gtst1 = fmax(gtst1, fabs(S.d[gl]) + fabs(S.e[gl]));
+                        gtst1 = fmax(gtst1, fabs(Sd[gl]) + fabs(Se[gl]));
                         // m = first index >= l with a negligible e[m] (n if none): 64 at a time
                         int mfound = n;
                         for (int m0 = gl; m0 < n; m0 += 64) {
                             const int mi = m0 + lane;
-                            const bool neg = mi < n && fabs(S.e[mi]) <= eps * gtst1;
+                            const bool neg = mi < n && fabs(Se[mi]) <= eps * gtst1;
                             const unsigned long long bal = __ballot(neg);
                             if (bal) {
                                 mfound = m0 + __builtin_ctzll(bal);
@@ -628,8 +724,8 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                         gm = mfound;
                         if (gm == gl) {
                             if (lane == 0) {
-                                S.d[gl] += gf;
-                                S.e[gl] = 0.0;
+                                Sd[gl] += gf;
+                                Se[gl] = 0.0;
                             }
                             ++gl;
                             continue;
@@ -645,17 +741,18 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     }
                     double hsh = 0.0;
                     if (lane == 0) {
-                        const double g0 = S.d[l];
-                        double p = (S.d[l + 1] - g0) / (2.0 * S.e[l]);
+                        const double g0 = Sd[l];
+                        double p = (Sd[l + 1] - g0) / (2.0 * Se[l]);
                         double r = hypot(p, 1.0);
                         if (p < 0) r = -r;
-                        S.d[l] = S.e[l] / (p + r);
-                        S.d[l + 1] = S.e[l] * (p + r);
-                        hsh = g0 - S.d[l];
+                        Sd[l] = Se[l] / (p + r);
+                        Sd[l + 1] = Se[l] * (p + r);
+                        hsh = g0 - Sd[l];
                     }
                     hsh = __shfl(hsh, 0);
-                    for (int i = l + 2 + lane; i < n; i += 64) S.d[i] -= hsh;
+                    for (int i = l + 2 + lane; i < n; i += 64) Sd[i] -= hsh;
                     gf += hsh;
+                    if constexpr (HUGE) __threadfence_block();   // lane 0's d[l + 1], the shifted d
                     // the bulge chase, in two phases per 64 positions.  (A) the serial
                     // chain alone, on wave-uniform values: p and 1/r of each rotation, with
                     // e_i^2 and d_i broadcast from a per-lane block by v_readlane and the
@@ -666,9 +763,9 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     // tools/probes/fp64_chain_probe.hip: 167 cycles per rotation against
                     // 272 for the one-phase loop (whose stores and extra VALU sat in the
                     // chain's issue stream).
-                    const double dl1 = S.d[l + 1];
-                    const double el1 = S.e[l + 1];
-                    double p = S.d[m];
+                    const double dl1 = Sd[l + 1];
+                    const double el1 = Se[l + 1];
+                    double p = Sd[m];
                     double c = 1.0;
                     // c of the last three rotations and s of the last two (QL's c, c2, c3,
                     // s, s2 at the end of the chase)
@@ -676,8 +773,8 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                     for (int ib = m - 1; ib >= l; ib -= 64) {
                         const int cnt = min(64, ib - l + 1);
                         const int pos = ib - lane;
-                        double eL = lane < cnt ? S.e[pos] : 0.0;
-                        double dL = lane < cnt ? S.d[pos] : 0.0;
+                        double eL = lane < cnt ? Se[pos] : 0.0;
+                        double dL = lane < cnt ? Sd[pos] : 0.0;
                         // a register redefinition: the loads are waited for here, once
                         asm volatile("" : "+v"(eL), "+v"(dL));
                         const double e2L = eL * eL;
@@ -713,8 +810,8 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                         const double en = sP * rT;
                         const double dn = cP * pT + sT * (cT * g + sT * dL);
                         if (lane < cnt) {
-                            S.e[pos + 1] = en;
-                            S.d[pos + 1] = dn;
+                            Se[pos + 1] = en;
+                            Sd[pos + 1] = dn;
                             G[(size_t)(pos - nseq + OFF) * QB + nseq] = make_double2(cT, sT);
                         }
                         const double b1 = __shfl(cT, cnt - 1), b2 = __shfl(cT, max(cnt - 2, 0)),
@@ -728,18 +825,18 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                         hs2 = cnt >= 2 ? q2 : os1;
                     }
                     const double sn = hs1;
-                    p = -sn * hs2 * hc3 * el1 * S.e[l] / dl1;
+                    p = -sn * hs2 * hc3 * el1 * Se[l] / dl1;
                     c = hc1;
                     const double e_l = sn * p;
                     const int conv = !(fabs(e_l) > eps * gtst1 && giter < 60);
                     if (lane == 0) {
-                        S.e[l] = e_l;
-                        S.d[l] = c * p;
+                        Se[l] = e_l;
+                        Sd[l] = c * p;
                         seq_l[buf * QB + nseq] = l;
                         seq_m[buf * QB + nseq] = m;
                         if (conv) {
-                            S.d[l] += gf;
-                            S.e[l] = 0.0;
+                            Sd[l] += gf;
+                            Se[l] = 0.0;
                         }
                     }
                     ++nseq;
@@ -843,7 +940,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         const unsigned long long t4 = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
         if (st == 2) {   // the eigenvalues (every part computed the same d) to the slot
             if (part == 0) {
-                for (int i = tid; i < n; i += SP_T) M[a.big_off + MC_DF + i] = S.d[i];
+                for (int i = tid; i < n; i += SP_T) M[a.big_off + Lo.df + i] = Sd[i];
                 if (a.phase && tid == 0) {
                     atomicAdd(&a.phase[4], t4 - t3);
                     atomicAdd(&a.phase[5], tgen);
@@ -888,7 +985,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         {
             double* Tm = stage;              // [SP_NB][SP_NB]
             double* Gm = stage + SP_NB * SP_NB;
-            double* Vs = S.e;               // [SP_RC][SP_NB + 1]
+            double* Vs = HUGE ? HW.vsb : Se;   // [SP_RC][SP_NB + 1]
             constexpr int VLD = SP_NB + 1;
             for (int p = ((n - 2) / SP_NB) * SP_NB; p >= 0; p -= SP_NB) {
                 const int jb = min(SP_NB, n - 1 - p);
@@ -988,13 +1085,13 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         // with each column's rank kept in the slot's rc)
         int* rank_of = st == 4 ? reinterpret_cast<int*>(rc) : nullptr;
         for (int j = tid; j < n; j += SP_T) {
-            const double lj = S.d[j];
+            const double lj = Sd[j];
             int rank = 0;
             for (int i = 0; i < n; ++i) {
-                const double li = S.d[i];
+                const double li = Sd[i];
                 rank += (li < lj) || (li == lj && i < j);
             }
-            S.perm[rank] = j;
+            Sperm[rank] = j;
             if (rank_of) rank_of[j] = rank;
         }
         for (int cb = col_lo + wave * 64; cb < col_hi; cb += SP_W * 64) {
@@ -1012,24 +1109,25 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         }
         __syncthreads();
         if (tid == 0) {
-            float smm = 0.0f;
-            for (int i = 0; i < n; ++i)
-                if (smm < S.sig[i]) smm = S.sig[i];
-            smm = (float)((double)smm + 0.01);   // (:179-182)
-            int lim;
-            for (lim = 0; lim < n; ++lim)
-                if (S.d[S.perm[lim]] > (double)smm) break;   // (:186-188)
-            if (lim < 2) lim = 2;                             // (:190-191)
-            if (mode == 1 || mode == 3) lim = n;   // local_calc keeps every eigenpair (es(ll2), local_calc.cpp:378)
-            S.flag[3] = lim;
+            int lim = n;   // local_calc keeps every eigenpair (es(ll2), local_calc.cpp:378): modes 1, 3
+            if (mode == 0) {
+                float smm = 0.0f;
+                for (int i = 0; i < n; ++i)
+                    if (smm < sig_get(i)) smm = sig_get(i);
+                smm = (float)((double)smm + 0.01);   // (:179-182)
+                for (lim = 0; lim < n; ++lim)
+                    if (Sd[Sperm[lim]] > (double)smm) break;   // (:186-188)
+                if (lim < 2) lim = 2;                             // (:190-191)
+            }
+            s_flag[3] = lim;
             a.m_out[u] = lim;
         }
         __syncthreads();
-        const int mm = S.flag[3];
+        const int mm = s_flag[3];
         if (part == 0) {
             if (mode == 0)
-                for (int i = tid; i < n; i += SP_T) a.sigs[base + i] = (float)((double)S.sig[i] + 0.01);
-            for (int r = tid; r < mm; r += SP_T) a.evals[base + r] = (float)S.d[S.perm[r]];
+                for (int i = tid; i < n; i += SP_T) a.sigs[base + i] = (float)((double)sig_get(i) + 0.01);
+            for (int r = tid; r < mm; r += SP_T) a.evals[base + r] = (float)Sd[Sperm[r]];
         }
         if (st == 4) {
             const int w = col_hi - col_lo;
@@ -1047,7 +1145,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         }
         for (size_t idx = tid; idx < (size_t)n * mm; idx += SP_T) {
             const int i = (int)(idx / mm), r = (int)(idx - (size_t)i * mm);
-            const int j = S.perm[r];
+            const int j = Sperm[r];
             Wt[idx] = (float)(Zb[(size_t)i * n + j] * rs[j]);
         }
         __syncthreads();
@@ -1083,8 +1181,15 @@ struct McArgs {
     const uint64_t* item_off;
     double* work;
     uint64_t stride;     // doubles per user slot
-    uint64_t big_off;    // rc (v), rs (y), tau, then MC_* (d, e, sig, xv, xw)
+    uint64_t big_off;    // rc (v), rs (y), tau, then McLayout's d, e, sig, xv, xw, ...
     int G;               // workgroups per user of spill_mc_symv / spill_mc_trail
+    uint64_t vs;         // McLayout vector stride
+    // the multi-workgroup assembly (spill_mc_deg / spill_mc_l2 / spill_mc_gram)
+    const uint32_t* items;
+    GraphDev graph;
+    int mode;            // cf_spill_local::mode (0: compute_eigens)
+    float* l2;           // mode 1 writes the movie's L2, mode 3 reads it
+    const uint64_t* l2_off;
 };
 
 __device__ __forceinline__ int mc_n(const McArgs& a, uint32_t u) {
@@ -1102,8 +1207,9 @@ __global__ __launch_bounds__(SP_T) void spill_mc_col(McArgs a, int j, int p) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, jj = j - p;
     double* M = a.work + (size_t)u * a.stride;
     double* Wp = M + 2 * (size_t)n * n;
+    const McLayout Lo(a.vs);
     double* rc = M + a.big_off;
-    double* tau = rc + 2 * CF_SPILL_MAX_K;
+    double* tau = rc + 2 * Lo.vs;
     double* mc = M + a.big_off;
     double* colj = M + (size_t)j * n;
     if (jj > 0) {
@@ -1134,8 +1240,8 @@ __global__ __launch_bounds__(SP_T) void spill_mc_col(McArgs a, int j, int p) {
         scal = 1.0 / (alpha - beta);
     }
     if (tid == 0) {
-        mc[MC_D + j] = ajj;
-        mc[MC_E + j] = beta;
+        mc[Lo.d + j] = ajj;
+        mc[Lo.e + j] = beta;
         tau[j] = tj;
     }
     for (int r = j + 1 + tid; r < n; r += SP_T) {
@@ -1153,7 +1259,7 @@ __global__ __launch_bounds__(SP_T) void spill_mc_col(McArgs a, int j, int p) {
         double sdot = 0.0;
         for (int r = r0 + lane; r < n; r += 64) sdot += src[r] * rc[r];
         sdot = wave_sum(sdot);
-        if (lane == 0) mc[((q & 1) ? MC_XW : MC_XV) + t] = sdot;
+        if (lane == 0) mc[((q & 1) ? Lo.xw : Lo.xv) + t] = sdot;
     }
 }
 
@@ -1169,8 +1275,10 @@ __global__ __launch_bounds__(SP_T) void spill_mc_col(McArgs a, int j, int p) {
 // by one lane in ascending R: deterministic.  spill_mc_fin forms y = y_R + sum_g z_g in order.
 constexpr int MC_SYMV_T = 256;
 constexpr int MC_TQ = 16 * 65;   // a wave's slab transposition scratch: 16 columns x 64 rows (+1 pad)
+// HUGE (k > CF_SPILL_MAX_K): v is read from the slot (L2-resident) instead of an LDS copy.
+template <bool HUGE>
 __global__ __launch_bounds__(MC_SYMV_T) void spill_mc_symv(McArgs a, int j) {
-    __shared__ double vs[CF_SPILL_MAX_K];
+    __shared__ double vs_lds[HUGE ? 1 : CF_SPILL_MAX_K];
     __shared__ double part[MC_SYMV_T / 64][64];
     __shared__ double tq[MC_SYMV_T / 64][MC_TQ];
     const uint32_t u = blockIdx.x / a.G;
@@ -1178,18 +1286,21 @@ __global__ __launch_bounds__(MC_SYMV_T) void spill_mc_symv(McArgs a, int j) {
     const int n = mc_n(a, u);
     if (j >= n - 1) return;
     double* M = a.work + (size_t)u * a.stride;
+    const McLayout Lo(a.vs);
     const double* rc = M + a.big_off;
-    double* rs = M + a.big_off + CF_SPILL_MAX_K;
-    const double tj = rc[2 * CF_SPILL_MAX_K + j];
+    double* rs = M + a.big_off + Lo.vs;
+    const double tj = rc[2 * Lo.vs + j];
     if (tj == 0.0) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const double* vs = HUGE ? rc : vs_lds;
     constexpr int NWV = MC_SYMV_T / 64;
     const int r0 = j + 1;
     const int nrb = (n - r0 + 63) >> 6;
     const int npair = (nrb + 1) >> 1;
     if (g >= npair) return;   // uniform; spill_mc_fin sums z over g < min(G, npair)
-    double* z = M + a.big_off + MC_Z + (size_t)g * CF_SPILL_MAX_K;
-    for (int c = r0 + tid; c < n; c += MC_SYMV_T) vs[c] = rc[c];
+    double* z = M + a.big_off + Lo.gbuf + (size_t)g * Lo.vs;
+    if (!HUGE)
+        for (int c = r0 + tid; c < n; c += MC_SYMV_T) vs_lds[c] = rc[c];
     // z_g = 0 on this wave's column blocks, by the lanes that update them below
     for (int C = wave; C < nrb; C += NWV)
         for (int s16 = 0; s16 < 64; s16 += 16) {
@@ -1254,27 +1365,28 @@ __global__ __launch_bounds__(SP_T) void spill_mc_fin(McArgs a, int j, int p) {
     const int tid = threadIdx.x, jj = j - p;
     double* M = a.work + (size_t)u * a.stride;
     double* Wp = M + 2 * (size_t)n * n;
+    const McLayout Lo(a.vs);
     const double* rc = M + a.big_off;
-    double* rs = M + a.big_off + CF_SPILL_MAX_K;
+    double* rs = M + a.big_off + Lo.vs;
     const double* mc = M + a.big_off;
-    const double tj = rc[2 * CF_SPILL_MAX_K + j];
+    const double tj = rc[2 * Lo.vs + j];
     const int r0 = j + 1;
     if (tj == 0.0) {
         for (int r = tid; r < n; r += SP_T) Wp[(size_t)jj * n + r] = 0.0;
         return;
     }
     if (tid < jj) {
-        xv[tid] = mc[MC_XV + tid];
-        xw[tid] = mc[MC_XW + tid];
+        xv[tid] = mc[Lo.xv + tid];
+        xw[tid] = mc[Lo.xw + tid];
     }
     __syncthreads();
     // y = the row-block partials + the transposed partials z_g of spill_mc_symv, in order
     const int gz = min(a.G, (((n - r0 + 63) >> 6) + 1) >> 1);
-    const double* z = mc + MC_Z;
+    const double* z = mc + Lo.gbuf;
     double yv = 0.0;
     for (int r = r0 + tid; r < n; r += SP_T) {
         double y = rs[r];
-        for (int g = 0; g < gz; ++g) y += z[(size_t)g * CF_SPILL_MAX_K + r];
+        for (int g = 0; g < gz; ++g) y += z[(size_t)g * Lo.vs + r];
         for (int t = 0; t < jj; ++t) y -= M[(size_t)(p + t) * n + r] * xv[t] + Wp[(size_t)t * n + r] * xw[t];
         y *= tj;
         rs[r] = y;
@@ -1366,8 +1478,171 @@ __global__ void spill_mc_end(McArgs a) {
     const int n = mc_n(a, u);
     double* M = a.work + (size_t)u * a.stride;
     double* mc = M + a.big_off;
-    mc[MC_D + n - 1] = M[(size_t)(n - 1) * n + (n - 1)];
-    mc[MC_E + n - 1] = 0.0;
+    const McLayout Lo(a.vs);
+    mc[Lo.d + n - 1] = M[(size_t)(n - 1) * n + (n - 1)];
+    mc[Lo.e + n - 1] = 0.0;
+}
+
+// ---- multi-workgroup assembly of the staged users (stage 1 of eigen_spill_kernel, spread) -----
+// One wave per row over every CU instead of one workgroup per user: at k = 10,000 the
+// assembly moves ~1.6 GB per unit, which one CU takes tens of seconds to stream.  Same
+// arithmetic and summation order per row as the single-workgroup stage 1 (lane-strided partial
+// sums, the xor butterfly), so the results are bit-identical.  grid = (blocks per unit, units).
+__device__ __forceinline__ float mc_weight(const McArgs& a, uint64_t base, int i, int j, const GraphRow& grow,
+                                           const GraphRow& grow0) {
+    float w = grow[a.items[base + j]];
+    if (a.mode == 1) {   // the star-shaped local graph (local_calc.cpp:326-334), w > 0.1
+        if (j == 0) w = (i == 0) ? 0.0f : grow0[a.items[base + i]];
+        if (!((double)w > 0.1)) w = 0.0f;
+    }
+    return w;
+}
+
+// d_i (fp64, with the 0 -> 1 rule for users only, precompute_local_threads.cpp:137-140 vs
+// local_calc.cpp:354-360) into rs, s_i = sqrt(1/d_i) (:149-153) into rc
+__global__ __launch_bounds__(256) void spill_mc_deg(McArgs a) {
+    const uint32_t ui = blockIdx.y;
+    const uint32_t unit = a.order[a.first + ui];
+    const uint64_t base = a.item_off[unit];
+    const int n = (int)(a.item_off[unit + 1] - base);
+    double* M = a.work + (size_t)ui * a.stride;
+    double* rc = M + a.big_off;
+    double* rs = rc + McLayout(a.vs).vs;
+    const int lane = threadIdx.x & 63;
+    const GraphRow grow0 = a.graph.row(a.items[base]);
+    for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4) {
+        const GraphRow grow = a.graph.row(a.items[base + i]);
+        double ds = 0.0;
+        for (int j = lane; j < n; j += 64) ds += (double)mc_weight(a, base, i, j, grow, grow0);
+        ds = wave_sum(ds);
+        if (lane == 0) {
+            const double d = (ds == 0.0 && a.mode == 0) ? 1.0 : ds;
+            rs[i] = d;
+            rc[i] = sqrt(1.0 / d);
+        }
+    }
+}
+
+// L2(i, j) = (s_i L(i, j)) s_j (:155) in fp64, A = sym_lower(L2) full symmetric column-major in
+// the slot, sig_i = |L2(i, :)| (:169-177) to the slot, and (mode 1) the unsymmetrised fp32 L2
+// for the w_lim pass
+__global__ __launch_bounds__(256) void spill_mc_l2(McArgs a) {
+    const uint32_t ui = blockIdx.y;
+    const uint32_t unit = a.order[a.first + ui];
+    const uint64_t base = a.item_off[unit];
+    const int n = (int)(a.item_off[unit + 1] - base);
+    double* M = a.work + (size_t)ui * a.stride;
+    const McLayout Lo(a.vs);
+    const double* rc = M + a.big_off;
+    const double* rs = rc + Lo.vs;
+    double* sig = M + a.big_off + Lo.sig;
+    float* L2out = a.mode == 1 ? a.l2 + a.l2_off[unit] : nullptr;
+    const int lane = threadIdx.x & 63;
+    const GraphRow grow0 = a.graph.row(a.items[base]);
+    for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4) {
+        const GraphRow grow = a.graph.row(a.items[base + i]);
+        const double si = rc[i], di = rs[i];
+        double sq = 0.0;
+        for (int j = lane; j < n; j += 64) {
+            const double l = (j == i ? di : 0.0) - (double)mc_weight(a, base, i, j, grow, grow0);
+            const double l2 = (si * l) * rc[j];
+            sq += l2 * l2;
+            if (L2out) L2out[(size_t)i * n + j] = (float)l2;
+            if (j <= i) {
+                M[(size_t)j * n + i] = l2;
+                M[(size_t)i * n + j] = l2;
+            }
+        }
+        sq = wave_sum(sq);
+        if (lane == 0) sig[i] = (double)sqrtf((float)sq);
+    }
+}
+
+// mode 3: B = L2 L2^T of the movie (the w_lim bisection's matrix, local_calc.cpp:425-435 with
+// every row), exact fp32 x fp32 products summed in fp64 on v_mfma_f64_16x16x4_f64: one 64 x 64
+// tile of the lower triangle per workgroup (4 waves of 32 x 32, 2 x 2 MFMA tiles each), the
+// depth staged 16 columns at a time through LDS, the next chunk's loads in flight; the tile and
+// its mirror go to the slot's column-major A.  grid = (lower tiles of the wave's kmax, units).
+constexpr int MC_GRAM_LD = 68;
+__global__ __launch_bounds__(256) void spill_mc_gram(McArgs a) {
+    using f64x4 = __attribute__((ext_vector_type(4))) double;
+    __shared__ double As[16 * MC_GRAM_LD], Bs[16 * MC_GRAM_LD];
+    const uint32_t ui = blockIdx.y;
+    const uint32_t unit = a.order[a.first + ui];
+    const int n = (int)(a.item_off[unit + 1] - a.item_off[unit]);
+    const int nt = (n + 63) >> 6;
+    // lower-triangle tile t -> (ti, tj), tj <= ti
+    const int t = blockIdx.x;
+    int ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while (ti * (ti + 1) / 2 > t) --ti;
+    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+    const int tj = t - ti * (ti + 1) / 2;
+    if (ti >= nt) return;   // uniform: a smaller unit of the wave
+    const float* L2m = a.l2 + a.l2_off[unit];
+    double* M = a.work + (size_t)ui * a.stride;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int i0 = ti * 64, j0 = tj * 64;
+    // staging: thread e loads rows (e >> 2) of both operands, depth 4 (e & 3) .. + 3
+    const int sr = tid >> 2, sd = (tid & 3) * 4;
+    const bool ra_ok = i0 + sr < n, rb_ok = j0 + sr < n;
+    const float* pa = L2m + (size_t)(ra_ok ? i0 + sr : 0) * n;
+    const float* pb = L2m + (size_t)(rb_ok ? j0 + sr : 0) * n;
+    float fa[4], fb[4];
+    auto fetch = [&](int l0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int l = l0 + sd + q;
+            fa[q] = (ra_ok && l < n) ? pa[l] : 0.0f;
+            fb[q] = (rb_ok && l < n) ? pb[l] : 0.0f;
+        }
+    };
+    f64x4 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
+    const bool diag = ti == tj;
+    fetch(0);
+    for (int l0 = 0; l0 < n; l0 += 16) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            As[(sd + q) * MC_GRAM_LD + sr] = (double)fa[q];
+            Bs[(sd + q) * MC_GRAM_LD + sr] = (double)fb[q];
+        }
+        __syncthreads();
+        if (l0 + 16 < n) fetch(l0 + 16);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int row = (4 * ks + (lane >> 4)) * MC_GRAM_LD + (lane & 15);
+            double av[2], bv[2];
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                av[x] = As[row + 32 * wr + 16 * x];
+                bv[x] = Bs[row + 32 * wc + 16 * x];
+            }
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+                    if (!diag || 32 * wc + 16 * y <= 32 * wr + 16 * x)   // uniform: tiles above the diagonal skip
+                        acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int gi = i0 + 32 * wr + 16 * x + (lane >> 4) + 4 * q;
+                const int gj = j0 + 32 * wc + 16 * y + (lane & 15);
+                if (gi < n && gj < n && gj <= gi) {
+                    M[(size_t)gj * n + gi] = acc[x][y][q];
+                    M[(size_t)gi * n + gj] = acc[x][y][q];
+                }
+            }
 }
 
 }  // namespace
@@ -1377,21 +1652,28 @@ __global__ void spill_mc_end(McArgs a) {
 // the spill_mc_* launches, then eigen_spill_kernel again for QL (stage 2, MC_QL_ROWS-row parts,
 // each with its own copy of the serial generator), Z to row-major (stage 3) and the
 // back-transform + output (stage 4, MC_BT_COLS-column parts).
+// d / e of a HUGE launch's QL parts in LDS when they fit (CF_SPILL_HUGE_DE=global forces the
+// slot copies, for tests of that path at sizes that would fit)
+static bool huge_de_lds(uint64_t vs) {
+    static const bool force_global = [] {
+        const char* e = getenv("CF_SPILL_HUGE_DE");
+        return e && std::string(e) == "global";
+    }();
+    return !force_global && vs <= kHugeDeLdsMax;
+}
+
+template <bool HUGE>
 static int spill_mc_launch(cf_ctx* ctx, const cf_plan* plan, SpillArgs a, uint32_t first, uint32_t count,
                            uint32_t slots, uint32_t n_cu, hipStream_t st) {
-    const size_t lds = sizeof(SpillSmemT<CF_SPILL_MAX_K, true>);
-    CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_spill_kernel<CF_SPILL_MAX_K, true>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    constexpr int NL = HUGE ? 1 : CF_SPILL_MAX_K;
+    const auto kern = eigen_spill_kernel<NL, true, HUGE>;
+    a.de_lds = HUGE && huge_de_lds(a.vs);
+    const size_t lds = HUGE ? huge_lds_bytes(a.vs, a.de_lds) : sizeof(SpillSmemT<CF_SPILL_MAX_K, true>);
+    CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     for (uint32_t w0 = 0; w0 < count; w0 += slots) {
         const uint32_t cnt = std::min(slots, count - w0);
         a.first = first + w0;
         a.count = cnt;
-        const uint32_t grid = std::min(cnt, n_cu);
-        a.mc_stage = 1;
-        a.mc_parts = 1;
-        CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
-        hipLaunchKernelGGL((eigen_spill_kernel<CF_SPILL_MAX_K, true>), dim3(grid), dim3(SP_T), lds, st, a);
-        CF_HIP_CHECK(ctx, hipGetLastError());
         McArgs m{};
         m.order = a.order;
         m.first = a.first;
@@ -1400,9 +1682,25 @@ static int spill_mc_launch(cf_ctx* ctx, const cf_plan* plan, SpillArgs a, uint32
         m.work = a.work;
         m.stride = a.work_stride;
         m.big_off = a.big_off;
+        m.vs = a.vs;
+        m.items = a.items;
+        m.graph = a.graph;
+        m.mode = a.loc.mode;
+        m.l2 = a.loc.l2;
+        m.l2_off = a.loc.l2_off;
         // the largest k of this wave (plan order: the wave's first user)
         const uint32_t unit0 = plan->h_order[a.first];
         const uint32_t kmax = (uint32_t)(plan->h_item_off[unit0 + 1] - plan->h_item_off[unit0]);
+        // assembly over every CU: B = L2 L2^T on the matrix cores (mode 3), else degrees then L2
+        if (m.mode == 3) {
+            const uint32_t nt = (kmax + 63) / 64;
+            hipLaunchKernelGGL(spill_mc_gram, dim3(nt * (nt + 1) / 2, cnt), dim3(256), 0, st, m);
+        } else {
+            const uint32_t rb = std::max<uint32_t>(1, std::min<uint32_t>((kmax + 3) / 4, (8 * n_cu + cnt - 1) / cnt));
+            hipLaunchKernelGGL(spill_mc_deg, dim3(rb, cnt), dim3(256), 0, st, m);
+            hipLaunchKernelGGL(spill_mc_l2, dim3(rb, cnt), dim3(256), 0, st, m);
+        }
+        CF_HIP_CHECK(ctx, hipGetLastError());
         // ~4 workgroups per CU over the batch for the memory-bound products, at least 64 rows each
         m.G = (int)std::max<uint32_t>(1, std::min<uint32_t>((4 * n_cu + cnt - 1) / cnt, (kmax + 63) / 64));
         for (int p = 0; p < (int)kmax - 1; p += SP_NB) {
@@ -1410,7 +1708,7 @@ static int spill_mc_launch(cf_ctx* ctx, const cf_plan* plan, SpillArgs a, uint32
             for (int jj = 0; jj < jbmax; ++jj) {
                 const int j = p + jj;
                 hipLaunchKernelGGL(spill_mc_col, dim3(cnt), dim3(SP_T), 0, st, m, j, p);
-                hipLaunchKernelGGL(spill_mc_symv, dim3(cnt * m.G), dim3(MC_SYMV_T), 0, st, m, j);
+                hipLaunchKernelGGL(spill_mc_symv<HUGE>, dim3(cnt * m.G), dim3(MC_SYMV_T), 0, st, m, j);
                 hipLaunchKernelGGL(spill_mc_fin, dim3(cnt), dim3(SP_T), 0, st, m, j, p);
             }
             hipLaunchKernelGGL(spill_mc_trail, dim3(cnt * m.G), dim3(SP_T), 0, st, m, p);
@@ -1430,29 +1728,34 @@ static int spill_mc_launch(cf_ctx* ctx, const cf_plan* plan, SpillArgs a, uint32
             a.mc_parts = parts[s];
             const uint32_t g = std::min<uint32_t>(cnt * (uint32_t)parts[s], n_cu);
             CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
-            hipLaunchKernelGGL((eigen_spill_kernel<CF_SPILL_MAX_K, true>), dim3(g), dim3(SP_T), lds, st, a);
+            hipLaunchKernelGGL(kern, dim3(g), dim3(SP_T), lds, st, a);
             CF_HIP_CHECK(ctx, hipGetLastError());
         }
     }
     return CF_OK;
 }
 
-// The spill bucket (users sorted by k, largest first) in two k ranges, each launch with slots
-// sized for its own largest k, so a few k = 5000 users (400 MB slots) no longer cap the number
-// of workgroups for the many smaller ones: (3072, 5000] in the BIG layout on ctx->spill_side,
-// beside (192, 3072] on `stream`.  The workspace is split between the two.
+// The spill bucket (users sorted by k, largest first) in k ranges, each launch with slots sized
+// for its own largest k, so a few k = 5000 users (400 MB slots) no longer cap the number of
+// workgroups for the many smaller ones: k > CF_SPILL_MAX_K (HUGE: local_calc's units only; every
+// k-long vector in the slot) and (3072, 5000] (BIG layout; for whole units from mc_min = 1536
+// on) one after the other on ctx->spill_side, beside (192, 3072] on `stream`.  The two side
+// ranges share one workspace region (same stream, in order); the rest has its own.
 int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, const uint64_t* d_item_off,
                           const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs,
                           float* d_evals, float* d_evecs, hipStream_t stream, const cf_spill_local* loc,
                           bool defer_join) {
     if (b.count == 0) return CF_OK;
-    if (b.kmax > (uint32_t)CF_SPILL_MAX_K) return cf_set_error(ctx, CF_ERANGE, "spill eigen: k above CF_SPILL_MAX_K");
+    // compute_eigens users stop at CF_SPILL_MAX_K (cf_plan_create); local_calc's units do not
+    if (b.kmax > (uint32_t)CF_SPILL_MAX_K && !loc)
+        return cf_set_error(ctx, CF_ERANGE, "spill eigen: k above CF_SPILL_MAX_K");
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
     // k ranges over the bucket's plan positions (k non-increasing)
+    enum Kind { kRest = 0, kBig = 1, kHuge = 2 };
     struct Range {
         uint32_t first, count, kmax;
-        bool big;
+        int kind;
     };
     std::vector<Range> rs;
     {
@@ -1470,22 +1773,35 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
         // every whole-unit mode (a user; local_calc's movie graph and its B = L2 L2^T) may take the
         // staged multi-CU path; the per-pair w_lim mode (its n is the pair's unrated rows) may not
         const bool unit_mode = !loc || loc->mode != 2;
-        const uint32_t cuts[2] = {unit_mode ? mc_min : (uint32_t)SP_NL, 0u};
+        // HUGE from CF_SPILL_MAX_K on (CF_SPILL_HUGE_MIN lowers the cut, for tests that run the
+        // HUGE layout against the BIG one on the same units: the arithmetic is the same)
+        static const uint32_t huge_min = [] {
+            const char* e = getenv("CF_SPILL_HUGE_MIN");
+            const long v = e ? atol(e) : (long)CF_SPILL_MAX_K;
+            return (uint32_t)std::max<long>(CF_MAX_K, std::min<long>(v, CF_SPILL_MAX_K));
+        }();
+        const uint32_t cuts[3] = {huge_min, unit_mode ? std::min(mc_min, huge_min) : std::min<uint32_t>(SP_NL, huge_min), 0u};
+        const int kinds[3] = {kHuge, kBig, kRest};
         uint32_t j = b.first;
         const uint32_t end = b.first + b.count;
         auto kof = [&](uint32_t pos) {
             const uint32_t u = plan->h_order[pos];
             return (uint32_t)(plan->h_item_off[u + 1] - plan->h_item_off[u]);
         };
-        for (int c = 0; c < 2 && j < end; ++c) {
+        for (int c = 0; c < 3 && j < end; ++c) {
             const uint32_t j0 = j;
             while (j < end && kof(j) > cuts[c]) ++j;
-            if (j > j0) rs.push_back({j0, j - j0, kof(j0), c == 0});
+            if (j > j0) rs.push_back({j0, j - j0, kof(j0), kinds[c]});
         }
-        if (j < end) rs.push_back({j, end - j, kof(j), false});   // (degenerate: k <= 0)
+        if (j < end) rs.push_back({j, end - j, kof(j), kRest});   // (degenerate: k <= 0)
     }
     auto base_stride = [](uint64_t kmax) {
         return 2ull * kmax * kmax + (uint64_t)SP_NB * kmax + 4ull * SP_QB * (kmax + 2 * SP_QB + 4) + 64;
+    };
+    // the k-long vector stride of a range's slots (McLayout): BIG keeps CF_SPILL_MAX_K, HUGE its
+    // own kmax rounded to 64
+    auto vs_of = [](const Range& r) -> uint64_t {
+        return r.kind == kHuge ? ((uint64_t)r.kmax + 63) / 64 * 64 : (uint64_t)CF_SPILL_MAX_K;
     };
     // BIG users of compute_eigens take the staged multi-CU path (CF_SPILL_MC=0: the
     // single-workgroup kernel); their slots carry d, e, sig and the panel dot products too
@@ -1495,31 +1811,35 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     }();
     const bool mc_on = mc_env && (!loc || loc->mode != 2);
     auto stride_of = [&](const Range& r) {
-        return base_stride(r.kmax) + (r.big ? (mc_on ? MC_EXTRA : 3ull * CF_SPILL_MAX_K) : 0ull);
+        const McLayout lo(vs_of(r));
+        const uint64_t extra = r.kind == kHuge ? lo.extra_huge : r.kind == kBig ? (mc_on ? lo.extra_big : 3ull * lo.vs) : 0ull;
+        return base_stride(r.kmax) + extra;
     };
     // workspace cap: a fifth of this context's share of the free HBM (>= 24 GB, but at most half
-    // the share: cf_hbm_budget); the BIG range gets up to half of it.  A failed allocation
+    // the share: cf_hbm_budget); the side ranges get up to half of it.  A failed allocation
     // halves the cap (fewer slots: the users run in more waves) down to one slot per range.
     uint64_t budget = cf_hbm_budget(ctx, ctx->spill_bytes, 0.2, 24ull << 30);
-    const bool has_big = !rs.empty() && rs.front().big;
-    const bool has_rest = rs.size() > (has_big ? 1u : 0u);
+    const bool has_side = !rs.empty() && rs.front().kind != kRest;
+    const bool has_rest = !rs.empty() && rs.back().kind == kRest;
     std::vector<uint32_t> grid(rs.size());
-    uint64_t big_bytes = 0, rest_bytes = 0;
+    uint64_t side_bytes = 0, rest_bytes = 0;
     for (;;) {
-        big_bytes = rest_bytes = 0;
+        side_bytes = rest_bytes = 0;
         bool minimal = true;
         for (size_t i = 0; i < rs.size(); ++i) {
             const uint64_t slot = stride_of(rs[i]) * sizeof(double);
-            const uint64_t share = rs[i].big ? (has_rest ? budget / 2 : budget) : (has_big ? budget / 2 : budget);
-            // staged BIG users hold one slot each for the whole launch (in waves if the share is short)
-            uint32_t g = std::min<uint32_t>(rs[i].count, rs[i].big && mc_on ? rs[i].count : (uint32_t)n_cu);
+            const bool side = rs[i].kind != kRest;
+            const uint64_t share = side ? (has_rest ? budget / 2 : budget) : (has_side ? budget / 2 : budget);
+            // staged users hold one slot each for the whole launch (in waves if the share is short)
+            const bool staged = side && mc_on;
+            uint32_t g = std::min<uint32_t>(rs[i].count, staged ? rs[i].count : (uint32_t)n_cu);
             g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, share / slot));
             grid[i] = g;
             minimal = minimal && g == 1;
-            if (rs[i].big) big_bytes = (uint64_t)g * slot;
+            if (side) side_bytes = std::max<uint64_t>(side_bytes, (uint64_t)g * slot);
             else rest_bytes = std::max<uint64_t>(rest_bytes, (uint64_t)g * slot);
         }
-        const size_t need = 256 + big_bytes + rest_bytes;
+        const size_t need = 256 + side_bytes + rest_bytes;
         if (need <= ctx->spill_bytes) break;
         // the previous launches on either stream may still read the old workspace
         CF_HIP_CHECK(ctx, hipStreamSynchronize(stream));
@@ -1537,7 +1857,7 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
         if (minimal) return cf_set_error(ctx, CF_ENOMEM, "spill workspace (" + std::to_string(need) + " bytes)");
         budget /= 2;
     }
-    if (has_big && !ctx->spill_side) {
+    if (has_side && !ctx->spill_side) {
         CF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->spill_side, hipStreamNonBlocking));
         for (hipEvent_t& e : ctx->spill_side_ev) CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
@@ -1556,22 +1876,34 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     if (loc) a.loc = *loc;
     a.mc_parts = 1;
     a.phase = ctx->spill_debug ? reinterpret_cast<unsigned long long*>(ws + 64) : nullptr;
+    bool side_started = false;
     for (size_t i = 0; i < rs.size(); ++i) {
         const Range& r = rs[i];
-        hipStream_t st = r.big ? ctx->spill_side : stream;
-        if (r.big) {   // the side stream starts where `stream` is
+        const bool side = r.kind != kRest;
+        hipStream_t st = side ? ctx->spill_side : stream;
+        if (side && !side_started) {   // the side stream starts where `stream` is
             CF_HIP_CHECK(ctx, hipEventRecord(ctx->spill_side_ev[0], stream));
             CF_HIP_CHECK(ctx, hipStreamWaitEvent(st, ctx->spill_side_ev[0], 0));
+            side_started = true;
         }
         a.first = r.first;
         a.count = r.count;
-        a.counter = reinterpret_cast<unsigned int*>(ws) + (r.big ? 0 : 1);   // one claim counter per stream
-        a.work = reinterpret_cast<double*>(ws + 256 + (r.big ? 0 : big_bytes));
+        a.counter = reinterpret_cast<unsigned int*>(ws) + (side ? 0 : 1);   // one claim counter per stream
+        a.work = reinterpret_cast<double*>(ws + 256 + (side ? 0 : side_bytes));
         a.work_stride = stride_of(r);
         a.big_off = base_stride(r.kmax);
-        if (r.big && mc_on) {
-            CF_TRY(spill_mc_launch(ctx, plan, a, r.first, r.count, grid[i], (uint32_t)n_cu, st));
-        } else if (r.big) {
+        a.vs = vs_of(r);
+        a.de_lds = 0;
+        if (side && mc_on) {
+            if (r.kind == kHuge) CF_TRY(spill_mc_launch<true>(ctx, plan, a, r.first, r.count, grid[i], (uint32_t)n_cu, st));
+            else CF_TRY(spill_mc_launch<false>(ctx, plan, a, r.first, r.count, grid[i], (uint32_t)n_cu, st));
+        } else if (r.kind == kHuge) {   // one workgroup per unit, every vector in the slot
+            CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
+            const size_t lds = huge_lds_bytes(a.vs, false);
+            CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_spill_kernel<1, true, true>,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL((eigen_spill_kernel<1, true, true>), dim3(grid[i]), dim3(SP_T), lds, st, a);
+        } else if (r.kind == kBig) {
             CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
             const size_t lds = sizeof(SpillSmemT<CF_SPILL_MAX_K, true>);
             CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_spill_kernel<CF_SPILL_MAX_K, true>,
@@ -1585,7 +1917,7 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
             hipLaunchKernelGGL((eigen_spill_kernel<SP_NL, false>), dim3(grid[i]), dim3(SP_T), lds, st, a);
         }
         CF_HIP_CHECK(ctx, hipGetLastError());
-        if (r.big) {
+        if (side) {
             CF_HIP_CHECK(ctx, hipEventRecord(ctx->spill_side_ev[1], st));
             ctx->spill_side_pending = true;
         }

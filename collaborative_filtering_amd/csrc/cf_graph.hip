@@ -38,10 +38,15 @@ __global__ __launch_bounds__(kGT) void row_nnz_kernel(uint64_t n, const float* d
 
 // Optional top-K per row (cf_set_knn2_topk): the K largest weights of the row, ties at the
 // K-th value broken by ascending column.  One workgroup per row finds the K-th largest key by
-// a 4 x 8-bit radix select over the float bits (the weights are positive, so their bit
-// patterns order like their values); thr[r] = that key, take[r] = how many of the entries
+// a 4 x 8-bit radix select over order-preserving keys of the float bits (sign bit set for
+// positives, all bits flipped for negatives: a w_min < 0 keeps negative cosines, which must
+// rank below every positive weight); thr[r] = that key, take[r] = how many of the entries
 // equal to it are kept (the first ones in column order), cnt[r] = min(nnz, K).  Rows with at
 // most K entries keep them all (thr 0).
+__device__ __forceinline__ uint32_t order_key(uint32_t bits) {
+    return (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+}
+
 __global__ __launch_bounds__(kGT) void row_topk_kernel(uint64_t n, const float* dense, uint32_t K, uint32_t* thr,
                                                        uint32_t* take, uint64_t* cnt) {
     __shared__ unsigned int s_hist[256];
@@ -69,8 +74,8 @@ __global__ __launch_bounds__(kGT) void row_topk_kernel(uint64_t n, const float* 
             s_hist[threadIdx.x] = 0u;   // kGT == 256 bins
             __syncthreads();
             for (uint64_t j = threadIdx.x; j < n; j += kGT) {
-                const uint32_t key = row[j];
-                if ((key << 1) != 0u && (key & mask) == prefix) atomicAdd(&s_hist[(key >> shift) & 255u], 1u);
+                const uint32_t bits = row[j], key = order_key(bits);
+                if ((bits << 1) != 0u && (key & mask) == prefix) atomicAdd(&s_hist[(key >> shift) & 255u], 1u);
             }
             __syncthreads();
             if (threadIdx.x == 0) {
@@ -111,7 +116,7 @@ __global__ __launch_bounds__(kGT) void row_compact_kernel(uint64_t n, const floa
         for (uint64_t j0 = 0; j0 < n; j0 += kGT) {
             const uint64_t j = j0 + threadIdx.x;
             const float v = j < n ? row[j] : 0.0f;
-            const uint32_t key = __float_as_uint(v);
+            const uint32_t key = order_key(__float_as_uint(v));
             const bool nz = v != 0.0f;
             const bool tie = nz && thr && key == T;
             const unsigned long long tb = __ballot(tie);
@@ -436,10 +441,12 @@ int cf_item_cosine_edges(cf_ctx* ctx, uint32_t n_users, uint32_t n_items, const 
                     rc = cf_set_error(ctx, CF_EHIP, "top-k dense graph reset");
                 if (rc == CF_OK && hipDeviceSynchronize() != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, "top-k scatter");
             }
-            ctx->d_graph = dW;
-            dW = nullptr;
+            if (rc == CF_OK) {   // a failed reset / scatter leaves the context with no graph (dW freed below)
+                ctx->d_graph = dW;
+                dW = nullptr;
+            }
         }
-        ctx->n_items = n_items;
+        if (rc == CF_OK) ctx->n_items = n_items;
     }
     if (rp) (void)hipFree(rp);
     if (col) (void)hipFree(col);

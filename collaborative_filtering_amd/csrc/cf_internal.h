@@ -77,8 +77,10 @@ struct cf_ctx {
     uint32_t* d_pred_next = nullptr;
     // the complement masks the eigen kernel hands to the predictor (24 B per rating), valid for
     // the plan / item arrays / graph generation of the eigen run that wrote them (cf_cmask_*)
-    void* d_cmask = nullptr;
+    void* d_cmask = nullptr;            // 3 words per rating at 3 * item_off[u]
     size_t cmask_bytes = 0;
+    uint64_t* d_cmask_fp = nullptr;     // one item-list fingerprint per user (cf_items_fp)
+    uint32_t cmask_users = 0;           // its capacity
     uint64_t cmask_plan = 0;                            // cf_plan::id of that run
     const void* cmask_key[2] = {nullptr, nullptr};      // its item_off, items
     uint64_t cmask_gen = ~0ull;
@@ -130,6 +132,13 @@ struct cf_ctx {
     hipEvent_t aux_event[kAuxStreams + 1] = {};
     // fused step (cf_step_run): two predictor streams beside the two aux (eigen) streams, an
     // event per eigen bucket, and timing events {start, eigen done, end}
+    // per-bucket timing of the eigen launches (cf_eigen_bucket_timing): an event pair per
+    // k-bucket and eigen run, for the last kBucketRuns runs (a ring), read and cleared together
+    static constexpr int kBucketRuns = 16;
+    bool bucket_timing = false;
+    hipEvent_t bucket_ev[kBucketRuns][13][2] = {};
+    bool bucket_recorded[kBucketRuns][13] = {};
+    int bucket_run = 0;   // runs recorded since the last read
     hipStream_t step_stream[2] = {};
     hipEvent_t step_bucket_ev[16] = {};
     hipEvent_t step_sync_ev[4] = {};
@@ -140,7 +149,7 @@ struct cf_ctx {
 };
 
 // One launch of the eigen / predict kernels covers the users of one k-bucket.
-constexpr int kSpillBucket = -1;   // cf_bucket::emax of the CF_MAX_K < k <= CF_SPILL_MAX_K users
+constexpr int kSpillBucket = -1;   // cf_bucket::emax of the k > CF_MAX_K users (the spill paths)
 
 struct cf_bucket {
     int emax = 0;              // elements per lane of a column (k <= 16*emax); kSpillBucket
@@ -183,6 +192,30 @@ struct cf_plan {
 };
 
 int cf_set_error(cf_ctx* ctx, int code, const std::string& msg);
+
+// Fingerprint of a user's (item_off[u], k, items) for the eigen -> predictor complement-mask
+// handoff (cf_cmask_*): the eigen kernel stores it per user beside the masks, the predictor's
+// basis kernel recomputes it from the arrays it is given and takes the masks only on a match
+// (else it gathers the graph rows itself), so rewritten or reallocated item arrays cannot
+// reach stale masks.  Wave-wide: every lane of the calling wave gets the value.
+__device__ __forceinline__ uint64_t cf_fp_mix(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+__device__ inline uint64_t cf_items_fp(const uint32_t* items, int k, uint64_t base, int lane) {
+    uint64_t h = 0;
+    for (int i = lane; i < k; i += 64) h += cf_fp_mix(((uint64_t)items[i] << 32) | (uint32_t)i);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) h += (uint64_t)__shfl_xor((unsigned long long)h, o);
+    return cf_fp_mix(h ^ cf_fp_mix(base * 0x9e3779b97f4a7c15ull + (uint64_t)k)) | 1ull;   // never 0
+}
+// cf_plan_create with another largest k: local_calc's movie units and pairs (cf_local.hip) are
+// not capped at CF_SPILL_MAX_K (their spill launches take the HUGE layout above it)
+int cf_plan_create_cap(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, uint64_t kcap, cf_plan** out);
 
 inline bool has_graph(const cf_ctx* ctx) { return ctx->d_graph || ctx->graph_csr; }
 inline GraphDev graph_dev(const cf_ctx* ctx) {
@@ -259,7 +292,7 @@ int cf_launch_local_sigma(cf_ctx* ctx, const cf_plan* pair_plan, const uint64_t*
                           const uint32_t* d_pair_user, const float* d_l2, const uint64_t* d_l2_off,
                           const uint64_t* d_test_off, const uint32_t* d_test_user,
                           const float* d_test_rating, float* d_wlim, hipStream_t stream,
-                          const uint8_t* d_solved = nullptr);
+                          const uint8_t* d_solved = nullptr, bool skip_spill = false);
 
 // a8 (local_calc) modes of the spill eigen kernel for units with n > CF_MAX_K.
 struct cf_spill_local {

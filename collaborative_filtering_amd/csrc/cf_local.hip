@@ -378,10 +378,11 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
     std::vector<uint64_t> pair_out, pair_k;
     for (uint32_t v = 0; v < n_movies; ++v) {
         const uint64_t n = movie_off[v + 1] - movie_off[v];
-        if (n > CF_SPILL_MAX_K)
-            return cf_set_error(ctx, CF_ERANGE, "cf_local_calc: movie unit " + std::to_string(v) + " has " +
-                                                    std::to_string(n - 1) + " out-neighbours; at most " +
-                                                    std::to_string(CF_SPILL_MAX_K - 1) + " are supported");
+        // no neighbourhood cap (local_calc.cpp:269-272 builds any unit): units with n >
+        // CF_SPILL_MAX_K take the HUGE layout of the spill kernels (cf_eigen_spill.hip), bounded
+        // only by HBM (CF_ENOMEM: the n x n blocks below and the solver's 2 n^2 fp64 slot)
+        if (n > 0xFFFFFFFFull / 4)
+            return cf_set_error(ctx, CF_ERANGE, "cf_local_calc: movie unit " + std::to_string(v) + " too large");
         sq_off[v + 1] = sq_off[v] + n * n;
         if (n < 3) continue;
         const uint32_t m = movie_items[movie_off[v]];
@@ -424,8 +425,8 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
     for (uint32_t p = 0; p < n_pairs; ++p) pplan_off[p + 1] = pplan_off[p] + pair_k[p];
     cf_plan* mplan = nullptr;
     cf_plan* pplan = nullptr;
-    CF_TRY(cf_plan_create(ctx, n_movies, plan_off.data(), &mplan));
-    int rc = cf_plan_create(ctx, n_pairs, pplan_off.data(), &pplan);
+    CF_TRY(cf_plan_create_cap(ctx, n_movies, plan_off.data(), ~0ull, &mplan));
+    int rc = cf_plan_create_cap(ctx, n_pairs, pplan_off.data(), ~0ull, &pplan);
     if (rc != CF_OK) {
         cf_plan_destroy(mplan);
         return rc;
@@ -440,6 +441,7 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
     // spill pairs' w_lim by bisection on the movie's B = L2 L2^T (local_wlim_kernel), unless
     // cf_set_local_wlim(ctx, 0) keeps the per-pair tridiagonalisation for every one
     const bool use_bisect = ctx->local_wlim_bisect && n_pairs > n_small;
+    bool all_solved = false;
     auto alloc_copy = [&](DevBuf& b, const void* h, size_t bytes) -> int {
         CF_TRY(dev_alloc(ctx, b, bytes));
         if (h && bytes) CF_HIP_CHECK(ctx, hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice));
@@ -513,13 +515,23 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
                 rc = cf_set_error(ctx, CF_EHIP, "local_wlim_kernel launch");
                 break;
             }
+            // the per-pair solver's workspace is sized by the largest unit (2 n^2 fp64 per slot:
+            // 1.6 GB at n = 10,000): skip its launch when the bisection solved every spill pair
+            std::vector<uint8_t> sv(n_pairs - n_small);
+            if (hipMemcpy(sv.data(), static_cast<uint8_t*>(d_solved.p) + n_small, sv.size(), hipMemcpyDeviceToHost) !=
+                hipSuccess) {
+                rc = cf_set_error(ctx, CF_EHIP, "cf_local_calc: copy solved flags");
+                break;
+            }
+            all_solved = std::all_of(sv.begin(), sv.end(), [](uint8_t f) { return f != 0; });
         }
         if ((rc = cf_launch_local_sigma(ctx, pplan, moff, mit, static_cast<const uint32_t*>(d_pm.p),
                                         static_cast<const uint32_t*>(d_pu.p), static_cast<const float*>(d_l2.p),
                                         sqo, static_cast<const uint64_t*>(d_toff.p),
                                         static_cast<const uint32_t*>(d_tuser.p),
                                         static_cast<const float*>(d_trat.p), static_cast<float*>(d_wlim.p), 0,
-                                        use_bisect ? static_cast<const uint8_t*>(d_solved.p) : nullptr)))
+                                        use_bisect ? static_cast<const uint8_t*>(d_solved.p) : nullptr,
+                                        all_solved)))
             break;
         if (n_pairs > n_small) {
             int nbig = 3;

@@ -111,6 +111,8 @@ struct PredArgs {
     int tail_basis;        // 1: the last joint step writes only X's columns from Lmin on
     const uint64_t* cmask_in;   // the eigen kernel's complement masks (fused step), or null
     uint64_t cmask_words;       // their extent (users beyond it gather the graph)
+    const uint64_t* cmask_fp;   // per user: the fingerprint of the items they were built from
+    uint32_t cmask_users;
     double* slots;         // per-user slots of the chunk
     SlotOff so;
 };
@@ -482,7 +484,16 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
         // complement masks: from the eigen kernel, which gathered the same graph entries (fused
         // step), else kMaskRows graph rows in flight per wave (unconditional clamped loads, see
         // block_gemm); nc of every row in s_slow (free until the fast path)
-        if (a.cmask_in && 3 * (base + (uint64_t)k) <= a.cmask_words) {
+        // the masks only if the eigen run built them from this very item list (fingerprint;
+        // s_cnt[7], uniform after the barrier)
+        if (a.cmask_in && 3 * (base + (uint64_t)k) <= a.cmask_words && u < a.cmask_users && wave == 0) {
+            const uint64_t fp = cf_items_fp(s_item, k, base, lane);
+            if (lane == 0) s_cnt[7] = fp == a.cmask_fp[u];
+        } else if (tid == 0) {
+            s_cnt[7] = 0;
+        }
+        __syncthreads();
+        if (s_cnt[7]) {
             const uint64_t* cm = a.cmask_in + 3 * base;
             for (int i = tid; i < 3 * k; i += kThreads) s_cmask[i] = cm[i];
             __syncthreads();
@@ -725,7 +736,9 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
                     block_gemm<false, false, true>(
                         k, k, [&](int i, int l) { return Xs[(size_t)l * ld + i]; }, as_double,
                         [&](int l, int j) { return Xs[(size_t)l * ld + j]; }, as_double, [&](int) { return k; },
-                        [glo](int i0, int j0) { return j0 <= i0 && i0 >= glo; },
+                        // (+ the leading block's diagonal tiles, so the convergence decision
+                        // below also sees the deviation of those columns: ADVICE r4)
+                        [glo](int i0, int j0) { return j0 <= i0 && (i0 >= glo || i0 == j0); },
                         [&](int i, int j, double v) {
                             if (j > i) return;
                             AP[tri(i, j)] = v;
@@ -1644,7 +1657,9 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
     args.phase_cycles = ctx->d_phase;
     args.tail_basis = pred_tail_basis();
     args.cmask_in = cf_cmask_lookup(ctx, plan, d_item_off, d_items);
-    args.cmask_words = ctx->cmask_bytes / sizeof(uint64_t);
+    args.cmask_words = args.cmask_in ? ctx->cmask_bytes / sizeof(uint64_t) : 0;
+    args.cmask_fp = args.cmask_in ? ctx->d_cmask_fp : nullptr;
+    args.cmask_users = args.cmask_in ? ctx->cmask_users : 0;
     int rc = CF_OK;
     // Slots for one chunk of the largest LDS bucket, per stream; the chunks of every bucket
     // alternate between two context-owned streams (fork/join by events with the caller's
@@ -1807,7 +1822,9 @@ int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
     uint64_t* d_cmask = cf_cmask_buffer(ctx, plan);
     cf_cmask_mark(ctx, plan, d_item_off, d_items, false);
     args.cmask_in = d_cmask;
-    args.cmask_words = ctx->cmask_bytes / sizeof(uint64_t);
+    args.cmask_words = d_cmask ? ctx->cmask_bytes / sizeof(uint64_t) : 0;
+    args.cmask_fp = d_cmask ? ctx->d_cmask_fp : nullptr;
+    args.cmask_users = d_cmask ? ctx->cmask_users : 0;
     uint32_t kChunk = fit_chunk(ctx, plan, 2);
     CF_TRY(ensure_slot_scratch(ctx, plan, 2, kChunk));
     const size_t need = chunk_slot_bytes(plan, kChunk);   // one copy
@@ -1893,6 +1910,18 @@ int cf_launch_step(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
 uint64_t* cf_cmask_buffer(cf_ctx* ctx, const cf_plan* plan) {
     if (!ctx->step_masks || !plan->n_users) return nullptr;
     const size_t mb = 3 * sizeof(uint64_t) * (size_t)plan->h_item_off[plan->n_users];
+    if (plan->n_users > ctx->cmask_users) {   // the fingerprints: a separate buffer, so plans of
+        if (ctx->d_cmask_fp) (void)hipFree(ctx->d_cmask_fp);   // different sizes never overlap
+        ctx->d_cmask_fp = nullptr;
+        ctx->cmask_users = 0;
+        ctx->cmask_gen = ~0ull;
+        if (hipMalloc(&ctx->d_cmask_fp, sizeof(uint64_t) * plan->n_users) != hipSuccess) {
+            (void)hipGetLastError();
+            ctx->d_cmask_fp = nullptr;
+            return nullptr;
+        }
+        ctx->cmask_users = plan->n_users;
+    }
     if (mb > ctx->cmask_bytes) {
         if (ctx->d_cmask) (void)hipFree(ctx->d_cmask);
         ctx->d_cmask = nullptr;

@@ -1041,13 +1041,18 @@ struct LocSpArgs {
     double* fa;
     size_t fa_d;
     unsigned int* counter;
+    // units with n > CF_SPILL_MAX_K (local_calc has no neighbourhood cap): per-workgroup HBM rows
+    // for the ratings and the rated-row list, rows_d entries each (null when no unit needs them)
+    float* rat_h;
+    int* c_h;
+    size_t rows_d;
 };
 
 __global__ __launch_bounds__(kT) void local_predict_spill_kernel(LocSpArgs a) {
     __shared__ double sA[16 * kSt], sB[16 * kSt];
     __shared__ double s_la[kLdsA];
-    __shared__ float s_rat[CF_SPILL_MAX_K];
-    __shared__ int s_c[CF_SPILL_MAX_K];
+    __shared__ float s_rat_lds[CF_SPILL_MAX_K];
+    __shared__ int s_c_lds[CF_SPILL_MAX_K];
     __shared__ double s_misc[4];
     __shared__ int s_tmp[kW];
     __shared__ int s_lim;
@@ -1065,6 +1070,9 @@ __global__ __launch_bounds__(kT) void local_predict_spill_kernel(LocSpArgs a) {
         const uint64_t base = a.item_off[mv];
         const int n = (int)(a.item_off[mv + 1] - base);
         const float* U = a.evecs + a.evec_off[mv];
+        const bool rows_lds = n <= CF_SPILL_MAX_K;   // uniform
+        float* s_rat = rows_lds ? s_rat_lds : a.rat_h + blockIdx.x * a.rows_d;
+        int* s_c = rows_lds ? s_c_lds : a.c_h + blockIdx.x * a.rows_d;
         // ratings of the local graph's rows by this user; row 0 is the unknown (:400-405)
         for (int i = tid; i < n; i += kT) {
             const uint32_t it = a.items[base + i];
@@ -1368,7 +1376,6 @@ int cf_launch_local_predict_spill(cf_ctx* ctx, uint32_t n_pairs, int nmax, const
                                   const uint32_t* d_test_user, const float* d_test_rating, float* d_mse,
                                   int32_t* d_kk, double* d_pred, int32_t* d_lim, hipStream_t stream) {
     if (n_pairs == 0) return CF_OK;
-    if (nmax > CF_SPILL_MAX_K) return cf_set_error(ctx, CF_ERANGE, "local predict spill: n above CF_SPILL_MAX_K");
     LocSpArgs a{};
     a.pair_movie = d_pair_movie;
     a.pair_user = d_pair_user;
@@ -1390,7 +1397,9 @@ int cf_launch_local_predict_spill(cf_ctx* ctx, uint32_t n_pairs, int nmax, const
     a.fa_d = (size_t)(nmax + 2) * (nmax + 3) / 2;
     const int blocks = (int)std::min<size_t>(
         n_pairs, std::max<size_t>(32, std::min<size_t>(512, ((size_t)4 << 30) / (a.fa_d * 8))));
-    const size_t need = 256 + (size_t)blocks * a.fa_d * sizeof(double);
+    a.rows_d = nmax > CF_SPILL_MAX_K ? ((size_t)nmax + 63) / 64 * 64 : 0;
+    const size_t fa_bytes = (size_t)blocks * a.fa_d * sizeof(double);
+    const size_t need = 256 + fa_bytes + (size_t)blocks * a.rows_d * (sizeof(float) + sizeof(int));
     if (need > ctx->pspill_bytes) {
         if (ctx->d_pspill) (void)hipFree(ctx->d_pspill);
         ctx->d_pspill = nullptr;
@@ -1400,6 +1409,10 @@ int cf_launch_local_predict_spill(cf_ctx* ctx, uint32_t n_pairs, int nmax, const
     }
     a.counter = reinterpret_cast<unsigned int*>(ctx->d_pspill);
     a.fa = reinterpret_cast<double*>(static_cast<char*>(ctx->d_pspill) + 256);
+    if (a.rows_d) {
+        a.rat_h = reinterpret_cast<float*>(static_cast<char*>(ctx->d_pspill) + 256 + fa_bytes);
+        a.c_h = reinterpret_cast<int*>(a.rat_h + (size_t)blocks * a.rows_d);
+    }
     CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), stream));
     hipLaunchKernelGGL(local_predict_spill_kernel, dim3(blocks), dim3(kT), 0, stream, a);
     CF_HIP_CHECK(ctx, hipGetLastError());

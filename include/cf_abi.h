@@ -116,6 +116,16 @@ int cf_debug_phases(cf_ctx* ctx, int enable, uint64_t* out16);
  * Gram bound is lmax = 16 ceil(k / 16): ratings above it take the block-wide path.  -1 if
  * lmax is out of range.  (Test / diagnostics helper.) */
 int cf_debug_predict_nmax(int lmax);
+/* Per-bucket device time of compute_eigens (cf_eigen_run / cf_eigen_batch, Jacobi path):
+ * enable != 0 records a HIP event pair around every LDS k-bucket launch on the stream it is
+ * launched on (bucket e holds 16(e-1) < k <= 16e; e = 12 is eigen_kernel<12, narrow>, the
+ * dominant kernel of the C4 step).  ms13 (optional) receives, after the recorded work has
+ * finished, the mean milliseconds of each bucket's launch over the eigen runs since the last
+ * read (at most the last 16; -1: not launched; [0] unused: the spill bucket runs on its own
+ * streams) and clears the record.  Launches of
+ * other buckets may co-run on the second stream, so these are the kernels' in-step
+ * durations, as a profiler's per-dispatch trace shows them. */
+int cf_eigen_bucket_timing(cf_ctx* ctx, int enable, float* ms13);
 
 /* ---- item graph (out_fin_) ---------------------------------------------------
  * Directed weighted graph exactly as parsed: w(a,b) and w(b,a) are independent.
@@ -329,8 +339,10 @@ int cf_knn2_chunks(cf_ctx* ctx, int* n_chunks);
  * out_fin_ weights; edges count iff w > 0.1, graph_loader :113).  Movie unit v lists
  * movie_items[movie_off[v] .. movie_off[v+1]) = [m, the out-neighbours of m with w > 0.1]
  * (compact ids, any order: results are permutation-equivariant).  Units with fewer than 2
- * out-neighbours are skipped (:271-272); up to 191 run on the LDS kernels, up to
- * CF_SPILL_MAX_K - 1 on the fp64 spill kernels (HBM workspace), more is CF_ERANGE.
+ * out-neighbours are skipped (:271-272); up to 191 run on the LDS kernels, more on the fp64
+ * spill kernels (HBM workspace; above CF_SPILL_MAX_K - 1 in their HUGE layout).  There is no
+ * neighbourhood cap, as in the reference: a unit whose n x n blocks and 2 n^2 fp64 solver slot
+ * do not fit in HBM returns CF_ENOMEM.
  * Test ratings: CSR over all n_items compact ids, test_off[n_items + 1], users ascending
  * within an item.  For every test entry t of a processed movie m (test_off[m] <= t <
  * test_off[m+1]): mse[t] (float, :499), kk[t] (rated rows of the local graph), and when

@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <map>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -811,6 +812,71 @@ int cfo_graph_filter(int kind, int n, int64_t n_lines, const int32_t* va, const 
         }
     }
     for (int i = 0; i < n; ++i) out[i] = val[i];
+    return 0;
+}
+
+// knn regroup (knn.cpp:83-111 loader, :160-205 rating maps with the last assignment winning,
+// :212-298 co-rated sets of both roles, written sorted by :337-357) with the reference's
+// container semantics -- a std::map per movie and role, a sorted unique co-rated list per movie
+// -- on n_threads host threads, each owning the movies m % n_threads == t (the CPU baseline of
+// bench.py's data-prep leg; the GPU path is cf_knn_regroup).  counts[3] = train entries, test
+// entries, co-rated entries.
+int cfo_knn_regroup_mt(int64_t n, const uint32_t* user, const uint32_t* movie, const float* rating,
+                       const uint8_t* validate, int n_movies, int n_users, int n_threads, uint64_t* counts) {
+    n_threads = std::max(1, n_threads);
+    // every user's movie set (both roles), built once and shared read-only
+    std::vector<std::vector<uint32_t>> sets(n_users);
+    for (int64_t i = 0; i < n; ++i) sets[user[i]].push_back(movie[i]);
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < n_threads; ++t)
+            th.emplace_back([&, t] {
+                for (int u = t; u < n_users; u += n_threads) {
+                    auto& v = sets[u];
+                    std::sort(v.begin(), v.end());
+                    v.erase(std::unique(v.begin(), v.end()), v.end());
+                }
+            });
+        for (auto& x : th) x.join();
+    }
+    std::vector<uint64_t> c_tr(n_threads, 0), c_te(n_threads, 0), c_co(n_threads, 0);
+    std::vector<std::thread> th;
+    for (int t = 0; t < n_threads; ++t)
+        th.emplace_back([&, t] {
+            const int mine = (n_movies - t + n_threads - 1) / n_threads;
+            std::vector<std::map<uint32_t, float>> tr(mine), te(mine);
+            for (int64_t i = 0; i < n; ++i) {
+                const uint32_t m = movie[i];
+                if ((int)(m % n_threads) != t) continue;
+                auto& mp = (validate && validate[i]) ? te[m / n_threads] : tr[m / n_threads];
+                mp[user[i]] = rating[i];   // the last assignment wins
+            }
+            std::vector<std::vector<uint32_t>> co(mine);
+            for (int u = 0; u < n_users; ++u) {
+                const auto& v = sets[u];
+                for (uint32_t a : v) {
+                    if ((int)(a % n_threads) != t) continue;
+                    auto& c = co[a / n_threads];
+                    for (uint32_t b : v)
+                        if (b != a) c.push_back(b);
+                }
+            }
+            for (int j = 0; j < mine; ++j) {
+                auto& c = co[j];
+                std::sort(c.begin(), c.end());
+                c.erase(std::unique(c.begin(), c.end()), c.end());
+                c_tr[t] += tr[j].size();
+                c_te[t] += te[j].size();
+                c_co[t] += c.size();
+            }
+        });
+    for (auto& x : th) x.join();
+    counts[0] = counts[1] = counts[2] = 0;
+    for (int t = 0; t < n_threads; ++t) {
+        counts[0] += c_tr[t];
+        counts[1] += c_te[t];
+        counts[2] += c_co[t];
+    }
     return 0;
 }
 

@@ -185,12 +185,9 @@ def test_local_calc_spill_wlim_bisection(gpu_ctx):
           f"lim equal {int(same_lim.sum())}; oracle: {n_wl} w_lim, {n_cmp} predictions compared")
 
 
-def test_local_calc_unit_above_mc_cut(gpu_ctx):
-    """Movies with n > 1536 rows take the staged multi-CU spill solver for both per-movie
-    eigendecompositions (the local graph's, and B = L2 L2^T's for the w_lim bisection): two
-    movies of n ~ 1650 on a dense 1700-item graph; every pair's kk exact and w_lim against
-    LAPACK's smallest eigenvalue of L2_h L2_h^T (numpy eigvalsh; the C++ oracle's tql2 at
-    n = 1650 per pair would take minutes), 1e-4 relative; predictions finite and clamped."""
+def mc_cut_case():
+    """Two movies of n ~ 1650 on a dense 1700-item graph, ten test users rating both and ~30
+    other items: (G, moff, mitems, toff, tuser, trat, units, test)."""
     rng = np.random.default_rng(21)
     n_items = 1700
     G = rng.random((n_items, n_items)).astype(np.float32)
@@ -216,9 +213,29 @@ def test_local_calc_unit_above_mc_cut(gpu_ctx):
         units.append((mv, nbrs))
         mitems += [mv] + nbrs
         moff.append(len(mitems))
+    return G, np.array(moff), np.array(mitems), toff, np.array(tuser), np.array(trat), (units, test)
+
+
+def staged_user_case(G):
+    """compute_eigens users with k > 1536 (the staged multi-CU solver) on graph G: k = 1600,
+    1650, 1690, items ascending."""
+    rng = np.random.default_rng(22)
+    off, items = [0], []
+    for k in (1690, 1650, 1600):
+        items += sorted(rng.choice(G.shape[0], size=k, replace=False).tolist())
+        off.append(len(items))
+    return np.array(off, np.uint64), np.array(items, np.uint32)
+
+
+def test_local_calc_unit_above_mc_cut(gpu_ctx):
+    """Movies with n > 1536 rows take the staged multi-CU spill solver for both per-movie
+    eigendecompositions (the local graph's, and B = L2 L2^T's for the w_lim bisection): two
+    movies of n ~ 1650 on a dense 1700-item graph; every pair's kk exact and w_lim against
+    LAPACK's smallest eigenvalue of L2_h L2_h^T (numpy eigvalsh; the C++ oracle's tql2 at
+    n = 1650 per pair would take minutes), 1e-4 relative; predictions finite and clamped."""
+    G, moff, mitems, toff, tuser, trat, (units, test) = mc_cut_case()
     gpu_ctx.upload_graph_dense(G)
-    mse, kk, pred, wlim, lim = gpu_ctx.local_calc(np.array(moff), np.array(mitems), toff, np.array(tuser),
-                                                  np.array(trat))
+    mse, kk, pred, wlim, lim = gpu_ctx.local_calc(moff, mitems, toff, tuser, trat)
     bad, n_wl = [], 0
     for mv, nbrs in units:
         assert len(nbrs) + 1 > 1536, len(nbrs)
@@ -244,3 +261,178 @@ def test_local_calc_unit_above_mc_cut(gpu_ctx):
     assert not bad, bad[:10]
     assert n_wl >= 20, n_wl
     print(f"units above the multi-CU cut: n {[len(nb) + 1 for _, nb in units]}; w_lim compared {n_wl}")
+
+
+def test_spill_huge_layout_bit_identical(gpu_ctx, tmp_path):
+    """The HUGE layout of the spill solver (units with n > CF_SPILL_MAX_K: every k-long vector
+    in the HBM slot, QL's d / e in the LDS tail or, past ~10,100 rows, in per-part slot copies
+    the generator reads through global memory) runs the same arithmetic as the BIG layout.
+    Child processes lower the HUGE cut to 1537 (CF_SPILL_HUGE_MIN) -- once with d / e in LDS,
+    once forced into the slot (CF_SPILL_HUGE_DE=global) -- and every output of the staged cases
+    (local_calc's n ~ 1650 units: modes 1 and 3; three compute_eigens users with k > 1536: mode
+    0) must equal this process's BIG-layout run bit for bit."""
+    import os
+    import subprocess
+    import sys
+
+    from spill_layout_child import run_cases
+
+    ref = run_cases(gpu_ctx)
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "spill_layout_child.py")
+    for de in ("lds", "global"):
+        env = dict(os.environ, CF_SPILL_HUGE_MIN="1537")
+        if de == "global":
+            env["CF_SPILL_HUGE_DE"] = "global"
+        out = tmp_path / f"huge_{de}.npz"
+        r = subprocess.run([sys.executable, child, str(out)], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, (de, r.stdout[-2000:], r.stderr[-2000:])
+        got = np.load(out)
+        for k, v in ref.items():
+            g = got[k]
+            same = np.array_equal(g, v, equal_nan=True) if g.dtype.kind == "f" else np.array_equal(g, v)
+            assert same, (de, k, int(np.sum(g != v)))
+        print(f"HUGE layout (d/e {de}) == BIG layout: {sorted(ref)}")
+
+
+def huge_unit_case(n_items=6300, seed=31, cross=0.25, n_users=64, extra=40):
+    """One movie whose unit has n > CF_SPILL_MAX_K rows: a two-community dense graph (the
+    cross-community weights scaled by `cross`), so the local spectrum has one eigenvalue
+    well below the bulk and lim = 2 sits at a wide gap (the bulk of a dense random graph
+    has ~1e-5 spacing, where the span of the kept eigenvectors -- and so the reference's own
+    prediction -- is not determined).  n_users test users rate the movie and `extra` random
+    other items each."""
+    rng = np.random.default_rng(seed)
+    G = rng.random((n_items, n_items)).astype(np.float32)
+    G = ((G + G.T) / 2).astype(np.float32)
+    half = n_items // 2
+    G[:half, half:] *= np.float32(cross)
+    G[half:, :half] *= np.float32(cross)
+    G[G < 0.05] = 0
+    np.fill_diagonal(G, 0)
+    mv = 7
+    test = {mv: {}}
+    for u in range(n_users):
+        test[mv][u] = float(rng.integers(1, 6))
+        for it in rng.choice(n_items, size=extra, replace=False):
+            if int(it) != mv:
+                test.setdefault(int(it), {})[u] = float(rng.integers(1, 6))
+    return G, mv, test
+
+
+def wlim_by_inertia(theta, Wb, rated, iters=80):
+    """sqrt(lambda_min(B_hh)), B = L2 L2^T = Wb diag(theta) Wb^T (numpy eigh), h = the rows
+    outside `rated`, by bisection on Haynsworth's inertia count (an independent host
+    implementation of the rule local_wlim_kernel follows)."""
+    c = len(rated)
+    if c == 0:
+        return float(np.sqrt(max(theta[0], 0.0)))
+    WR = Wb[rated]
+    lo, hi = float(theta[0]), float(theta[min(c, len(theta) - 1)])
+    for _ in range(iters):
+        mu = 0.5 * (lo + hi)
+        if not (lo < mu < hi):
+            break
+        F = (WR / (theta - mu)[None, :]) @ WR.T
+        below = int(np.sum(theta < mu)) - int(np.sum(np.linalg.eigvalsh(F) < 0))
+        if below >= 1:
+            hi = mu
+        else:
+            lo = mu
+    return float(np.sqrt(max(0.5 * (lo + hi), 0.0)))
+
+
+@pytest.mark.parametrize("n_items,n_lo,n_hi", [(2000, 1537, 5000), (6300, 5001, 10**9)])
+def test_local_calc_large_unit_predictions(gpu_ctx, n_items, n_lo, n_hi):
+    """local_calc has no neighbourhood cap (local_calc.cpp:269-272 builds any unit): a movie
+    unit above the multi-CU cut (n ~ 1650: the staged solver's BIG layout) and one with n >
+    CF_SPILL_MAX_K (= 5000) rows (its HUGE layout, and the spill predictor with its rows in
+    HBM), each through both per-movie eigendecompositions.
+    Against numpy: kk exact; w_lim of every pair to 1e-4 relative against the inertia
+    bisection over numpy eigh(L2 L2^T), and of 4 pairs against LAPACK's smallest eigenvalue
+    of L2_h L2_h^T itself (scipy dsyevr, the reference's es0 of :435); lim exact unless a
+    tie; the predictions of >= 50 pairs with cond(U_C^T U_C) <= 1e4 and an eigengap >= 1e-3
+    at the lim cut to 1e-3 * max(1, mse) against numpy's restatement of :440-499 (numpy eigh
+    of sym_lower(L2), tests/test_oracle_local.py's np_local)."""
+    import scipy.linalg as sla
+
+    G, mv, test = huge_unit_case(n_items=n_items)
+    nbrs = [j for j in range(n_items) if float(G[mv, j]) > 0.1]
+    n = len(nbrs) + 1
+    assert n_lo <= n <= n_hi, n
+    toff = np.zeros(n_items + 1, np.uint64)
+    tuser, trat = [], []
+    for it in range(n_items):
+        us = sorted(test.get(it, {}))
+        tuser += us
+        trat += [test[it][u] for u in us]
+        toff[it + 1] = toff[it] + len(us)
+    moff = np.array([0, n], np.uint64)
+    mitems = np.array([mv] + nbrs, np.uint32)
+    gpu_ctx.upload_graph_dense(G)
+    mse, kk, pred, wlim, lim = gpu_ctx.local_calc(moff, mitems, toff, np.array(tuser), np.array(trat))
+    # numpy side
+    W = orc.local_graph(mv, nbrs, G)
+    users, R = orc.local_ratings(mv, nbrs, test)
+    d = W.sum(1)
+    L2 = (np.sqrt(1 / d)[:, None] * (np.diag(d) - W)) * np.sqrt(1 / d)[None, :]
+    ev, V = np.linalg.eigh(orc.sym_lower(L2))
+    theta, Wb = np.linalg.eigh(L2 @ L2.T)
+    b = int(toff[mv])
+    bad, n_wl, n_cmp, n_direct = [], 0, 0, 0
+    cat = {"c=0": 0, "tie": 0, "rank-deficient": 0, "ill-conditioned": 0, "small gap": 0}
+    for t, u in enumerate(users):
+        g = b + t
+        rated = [i for i in range(1, n) if R[i, t] != 0]
+        c = len(rated)
+        if kk[g] != c:
+            bad.append((u, "kk", int(kk[g]), c))
+            continue
+        if c == 0:
+            cat["c=0"] += 1
+            if not np.isnan(mse[g]):
+                bad.append((u, "c=0 not NaN", float(mse[g])))
+            continue
+        wl = wlim_by_inertia(theta, Wb, rated)
+        n_wl += 1
+        if n_direct < 4:   # LAPACK on L2_h L2_h^T itself
+            h = np.array([i for i in range(n) if i == 0 or R[i, t] == 0])
+            Lh = L2[h]
+            lmin = sla.eigh(Lh @ Lh.T, eigvals_only=True, subset_by_index=[0, 0], driver="evr")[0]
+            wd = float(np.sqrt(max(lmin, 0.0)))
+            n_direct += 1
+            if abs(wd - wl) > 1e-6 * max(1e-3, wd) or abs(float(wlim[g]) - wd) > 1e-4 * max(1e-3, wd):
+                bad.append((u, "w_lim vs LAPACK", float(wlim[g]), wl, wd))
+                continue
+        if abs(float(wlim[g]) - wl) > 1e-4 * max(1e-3, wl):
+            bad.append((u, "w_lim", float(wlim[g]), wl))
+            continue
+        lim_o = max(int(np.searchsorted(ev, wl, side="right")), 2)
+        if lim[g] != lim_o:
+            cat["tie"] += 1
+            if np.min(np.abs(ev - wl)) >= 1e-4:
+                bad.append((u, "lim", int(lim[g]), lim_o))
+            continue
+        if c < lim_o:
+            cat["rank-deficient"] += 1
+            continue
+        Uc = V[np.ix_(rated, range(lim_o))]
+        M = Uc.T @ Uc
+        if np.linalg.cond(M) > 1e4:
+            cat["ill-conditioned"] += 1
+            continue
+        gap = ev[lim_o] - ev[lim_o - 1] if lim_o < n else 1.0
+        if gap < 1e-3:
+            cat["small gap"] += 1
+            continue
+        r = R[:, t]
+        mean = r[rated].mean()
+        p = float(V[0, :lim_o] @ np.linalg.solve(M, Uc.T @ (r[rated] - mean)) + mean)
+        p = min(max(p, 1.0), 5.0)
+        mse_o = float(np.float32((r[0] - p) ** 2))
+        n_cmp += 1
+        if abs(float(mse[g]) - mse_o) > 1e-3 * max(1.0, mse_o):
+            bad.append((u, "mse", float(mse[g]), mse_o, float(pred[g]), p))
+    print(f"unit n = {n}: w_lim compared {n_wl} ({n_direct} vs LAPACK directly), predictions compared "
+          f"{n_cmp}; outside the comparison {cat}")
+    assert not bad, bad[:10]
+    assert n_wl >= 60 and n_cmp >= 50, (n_wl, n_cmp)

@@ -151,3 +151,56 @@ def test_mask_handoff_bit_identical_and_invalidated(gpu_ctx):
         gpu_ctx.set_step_masks(True)
         gpu_ctx.set_graph_layout("dense")
         plan.close()
+
+
+def test_mask_handoff_items_rewritten_in_place(gpu_ctx):
+    """the mask handoff is keyed by plan, graph generation and the item-array
+    pointers, so a caller that rewrites d_items IN PLACE between eigen_run and predict_run
+    keeps every key.  The eigen kernel stores a fingerprint of each user's (offset, k, items)
+    beside the masks and the basis kernel recomputes it from the arrays it is handed: rewritten
+    users must gather the graph themselves, so the predictions equal a masks-off run on the
+    new items bit for bit."""
+    torch = pytest.importorskip("torch")
+    seed, n_items = 2026101507, 1500
+    k = synth.degrees(seed, 2000, k_median=80.0, sigma=0.6, kmin=2, kmax=192)
+    off, items, rats = synth.user_items(seed, k, n_items, threads=8)
+    W = synth.graph_model(seed, n_items, threads=8)
+    dev = torch.device("cuda")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    eoff, ne = evec_offsets(off)
+    n, U = int(off[-1]), len(k)
+    d_off, d_items, d_rat, d_eoff = T(off.view(np.int64)), T(items.view(np.int32)), T(rats), T(eoff.view(np.int64))
+    plan = gpu_ctx.plan(off)
+    rec = dict(m=torch.zeros(U, dtype=torch.int32, device=dev), sigs=torch.zeros(n, device=dev),
+               evals=torch.zeros(n, device=dev), evecs=torch.zeros(ne, device=dev))
+
+    def predict(masks):
+        gpu_ctx.set_step_masks(masks)
+        o = dict(mse=torch.zeros(n, device=dev), kk=torch.zeros(n, dtype=torch.int32, device=dev),
+                 pred=torch.zeros(n, dtype=torch.float64, device=dev))
+        plan.predict_run(d_off, d_items, d_rat, rec["m"], rec["evals"], d_eoff, rec["evecs"], rec["sigs"],
+                         CF_SIGS_COMPAT, o["mse"], o["kk"], o["pred"])
+        torch.cuda.synchronize()
+        return {key: v.cpu().numpy() for key, v in o.items()}
+
+    try:
+        gpu_ctx.upload_graph_dense(W)
+        gpu_ctx.set_step_masks(True)
+        plan.eigen_run(d_off, d_items, d_eoff, rec["m"], rec["sigs"], rec["evals"], rec["evecs"])
+        torch.cuda.synchronize()
+        # rewrite every other user's items in place (new ascending sets, same k, same pointers)
+        rng = np.random.default_rng(5)
+        items2 = items.copy()
+        for u in range(0, U, 2):
+            b, e = int(off[u]), int(off[u + 1])
+            items2[b:e] = np.sort(rng.choice(n_items, size=e - b, replace=False)).astype(np.uint32)
+        d_items.copy_(T(items2.view(np.int32)))
+        torch.cuda.synchronize()
+        handed = predict(True)      # keys still match: the fingerprints must reject the rewritten users
+        gathered = predict(False)   # the predictor's own graph gather on the new items
+        for key in ("mse", "kk", "pred"):
+            assert np.array_equal(handed[key].view(np.uint8), gathered[key].view(np.uint8)), key
+        assert not np.array_equal(items, items2)
+    finally:
+        gpu_ctx.set_step_masks(True)
+        plan.close()

@@ -46,6 +46,25 @@ def test_host_shuffle_is_cpython():
             assert p.tolist() == x, (seed, n)
 
 
+def test_regroup_cpu_baseline_matches_restatement():
+    """The bench's data-prep CPU baseline (oracle cfo_knn_regroup_mt: the reference's containers
+    on host threads) keeps the same entries as the Python restatement of knn.cpp's maps,
+    duplicates (last read wins) and both roles included, for 1 and 3 threads."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "libcf_oracle.so"))
+    lib.cfo_knn_regroup_mt.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int] * 3 + [ctypes.c_void_p]
+    n_users, n_movies = 300, 120
+    user, movie, rating, val = regroup_case(5, n_users, n_movies, 6000)
+    tr, te, co = prep.knn_regroup(n_movies, user, movie, rating, val)
+    want = [sum(len(x) for x in tr), sum(len(x) for x in te), sum(len(x) for x in co)]
+    P = lambda a: np.ascontiguousarray(a).ctypes.data_as(ctypes.c_void_p)
+    u32, m32 = np.ascontiguousarray(user, np.uint32), np.ascontiguousarray(movie, np.uint32)
+    r32, v8 = np.ascontiguousarray(rating, np.float32), np.ascontiguousarray(val, np.uint8)
+    for threads in (1, 3):
+        cnt = np.zeros(3, np.uint64)
+        lib.cfo_knn_regroup_mt(len(user), P(u32), P(m32), P(r32), P(v8), n_movies, n_users, threads, P(cnt))
+        assert cnt.tolist() == want, (threads, cnt.tolist(), want)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", CASES)
 def test_fold_binary_byte_identical(tmp_path, name):

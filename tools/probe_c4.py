@@ -1,6 +1,6 @@
 """Diagnostics on the C4 workload (knn2 graph, 50k items): predictor phase cycles, the nc /
 c / lim distribution of the ratings, and stage times of a user range.
-usage: probe_c4.py [users=125000] [first=0]"""
+usage: probe_c4.py [users=125000] [first=0]   (PROBE_CFG=c2 for the C2 workload)"""
 import os
 import sys
 import time
@@ -15,10 +15,11 @@ from collaborative_filtering_amd.api import CF_SIGS_COMPAT, Context, evec_offset
 
 users = int(sys.argv[1]) if len(sys.argv) > 1 else 125_000
 first = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-cfg = wlm.CONFIGS["c4"]
+cname = os.environ.get("PROBE_CFG", "c4")
+cfg = wlm.CONFIGS[cname]
 dev = torch.device("cuda")
 t0 = time.time()
-d_W, _, gs = wlm.config_graph("c4", Context, 0, dev, torch)
+d_W, _, gs = wlm.config_graph(cname, Context, 0, dev, torch)
 print("graph", gs, f"{time.time() - t0:.1f}s", flush=True)
 k_all = wlm.user_degrees(cfg)
 k = k_all[first:first + users]
