@@ -555,6 +555,9 @@ def main():
                 f12, w12 = tr["eigen12"]
                 dom["traffic"] = 2.0 * f12 + w12
                 dom["traffic_note"] = "2 x FETCH_SIZE + WRITE_SIZE of the one eigen_kernel<12, true> launch of a child step"
+            if "predict_by_kernel" in tr:
+                roof_pred["traffic_by_kernel"] = {kname: {"fetch_raw": f, "write": w_, "traffic": 2.0 * f + w_}
+                                                  for kname, (f, w_) in tr["predict_by_kernel"].items()}
             for key, roof in (("predict", roof_pred), ("eigen", roof_eigen)):
                 fetch, write = tr[key]
                 roof["traffic"] = 2.0 * fetch + write
@@ -751,7 +754,8 @@ def c2_leg(args, ctx, dev_index, dev, torch):
         out["text_io"] = f"skipped: {exc}"
     # ---- local_calc (a8) on the same graph: `local_calc --pct 1` ------------------------
     try:
-        out["local_calc"] = local_calc_leg(ctx, wl, d_W.view(cfg["items"], cfg["items"]), pct=1)
+        out["local_calc"] = local_calc_leg(ctx, wl, d_W.view(cfg["items"], cfg["items"]), pct=1,
+                                           cpu_seconds=0.0 if args.no_cpu_baseline else 40.0)
     except Exception as exc:   # reported, never fatal for the headline
         out["local_calc"] = f"failed: {exc}"
     del d_W
@@ -759,7 +763,7 @@ def c2_leg(args, ctx, dev_index, dev, torch):
     return out
 
 
-def local_calc_leg(ctx, wl, W, pct=1, seed=2026, nmax=None):
+def local_calc_leg(ctx, wl, W, pct=1, seed=2026, nmax=None, cpu_seconds=40.0):
     """local_calc's engine 2 (local_calc.cpp:262-526, cf_local_calc) as `bin/local_calc --pct P`
     runs it: movies sampled with probability P %, each movie's unit = [m, out-neighbours with
     w > 0.1] of the resident knn2 graph, test ratings = the config's user ratings grouped by
@@ -798,6 +802,12 @@ def local_calc_leg(ctx, wl, W, pct=1, seed=2026, nmax=None):
     dt = time.perf_counter() - t
     pairs = int(np.sum(kk >= 0))
     sel = kk > 0
+    cpu = None
+    if cpu_seconds > 0 and len(ns):
+        try:
+            cpu = local_calc_cpu_baseline(W, moff, mitems, ns, toff, tuser, trat, kk, wlim, cpu_seconds)
+        except Exception as exc:   # reported, never fatal
+            cpu = f"failed: {exc}"
     return {"movies_sampled": int(len(movies)), "units": int(len(ns)),
             "unit_n": {"mean": float(ns.mean()) if len(ns) else 0.0, "max": int(ns.max()) if len(ns) else 0,
                        "gt_192": int(np.sum(ns > 192)), "gt_5000": int(np.sum(ns > 5000))},
@@ -807,8 +817,71 @@ def local_calc_leg(ctx, wl, W, pct=1, seed=2026, nmax=None):
                                f"units with n > {nmax} left out of the call"},
             "predictions": pairs, "seconds": dt, "predictions_per_s": pairs / dt if dt > 0 else 0.0,
             "rank_deficient_frac": float(np.mean(kk[sel] < lim[sel])) if sel.any() else 0.0,
+            "cpu_baseline": cpu,
             "note": f"bin/local_calc --pct {pct} on this config's knn2 graph: {len(ns)} movie units, every (movie, "
                     "test user) pair of them; host-pointer cf_local_calc (PCIe included)"}
+
+
+def local_calc_cpu_baseline(W, moff, mitems, ns, toff, tuser, trat, kk_g, wlim_g, budget_s):
+    """The oracle's local_calc (cfo_local_calc: fp64 tridiagonal QL for es(ll2) once per movie,
+    then per pair L2_h L2_h^T and its eigensolve, local_calc.cpp:262-526) on the sampled units
+    of the leg, one host thread per movie as GraphLab's engine schedules vertex programs: the
+    smallest units first, each with as many of its pairs as the time budget allows (cost model
+    5.8e-9 n^3 s per movie + 3.5e-9 n^3 s per pair, fp64 on one core: 1.3x the n = 1200 timing).  Also checks its kk and
+    w_lim against the device's on those pairs."""
+    import concurrent.futures as cf
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ref as orc
+
+    threads, _ = host_threads()
+    order = np.argsort(ns)
+    Wh = W.cpu().numpy()
+    jobs = []
+    for v in order[:threads]:
+        n = int(ns[v])
+        t_movie, t_pair = 5.8e-9 * n ** 3, 3.5e-9 * n ** 3
+        npairs = int((budget_s - t_movie) // t_pair)
+        if npairs < 1:
+            break
+        b, e = int(moff[v]), int(moff[v + 1])
+        m = int(mitems[b])
+        nbrs = [int(x) for x in mitems[b + 1:e]]
+        t0, t1 = int(toff[m]), int(toff[m + 1])
+        users = tuser[t0:t1][:npairs]
+        jobs.append((v, m, nbrs, t0, users))
+    if not jobs:
+        return {"skipped": f"the smallest sampled unit has n = {int(ns[order[0]])}: one movie's eigensolve alone "
+                           f"exceeds the {budget_s:.0f} s budget on one core"}
+    test = {}
+    for it in set([j[1] for j in jobs] + [x for j in jobs for x in j[2]]):
+        us, rs = tuser[int(toff[it]):int(toff[it + 1])], trat[int(toff[it]):int(toff[it + 1])]
+        test[it] = dict(zip(us.tolist(), rs.tolist()))
+
+    def one(job):
+        v, m, nbrs, t0, users = job
+        Wl = orc.local_graph(m, nbrs, Wh)
+        sub = {m: {u: test[m][u] for u in users.tolist()}}
+        for it in nbrs:
+            sub[it] = test.get(it, {})
+        _, R = orc.local_ratings(m, nbrs, sub)
+        return v, t0, orc.local_calc(Wl, R)
+
+    t = time.perf_counter()
+    with cf.ThreadPoolExecutor(len(jobs)) as ex:
+        res = list(ex.map(one, jobs))
+    dt = time.perf_counter() - t
+    n_pred = sum(len(j[4]) for j in jobs)
+    kk_eq, wl_err = 0, 0.0
+    for v, t0, (mse_o, kk_o, pred_o, wl_o, lim_o) in res:
+        for i in range(len(kk_o)):
+            kk_eq += int(kk_g[t0 + i] == kk_o[i])
+            if kk_o[i] > 0:
+                wl_err = max(wl_err, abs(float(wlim_g[t0 + i]) - wl_o[i]) / max(1e-3, wl_o[i]))
+    return {"value": n_pred / dt, "unit": "predictions/s", "cores": len(jobs), "kind": "port",
+            "sample": f"{len(jobs)} smallest sampled units (n {[int(ns[j[0]]) for j in jobs]}), {n_pred} (movie, test "
+                      f"user) pairs, oracle cfo_local_calc, one thread per movie", "seconds": dt,
+            "kk_equal_device": f"{kk_eq}/{n_pred}", "wlim_max_rel_diff_device": wl_err}
 
 
 def text_phases(wl, text_users=None, label="whole C2 record set"):
@@ -1272,10 +1345,14 @@ def pmc_traffic(args, knn2=False):
                     if re.search(r"knn2_(code|i8|f32)_kernel", name) and r["Counter_Name"] == counter:
                         out["knn2"][slot] += float(r["Counter_Value"]) * 1024.0
                     continue
-                key = "predict" if re.search(r"pred_(basis|rating)_kernel<|spill_(basis|predict)_kernel<", name) else \
-                      "eigen" if re.search(r"eigen_kernel<", name) else None
+                key = "predict" if re.search(r"pred_(basis|rating|dense)_kernel<|spill_(basis|predict)_kernel<", name) \
+                    else "eigen" if re.search(r"eigen_kernel<", name) else None
                 if key and r["Counter_Name"] == counter:
                     out[key][slot] += float(r["Counter_Value"]) * 1024.0   # the counter is in KiB
+                    kn = re.search(r"(pred_basis|pred_rating|pred_dense|spill_basis|spill_predict)_kernel", name)
+                    if kn:   # the predictor's split per kernel
+                        out.setdefault("predict_by_kernel", {}).setdefault(kn.group(1), [0.0, 0.0])[slot] += \
+                            float(r["Counter_Value"]) * 1024.0
                     if re.search(r"eigen_kernel<12, ?true>", name):   # the dominant kernel alone
                         out["eigen12"][slot] += float(r["Counter_Value"]) * 1024.0
         except (subprocess.SubprocessError, OSError, KeyError, ValueError):

@@ -102,6 +102,8 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_phase) (void)hipFree(ctx->d_phase);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_pred_next) (void)hipFree(ctx->d_pred_next);
+    if (ctx->d_dense_q) (void)hipFree(ctx->d_dense_q);
+    if (ctx->d_dense_ws) (void)hipFree(ctx->d_dense_ws);
     if (ctx->d_cmask) (void)hipFree(ctx->d_cmask);
     if (ctx->d_cmask_fp) (void)hipFree(ctx->d_cmask_fp);
     if (ctx->d_knn) (void)hipFree(ctx->d_knn);

@@ -75,6 +75,12 @@ struct cf_ctx {
     size_t scratch_bytes = 0;
     // fused predictor: one user counter per predictor stream (zeroed before each launch)
     uint32_t* d_pred_next = nullptr;
+    // block-wide rating queue per predictor stream and the dense workgroups' factorisation
+    // regions (pred_dense_kernel, cf_predict.hip), grown on demand
+    uint32_t* d_dense_q = nullptr;
+    size_t dense_q_words = 0;   // per stream
+    double* d_dense_ws = nullptr;
+    size_t dense_ws_doubles = 0;   // per stream
     // the complement masks the eigen kernel hands to the predictor (24 B per rating), valid for
     // the plan / item arrays / graph generation of the eigen run that wrote them (cf_cmask_*)
     void* d_cmask = nullptr;            // 3 words per rating at 3 * item_off[u]

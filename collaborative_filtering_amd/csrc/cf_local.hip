@@ -165,15 +165,34 @@ __global__ __launch_bounds__(kThreads) void local_predict_kernel(LocalPredArgs a
 // eigenvalue, Haynsworth's inertia additivity on B - mu (whose inverse has the R-block
 // F(mu) = W_R (Theta - mu)^-1 W_R^T, the inverse of the Schur complement of B_hh - mu) gives
 //   #{eigenvalues of B_hh below mu} = #{theta_j < mu} - #{negative eigenvalues of F(mu)},
-// and interlacing puts lambda_min(B_hh) in [theta_0, theta_c] (c = |R|).  Bisection on that
-// count -- per step one c x c F (VALU fp64 over W_R staged through LDS 16 columns at a time)
-// and its LDL^T inertia -- replaces the per-pair fp64 Gram + tridiagonalisation of n x n (mode 2
-// of eigen_spill_kernel, ~n^3 per pair): ~22 c^2 n per pair.  One workgroup per pair; pairs with
-// c > kWlimCmax keep mode 2 (solved = 0).
+// and interlacing puts lambda_min(B_hh) in [theta_0, theta_c] (c = |R|).  The bracket shrinks
+// on that count: per step one c x c F(mu) on the fp64 matrix cores and its LDL^T inertia
+// (replacing the per-pair fp64 Gram + tridiagonalisation of n x n, mode 2 of
+// eigen_spill_kernel, ~n^3 per pair).  Inside a bracket with no pole theta_j, F is smooth and
+// exactly one of its eigenvalues crosses zero at lambda_min(B_hh) (dF/dmu = W_R (Theta -
+// mu)^-2 W_R^T is positive definite, so they all increase), so det F changes sign there:
+// the next mu is the Illinois regula-falsi point on det F (its log and sign from the LDL^T
+// pivots) when both ends carry opposite signs, the midpoint otherwise -- ~10-15 steps to the
+// fp32 result instead of 44 bisections.  One workgroup per pair; pairs with c > kWlimCmax
+// keep mode 2 (solved = 0).
+//
+// F on v_mfma_f64_16x16x4_f64: F's 16 x 16 lower tiles (<= 78 at c = 184) are spread over the
+// four waves (row tiles snake-assigned: at most 21 accumulator tiles per wave), W_R's columns
+// staged through LDS kWlimKc at a time as fp64 (exact: fp32 values), the scaling d_j =
+// 1 / (theta_j - mu) applied to the A operand in registers; the next chunk's loads are in
+// flight while the current one is multiplied.  The accumulators then move to the packed
+// lower triangle (which aliases the staging area) for the LDL^T.
 constexpr int kWlimCmax = 184;   // F packed fp64 in LDS (133 KB): every pair of a k <= 180 user
-constexpr int kWlimJc = 16;      // columns of W_R staged per chunk (LDS 149 KB in all)
-constexpr int kWlimItems = 5;    // 4 x 4 tiles per thread: ceil(1081 / 256) at c = 184
-constexpr int kWlimIters = 44;
+constexpr int kWlimTiles = (kWlimCmax + 15) / 16;   // 12 row tiles
+constexpr int kWlimKc = 16;      // columns of W_R staged per chunk
+constexpr int kWlimLd = 16 * kWlimTiles + 4;        // staged row stride (doubles)
+constexpr int kWlimSlots = 21;   // lower tiles of the busiest wave at 12 row tiles
+constexpr int kWlimLoads = (kWlimCmax * kWlimKc + kThreads - 1) / kThreads;   // 12 floats per thread
+constexpr int kWlimIters = 64;
+constexpr double kWlimTol = 1e-10;   // relative bracket width at exit (w_lim is fp32)
+constexpr int kWlimFElems = kWlimCmax * (kWlimCmax + 1) / 2;
+constexpr int kWlimStageElems = kWlimKc * kWlimLd + kWlimKc;
+static_assert(kWlimStageElems <= kWlimFElems, "the staging area fits inside F's packed triangle");
 struct WlimArgs {
     uint32_t n_pairs;
     const uint32_t* pair_movie;
@@ -190,13 +209,26 @@ struct WlimArgs {
     uint8_t* solved;
 };
 
+// #{theta_j < x} (or <= x) over the ascending eigenvalues
+__device__ __forceinline__ int count_below(const float* th, int n, double x, bool le = false) {
+    int l = 0, h = n;
+    while (l < h) {
+        const int md = (l + h) >> 1;
+        const double t = (double)th[md];
+        if (t < x || (le && t == x)) l = md + 1;
+        else h = md;
+    }
+    return l;
+}
+
 __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
-    __shared__ float s_W[kWlimCmax * kWlimJc];
-    __shared__ double s_d[kWlimJc];
-    __shared__ double s_F[kWlimCmax * (kWlimCmax + 1) / 2];
+    using f64x4 = __attribute__((ext_vector_type(4))) double;
+    __shared__ double s_F[kWlimFElems];   // packed lower F; the staging tiles alias its start
     __shared__ int s_R[kWlimCmax];
     __shared__ int s_c[kThreads / 64];
-    __shared__ double s_x[2];
+    __shared__ double s_x[4];
+    double* const Ws = s_F;                        // [kWlimKc][kWlimLd]
+    double* const Ds = s_F + kWlimKc * kWlimLd;    // [kWlimKc]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     LocalPredArgs la{};   // lookup_rating's test arrays
     la.test_off = a.test_off;
@@ -230,81 +262,118 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
         }
         const float* th = a.theta + base;
         const float* Wv = a.W + a.w_off[v];
+        // this wave's row tiles (snake order over the rows, largest first) and tile slots
+        const int nt = (c + 15) >> 4;
+        const int pr[3] = {wave, 7 - wave, 8 + wave};
+        int rows[3], rstart[3], nslot = 0;
+#pragma unroll
+        for (int x = 0; x < 3; ++x) {
+            rows[x] = pr[x] < nt ? nt - 1 - pr[x] : -1;
+            rstart[x] = nslot;
+            nslot += rows[x] >= 0 ? rows[x] + 1 : 0;
+        }
+        auto slot_ij = [&](int sl, int& I, int& J) {
+            const int x = sl >= rstart[2] && rows[2] >= 0 ? 2 : (sl >= rstart[1] && rows[1] >= 0 ? 1 : 0);
+            I = rows[x];
+            J = sl - rstart[x];
+        };
+        // this thread's staged elements: column tid & 31 of the chunk, rows (tid >> 5) + 8 q
+        static_assert(kThreads % kWlimKc == 0, "one staged column per thread");
+        const int scol = tid % kWlimKc, srow0 = tid / kWlimKc;
+        constexpr int kRowStep = kThreads / kWlimKc;
+        int sR[kWlimLoads];   // the graph row of each staged row (-1: past c)
+#pragma unroll
+        for (int q = 0; q < kWlimLoads; ++q) {
+            const int r = srow0 + kRowStep * q;
+            sR[q] = r < c ? s_R[r] : -1;
+        }
         double lo = (double)th[0], hi = (double)th[min(c, n - 1)];
-        // 4 x 4 micro-tiles of F's lower triangle; with few tiles, several threads split a
-        // tile's columns (segments) and their partial sums meet in LDS
-        const int nb = (c + 3) >> 2, ntile = nb * (nb + 1) / 2;
-        const int nseg = ntile == 0 ? 1 : max(1, min(kThreads / ntile, kWlimJc / 4));
-        const int nwork = ntile * nseg;   // <= 1081 (c <= 184): at most kWlimItems per thread
-        const int cp = 4 * nb;            // staged rows (zero beyond c)
-        for (int it = 0; it < kWlimIters && c > 0 && hi - lo > 1e-11 * fabs(hi); ++it) {
-            const double mu = 0.5 * (lo + hi);
-            for (int e = tid; e < c * (c + 1) / 2; e += kThreads) s_F[e] = 0.0;
-            double acc[kWlimItems][16];
+        double Llo = 0.0, Lhi = 0.0;      // log |det F| at the ends (valid when s*** != 0)
+        int slo = 0, shi = 0;             // sign of det F at the ends (0: unknown)
+        int kept = 0;                     // +1 / -1: which end the last two steps kept
+        int last_secant = 0;
+        double w_prev = hi - lo;
+        for (int it = 0; it < kWlimIters && c > 0 && hi - lo > kWlimTol * fabs(hi); ++it) {
+            // ---- next mu: Illinois regula falsi inside a pole-free bracket, else bisection
+            double mu = 0.5 * (lo + hi);
+            const int poles = count_below(th, n, hi) - count_below(th, n, lo, true);   // theta_j in (lo, hi)
+            const bool secant = slo != 0 && shi != 0 && slo != shi && poles <= 0 &&
+                                !(last_secant && (hi - lo) > 0.5 * w_prev);
+            if (secant) {
+                const double t = 1.0 / (1.0 + exp(fmin(fmax(Lhi - Llo, -700.0), 700.0)));   // |f_lo| / (|f_lo| + |f_hi|)
+                const double m2 = lo + t * (hi - lo);
+                if (m2 > lo && m2 < hi) mu = m2;
+            }
+            last_secant = secant;
+            w_prev = hi - lo;
+            // ---- F(mu) = W_R diag(1 / (theta - mu)) W_R^T on the matrix cores
+            f64x4 acc[kWlimSlots];
 #pragma unroll
-            for (int q = 0; q < kWlimItems; ++q)
+            for (int sl = 0; sl < kWlimSlots; ++sl) acc[sl] = f64x4{0.0, 0.0, 0.0, 0.0};
+            float nxt[kWlimLoads];
+            auto fetch = [&](int j0) {
 #pragma unroll
-                for (int x = 0; x < 16; ++x) acc[q][x] = 0.0;
-            for (int j0 = 0; j0 < n; j0 += kWlimJc) {
-                __syncthreads();   // the previous chunk is consumed (and s_F zeroed)
-                for (int e = tid; e < cp * kWlimJc; e += kThreads) {
-                    const int r = e / kWlimJc, jj = e - r * kWlimJc;
-                    s_W[e] = (r < c && j0 + jj < n) ? Wv[(size_t)s_R[r] * n + j0 + jj] : 0.0f;
+                for (int q = 0; q < kWlimLoads; ++q)
+                    nxt[q] = (sR[q] >= 0 && j0 + scol < n) ? Wv[(size_t)sR[q] * n + j0 + scol] : 0.0f;
+            };
+            fetch(0);
+            for (int j0 = 0; j0 < n; j0 += kWlimKc) {
+                __syncthreads();   // the previous chunk is consumed
+#pragma unroll
+                for (int q = 0; q < kWlimLoads; ++q) {
+                    const int r = srow0 + kRowStep * q;
+                    if (r < kWlimCmax) Ws[scol * kWlimLd + r] = (double)nxt[q];
                 }
-                for (int jj = tid; jj < kWlimJc; jj += kThreads)
-                    s_d[jj] = j0 + jj < n ? 1.0 / ((double)th[j0 + jj] - mu) : 0.0;
+                for (int jj = tid; jj < kWlimKc; jj += kThreads)
+                    Ds[jj] = j0 + jj < n ? 1.0 / ((double)th[j0 + jj] - mu) : 0.0;
+                // rows c .. 16 nt - 1 of the tiles stay zero (staged as 0.0 above: srow < 0)
                 __syncthreads();
+                if (j0 + kWlimKc < n) fetch(j0 + kWlimKc);
 #pragma unroll
-                for (int q = 0; q < kWlimItems; ++q) {
-                    const int w = tid + q * kThreads;
-                    if (w >= nwork) continue;
-                    const int t = w / nseg, g = w - t * nseg;
-                    int bi = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-                    while (bi * (bi + 1) / 2 > t) --bi;
-                    while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
-                    const int bj = t - bi * (bi + 1) / 2;
-                    const float* ra = s_W + 4 * bi * kWlimJc;
-                    const float* rb = s_W + 4 * bj * kWlimJc;
-                    for (int jj = g; jj < kWlimJc; jj += nseg) {
-                        const double d = s_d[jj];
-                        double xa[4], xb[4];
+                for (int ks = 0; ks < kWlimKc / 4; ++ks) {
+                    const int kk = 4 * ks + (lane >> 4);
+                    const double dk = Ds[kk];
+                    const double* wrow = Ws + kk * kWlimLd + (lane & 15);
+                    int pI = -1;
+                    double av = 0.0;
 #pragma unroll
-                        for (int x = 0; x < 4; ++x) {
-                            xa[x] = (double)ra[x * kWlimJc + jj] * d;
-                            xb[x] = (double)rb[x * kWlimJc + jj];
+                    for (int sl = 0; sl < kWlimSlots; ++sl) {
+                        if (sl < nslot) {
+                            int I, J;
+                            slot_ij(sl, I, J);
+                            if (I != pI) {
+                                av = wrow[16 * I] * dk;
+                                pI = I;
+                            }
+                            const double bv = wrow[16 * J];
+                            acc[sl] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[sl], 0, 0, 0);
                         }
-#pragma unroll
-                        for (int x = 0; x < 4; ++x)
-#pragma unroll
-                            for (int y = 0; y < 4; ++y) acc[q][4 * x + y] = fma(xa[x], xb[y], acc[q][4 * x + y]);
                     }
                 }
             }
-            // partial tiles into the packed lower triangle of F
+            __syncthreads();   // every wave is done with the staging area (F aliases it)
 #pragma unroll
-            for (int q = 0; q < kWlimItems; ++q) {
-                const int w = tid + q * kThreads;
-                if (w >= nwork) continue;
-                const int t = w / nseg;
-                int bi = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-                while (bi * (bi + 1) / 2 > t) --bi;
-                while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
-                const int bj = t - bi * (bi + 1) / 2;
+            for (int sl = 0; sl < kWlimSlots; ++sl) {
+                if (sl < nslot) {
+                    int I, J;
+                    slot_ij(sl, I, J);
 #pragma unroll
-                for (int x = 0; x < 4; ++x)
-#pragma unroll
-                    for (int y = 0; y < 4; ++y) {
-                        const int ia = 4 * bi + x, ib = 4 * bj + y;
-                        if (ia < c && ib <= ia) atomicAdd(&s_F[tri(ia, ib)], acc[q][4 * x + y]);
+                    for (int q = 0; q < 4; ++q) {
+                        const int ia = 16 * I + (lane >> 4) + 4 * q, ib = 16 * J + (lane & 15);
+                        if (ia < c && ib <= ia) s_F[tri(ia, ib)] = acc[sl][q];
                     }
+                }
             }
             __syncthreads();
-            // inertia of F: right-looking LDL^T, negative pivots counted (thread 0)
-            int neg = 0;
+            // ---- inertia and det of F: right-looking LDL^T, negative pivots counted
+            int neg = 0, sgn = 1;
+            double ldet = 0.0;
             for (int k = 0; k < c; ++k) {
                 const double dk = s_F[tri(k, k)];
                 neg += dk < 0.0;
+                sgn = dk < 0.0 ? -sgn : (dk == 0.0 ? 0 : sgn);
                 if (dk != 0.0) {
+                    ldet += log(fabs(dk));
                     const double rdk = 1.0 / dk;
                     const int m = c - 1 - k;   // trailing rows k+1 .. c-1
                     for (int e = tid; e < m * (m + 1) / 2; e += kThreads) {
@@ -318,20 +387,37 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
                 __syncthreads();
             }
             if (tid == 0) {
-                // #{theta_j < mu} by binary search over the ascending eigenvalues
-                int l = 0, h = n;
-                while (l < h) {
-                    const int md = (l + h) >> 1;
-                    if ((double)th[md] < mu) l = md + 1;
-                    else h = md;
+                const bool below = count_below(th, n, mu) - neg >= 1;   // lambda_min(B_hh) < mu
+                // Illinois: an end kept twice in a row has its |f| halved
+                if (below) {
+                    hi = mu;
+                    shi = sgn;
+                    Lhi = ldet;
+                    if (kept == -1 && slo != 0) Llo -= 0.6931471805599453;
+                    kept = -1;
+                } else {
+                    lo = mu;
+                    slo = sgn;
+                    Llo = ldet;
+                    if (kept == 1 && shi != 0) Lhi -= 0.6931471805599453;
+                    kept = 1;
                 }
-                const bool below = l - neg >= 1;   // lambda_min(B_hh) < mu
-                s_x[0] = below ? lo : mu;
-                s_x[1] = below ? mu : hi;
+                s_x[0] = lo;
+                s_x[1] = hi;
+                s_x[2] = Llo;
+                s_x[3] = Lhi;
+                s_c[0] = slo;
+                s_c[1] = shi;
+                s_c[2] = kept;
             }
             __syncthreads();
             lo = s_x[0];
             hi = s_x[1];
+            Llo = s_x[2];
+            Lhi = s_x[3];
+            slo = s_c[0];
+            shi = s_c[1];
+            kept = s_c[2];
             __syncthreads();
         }
         if (tid == 0) {

@@ -115,6 +115,11 @@ struct PredArgs {
     uint32_t cmask_users;
     double* slots;         // per-user slots of the chunk
     SlotOff so;
+    // block-wide ratings handed to pred_dense_kernel (null: the rating kernel's block runs its
+    // user's own): dq[0] = count, dq[1] = claim counter, then 2 words per rating (plan
+    // position, row | lim << 16); dense_ws: one factorisation region per dense workgroup
+    uint32_t* dq;
+    double* dense_ws;
 };
 
 
@@ -905,6 +910,166 @@ constexpr size_t kRatingLds = 163840 / CF_PRED_RATING_OCC;
 #endif
 constexpr int kLdlPw = CF_PRED_LDL_PW;
 static_assert(kLdlPw == 4 || kLdlPw == 8, "panel width: one or two MFMA k-steps");
+// The dense path of one rating (row r, lim) of a user: the rating's own bordered Gram matrix
+// M = U_CS^T U_CS, blocked LDL^T, block-wide (local_calc_precomp.cpp:254-327).  Called by the
+// rating kernel's block for its user, or by pred_dense_kernel.  s_item / s_rat hold the user's
+// items and ratings; A is the LDS factorisation region (a.a_elems doubles), Ahbm the HBM one.
+template <typename T>
+__device__ __forceinline__ void dense_rating(const PredArgs<T>& a, int r, int lim, int k, int m, uint64_t base,
+                                             const T* U, const double* Gb, double* A, double* Ahbm,
+                                             const uint32_t* s_item, const float* s_rat, int* s_conn, int* s_nconn,
+                                             int* s_keep, int* s_cnt, double* s_misc) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int lmax = a.lmax;
+    // connected set C: the user's items that are out-neighbours of movie r (:254-265)
+    const GraphRow nrow = a.graph.row(s_item[r]);
+    const bool conn = tid < k && (double)nrow[s_item[tid < k ? tid : 0]] > 0.1;
+    const int c = block_compact(conn, tid, s_conn, s_cnt);
+    const int nc = block_compact(tid < k && !conn, tid, s_nconn, s_cnt);
+    const bool use_complement = nc < c;
+    double* AW = (a.big_lds || (size_t)(nc + 2) * (nc + 3) / 2 <= (size_t)a.a_elems) ? A : Ahbm;
+
+    // zero-column filter: keep column j < lim iff some U(C, j) >= 1e-4 (:284-304)
+    bool keep = false;
+    if (tid < lim) {
+        for (int i = 0; i < c; ++i)
+            if ((double)U[(size_t)s_conn[i] * m + tid] >= 0.0001) {
+                keep = true;
+                break;
+            }
+    }
+    const int L = block_compact(keep, tid, s_keep, s_cnt);
+    AW = (a.big_lds || (size_t)(L + 2) * (L + 3) / 2 <= (size_t)a.a_elems) ? A : Ahbm;
+
+    // mean of the connected ratings (:311)
+    if (wave == 0) {
+        double sum = 0.0;
+        for (int i = lane; i < c; i += 64) sum += (double)s_rat[s_conn[i]];
+        sum = wave_sum(sum);
+        if (lane == 0) s_misc[0] = sum / (double)c;
+    }
+    __syncthreads();
+    const double mean = s_misc[0];
+
+    // bordered Gram: AW[i][j] = (G^T G)_ij (j <= i < L), AW[L][j] = t_j, AW[L+1][j] = v_j
+    {
+        const int nt4 = (L + 3) >> 2;
+        const int ntile = nt4 * (nt4 + 1) / 2;
+        for (int tix = tid; tix < ntile; tix += kThreads) {
+            int ta = 0, rem = tix;
+            while (rem > ta) {
+                rem -= ta + 1;
+                ++ta;
+            }
+            const int tb = rem;
+            int ca[4], cb[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int ia = 4 * ta + q, ib = 4 * tb + q;
+                ca[q] = s_keep[ia < L ? ia : L - 1];
+                cb[q] = s_keep[ib < L ? ib : L - 1];
+            }
+            double acc[4][4];
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+            const int nrows = use_complement ? nc : c;
+            const int* rows = use_complement ? s_nconn : s_conn;
+            int i = 0;
+            for (; i + 1 < nrows; i += 2) {   // two rows in flight: 16 independent loads
+                const T* row0 = U + (size_t)rows[i] * m;
+                const T* row1 = U + (size_t)rows[i + 1] * m;
+                double va0[4], vb0[4], va1[4], vb1[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    va0[q] = (double)row0[ca[q]];
+                    vb0[q] = (double)row0[cb[q]];
+                    va1[q] = (double)row1[ca[q]];
+                    vb1[q] = (double)row1[cb[q]];
+                }
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                    for (int y = 0; y < 4; ++y)
+                        acc[x][y] = fma(va1[x], vb1[y], fma(va0[x], vb0[y], acc[x][y]));
+            }
+            for (; i < nrows; ++i) {
+                const T* row = U + (size_t)rows[i] * m;
+                double va[4], vb[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    va[q] = (double)row[ca[q]];
+                    vb[q] = (double)row[cb[q]];
+                }
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                    for (int y = 0; y < 4; ++y) acc[x][y] = fma(va[x], vb[y], acc[x][y]);
+            }
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) {
+                    const int ia = 4 * ta + x, ib = 4 * tb + y;
+                    if (ia < L && ib <= ia)
+                        AW[tri(ia, ib)] = use_complement
+                                             ? Gb[(size_t)min(ca[x], cb[y]) * lmax + max(ca[x], cb[y])] -
+                                                   acc[x][y]
+                                             : acc[x][y];
+                }
+        }
+        // t = G^T (r - mean): 4 lanes per column, each a strided quarter of C;
+        // v = U(r, S).
+        for (int e = tid; e < 4 * L; e += kThreads) {
+            const int j = e >> 2, part = e & 3;
+            const int cj = s_keep[j];
+            double acc0 = 0.0, acc1 = 0.0;
+            int i = part;
+            for (; i + 4 < c; i += 8) {
+                const int r0 = s_conn[i], r1 = s_conn[i + 4];
+                acc0 = fma((double)U[(size_t)r0 * m + cj], (double)s_rat[r0] - mean, acc0);
+                acc1 = fma((double)U[(size_t)r1 * m + cj], (double)s_rat[r1] - mean, acc1);
+            }
+            for (; i < c; i += 4) {
+                const int r0 = s_conn[i];
+                acc0 = fma((double)U[(size_t)r0 * m + cj], (double)s_rat[r0] - mean, acc0);
+            }
+            double acc = acc0 + acc1;
+            acc += __shfl_xor(acc, 1);
+            acc += __shfl_xor(acc, 2);
+            if (part == 0) {
+                AW[tri(L, j)] = acc;
+                AW[tri(L + 1, j)] = (double)U[(size_t)r * m + cj];
+            }
+        }
+    }
+    __syncthreads();
+
+    ldlt_bordered<kThreads, 8>(AW, L, L + 2);
+
+    // pred = v^T M^-1 t + mean = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean (:314-327)
+    if (wave == 0) {
+        double dot = 0.0;
+        const double* y = AW + tri(L, 0);
+        const double* z = AW + tri(L + 1, 0);
+        for (int j = lane; j < L; j += 64) dot = fma(y[j] * z[j], AW[tri(j, j)], dot);
+        dot = wave_sum(dot);
+        if (lane == 0) {
+            double pred = dot + mean;
+            if (pred > 5) pred = 5;
+            if (pred < 1) pred = 1;
+            const double d = (double)s_rat[r] - pred;
+            a.mse[base + r] = (float)(d * d);
+            a.kk[base + r] = c;
+            if (a.pred) a.pred[base + r] = pred;
+        }
+    }
+    __syncthreads();
+}
+
 // Every rating of one user (position uo of the plan's order) from `slot`: the body of
 // pred_rating_kernel and the second half of pred_fused_kernel.
 template <typename T>
@@ -1271,157 +1436,23 @@ __device__ __forceinline__ void rating_user(const PredArgs<T> a, uint32_t uo, do
         // resident blocks per CU, else in this block's HBM region AP (L2-resident while
         // used; the basis no longer needs it).  (The per-wave fast-path scratch in A is dead
         // by now: a system that fits in A -- (n + 2)(n + 3)/2 doubles for n rows -- uses it
-        // whatever big_lds says.)
-        double* const Ahbm = AP;
+        // whatever big_lds says.)  pred_dense_kernel uses a region of its own per workgroup.
         // ---- dense path: the rating's own bordered Gram matrix, block-wide -----------------
-        for (int si = 0; si < nslow; ++si) {
-            const int r = s_slow[si] & 0xffff;
-            // connected set C: the user's items that are out-neighbours of movie r (:254-265)
-            const GraphRow nrow = a.graph.row(s_item[r]);
-            const bool conn = tid < k && (double)nrow[s_item[tid < k ? tid : 0]] > 0.1;
-            const int c = block_compact(conn, tid, s_conn, s_cnt);
-            const int nc = block_compact(tid < k && !conn, tid, s_nconn, s_cnt);
-            const bool use_complement = nc < c;
-            const int lim = s_lim[r];
-            double* AW = (a.big_lds || (size_t)(nc + 2) * (nc + 3) / 2 <= (size_t)a.a_elems) ? A : Ahbm;
-
-            // zero-column filter: keep column j < lim iff some U(C, j) >= 1e-4 (:284-304)
-            bool keep = false;
-            if (tid < lim) {
-                for (int i = 0; i < c; ++i)
-                    if ((double)U[(size_t)s_conn[i] * m + tid] >= 0.0001) {
-                        keep = true;
-                        break;
-                    }
+        // (queued for pred_dense_kernel when a.dq is set: a few users with many block-wide
+        // ratings would otherwise run them one after another in one block, a tail of the launch)
+        if (a.dq && nslow > 0) {
+            if (tid < nslow) {
+                const int r = s_slow[tid] & 0xffff;
+                const uint32_t q = atomicAdd(a.dq, 1u);
+                a.dq[4 + 2 * (size_t)q] = uo;
+                a.dq[4 + 2 * (size_t)q + 1] = (uint32_t)r | ((uint32_t)s_lim[r] << 16);
             }
-            const int L = block_compact(keep, tid, s_keep, s_cnt);
-            AW = (a.big_lds || (size_t)(L + 2) * (L + 3) / 2 <= (size_t)a.a_elems) ? A : Ahbm;
-
-            // mean of the connected ratings (:311)
-            if (wave == 0) {
-                double sum = 0.0;
-                for (int i = lane; i < c; i += 64) sum += (double)s_rat[s_conn[i]];
-                sum = wave_sum(sum);
-                if (lane == 0) s_misc[0] = sum / (double)c;
+        } else {
+            for (int si = 0; si < nslow; ++si) {
+                const int r = s_slow[si] & 0xffff;
+                dense_rating<T>(a, r, s_lim[r], k, m, base, U, Gb, A, AP, s_item, s_rat, s_conn, s_nconn, s_keep,
+                                s_cnt, s_misc);
             }
-            __syncthreads();
-            const double mean = s_misc[0];
-
-            // bordered Gram: AW[i][j] = (G^T G)_ij (j <= i < L), AW[L][j] = t_j, AW[L+1][j] = v_j
-            {
-                const int nt4 = (L + 3) >> 2;
-                const int ntile = nt4 * (nt4 + 1) / 2;
-                for (int tix = tid; tix < ntile; tix += kThreads) {
-                    int ta = 0, rem = tix;
-                    while (rem > ta) {
-                        rem -= ta + 1;
-                        ++ta;
-                    }
-                    const int tb = rem;
-                    int ca[4], cb[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int ia = 4 * ta + q, ib = 4 * tb + q;
-                        ca[q] = s_keep[ia < L ? ia : L - 1];
-                        cb[q] = s_keep[ib < L ? ib : L - 1];
-                    }
-                    double acc[4][4];
-#pragma unroll
-                    for (int x = 0; x < 4; ++x)
-#pragma unroll
-                        for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
-                    const int nrows = use_complement ? nc : c;
-                    const int* rows = use_complement ? s_nconn : s_conn;
-                    int i = 0;
-                    for (; i + 1 < nrows; i += 2) {   // two rows in flight: 16 independent loads
-                        const T* row0 = U + (size_t)rows[i] * m;
-                        const T* row1 = U + (size_t)rows[i + 1] * m;
-                        double va0[4], vb0[4], va1[4], vb1[4];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            va0[q] = (double)row0[ca[q]];
-                            vb0[q] = (double)row0[cb[q]];
-                            va1[q] = (double)row1[ca[q]];
-                            vb1[q] = (double)row1[cb[q]];
-                        }
-#pragma unroll
-                        for (int x = 0; x < 4; ++x)
-#pragma unroll
-                            for (int y = 0; y < 4; ++y)
-                                acc[x][y] = fma(va1[x], vb1[y], fma(va0[x], vb0[y], acc[x][y]));
-                    }
-                    for (; i < nrows; ++i) {
-                        const T* row = U + (size_t)rows[i] * m;
-                        double va[4], vb[4];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            va[q] = (double)row[ca[q]];
-                            vb[q] = (double)row[cb[q]];
-                        }
-#pragma unroll
-                        for (int x = 0; x < 4; ++x)
-#pragma unroll
-                            for (int y = 0; y < 4; ++y) acc[x][y] = fma(va[x], vb[y], acc[x][y]);
-                    }
-#pragma unroll
-                    for (int x = 0; x < 4; ++x)
-#pragma unroll
-                        for (int y = 0; y < 4; ++y) {
-                            const int ia = 4 * ta + x, ib = 4 * tb + y;
-                            if (ia < L && ib <= ia)
-                                AW[tri(ia, ib)] = use_complement
-                                                     ? Gb[(size_t)min(ca[x], cb[y]) * lmax + max(ca[x], cb[y])] -
-                                                           acc[x][y]
-                                                     : acc[x][y];
-                        }
-                }
-                // t = G^T (r - mean): 4 lanes per column, each a strided quarter of C;
-                // v = U(r, S).
-                for (int e = tid; e < 4 * L; e += kThreads) {
-                    const int j = e >> 2, part = e & 3;
-                    const int cj = s_keep[j];
-                    double acc0 = 0.0, acc1 = 0.0;
-                    int i = part;
-                    for (; i + 4 < c; i += 8) {
-                        const int r0 = s_conn[i], r1 = s_conn[i + 4];
-                        acc0 = fma((double)U[(size_t)r0 * m + cj], (double)s_rat[r0] - mean, acc0);
-                        acc1 = fma((double)U[(size_t)r1 * m + cj], (double)s_rat[r1] - mean, acc1);
-                    }
-                    for (; i < c; i += 4) {
-                        const int r0 = s_conn[i];
-                        acc0 = fma((double)U[(size_t)r0 * m + cj], (double)s_rat[r0] - mean, acc0);
-                    }
-                    double acc = acc0 + acc1;
-                    acc += __shfl_xor(acc, 1);
-                    acc += __shfl_xor(acc, 2);
-                    if (part == 0) {
-                        AW[tri(L, j)] = acc;
-                        AW[tri(L + 1, j)] = (double)U[(size_t)r * m + cj];
-                    }
-                }
-            }
-            __syncthreads();
-
-            ldlt_bordered<kThreads, 8>(AW, L, L + 2);
-
-            // pred = v^T M^-1 t + mean = sum_j (L^-1 v)_j (L^-1 t)_j / D_j + mean (:314-327)
-            if (wave == 0) {
-                double dot = 0.0;
-                const double* y = AW + tri(L, 0);
-                const double* z = AW + tri(L + 1, 0);
-                for (int j = lane; j < L; j += 64) dot = fma(y[j] * z[j], AW[tri(j, j)], dot);
-                dot = wave_sum(dot);
-                if (lane == 0) {
-                    double pred = dot + mean;
-                    if (pred > 5) pred = 5;
-                    if (pred < 1) pred = 1;
-                    const double d = (double)s_rat[r] - pred;
-                    a.mse[base + r] = (float)(d * d);
-                    a.kk[base + r] = c;
-                    if (a.pred) a.pred[base + r] = pred;
-                }
-            }
-            __syncthreads();
         }
         PHASE_STAMP(3);
     }
@@ -1438,6 +1469,53 @@ __global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_rating_kern
     // every wave
     if (a.phase_cycles && threadIdx.x == 0)
         for (int ph = 0; ph < 8; ++ph) atomicAdd(&a.phase_cycles[ph], ph_acc[ph]);
+}
+
+// Block-wide ratings queued by pred_rating_kernel (a.dq), one rating per claim, persistent
+// workgroups: the rating's user's items and ratings, its slot's Gbar (the launch's chunk starts
+// at plan position `first`), and a factorisation region of its own in HBM.  Every workgroup
+// leaves when the claims pass the count the rating kernel wrote.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void pred_dense_kernel(PredArgs<T> a, uint32_t first) {
+    extern __shared__ double dsm[];
+    double* A = dsm;
+    double* s_misc = A + a.a_elems;
+    double* s_gx = s_misc + 4;
+    double* s_hx = s_gx + CF_MAX_K;
+    uint32_t* s_item = reinterpret_cast<uint32_t*>(s_hx + CF_MAX_K);
+    float* s_rat = reinterpret_cast<float*>(s_item + CF_MAX_K);
+    int* s_conn = reinterpret_cast<int*>(s_rat + CF_MAX_K);
+    int* s_keep = s_conn + CF_MAX_K;
+    int* s_nconn = s_keep + CF_MAX_K;
+    int* s_lim = s_nconn + CF_MAX_K;
+    int* s_cpos = s_lim + CF_MAX_K;
+    int* s_slow = s_cpos + CF_MAX_K;
+    int* s_cnt = s_slow + CF_MAX_K;
+    const int tid = threadIdx.x;
+    double* Ahbm = a.dense_ws + (size_t)blockIdx.x * ((size_t)(a.lmax + 2) * (a.lmax + 3) / 2);
+    for (;;) {
+        if (tid == 0) s_cnt[8] = (int)atomicAdd(a.dq + 1, 1u);
+        __syncthreads();
+        const uint32_t q = (uint32_t)s_cnt[8];
+        __syncthreads();
+        if (q >= a.dq[0]) break;   // uniform: every wave of every workgroup reaches this exit
+        const uint32_t uo = a.dq[4 + 2 * (size_t)q];
+        const uint32_t rl = a.dq[4 + 2 * (size_t)q + 1];
+        const int r = (int)(rl & 0xffffu), lim = (int)(rl >> 16);
+        const uint32_t u = a.order[uo];
+        const uint64_t base = a.item_off[u];
+        const int k = (int)(a.item_off[u + 1] - base);
+        const int m = a.m[u];
+        const T* U = a.evecs + a.evec_off[u];
+        const double* Gb = a.slots + (size_t)(uo - first) * a.so.stride + a.so.gb;
+        for (int i = tid; i < k; i += kThreads) {
+            s_item[i] = a.items[base + i];
+            s_rat[i] = a.ratings[base + i];
+        }
+        __syncthreads();
+        dense_rating<T>(a, r, lim, k, m, base, U, Gb, A, Ahbm, s_item, s_rat, s_conn, s_nconn, s_keep, s_cnt,
+                        s_misc);
+    }
 }
 
 // ---- fused: basis then ratings of one user in the same workgroup, users claimed from a
@@ -1588,6 +1666,8 @@ int setup_bucket(cf_ctx* ctx, PredArgs<T>& args, int lmax, size_t& rating_lds) {
     args.so = slot_layout(lmax);
     rating_lds = sizeof(double) * (size_t)args.a_elems + lds_fixed;
     if (rating_lds > 163840) return cf_set_error(ctx, CF_ERANGE, "predict bucket exceeds LDS");
+    CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)pred_dense_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)rating_lds));
     CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)pred_rating_kernel<T>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)rating_lds));
     CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)pred_basis_kernel<T>,
@@ -1680,6 +1760,29 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
     CF_TRY(ensure_slot_scratch(ctx, plan, copies, kChunk));
     if (fused && kChunk != fused_max)   // one slot per resident workgroup is not negotiable
         return cf_set_error(ctx, CF_ENOMEM, "fused predictor slots");
+    // block-wide ratings of the chunked path go to pred_dense_kernel: a queue per stream (every
+    // rating of a chunk at most once) and one factorisation region per dense workgroup
+    int n_cu = 0;
+    CF_HIP_CHECK(ctx, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    const uint32_t dense_grid = 2u * (uint32_t)std::max(1, n_cu);
+    if (!fused) {
+        const size_t qw = 4 + 2 * (size_t)kChunk * (size_t)std::max<uint32_t>(plan->kmax, 2);
+        const size_t ww = (size_t)dense_grid * ((size_t)(CF_MAX_K + 2) * (CF_MAX_K + 3) / 2);
+        if (qw > ctx->dense_q_words) {
+            if (ctx->d_dense_q) (void)hipFree(ctx->d_dense_q);
+            ctx->d_dense_q = nullptr;
+            ctx->dense_q_words = 0;
+            CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_dense_q, sizeof(uint32_t) * qw * copies));
+            ctx->dense_q_words = qw;
+        }
+        if (ww > ctx->dense_ws_doubles) {
+            if (ctx->d_dense_ws) (void)hipFree(ctx->d_dense_ws);
+            ctx->d_dense_ws = nullptr;
+            ctx->dense_ws_doubles = 0;
+            CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_dense_ws, sizeof(double) * ww * copies));
+            ctx->dense_ws_doubles = ww;
+        }
+    }
     const size_t need = chunk_slot_bytes(plan, kChunk);   // one copy
     if (fused) kChunk = 0;
     if (overlap) {
@@ -1744,8 +1847,17 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
             // one workgroup per user of the chunk: the hardware dispatcher balances the
             // per-user cost (~k^3) dynamically
             hipLaunchKernelGGL(pred_basis_kernel<T>, dim3(cnt), dim3(kThreads), basis_lds(), st, args, b.first + c0, cnt);
+            args.dq = ctx->d_dense_q + si * ctx->dense_q_words;
+            args.dense_ws = ctx->d_dense_ws + si * ctx->dense_ws_doubles;
+            if (hipMemsetAsync(args.dq, 0, 4 * sizeof(uint32_t), st) != hipSuccess) {
+                rc = cf_set_error(ctx, CF_EHIP, "dense queue reset failed");
+                break;
+            }
             hipLaunchKernelGGL(pred_rating_kernel<T>, dim3(cnt), dim3(kThreads), rating_lds, st, args, b.first + c0,
                                cnt);
+            hipLaunchKernelGGL(pred_dense_kernel<T>, dim3(dense_grid), dim3(kThreads), rating_lds, st, args,
+                               b.first + c0);
+            args.dq = nullptr;
             if (hipGetLastError() != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, "predict launch failed");
         }
         if (rc != CF_OK) break;

@@ -35,5 +35,6 @@ d_W, _, gs = bench.train_graph(Context, 0, dev, torch, cfg["seed"], cfg["train_u
 ctx = Context(0)
 wl = bench.Workload(args, cfg, 0, 1, dev, torch, ctx, d_W.view(cfg["items"], cfg["items"]))
 print("setup", f"{time.time() - t0:.1f}s", flush=True)
-out = bench.local_calc_leg(ctx, wl, d_W.view(cfg["items"], cfg["items"]), pct=pct)
+out = bench.local_calc_leg(ctx, wl, d_W.view(cfg["items"], cfg["items"]), pct=pct,
+                           cpu_seconds=float(os.environ.get("LOCAL_CPU_SECONDS", "0")))
 print(json.dumps(out), flush=True)
