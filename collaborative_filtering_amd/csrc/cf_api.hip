@@ -117,6 +117,9 @@ void cf_destroy(cf_ctx* ctx) {
             for (hipEvent_t& e : pr)
                 if (e) (void)hipEventDestroy(e);
     if (ctx->d_spill) (void)hipFree(ctx->d_spill);
+    if (ctx->d_spill_off) (void)hipFree(ctx->d_spill_off);
+    if (ctx->h_spill_off) (void)hipHostFree(ctx->h_spill_off);
+    if (ctx->spill_off_ev) (void)hipEventDestroy(ctx->spill_off_ev);
     for (hipEvent_t& e : ctx->spill_side_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->spill_side) (void)hipStreamDestroy(ctx->spill_side);

@@ -32,6 +32,7 @@
 // ~ (#rotations) x 6k flops over one Z pass per 16 iterations, back-transform 2k^3; see
 // DESIGN.md 3.6.
 
+#include <cstring>
 #include <vector>
 
 #include "cf_internal.h"
@@ -73,6 +74,7 @@ struct SpillArgs {
     int mc_stage;
     int mc_parts;
     uint64_t vs;   // BIG / HUGE: stride of the slot's k-long vectors (McLayout), >= the launch's kmax
+    const uint64_t* slot_off;   // staged stages: per unit of the wave, its slot's offset in `work`
     int de_lds;    // HUGE: QL's d / e in the dynamic LDS tail (else in the slot's per-part pair)
 };
 
@@ -102,6 +104,11 @@ struct McLayout {
         extra_huge = perm + v;
     }
 };
+// Slot of a staged unit of k rows: the k x k matrix, Z, the panel W, the QL coefficient buffers
+// of stage 0, then (at this offset) the McLayout vectors.
+__host__ __device__ constexpr uint64_t spill_base_stride(uint64_t k) {
+    return 2ull * k * k + (uint64_t)SP_NB * k + 4ull * SP_QB * (k + 2 * SP_QB + 4) + 64;
+}
 // the symv's transposed partials z_g (G <= ceil(vs / 64) rows of vs) share the QL buffers'
 // space (gbuf): the tridiagonalisation is over before QL starts.  ceil(v/64) v <= ceil(v/896)
 // 64 (v + 36) for every v >= 1, so they fit.
@@ -202,10 +209,11 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
     const McLayout Lo(a.vs);
     constexpr bool SLOTV = BIG || HUGE;   // rc / rs / tau in the slot
     double* M = a.mc_stage ? nullptr : a.work + (size_t)blockIdx.x * a.work_stride;
+    uint64_t bo = a.big_off;   // offset of the McLayout vectors in the slot
     // per-row vectors and the staging tiles (see SpillSmemT)
-    double* rc = SLOTV && M ? M + a.big_off : S.rc;
-    double* rs = SLOTV && M ? M + a.big_off + Lo.vs : S.rs;
-    double* tau = SLOTV && M ? M + a.big_off + 2 * Lo.vs : S.tau;
+    double* rc = SLOTV && M ? M + bo : S.rc;
+    double* rs = SLOTV && M ? M + bo + Lo.vs : S.rs;
+    double* tau = SLOTV && M ? M + bo + 2 * Lo.vs : S.tau;
     double* const stage = HUGE ? HW.stage : (BIG ? S.stage : S.rc);
     // QL's d / e, the rank / row list, the sigs: LDS (SpillSmemT) or the slot (HUGE, set per unit)
     double* Sd = S.d;
@@ -222,12 +230,20 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         const int P = st ? a.mc_parts : 1;
         if (idx >= (int)a.count * P) break;   // uniform: every wave leaves together
         const int ui = idx / P, part = idx - ui * P;
-        if (st) {
-            M = a.work + (size_t)ui * a.work_stride;
+        const int mode = a.loc.mode;
+        const uint32_t unit = a.order[a.first + ui];
+        const uint32_t u = mode == 2 ? a.loc.pair_movie[unit] : unit;   // the unit whose items index the graph
+        if (mode == 2 && a.loc.solved && a.loc.solved[unit]) continue;   // w_lim by bisection already
+        const uint64_t base = a.item_off[u];
+        const int nrows = (int)(a.item_off[u + 1] - base);
+        int n = nrows;
+        if (st) {   // staged: the unit's own slot (sized for its k when slot_off is given)
+            M = a.work + (a.slot_off ? a.slot_off[ui] : (uint64_t)ui * a.work_stride);
+            bo = a.slot_off ? spill_base_stride((uint64_t)nrows) : a.big_off;
             if (SLOTV) {
-                rc = M + a.big_off;
-                rs = M + a.big_off + Lo.vs;
-                tau = M + a.big_off + 2 * Lo.vs;
+                rc = M + bo;
+                rs = M + bo + Lo.vs;
+                tau = M + bo + 2 * Lo.vs;
             }
         }
         if constexpr (HUGE) {
@@ -235,7 +251,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             // tail when it fits (de_lds) or in the part's pair of the slot; the back-transform
             // reads the eigenvalues where part 0 of QL left them; stage 0 (one workgroup per
             // unit) uses the slot's d / e
-            double* mc = M + a.big_off;
+            double* mc = M + bo;
             Sperm = reinterpret_cast<int*>(mc + Lo.perm);
             if (st == 2) {
                 Sd = a.de_lds ? de_tail : mc + Lo.pde + 2 * (uint64_t)part * Lo.vs;
@@ -247,13 +263,6 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
                 Se = mc + Lo.e;
             }
         }
-        const int mode = a.loc.mode;
-        const uint32_t unit = a.order[a.first + ui];
-        const uint32_t u = mode == 2 ? a.loc.pair_movie[unit] : unit;   // the unit whose items index the graph
-        if (mode == 2 && a.loc.solved && a.loc.solved[unit]) continue;   // w_lim by bisection already
-        const uint64_t base = a.item_off[u];
-        const int nrows = (int)(a.item_off[u + 1] - base);
-        int n = nrows;
         if (mode == 2) {
             // w_lim pass (local_calc.cpp:402-436): the unrated rows h of the movie's L2 (row 0,
             // the movie itself, counts as unrated, :405-413), in row order, into Sperm
@@ -301,18 +310,18 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         unsigned long long n_iter = 0, n_rot = 0;
         // the sigs of the rows: LDS, or the slot (HUGE)
         auto sig_set = [&](int i, float v) {
-            if constexpr (HUGE) M[a.big_off + Lo.sig + i] = (double)v;
+            if constexpr (HUGE) M[bo + Lo.sig + i] = (double)v;
             else S.sig[i] = v;
         };
         auto sig_get = [&](int i) -> float {
-            if constexpr (HUGE) return (float)M[a.big_off + Lo.sig + i];
+            if constexpr (HUGE) return (float)M[bo + Lo.sig + i];
             else return S.sig[i];
         };
 
         if (st >= 2) {
             // resume: d, e from the slot (the multi-CU tridiagonalisation left them there) for
             // QL, the eigenvalues and sigs for the output
-            const double* mc = M + a.big_off;
+            const double* mc = M + bo;
             if constexpr (HUGE) {
                 if (st == 2)   // this part's own copy (the generator updates it)
                     for (int i = tid; i < n; i += SP_T) {
@@ -395,7 +404,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
 
         if (a.mc_stage == 1) {   // assembly only: sig to the slot, the next user
             if constexpr (!HUGE)   // (HUGE: written there already)
-                for (int i = tid; i < n; i += SP_T) M[a.big_off + Lo.sig + i] = (double)S.sig[i];
+                for (int i = tid; i < n; i += SP_T) M[bo + Lo.sig + i] = (double)S.sig[i];
             __syncthreads();
             continue;
         }
@@ -678,7 +687,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
             constexpr int OFF = QB + 4;
             static_assert(QB == 16, "applier: 64 lanes = 4 steps x 16 stages");
             const int gld = n + 2 * QB + 4;                 // rows -OFF .. n+QB-1
-            double2* Gbuf = reinterpret_cast<double2*>(st == 2 ? M + a.big_off + Lo.gbuf + (size_t)part * Lo.gsz
+            double2* Gbuf = reinterpret_cast<double2*>(st == 2 ? M + bo + Lo.gbuf + (size_t)part * Lo.gsz
                                                                : Wp + (size_t)SP_NB * n);   // [2][gld][QB]
             int* const seqb = HUGE ? H.seq : Sperm;         // (BIG: perm is free until 4c)
             int* seq_l = seqb;                              // [2][QB]
@@ -940,7 +949,7 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         const unsigned long long t4 = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
         if (st == 2) {   // the eigenvalues (every part computed the same d) to the slot
             if (part == 0) {
-                for (int i = tid; i < n; i += SP_T) M[a.big_off + Lo.df + i] = Sd[i];
+                for (int i = tid; i < n; i += SP_T) M[bo + Lo.df + i] = Sd[i];
                 if (a.phase && tid == 0) {
                     atomicAdd(&a.phase[4], t4 - t3);
                     atomicAdd(&a.phase[5], tgen);
@@ -1180,8 +1189,8 @@ struct McArgs {
     uint32_t count;
     const uint64_t* item_off;
     double* work;
-    uint64_t stride;     // doubles per user slot
-    uint64_t big_off;    // rc (v), rs (y), tau, then McLayout's d, e, sig, xv, xw, ...
+    const uint64_t* slot_off;   // per user of the wave: its slot's offset in `work` (doubles); the
+                                // McLayout vectors start spill_base_stride(k) into the slot
     int G;               // workgroups per user of spill_mc_symv / spill_mc_trail
     uint64_t vs;         // McLayout vector stride
     // the multi-workgroup assembly (spill_mc_deg / spill_mc_l2 / spill_mc_gram)
@@ -1191,6 +1200,8 @@ struct McArgs {
     float* l2;           // mode 1 writes the movie's L2, mode 3 reads it
     const uint64_t* l2_off;
 };
+
+__device__ __forceinline__ double* mc_slot(const McArgs& a, uint32_t u) { return a.work + a.slot_off[u]; }
 
 __device__ __forceinline__ int mc_n(const McArgs& a, uint32_t u) {
     const uint32_t unit = a.order[a.first + u];
@@ -1205,12 +1216,13 @@ __global__ __launch_bounds__(SP_T) void spill_mc_col(McArgs a, int j, int p) {
     const int n = mc_n(a, u);
     if (j >= n - 1) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, jj = j - p;
-    double* M = a.work + (size_t)u * a.stride;
+    double* M = mc_slot(a, u);
+    const uint64_t bo = spill_base_stride((uint64_t)n);
     double* Wp = M + 2 * (size_t)n * n;
     const McLayout Lo(a.vs);
-    double* rc = M + a.big_off;
+    double* rc = M + bo;
     double* tau = rc + 2 * Lo.vs;
-    double* mc = M + a.big_off;
+    double* mc = M + bo;
     double* colj = M + (size_t)j * n;
     if (jj > 0) {
         if (tid < jj) {
@@ -1285,10 +1297,11 @@ __global__ __launch_bounds__(MC_SYMV_T) void spill_mc_symv(McArgs a, int j) {
     const int g = blockIdx.x % a.G;
     const int n = mc_n(a, u);
     if (j >= n - 1) return;
-    double* M = a.work + (size_t)u * a.stride;
+    double* M = mc_slot(a, u);
+    const uint64_t bo = spill_base_stride((uint64_t)n);
     const McLayout Lo(a.vs);
-    const double* rc = M + a.big_off;
-    double* rs = M + a.big_off + Lo.vs;
+    const double* rc = M + bo;
+    double* rs = M + bo + Lo.vs;
     const double tj = rc[2 * Lo.vs + j];
     if (tj == 0.0) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1298,7 +1311,7 @@ __global__ __launch_bounds__(MC_SYMV_T) void spill_mc_symv(McArgs a, int j) {
     const int nrb = (n - r0 + 63) >> 6;
     const int npair = (nrb + 1) >> 1;
     if (g >= npair) return;   // uniform; spill_mc_fin sums z over g < min(G, npair)
-    double* z = M + a.big_off + Lo.gbuf + (size_t)g * Lo.vs;
+    double* z = M + bo + Lo.gbuf + (size_t)g * Lo.vs;
     if (!HUGE)
         for (int c = r0 + tid; c < n; c += MC_SYMV_T) vs_lds[c] = rc[c];
     // z_g = 0 on this wave's column blocks, by the lanes that update them below
@@ -1363,12 +1376,13 @@ __global__ __launch_bounds__(SP_T) void spill_mc_fin(McArgs a, int j, int p) {
     const int n = mc_n(a, u);
     if (j >= n - 1) return;
     const int tid = threadIdx.x, jj = j - p;
-    double* M = a.work + (size_t)u * a.stride;
+    double* M = mc_slot(a, u);
+    const uint64_t bo = spill_base_stride((uint64_t)n);
     double* Wp = M + 2 * (size_t)n * n;
     const McLayout Lo(a.vs);
-    const double* rc = M + a.big_off;
-    double* rs = M + a.big_off + Lo.vs;
-    const double* mc = M + a.big_off;
+    const double* rc = M + bo;
+    double* rs = M + bo + Lo.vs;
+    const double* mc = M + bo;
     const double tj = rc[2 * Lo.vs + j];
     const int r0 = j + 1;
     if (tj == 0.0) {
@@ -1411,7 +1425,7 @@ __global__ __launch_bounds__(SP_T) void spill_mc_trail(McArgs a, int p) {
     const int q = p + jb, mq = n - q;
     if (mq <= 0) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    double* M = a.work + (size_t)u * a.stride;
+    double* M = mc_slot(a, u);
     const double* Wp = M + 2 * (size_t)n * n;
     const int nchunk = (mq + SP_CC - 1) / SP_CC;
     if (g >= nchunk) return;   // uniform
@@ -1476,8 +1490,9 @@ __global__ void spill_mc_end(McArgs a) {
     const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= a.count) return;
     const int n = mc_n(a, u);
-    double* M = a.work + (size_t)u * a.stride;
-    double* mc = M + a.big_off;
+    double* M = mc_slot(a, u);
+    const uint64_t bo = spill_base_stride((uint64_t)n);
+    double* mc = M + bo;
     const McLayout Lo(a.vs);
     mc[Lo.d + n - 1] = M[(size_t)(n - 1) * n + (n - 1)];
     mc[Lo.e + n - 1] = 0.0;
@@ -1505,8 +1520,9 @@ __global__ __launch_bounds__(256) void spill_mc_deg(McArgs a) {
     const uint32_t unit = a.order[a.first + ui];
     const uint64_t base = a.item_off[unit];
     const int n = (int)(a.item_off[unit + 1] - base);
-    double* M = a.work + (size_t)ui * a.stride;
-    double* rc = M + a.big_off;
+    double* M = mc_slot(a, ui);
+    const uint64_t bo = spill_base_stride((uint64_t)n);
+    double* rc = M + bo;
     double* rs = rc + McLayout(a.vs).vs;
     const int lane = threadIdx.x & 63;
     const GraphRow grow0 = a.graph.row(a.items[base]);
@@ -1531,11 +1547,12 @@ __global__ __launch_bounds__(256) void spill_mc_l2(McArgs a) {
     const uint32_t unit = a.order[a.first + ui];
     const uint64_t base = a.item_off[unit];
     const int n = (int)(a.item_off[unit + 1] - base);
-    double* M = a.work + (size_t)ui * a.stride;
+    double* M = mc_slot(a, ui);
+    const uint64_t bo = spill_base_stride((uint64_t)n);
     const McLayout Lo(a.vs);
-    const double* rc = M + a.big_off;
+    const double* rc = M + bo;
     const double* rs = rc + Lo.vs;
-    double* sig = M + a.big_off + Lo.sig;
+    double* sig = M + bo + Lo.sig;
     float* L2out = a.mode == 1 ? a.l2 + a.l2_off[unit] : nullptr;
     const int lane = threadIdx.x & 63;
     const GraphRow grow0 = a.graph.row(a.items[base]);
@@ -1579,7 +1596,7 @@ __global__ __launch_bounds__(256) void spill_mc_gram(McArgs a) {
     const int tj = t - ti * (ti + 1) / 2;
     if (ti >= nt) return;   // uniform: a smaller unit of the wave
     const float* L2m = a.l2 + a.l2_off[unit];
-    double* M = a.work + (size_t)ui * a.stride;
+    double* M = mc_slot(a, ui);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
     const int i0 = ti * 64, j0 = tj * 64;
@@ -1663,25 +1680,28 @@ static bool huge_de_lds(uint64_t vs) {
 }
 
 template <bool HUGE>
-static int spill_mc_launch(cf_ctx* ctx, const cf_plan* plan, SpillArgs a, uint32_t first, uint32_t count,
-                           uint32_t slots, uint32_t n_cu, hipStream_t st) {
+// Waves: [wave_start[w], wave_start[w + 1]) of the range's users; d_off holds, per user of the
+// range, its slot's offset from the start of its wave's region (slots sized for the user's own k).
+static int spill_mc_launch(cf_ctx* ctx, const cf_plan* plan, SpillArgs a, uint32_t first,
+                           const std::vector<uint32_t>& wave_start, const uint64_t* d_off, uint32_t n_cu,
+                           hipStream_t st) {
     constexpr int NL = HUGE ? 1 : CF_SPILL_MAX_K;
     const auto kern = eigen_spill_kernel<NL, true, HUGE>;
     a.de_lds = HUGE && huge_de_lds(a.vs);
     const size_t lds = HUGE ? huge_lds_bytes(a.vs, a.de_lds) : sizeof(SpillSmemT<CF_SPILL_MAX_K, true>);
     CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    for (uint32_t w0 = 0; w0 < count; w0 += slots) {
-        const uint32_t cnt = std::min(slots, count - w0);
+    for (size_t w = 0; w + 1 < wave_start.size(); ++w) {
+        const uint32_t w0 = wave_start[w], cnt = wave_start[w + 1] - w0;
         a.first = first + w0;
         a.count = cnt;
+        a.slot_off = d_off + w0;
         McArgs m{};
         m.order = a.order;
         m.first = a.first;
         m.count = cnt;
         m.item_off = a.item_off;
         m.work = a.work;
-        m.stride = a.work_stride;
-        m.big_off = a.big_off;
+        m.slot_off = a.slot_off;
         m.vs = a.vs;
         m.items = a.items;
         m.graph = a.graph;
@@ -1721,8 +1741,10 @@ static int spill_mc_launch(cf_ctx* ctx, const cf_plan* plan, SpillArgs a, uint32
         // a batch that fills the GPU on its own users runs one part per user, and a second
         // round of parts would double the stage)
         const uint32_t fill = std::max<uint32_t>(1, n_cu / cnt);   // every part in the first round
+        // (the back-transform's parts split columns, nothing is repeated: as many as its
+        // columns give, claimed dynamically over the CUs)
         const int parts[3] = {(int)std::min<uint32_t>(fill, (kmax + MC_QL_ROWS - 1) / MC_QL_ROWS), 1,
-                              (int)std::min<uint32_t>(fill, (kmax + MC_BT_COLS - 1) / MC_BT_COLS)};
+                              (int)((kmax + MC_BT_COLS - 1) / MC_BT_COLS)};
         for (int s = 0; s < 3; ++s) {
             a.mc_stage = 2 + s;
             a.mc_parts = parts[s];
@@ -1795,9 +1817,7 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
         }
         if (j < end) rs.push_back({j, end - j, kof(j), kRest});   // (degenerate: k <= 0)
     }
-    auto base_stride = [](uint64_t kmax) {
-        return 2ull * kmax * kmax + (uint64_t)SP_NB * kmax + 4ull * SP_QB * (kmax + 2 * SP_QB + 4) + 64;
-    };
+    auto base_stride = [](uint64_t kmax) { return spill_base_stride(kmax); };
     // the k-long vector stride of a range's slots (McLayout): BIG keeps CF_SPILL_MAX_K, HUGE its
     // own kmax rounded to 64
     auto vs_of = [](const Range& r) -> uint64_t {
@@ -1815,24 +1835,37 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
         const uint64_t extra = r.kind == kHuge ? lo.extra_huge : r.kind == kBig ? (mc_on ? lo.extra_big : 3ull * lo.vs) : 0ull;
         return base_stride(r.kmax) + extra;
     };
-    // workspace cap: a fifth of this context's share of the free HBM (>= 24 GB, but at most half
-    // the share: cf_hbm_budget); the side ranges get up to half of it.  A failed allocation
-    // halves the cap (fewer slots: the users run in more waves) down to one slot per range.
-    uint64_t budget = cf_hbm_budget(ctx, ctx->spill_bytes, 0.2, 24ull << 30);
+    // workspace cap: half of this context's share of the free HBM (>= 24 GB, but at most half
+    // the share: cf_hbm_budget); the side ranges get 60 % of it.  Staged users hold a slot sized
+    // for their own k for the whole launch, as many per wave as the side region holds: one wave
+    // lets every QL generator run at once (r04: 9 waves of 56 400-MB slots for C5's 10k users).
+    // A failed allocation halves the cap (more waves / fewer slots) down to one slot per range.
+    uint64_t budget = cf_hbm_budget(ctx, ctx->spill_bytes, 0.5, 24ull << 30);
     const bool has_side = !rs.empty() && rs.front().kind != kRest;
     const bool has_rest = !rs.empty() && rs.back().kind == kRest;
     std::vector<uint32_t> grid(rs.size());
     uint64_t side_bytes = 0, rest_bytes = 0;
+    auto user_slot = [&](const Range& r, uint32_t pos) {   // bytes of a staged user's own slot
+        const McLayout lo(vs_of(r));
+        const uint64_t k = (uint64_t)(plan->h_item_off[plan->h_order[pos] + 1] - plan->h_item_off[plan->h_order[pos]]);
+        return (spill_base_stride(k) + (r.kind == kHuge ? lo.extra_huge : lo.extra_big)) * sizeof(double);
+    };
     for (;;) {
         side_bytes = rest_bytes = 0;
         bool minimal = true;
         for (size_t i = 0; i < rs.size(); ++i) {
             const uint64_t slot = stride_of(rs[i]) * sizeof(double);
             const bool side = rs[i].kind != kRest;
-            const uint64_t share = side ? (has_rest ? budget / 2 : budget) : (has_side ? budget / 2 : budget);
-            // staged users hold one slot each for the whole launch (in waves if the share is short)
-            const bool staged = side && mc_on;
-            uint32_t g = std::min<uint32_t>(rs[i].count, staged ? rs[i].count : (uint32_t)n_cu);
+            const uint64_t share = side ? (has_rest ? budget / 5 * 3 : budget) : (has_side ? budget / 5 * 2 : budget);
+            if (side && mc_on) {   // staged: the whole range if it fits, else the share (>= its largest slot)
+                uint64_t all = 0;
+                for (uint32_t j = 0; j < rs[i].count; ++j) all += user_slot(rs[i], rs[i].first + j);
+                const uint64_t region = std::max<uint64_t>(user_slot(rs[i], rs[i].first), std::min<uint64_t>(all, share));
+                side_bytes = std::max<uint64_t>(side_bytes, region);
+                minimal = minimal && region == user_slot(rs[i], rs[i].first);
+                continue;
+            }
+            uint32_t g = std::min<uint32_t>(rs[i].count, (uint32_t)n_cu);
             g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, share / slot));
             grid[i] = g;
             minimal = minimal && g == 1;
@@ -1861,6 +1894,49 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
         CF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->spill_side, hipStreamNonBlocking));
         for (hipEvent_t& e : ctx->spill_side_ev) CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
+    // staged ranges: waves filled greedily up to the side region (largest k first), and per user
+    // its slot's offset from its wave's start, for every staged range in one table, uploaded once
+    // (the side stream orders the copy after the previous call's kernels; the pinned staging
+    // buffer is rewritten only after its previous copy has completed)
+    std::vector<std::vector<uint32_t>> waves(rs.size());
+    std::vector<size_t> off_base(rs.size(), 0);
+    std::vector<uint64_t> offs;
+    if (mc_on)
+        for (size_t i = 0; i < rs.size(); ++i) {
+            if (rs[i].kind == kRest) continue;
+            off_base[i] = offs.size();
+            uint64_t cur = 0;
+            waves[i].push_back(0);
+            for (uint32_t j = 0; j < rs[i].count; ++j) {
+                const uint64_t sz = user_slot(rs[i], rs[i].first + j);
+                if (cur > 0 && cur + sz > side_bytes) {
+                    waves[i].push_back(j);
+                    cur = 0;
+                }
+                offs.push_back(cur / sizeof(double));
+                cur += sz;
+            }
+            waves[i].push_back(rs[i].count);
+        }
+    if (!offs.empty()) {
+        const size_t bytes = offs.size() * sizeof(uint64_t);
+        if (!ctx->spill_off_ev) CF_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->spill_off_ev, hipEventDisableTiming));
+        else CF_HIP_CHECK(ctx, hipEventSynchronize(ctx->spill_off_ev));
+        if (bytes > ctx->spill_off_bytes) {
+            if (ctx->h_spill_off) (void)hipHostFree(ctx->h_spill_off);
+            if (ctx->d_spill_off) {
+                CF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->spill_side));   // its kernels may still read it
+                (void)hipFree(ctx->d_spill_off);
+            }
+            ctx->h_spill_off = nullptr;
+            ctx->d_spill_off = nullptr;
+            ctx->spill_off_bytes = 0;
+            CF_HIP_CHECK(ctx, hipHostMalloc(&ctx->h_spill_off, bytes));
+            CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_spill_off, bytes));
+            ctx->spill_off_bytes = bytes;
+        }
+        std::memcpy(ctx->h_spill_off, offs.data(), bytes);
+    }
     char* ws = static_cast<char*>(ctx->d_spill);
     SpillArgs a{};
     a.order = plan->d_order;
@@ -1885,6 +1961,11 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
             CF_HIP_CHECK(ctx, hipEventRecord(ctx->spill_side_ev[0], stream));
             CF_HIP_CHECK(ctx, hipStreamWaitEvent(st, ctx->spill_side_ev[0], 0));
             side_started = true;
+            if (!offs.empty()) {
+                CF_HIP_CHECK(ctx, hipMemcpyAsync(ctx->d_spill_off, ctx->h_spill_off, offs.size() * sizeof(uint64_t),
+                                                 hipMemcpyHostToDevice, st));
+                CF_HIP_CHECK(ctx, hipEventRecord(ctx->spill_off_ev, st));
+            }
         }
         a.first = r.first;
         a.count = r.count;
@@ -1895,8 +1976,9 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
         a.vs = vs_of(r);
         a.de_lds = 0;
         if (side && mc_on) {
-            if (r.kind == kHuge) CF_TRY(spill_mc_launch<true>(ctx, plan, a, r.first, r.count, grid[i], (uint32_t)n_cu, st));
-            else CF_TRY(spill_mc_launch<false>(ctx, plan, a, r.first, r.count, grid[i], (uint32_t)n_cu, st));
+            const uint64_t* d_off = ctx->d_spill_off + off_base[i];
+            if (r.kind == kHuge) CF_TRY(spill_mc_launch<true>(ctx, plan, a, r.first, waves[i], d_off, (uint32_t)n_cu, st));
+            else CF_TRY(spill_mc_launch<false>(ctx, plan, a, r.first, waves[i], d_off, (uint32_t)n_cu, st));
         } else if (r.kind == kHuge) {   // one workgroup per unit, every vector in the slot
             CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
             const size_t lds = huge_lds_bytes(a.vs, false);

@@ -103,6 +103,12 @@ struct cf_ctx {
     // the spill bucket's k > 3072 range runs on its own stream beside the smaller ranges:
     // fork / done events; spill_side_pending = its done event still has to be joined
     hipStream_t spill_side = nullptr;
+    // staged spill users' slot offsets (per-user slot sizes): pinned staging, device copy, and
+    // the event of the last copy out of the staging buffer
+    uint64_t* h_spill_off = nullptr;
+    uint64_t* d_spill_off = nullptr;
+    size_t spill_off_bytes = 0;
+    hipEvent_t spill_off_ev = nullptr;
     hipEvent_t spill_side_ev[2] = {};
     bool spill_side_pending = false;
     // predictor spill-path workspace (per-user Q / Gbar slots, per-workgroup LDL^T), grown on demand.

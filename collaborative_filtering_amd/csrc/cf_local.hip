@@ -693,5 +693,16 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
         }
     } while (false);
     cleanup();
+    // the spill workspaces of a large call (HUGE units: up to half the free HBM) are released
+    // here rather than held by the context for the next call (synchronous call: nothing reads
+    // them any more)
+    if (hipDeviceSynchronize() == hipSuccess) {
+        if (ctx->d_spill) (void)hipFree(ctx->d_spill);
+        ctx->d_spill = nullptr;
+        ctx->spill_bytes = 0;
+        if (ctx->d_pspill) (void)hipFree(ctx->d_pspill);
+        ctx->d_pspill = nullptr;
+        ctx->pspill_bytes = 0;
+    }
     return rc;
 }

@@ -71,6 +71,13 @@ constexpr double kPivMin = 1e-10;
 // ~1e-16 for any U within kOrthoMax of orthonormal
 constexpr double kOrthoMax = 1e-2;
 constexpr float kOrthoDone = 1e-8f;
+#ifndef CF_PRED_FS_PW
+// columns of the complement's forward-substitution register panels: 8 halves the basis
+// kernel's scratch (964 -> 516 B per lane; WRITE 241 -> 191 GB, predict 160.1 -> 152.7 ms on a
+// 125k-user C4 shard, bit-identical outputs, profiles/r05/pred_fs{16,8}_e1.log); 16 is the r04 layout
+#define CF_PRED_FS_PW 8
+#endif
+constexpr int kFsPw = CF_PRED_FS_PW;
 #ifndef CF_PRED_BASIS_OCC
 #define CF_PRED_BASIS_OCC 3    // basis-kernel blocks per CU: LDS ~50 KB each.  3 -> 168 VGPRs with
                                // spills still beats 2 (256, fewer spills): C4 shard predict 170.4
@@ -685,12 +692,12 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
                     // entries t < p0 are read once per panel (independent loads, 16 independent
                     // accumulators) instead of once per column in one dependent chain; each
                     // entry still accumulates t = 0 .. j-1 in order (bit-identical results)
-                    for (int p0 = 0; p0 < du; p0 += 16) {
-                        const int b = min(16, du - p0);
-                        double acc[16];
-                        int rb[16];
+                    for (int p0 = 0; p0 < du; p0 += kFsPw) {
+                        const int b = min(kFsPw, du - p0);
+                        double acc[kFsPw];
+                        int rb[kFsPw];
 #pragma unroll
-                        for (int q = 0; q < 16; ++q) {
+                        for (int q = 0; q < kFsPw; ++q) {
                             acc[q] = q < b ? xi[p0 + q] : 0.0;
                             rb[q] = tri(p0 + min(q, b - 1), 0);
                         }
@@ -698,14 +705,14 @@ __device__ __forceinline__ void basis_user(const PredArgs<T> a, uint32_t uo, dou
                         for (int t = 0; t < p0; ++t) {
                             const double xt = xi[t];
 #pragma unroll
-                            for (int q = 0; q < 16; ++q) acc[q] = fma(-LP[rb[q] + t], xt, acc[q]);
+                            for (int q = 0; q < kFsPw; ++q) acc[q] = fma(-LP[rb[q] + t], xt, acc[q]);
                         }
 #pragma unroll
-                        for (int q = 1; q < 16; ++q)
+                        for (int q = 1; q < kFsPw; ++q)
 #pragma unroll
                             for (int t = 0; t < q; ++t) acc[q] = fma(-LP[rb[q] + p0 + t], acc[t], acc[q]);
 #pragma unroll
-                        for (int q = 0; q < 16; ++q)
+                        for (int q = 0; q < kFsPw; ++q)
                             if (q < b) xi[p0 + q] = acc[q];
                     }
                     for (int j = 0; j < du; ++j) {

@@ -305,8 +305,8 @@ def escape_summary(escapes):
 # sweeps-only Jacobi left pairs at up to 16 tol relative off-diagonal, which at an oracle gap
 # just above the 1e-2 clustering gap moves a vector by ~tol mu / (2 gap) per neighbour (0.7-1.4 %
 # of the C2 / C4 / C5 clusters escaped, largest 2.7e-3).  The eigen kernel's first-order Gram
-# refinement corrects every pair more than refine_delta = 5e-3 apart, and pairs
-# closer than that lie inside one 1e-2 cluster.
+# refinement corrects every pair more than refine_delta = 1e-2 apart (the default,
+# cf_internal.h), and pairs closer than that lie inside one 1e-2 cluster.
 ESCAPE_CAP = 0.0
 
 
