@@ -250,12 +250,14 @@ def pinv_prediction(U, ev, w_lim, Wu, rat, r, k):
     return min(max(pred, 1.0), 5.0), cond, "pinned"
 
 
-def well_conditioned_rows(run: FusedRun, u, want, max_try=160, lim_max=1024, seed=0):
+def well_conditioned_rows(run: FusedRun, u, want, max_try=160, seed=0):
     """Up to `want` rows of user u that the oracle comparison can use: U_CS^T U_CS full rank
     (|S| <= |C|: no more kept columns than connected items) and cond <= 1e8, chosen deliberately
     -- candidates with the fewest kept columns first (the oracle's explicit inverse is O(|S|^3)
-    per row; lim <= lim_max) -- instead of sampled at random, where at large k most rows are
-    rank-deficient.  Returns (rows, candidates)."""
+    per row) -- instead of sampled at random, where at large k most rows are rank-deficient.
+    (S can be far smaller than lim: the zero-column filter drops every column whose entries on
+    C are all below 1e-4, and the large users' eigenvectors are localised.)  Returns (rows,
+    candidates)."""
     from collaborative_filtering_amd.api import CF_SIGS_COMPAT
 
     it, rat, Wu, m, sig_g, ev_g, U_g = run.user(u)
@@ -270,7 +272,7 @@ def well_conditioned_rows(run: FusedRun, u, want, max_try=160, lim_max=1024, see
     for r in range(k):   # the same C and S as gram_cond (local_calc_precomp.cpp:254-304)
         C = np.nonzero(W[r] > 0.1)[0]
         nconn[r] = len(C)
-        if len(C) and lim[r] <= lim_max:
+        if len(C):
             nkeep[r] = int((U[C, :lim[r]] >= 1e-4).any(axis=0).sum())
     cand = np.nonzero((nkeep > 0) & (nkeep <= nconn))[0]
     rng = np.random.default_rng(seed)
@@ -289,6 +291,48 @@ def well_conditioned_rows(run: FusedRun, u, want, max_try=160, lim_max=1024, see
         if i % 20 == 19:
             print(f"  user {u}: {i + 1} candidates examined, {len(rows)} well-conditioned", flush=True)
     return np.array(sorted(rows), dtype=np.int64), n_cand
+
+
+def predict_check_chunked(run: FusedRun, u, rows, st, chunk=4):
+    """predict_check on user u's rows a few at a time, printing progress (the oracle's explicit
+    inverse per row takes seconds at k > 2000)."""
+    good = ill = 0
+    bad = []
+    for c0 in range(0, len(rows), chunk):
+        g, i, b = predict_check(run, [u], rows_of={u: rows[c0:c0 + chunk]}, ill_stats=st)
+        good, ill, bad = good + g, ill + i, bad + b
+        print(f"  user {u}: rows {c0 + min(chunk, len(rows) - c0)}/{len(rows)} checked", flush=True)
+    return good, ill, bad
+
+
+def lstsq_value_check(run: FusedRun, u, rows):
+    """Rows of user u against numpy: kk = |C| exactly, the prediction equal to pinv_prediction's
+    least-squares (full rank) or minimum-norm (rank-deficient) evaluation within pin_tol.
+    Returns (rows compared by value, mismatches)."""
+    from collaborative_filtering_amd.api import CF_SIGS_COMPAT
+
+    it, rat, Wu, m, sig_g, ev_g, U_g = run.user(u)
+    k = len(it)
+    b = int(run.off[u])
+    tab = run.sigs[:k] if run.sig_mode == CF_SIGS_COMPAT else sig_g
+    U = U_g.astype(np.float64)
+    ev = ev_g.astype(np.float64)
+    compared, bad = 0, []
+    for t, r in enumerate(rows):
+        g = b + int(r)
+        c = int(np.sum(Wu[int(r)].astype(np.float64) > 0.1))
+        if int(run.kk[g]) != c:
+            bad.append((u, int(r), "kk", int(run.kk[g]), c))
+            continue
+        want, cond, why = pinv_prediction(U, ev, float(tab[r]), Wu, rat.astype(np.float64), int(r), k)
+        if want is None:
+            continue
+        pg = float(run.pred[g])
+        if abs(pg - want) > pin_tol(why, cond, want):
+            bad.append((u, int(r), why, pg, want, cond))
+        compared += 1
+        print(f"  user {u}: row {t + 1}/{len(rows)} ({why}, cond {cond:.2g}) |diff| {abs(pg - want):.2g}", flush=True)
+    return compared, bad
 
 
 def value_rows(run: FusedRun, u, want, seed=0):
@@ -639,7 +683,7 @@ def test_c5_tail_k_up_to_5000(gpu_ctx, c4_graph):
         # rounding noise there.
         r2000 = value_rows(run, 0, 30, seed=10)
         st = {}
-        good, ill, badp = predict_check(run, [0], rows_of={0: r2000}, ill_stats=st)
+        good, ill, badp = predict_check_chunked(run, 0, r2000, st)
         _report("C5 k=2000", good, ill, len(r2000), st)
         assert not badp, badp
         assert good + st.get("pinv_pinned", 0) >= 20, (good, st)
@@ -659,13 +703,16 @@ def test_c5_tail_k_up_to_5000(gpu_ctx, c4_graph):
             err = float(np.max(np.abs(ev_g[:kv].astype(np.float64) - ev_ref[:kv])))
             print(f"C5 k={len(it)}: {kv} eigenvalues vs LAPACK eigvalsh, max err {err:.3g}", flush=True)
             assert err <= 1e-4, (len(it), err)
-        # predictor rows of the k = 3100 user, compared by value the same way
-        r3100 = value_rows(run, 1, 16, seed=11)
-        st = {}
-        good, ill, badp = predict_check(run, [1], rows_of={1: r3100}, ill_stats=st)
-        _report("C5 k=3100", good, ill, len(r3100), st)
+        # predictor rows of the k = 3100 user by value: its well-conditioned rows have |S| ~ 2700
+        # (c covers most of the items), where the oracle's explicit inverse takes about a minute a
+        # row, so the reference value is the reference's formula evaluated by numpy's lstsq on
+        # U_CS (pinv_prediction: the same least-squares fit, cond-scaled tolerance) -- the oracle
+        # itself is pinned to that evaluation on the k = 2000 rows above
+        r3100 = value_rows(run, 1, 12, seed=11)
+        compared, badp = lstsq_value_check(run, 1, r3100)
+        print(f"C5 k=3100: {compared} of {len(r3100)} rows equal to numpy's least-squares evaluation", flush=True)
         assert not badp, badp
-        assert good + st.get("pinv_pinned", 0) >= 10, (good, st)
+        assert compared >= 10, compared
     finally:
         run.free()
 

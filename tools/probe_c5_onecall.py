@@ -44,6 +44,11 @@ for name in parts:
     kf = ks.astype(np.float64)
     print(f"{name}: {len(ks)} users (k {ks.min()}..{ks.max()}, >3072: {(ks > 3072).sum()}) eigen {dt:.2f} s "
           f"({np.sum(9 * kf ** 3) / dt / 1e12:.2f} TFLOP/s of 9k^3)", flush=True)
+    if os.environ.get("PROBE_HASH"):   # bit-identity across builds: digests of every output
+        import hashlib
+        dig = {nm: hashlib.sha256(t.cpu().numpy().tobytes()).hexdigest()[:16]
+               for nm, t in (("m", d_m), ("sigs", d_s), ("evals", d_v), ("evecs", d_x))}
+        print(f"{name} digests {dig}", flush=True)
     plan.close()
     del d_x
     torch.cuda.empty_cache()
