@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)   # one pass, no output
     p.add_argument("--io", choices=["auto", "off"], default="auto",
                    help="C4-size out_eigen_ write/parse leg (binary all records, text the first 100k)")
+    p.add_argument("--io-text-users", type=int, default=100_000,
+                   help="records of the C4 text out_eigen_ round trip (the binary form always takes all)")
     p.add_argument("--c2", choices=["auto", "off"], default="auto",
                    help="N=1 secondary leg: BASELINE config 2 (100k x 10k) steps and the out_eigen_ text phases")
     p.add_argument("--knn2", choices=["auto", "off", "only"], default="auto",
@@ -587,7 +589,7 @@ def main():
         # the C4-size out_eigen_ round trip: binary form of all 1M records,
         # text form of the first 100k (the full text file would be ~128 GB)
         try:
-            result["config4_eigen_io"] = text_phases(wl, text_users=100_000, label="C4 record set")
+            result["config4_eigen_io"] = text_phases(wl, text_users=args.io_text_users, label="C4 record set")
         except OSError as exc:
             result["config4_eigen_io"] = f"skipped: {exc}"
     if solo and args.c2 == "auto" and args.config != "c2":
