@@ -942,8 +942,39 @@ def text_phases(wl, text_users=None, label="whole C2 record set"):
         for fmt, binary, n_rec in passes:
             k = np.diff(wl.off[:n_rec + 1].astype(np.int64))
             mm = m[:n_rec].astype(np.int64)
-            est = int(np.sum(12 + 8 * k + 4 * mm + 4 * k * mm)) * (3 if not binary else 1)
+            rec_est = (12 + 8 * k + 4 * mm + 4 * k * mm) * (3 if not binary else 1)
+            est = int(np.sum(rec_est))
             free = shutil.disk_usage(tmpdir).free
+            if est > 0.8 * free and not binary and n_rec == wl.n_users:
+                # the whole text form does not fit the disk: write and parse it in consecutive
+                # record ranges (each a complete out_eigen_ file of its users, deleted after its
+                # parse), so every record still goes through the text writer and parser
+                cum = np.cumsum(rec_est)
+                cuts, start = [0], 0
+                while start < n_rec:
+                    end = int(np.searchsorted(cum, (cum[start - 1] if start else 0) + 0.6 * free, side="right"))
+                    end = max(end, start + 1)
+                    cuts.append(min(end, n_rec))
+                    start = cuts[-1]
+                w_s = r_s = 0.0
+                size = 0
+                ok = True
+                for r0, r1 in zip(cuts[:-1], cuts[1:]):
+                    t = time.perf_counter()
+                    rc = L.cfh_write_eigen(path, 0, threads, 0, r1 - r0, ptr(uid[r0:]), ptr(wl.off[r0:]), ptr(m[r0:]),
+                                           ptr(wl.items), ptr(sigs), ptr(evals), ptr(poff[r0:]), ptr(packed))
+                    w_s += time.perf_counter() - t
+                    size += os.path.getsize(path.decode())
+                    t = time.perf_counter()
+                    n = L.cfh_load_eigen(path, threads, None, 0)
+                    r_s += time.perf_counter() - t
+                    ok = ok and rc == 0 and n == r1 - r0
+                    os.remove(path.decode())
+                res[fmt] = {"records": n_rec, "files": len(cuts) - 1, "write_s": w_s, "parse_s": r_s, "bytes": size,
+                            "write_GBps": size / w_s / 1e9, "parse_GBps": size / r_s / 1e9, "ok": bool(ok),
+                            "note": f"{len(cuts) - 1} consecutive record ranges (the {est / 1e9:.0f} GB estimate exceeds "
+                                    f"{free / 1e9:.0f} GB free in {tmpdir})"}
+                continue
             if est > 0.8 * free:
                 res[fmt] = f"skipped: ~{est / 1e9:.1f} GB would not fit the {free / 1e9:.1f} GB free in {tmpdir}"
                 continue
