@@ -393,6 +393,9 @@ __device__ void wave_gram_t(int nt, int inner, LOAD load, double* E) {
             }
 }
 
+#ifndef CF_PRED_GRAM_PF4
+#define CF_PRED_GRAM_PF4 4   // operand steps in flight of the 4 x 4-tile (nt > 48) Gram
+#endif
 template <class LOAD>
 __device__ void wave_gram(int nt, int inner, LOAD load, double* E) {
     if (nt <= 16)
@@ -402,7 +405,7 @@ __device__ void wave_gram(int nt, int inner, LOAD load, double* E) {
     else if (nt <= 48)
         wave_gram_t<3, 4>(nt, inner, load, E);
     else
-        wave_gram_t<4, 4>(nt, inner, load, E);
+        wave_gram_t<4, CF_PRED_GRAM_PF4>(nt, inner, load, E);
 }
 
 // Diagnostic phase stamps (thread 0 only; no effect on outputs): {user setup, basis,
