@@ -394,7 +394,9 @@ __device__ void wave_gram_t(int nt, int inner, LOAD load, double* E) {
 }
 
 #ifndef CF_PRED_GRAM_PF4
-#define CF_PRED_GRAM_PF4 4   // operand steps in flight of the 4 x 4-tile (nt > 48) Gram
+#define CF_PRED_GRAM_PF4 2   // operand steps in flight of the 4 x 4-tile (nt > 48) Gram: 2 (was 4) halves its
+// operand registers, so the rating kernel spills 76 instead of 156 B per lane (C4 shard predict 151.7 -> 149.6 ms,
+// rating-kernel WRITE 14.4 -> 6.2 GB, bit-identical; profiles/r05/pv_*_m1.log)
 #endif
 template <class LOAD>
 __device__ void wave_gram(int nt, int inner, LOAD load, double* E) {
