@@ -902,8 +902,12 @@ __global__ __launch_bounds__(kThreads, CF_PRED_BASIS_OCC) void pred_basis_kernel
     extern __shared__ double dsm[];
     unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long ph_t = 0;
-    for (uint32_t ub = blockIdx.x; ub < count; ub += gridDim.x)
-        basis_user(a, first + ub, a.slots + (size_t)ub * a.so.stride, dsm, ph_acc, ph_t);
+    // One user per workgroup: every launch uses grid = count.  Without a loop around the user
+    // the values set up before it are not kept live across iterations: scratch 516 -> 308 B per
+    // lane, C4 shard predict 149.7 -> 145.8 ms with the rating kernel's same change, bit-identical
+    // (profiles/r05/pv_*_m2.log)
+    const uint32_t ub = blockIdx.x;
+    if (ub < count) basis_user(a, first + ub, a.slots + (size_t)ub * a.so.stride, dsm, ph_acc, ph_t);
     if (a.phase_cycles && threadIdx.x == 0)
         for (int ph = 0; ph < 8; ++ph) atomicAdd(&a.phase_cycles[ph], ph_acc[ph]);
 }
@@ -1475,8 +1479,9 @@ __global__ __launch_bounds__(kThreads, CF_PRED_RATING_OCC) void pred_rating_kern
     extern __shared__ double dsm[];
     unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long ph_t = 0;
-    for (uint32_t ub = blockIdx.x; ub < count; ub += gridDim.x)
-        rating_user(a, first + ub, a.slots + (size_t)ub * a.so.stride, dsm, ph_acc, ph_t);
+    // one user per workgroup, grid = count (as the basis kernel): scratch 76 -> 8 B per lane
+    const uint32_t ub = blockIdx.x;
+    if (ub < count) rating_user(a, first + ub, a.slots + (size_t)ub * a.so.stride, dsm, ph_acc, ph_t);
     // slots 0-7 (thread 0 of the block); 8-15 are added per rating / user by lane 0 of
     // every wave
     if (a.phase_cycles && threadIdx.x == 0)
