@@ -452,9 +452,13 @@ def main():
         eig_s = float(np.median(eig_ms)) / 1e3
         pred_s = float(np.median(pred_ms)) / 1e3
     # Jacobi sweep counts of one more (untimed) eigen pass, for the executed-flop estimate
+    # (one stream: every k-bucket alone on the GPU, timed too -- the dominant kernel's
+    # stand-alone duration, which a rocprofv3 average over the run's launches mixes in)
     ctx.debug_stats(True)
+    ctx.eigen_bucket_timing(True)
     wl.eigen(sp)
     torch.cuda.synchronize(dev)
+    bucket_alone_ms = ctx.eigen_bucket_timing(False, read=True)
     jstats = ctx.debug_stats(False, read=True)
 
     # ---- accounting -------------------------------------------------------------------
@@ -473,7 +477,7 @@ def main():
     else:
         n_pred_total = n_pred_local
     value = wl.U / step_s
-    roof_eigen = eigen_roofline(wl.k, m_h, eig_s, jstats, bucket_ms)
+    roof_eigen = eigen_roofline(wl.k, m_h, eig_s, jstats, bucket_ms, bucket_alone_ms)
     pred_acc = predictor_flops(wl.off, wl.k, m_h, kk_h, evals_h, sigs_h)
     roof_pred = predict_roofline(pred_acc, pred_s)
     dominant_is_pred = pred_s >= eig_s
@@ -620,7 +624,7 @@ def main():
         dist.destroy_process_group()
 
 
-def eigen_roofline(k, m_h, eig_s, jstats, bucket_ms=None):
+def eigen_roofline(k, m_h, eig_s, jstats, bucket_ms=None, bucket_alone_ms=None):
     kf = k.astype(np.float64)
     flops = float(np.sum(9.0 * kf ** 3 + 4.0 * kf ** 2))
     # algorithmic bytes: item ids in, W_u entries (index+weight), sigs/evals/evecs out
@@ -646,11 +650,11 @@ def eigen_roofline(k, m_h, eig_s, jstats, bucket_ms=None):
         "executed_flops_per_stage": exe,
         "executed_TFLOPs": exe / eig_s / 1e12,
         "executed_frac": exe / eig_s / 1e12 / FP32_PEAK_TFLOPS,
-        **({"dominant": eigen_dominant(k, bucket_ms)} if bucket_ms is not None else {}),
+        **({"dominant": eigen_dominant(k, bucket_ms, bucket_alone_ms)} if bucket_ms is not None else {}),
     }
 
 
-def eigen_dominant(k, bucket_ms):
+def eigen_dominant(k, bucket_ms, bucket_alone_ms=None):
     """The dominant kernel of the eigen stage, eigen_kernel<12, true> (bucket 12: 176 < k <= 192,
     one launch per step), and every other LDS bucket: algorithmic flops per launch (9k^3 + 4k^2
     per user) over the launch's duration from cf_eigen_bucket_timing (HIP events on
@@ -678,6 +682,12 @@ def eigen_dominant(k, bucket_ms):
         out.update({"users": dom["users"], "flops_per_launch": dom["flops_per_launch"],
                     "ms_per_launch": dom["ms_per_launch"], "achieved": dom["achieved_TFLOPs"],
                     "frac": dom["frac"]})
+        if bucket_alone_ms is not None and float(bucket_alone_ms[dom["emax"]]) > 0:
+            ms_a = float(bucket_alone_ms[dom["emax"]])
+            out.update({"alone_ms": ms_a, "alone_frac": dom["flops_per_launch"] / ms_a / 1e9 / FP32_PEAK_TFLOPS,
+                        "alone_note": "the same launch alone on the GPU (one stream, the untimed sweep-count "
+                                      "pass); a rocprofv3 average over a run's launches mixes this one with the "
+                                      "co-running in-step ones"})
     return out
 
 
