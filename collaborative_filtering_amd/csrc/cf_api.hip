@@ -241,7 +241,8 @@ uint64_t cf_evec_offsets(uint32_t n_users, const uint64_t* item_off, uint64_t* e
 }
 
 int cf_plan_create(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, cf_plan** out) {
-    return cf_plan_create_cap(ctx, n_users, item_off, CF_SPILL_MAX_K, out);
+    // no k cap, as the reference: k > CF_SPILL_MAX_K takes the spill path's HUGE layout
+    return cf_plan_create_cap(ctx, n_users, item_off, ~0ull, out);
 }
 
 }  // extern "C"

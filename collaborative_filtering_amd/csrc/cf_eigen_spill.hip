@@ -1768,9 +1768,8 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
                           float* d_evals, float* d_evecs, hipStream_t stream, const cf_spill_local* loc,
                           bool defer_join) {
     if (b.count == 0) return CF_OK;
-    // compute_eigens users stop at CF_SPILL_MAX_K (cf_plan_create); local_calc's units do not
-    if (b.kmax > (uint32_t)CF_SPILL_MAX_K && !loc)
-        return cf_set_error(ctx, CF_ERANGE, "spill eigen: k above CF_SPILL_MAX_K");
+    // no k cap (compute_eigens users and local_calc's units alike): k > CF_SPILL_MAX_K takes
+    // the HUGE layout on the staged multi-CU path
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
     // k ranges over the bucket's plan positions (k non-increasing)

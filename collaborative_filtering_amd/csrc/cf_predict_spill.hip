@@ -82,6 +82,10 @@ struct SpArgs {
     unsigned int* counter;   // work-item counter of the predict kernel
     uint32_t w0, w1;         // predict launch: the chunk's work items [w0, w1)
     unsigned long long* phase;   // diagnostics (cf_debug_phases) or null: see spill_predict_kernel
+    // users with k > CF_SPILL_MAX_K (the <T, 0, 1> predict kernel): per workgroup, the per-row
+    // arrays (ratings, C, Cbar, kept columns) in HBM, 4 x rows_d words each
+    uint32_t* rows;
+    size_t rows_d;
 };
 
 __device__ __forceinline__ double wsum(double v) {
@@ -422,7 +426,10 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
     int* cpos = lim + k;
     int* hdr = cpos + k;
 
-    for (int j = tid; j < m; j += kT) s_ev[j] = (double)a.evals[base + j];
+    // the eigenvalues staged in LDS (m > CF_SPILL_MAX_K, uncapped users: read from HBM)
+    const bool ev_lds = m <= CF_SPILL_MAX_K;   // uniform
+    if (ev_lds)
+        for (int j = tid; j < m; j += kT) s_ev[j] = (double)a.evals[base + j];
     if (tid == 0) s_hdr[0] = 2;
     __syncthreads();
     // lim = first eigenvalue index above w_lim, clamped to [2, m] (:271-282)
@@ -430,7 +437,7 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
         const double w_lim = (double)a.sigtab[a.sig_mode == CF_SIGS_COMPAT ? (uint64_t)i : base + i];
         int l = m;
         for (int j = 0; j < m; ++j)
-            if (s_ev[j] > w_lim) {
+            if ((ev_lds ? s_ev[j] : (double)a.evals[base + j]) > w_lim) {
                 l = j;
                 break;
             }
@@ -538,7 +545,7 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
     // Y^T Y after Gbar's Lu x Lu in Gb, W^T r / W^T 1 after PG / PH.
     const int du = k - Lu;
     int gm = 0;
-    if (basis && du > 0 && du <= CF_SPILL_MAX_K) {
+    if (basis && du > 0) {
         const double* Q = Qb[cur];
         double* Wm = Gt;
         double* QO = Gb + (size_t)Lu * Lu;
@@ -650,13 +657,19 @@ template <typename T, int CAP, int OCC>
 __global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
     // GEMM staging: two buffers for the one-per-CU instantiation, one where two workgroups
     // must share a CU (the <kSmallCap, 2> LDS budget)
-    constexpr int kNbuf = CAP > kSmallCap ? 2 : 1;
+    // CAP = 0: users with k > CF_SPILL_MAX_K, the per-row arrays in the workgroup's HBM rows
+    constexpr int kNbuf = (CAP == 0 || CAP > kSmallCap) ? 2 : 1;
     __shared__ double sA[kNbuf * 16 * kSt], sB[kNbuf * 16 * kSt];
     __shared__ double s_la[kLdsA];
-    __shared__ float s_rat[CAP];
-    __shared__ int s_conn[CAP];
-    __shared__ int s_ncon[CAP];
-    __shared__ int s_keep[CAP];
+    __shared__ float s_rat_l[CAP ? CAP : 1];
+    __shared__ int s_conn_l[CAP ? CAP : 1];
+    __shared__ int s_ncon_l[CAP ? CAP : 1];
+    __shared__ int s_keep_l[CAP ? CAP : 1];
+    uint32_t* const rows_g = CAP ? nullptr : a.rows + (size_t)blockIdx.x * 4 * a.rows_d;
+    float* const s_rat = CAP ? s_rat_l : reinterpret_cast<float*>(rows_g);
+    int* const s_conn = CAP ? s_conn_l : reinterpret_cast<int*>(rows_g + a.rows_d);
+    int* const s_ncon = CAP ? s_ncon_l : reinterpret_cast<int*>(rows_g + 2 * a.rows_d);
+    int* const s_keep = CAP ? s_keep_l : reinterpret_cast<int*>(rows_g + 3 * a.rows_d);
     __shared__ double s_misc[4];
     __shared__ int s_tmp[kW];
     __shared__ unsigned int s_item;
@@ -1205,7 +1218,8 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
                             hipStream_t stream) {
     if (b.count == 0) return CF_OK;
     const int kmax = (int)b.kmax;
-    if (kmax > CF_SPILL_MAX_K) return cf_set_error(ctx, CF_ERANGE, "predict spill: k above CF_SPILL_MAX_K");
+    // k > CF_SPILL_MAX_K (no cap, as the reference): those users' predict workgroups keep their
+    // per-row arrays in HBM (the <T, 0, 1> kernel)
     SpArgs<T> a{};
     a.order = plan->d_order;
     a.kmax = kmax;
@@ -1245,10 +1259,14 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
     std::vector<Chunk> chunks;
     std::vector<uint64_t> meta;
     int blocks = 0;
-    size_t fa_bytes = 0, meta_bytes = 0, ws_bytes = 0;
+    size_t fa_bytes = 0, meta_bytes = 0, ws_bytes = 0, rows_bytes = 0;
+    a.rows_d = kmax > CF_SPILL_MAX_K ? ((size_t)kmax + 63) / 64 * 64 : 0;
+    // at least 32 regions (8 when one region is over 1 GB: k > ~16k)
+    const size_t min_blocks = a.fa_d * sizeof(double) > ((size_t)1 << 30) ? 8 : 32;
     for (;;) {
-        blocks = (int)std::max<size_t>(32, std::min<size_t>(512, kFaBudget / (a.fa_d * 8)));
+        blocks = (int)std::max<size_t>(min_blocks, std::min<size_t>(512, kFaBudget / (a.fa_d * 8)));
         fa_bytes = (size_t)blocks * a.fa_d * sizeof(double);
+        rows_bytes = (size_t)blocks * 4 * a.rows_d * sizeof(uint32_t);
         chunks.clear();
         meta.clear();
         size_t ws_max = 0, wsi_max = 0;
@@ -1279,7 +1297,7 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
         }
         meta_bytes = ((meta.size() * sizeof(uint64_t) + 255) / 256) * 256;
         ws_bytes = ws_max * sizeof(double);
-        const size_t need = 256 + meta_bytes + fa_bytes + ws_bytes + wsi_max * sizeof(int);
+        const size_t need = 256 + meta_bytes + fa_bytes + rows_bytes + ws_bytes + wsi_max * sizeof(int);
         if (need <= ctx->pspill_bytes) break;
         if (ctx->d_pspill) {
             CF_HIP_CHECK(ctx, hipStreamSynchronize(stream));   // earlier launches may still read it
@@ -1294,7 +1312,7 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
         (void)hipGetLastError();
         ctx->d_pspill = nullptr;
         // one user per chunk and the fewest regions is the smallest plan there is
-        if (blocks == 32 && std::all_of(chunks.begin(), chunks.end(), [](const Chunk& c) { return c.nu == 1; }))
+        if ((size_t)blocks == min_blocks && std::all_of(chunks.begin(), chunks.end(), [](const Chunk& c) { return c.nu == 1; }))
             return cf_set_error(ctx, CF_ENOMEM, "spill predictor workspace (" + std::to_string(need) + " bytes)");
         kSlotBudget /= 2;
         kFaBudget /= 2;
@@ -1303,8 +1321,9 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
     a.counter = reinterpret_cast<unsigned int*>(p);
     uint64_t* d_meta = reinterpret_cast<uint64_t*>(p + 256);
     a.fa = reinterpret_cast<double*>(p + 256 + meta_bytes);
-    a.ws = reinterpret_cast<double*>(p + 256 + meta_bytes + fa_bytes);
-    a.wsi = reinterpret_cast<int*>(p + 256 + meta_bytes + fa_bytes + ws_bytes);
+    a.rows = reinterpret_cast<uint32_t*>(p + 256 + meta_bytes + fa_bytes);
+    a.ws = reinterpret_cast<double*>(p + 256 + meta_bytes + fa_bytes + rows_bytes);
+    a.wsi = reinterpret_cast<int*>(p + 256 + meta_bytes + fa_bytes + rows_bytes + ws_bytes);
     // the tables go up in one asynchronous copy from the context's pinned staging buffer; the
     // previous call's copy out of it has completed before it is overwritten (its event)
     const size_t meta_n = meta.size() * sizeof(uint64_t);
@@ -1333,18 +1352,30 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
             const uint32_t u = plan->h_order[b.first + c.u0 + i];
             return plan->h_item_off[u + 1] - plan->h_item_off[u];
         };
-        uint32_t nb = 0;
+        uint32_t nh = 0, nb = 0;
+        while (nh < c.nu && k_of(nh) > (uint64_t)CF_SPILL_MAX_K) ++nh;
+        nb = nh;
         while (nb < c.nu && k_of(nb) > (uint64_t)kSmallCap) ++nb;
         CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, 256, stream));
         hipLaunchKernelGGL(spill_basis_kernel<T>, dim3(a.nu), dim3(kT), 0, stream, a);
         CF_HIP_CHECK(ctx, hipGetLastError());
+        const uint64_t hsplit = roff_h[nh];
+        if (hsplit > 0) {   // k > CF_SPILL_MAX_K: per-row arrays in HBM, one workgroup per CU
+            SpArgs<T> ah = a;
+            ah.counter = a.counter + 16;   // its own zeroed counter
+            ah.w0 = 0;
+            ah.w1 = (uint32_t)hsplit;
+            hipLaunchKernelGGL((spill_predict_kernel<T, 0, 1>), dim3((unsigned)std::min<uint64_t>(blocks, hsplit)),
+                               dim3(kT), 0, stream, ah);
+            CF_HIP_CHECK(ctx, hipGetLastError());
+        }
         const uint64_t split = roff_h[nb];
-        if (split > 0) {   // heaviest first, one workgroup per CU
+        if (split > hsplit) {   // heaviest first, one workgroup per CU
             SpArgs<T> ab = a;
-            ab.w0 = 0;
+            ab.w0 = (uint32_t)hsplit;
             ab.w1 = (uint32_t)split;
             hipLaunchKernelGGL((spill_predict_kernel<T, CF_SPILL_MAX_K, 1>),
-                               dim3((unsigned)std::min<uint64_t>(blocks, split)), dim3(kT), 0, stream, ab);
+                               dim3((unsigned)std::min<uint64_t>(blocks, split - hsplit)), dim3(kT), 0, stream, ab);
             CF_HIP_CHECK(ctx, hipGetLastError());
         }
         if (items > split) {

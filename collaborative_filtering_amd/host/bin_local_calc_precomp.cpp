@@ -66,8 +66,6 @@ int main(int argc, char** argv) {
     std::unordered_map<uint32_t, uint32_t> rec_of_user;
     for (uint32_t u = 0; u < n_users; ++u) {
         const uint64_t k = off[u + 1] - off[u];
-        if (k > CF_SPILL_MAX_K) cfcli::die("record with k > " + std::to_string(CF_SPILL_MAX_K) +
-                                           " is outside the supported buckets");
         rec_of_user[recs.user[u]] = u;   // a later record of the same user replaces it (:472)
         auto& ur = urat[recs.user[u]];
         const uint64_t nm = recs.eval_off[u + 1] - recs.eval_off[u];

@@ -47,9 +47,9 @@ extern "C" {
 #define CF_ESTATE (-5)  /* missing prerequisite (e.g. no item graph uploaded) */
 
 #define CF_MAX_K 192    /* largest per-user item count handled by the LDS eigen path */
-#define CF_SPILL_MAX_K 5000  /* largest k of the spill paths (fp64, HBM workspace): the eigen
-                                solver and the predictor (cf_predict_spill.hip); BASELINE config 5
-                                caps its power-law k at 5000 */
+#define CF_SPILL_MAX_K 5000  /* largest k of the spill paths' LDS layouts (fp64, HBM workspace);
+                                larger k (no cap, as the reference) takes their HUGE layouts, every
+                                k-long vector in HBM, bounded by HBM only (CF_ENOMEM) */
 
 typedef struct cf_ctx cf_ctx;
 typedef struct cf_plan cf_plan;

@@ -250,7 +250,7 @@ def pinv_prediction(U, ev, w_lim, Wu, rat, r, k):
     return min(max(pred, 1.0), 5.0), cond, "pinned"
 
 
-def well_conditioned_rows(run: FusedRun, u, want, max_try=160, seed=0):
+def well_conditioned_rows(run: FusedRun, u, want, max_try=160, seed=0, scan=None):
     """Up to `want` rows of user u that the oracle comparison can use: U_CS^T U_CS full rank
     (|S| <= |C|: no more kept columns than connected items) and cond <= 1e8, chosen deliberately
     -- candidates with the fewest kept columns first (the oracle's explicit inverse is O(|S|^3)
@@ -269,7 +269,9 @@ def well_conditioned_rows(run: FusedRun, u, want, max_try=160, seed=0):
     U = U_g.astype(np.float64)
     nkeep = np.zeros(k, np.int64)
     nconn = np.zeros(k, np.int64)
-    for r in range(k):   # the same C and S as gram_cond (local_calc_precomp.cpp:254-304)
+    # (scan: a random subset of the rows examined, for the largest users)
+    rows_scan = range(k) if scan is None or scan >= k else np.sort(np.random.default_rng(seed).choice(k, scan, replace=False))
+    for r in rows_scan:   # the same C and S as gram_cond (local_calc_precomp.cpp:254-304)
         C = np.nonzero(W[r] > 0.1)[0]
         nconn[r] = len(C)
         if len(C):
@@ -335,11 +337,11 @@ def lstsq_value_check(run: FusedRun, u, rows):
     return compared, bad
 
 
-def value_rows(run: FusedRun, u, want, seed=0):
+def value_rows(run: FusedRun, u, want, seed=0, scan=None):
     """`want` rows of user u for value comparisons: its well-conditioned rows first (the oracle
     comparison), then rows with c > 0 drawn at random (the rank-deficient ones are pinned to
     numpy's minimum-norm least-squares prediction by predict_check)."""
-    rows, n_cand = well_conditioned_rows(run, u, want, seed=seed)
+    rows, n_cand = well_conditioned_rows(run, u, want, seed=seed, scan=scan)
     b, k = int(run.off[u]), int(run.k[u])
     rest = np.setdiff1d(np.nonzero(run.kk[b:b + k] > 0)[0], rows)
     rng = np.random.default_rng(seed)
@@ -713,6 +715,48 @@ def test_c5_tail_k_up_to_5000(gpu_ctx, c4_graph):
         print(f"C5 k=3100: {compared} of {len(r3100)} rows equal to numpy's least-squares evaluation", flush=True)
         assert not badp, badp
         assert compared >= 10, compared
+    finally:
+        run.free()
+
+
+def test_uncapped_user_above_5000(gpu_ctx, c4_graph):
+    """A user with k = 5400 > CF_SPILL_MAX_K, as the reference takes any k
+    (precompute_local_threads.cpp:100-213 has no cap): the eigen path's HUGE layout on the
+    staged multi-CU solver, and the spill predictor with its per-row arrays in HBM.  Eigen
+    properties at full size, the eigenvalues against LAPACK's eigvalsh of the same fp64
+    sym_lower(L2), kk of every row exact, NaN iff c = 0, and prediction rows by value against
+    numpy's least-squares evaluation of the reference's formula."""
+    from collaborative_filtering_amd import synth, workloads as wlm
+
+    ks = np.array([5400], dtype=np.uint32)
+    off, items, rat = synth.user_items(wlm.CONFIGS["c5"]["seed"] + 13, ks, 50_000, threads=THREADS)
+    run = FusedRun(gpu_ctx, c4_graph[0], 50_000, off, items, rat)
+    try:
+        assert 2 <= run.m[0] <= ks[0]
+        bad = eigen_properties(run, [0])
+        assert not bad, bad
+        it, _, Wu, m, _, ev_g, _ = run.user(0)
+        W = Wu.astype(np.float64)
+        d = W.sum(axis=1)
+        d[d == 0] = 1.0
+        sq = np.sqrt(1.0 / d)
+        L2 = (sq[:, None] * (np.diag(d) - W)) * sq[None, :]
+        ev_ref = np.linalg.eigvalsh(orc.sym_lower(L2))
+        kv = min(m, len(it))
+        err = float(np.max(np.abs(ev_g[:kv].astype(np.float64) - ev_ref[:kv])))
+        print(f"k = {len(it)}: m = {m}, {kv} eigenvalues vs LAPACK eigvalsh, max err {err:.3g}", flush=True)
+        assert err <= 1e-4, err
+        kk = run.kk[:len(it)].astype(np.int64)
+        c = (W > 0.1).sum(axis=1)
+        assert np.array_equal(kk, c), int(np.sum(kk != c))
+        assert np.array_equal(np.isnan(run.mse[:len(it)]), kk == 0)
+        ok = ~np.isnan(run.mse[:len(it)])
+        assert np.all((run.pred[:len(it)][ok] >= 1.0) & (run.pred[:len(it)][ok] <= 5.0))
+        rows = value_rows(run, 0, 3, seed=13, scan=400)
+        compared, badp = lstsq_value_check(run, 0, rows)
+        print(f"k = {len(it)}: {compared} of {len(rows)} rows equal to numpy's least-squares evaluation", flush=True)
+        assert not badp, badp
+        assert compared >= 2, compared
     finally:
         run.free()
 
