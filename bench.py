@@ -1102,6 +1102,9 @@ def c5_leg(args, ctx, dev, torch, W):
         del off, items, ratings
         k = synth.degrees(seed + 1, n1, k_median=100.0, sigma=sigma, kmin=20, kmax=min(args.c5_kmax, CF_SPILL_MAX_K))
         off, items, _ = synth.user_items(seed + 1, k, n_items, threads=16)
+    # the predictor legs' spill workspace would shrink the eigen call's (both sized from free HBM);
+    # a drop-in precompute_local process has neither
+    ctx.release_workspaces()
     print(f"[c5] all: one eigen call over {len(k)} users ({int(np.sum(k > CF_MAX_K))} spill, "
           f"{int(np.sum(k > 3072))} with k > 3072)", file=sys.stderr, flush=True)
     eo, ne = evec_offsets(off)

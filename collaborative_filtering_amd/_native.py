@@ -32,6 +32,7 @@ SIGNATURES = {
     "cf_device_count": (c_int, []),
     "cf_create": (c_int, [c_int, POINTER(c_void_p)]),
     "cf_destroy": (None, [c_void_p]),
+    "cf_release_workspaces": (c_int, [c_void_p]),
     "cf_last_error": (c_char_p, [c_void_p]),
     "cf_set_jacobi": (c_int, [c_void_p, c_float, c_int]),
     "cf_set_eigen_refine": (c_int, [c_void_p, c_int, c_float, c_float]),

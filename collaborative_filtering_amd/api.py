@@ -69,6 +69,11 @@ class Context:
             self.lib.cf_destroy(self.h)
             self.h = None
 
+    def release_workspaces(self):
+        """cf_release_workspaces: free the cached HBM workspaces (the spill paths size theirs
+        from free HBM, so one stage's leftover shrinks the next stage's)."""
+        self._chk(self.lib.cf_release_workspaces(self.h), "cf_release_workspaces")
+
     def __enter__(self):
         return self
 

@@ -90,6 +90,23 @@ int cf_create(int device, cf_ctx** out) {
     return CF_OK;
 }
 
+int cf_release_workspaces(cf_ctx* ctx) {
+    if (!ctx) return CF_EINVAL;
+    CF_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    CF_HIP_CHECK(ctx, hipDeviceSynchronize());   // every stream of the context is done with them
+    const auto drop = [](void*& p, size_t& bytes) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    };
+    drop(ctx->d_spill, ctx->spill_bytes);
+    drop(ctx->d_pspill, ctx->pspill_bytes);
+    drop(ctx->d_tri, ctx->tri_bytes);
+    drop(ctx->d_scratch, ctx->scratch_bytes);
+    drop(ctx->d_knn, ctx->knn_bytes);
+    return CF_OK;
+}
+
 void cf_destroy(cf_ctx* ctx) {
     if (!ctx) return;
     g_ctx_per_device[ctx->device].fetch_sub(1);

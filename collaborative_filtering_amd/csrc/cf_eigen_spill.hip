@@ -32,6 +32,8 @@
 // ~ (#rotations) x 6k flops over one Z pass per 16 iterations, back-transform 2k^3; see
 // DESIGN.md 3.6.
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -1839,7 +1841,11 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     // for their own k for the whole launch, as many per wave as the side region holds: one wave
     // lets every QL generator run at once (r04: 9 waves of 56 400-MB slots for C5's 10k users).
     // A failed allocation halves the cap (more waves / fewer slots) down to one slot per range.
-    uint64_t budget = cf_hbm_budget(ctx, ctx->spill_bytes, 0.5, 24ull << 30);
+    static const double budget_frac = [] {   // (A/B: CF_SPILL_BUDGET)
+        const char* e = getenv("CF_SPILL_BUDGET");
+        return e ? atof(e) : 0.5;
+    }();
+    uint64_t budget = cf_hbm_budget(ctx, ctx->spill_bytes, budget_frac, 24ull << 30);
     const bool has_side = !rs.empty() && rs.front().kind != kRest;
     const bool has_rest = !rs.empty() && rs.back().kind == kRest;
     std::vector<uint32_t> grid(rs.size());
@@ -1916,6 +1922,11 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
                 cur += sz;
             }
             waves[i].push_back(rs[i].count);
+            if (getenv("CF_SPILL_VERBOSE"))
+                fprintf(stderr, "[spill] range %zu: %u users k %u..%u, %zu waves in a %.1f GB side region\n", i,
+                        rs[i].count, (unsigned)(plan->h_item_off[plan->h_order[rs[i].first + rs[i].count - 1] + 1] -
+                                                plan->h_item_off[plan->h_order[rs[i].first + rs[i].count - 1]]),
+                        (unsigned)rs[i].kmax, waves[i].size() - 1, side_bytes / 1e9);
         }
     if (!offs.empty()) {
         const size_t bytes = offs.size() * sizeof(uint64_t);

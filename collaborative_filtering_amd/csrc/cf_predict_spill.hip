@@ -82,7 +82,7 @@ struct SpArgs {
     unsigned int* counter;   // work-item counter of the predict kernel
     uint32_t w0, w1;         // predict launch: the chunk's work items [w0, w1)
     unsigned long long* phase;   // diagnostics (cf_debug_phases) or null: see spill_predict_kernel
-    // users with k > CF_SPILL_MAX_K (the <T, 0, 1> predict kernel): per workgroup, the per-row
+    // users with k > kSmallCap (the <T, 0, 2> predict kernel): per workgroup, the per-row
     // arrays (ratings, C, Cbar, kept columns) in HBM, 4 x rows_d words each
     uint32_t* rows;
     size_t rows_d;
@@ -649,15 +649,15 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
 }
 
 // ---- per-rating predictions --------------------------------------------------------------
-// CAP: the largest k the per-row LDS arrays hold; OCC: workgroups per CU.  Users with
-// k <= kSmallCap take <kSmallCap, 2> (81 KB of LDS, 256 registers: two ratings per CU overlap
-// their latency-bound phases), larger ones <CF_SPILL_MAX_K, 1> (116 KB, one per CU).
+// CAP: the largest k the per-row LDS arrays hold (0: the arrays in the workgroup's HBM rows);
+// OCC: workgroups per CU.  Users with k <= kSmallCap take <kSmallCap, 2> (81 KB of LDS, 256
+// registers: two ratings per CU overlap their latency-bound phases; one GEMM staging buffer),
+// larger ones <0, 2> (per-row arrays in HBM, any k; 57 KB of LDS with two staging buffers).
+// The r04 <5000, 1> instantiation (every array in LDS, 116 KB, one per CU) measured 3% slower
+// on the C5 sample's k > 2816 users than <0, 2>, bit-identical (profiles/r05/big2_r1.log).
 constexpr int kSmallCap = 2816;
 template <typename T, int CAP, int OCC>
 __global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
-    // GEMM staging: two buffers for the one-per-CU instantiation, one where two workgroups
-    // must share a CU (the <kSmallCap, 2> LDS budget)
-    // CAP = 0: users with k > CF_SPILL_MAX_K, the per-row arrays in the workgroup's HBM rows
     constexpr int kNbuf = (CAP == 0 || CAP > kSmallCap) ? 2 : 1;
     __shared__ double sA[kNbuf * 16 * kSt], sB[kNbuf * 16 * kSt];
     __shared__ double s_la[kLdsA];
@@ -1250,7 +1250,8 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
     // still fails (another process or context took the memory meanwhile) both budgets halve
     // and the chunks are planned again.
     size_t kSlotBudget = cf_hbm_budget(ctx, ctx->pspill_bytes, 1.0 / 3.0, (size_t)8 << 30);
-    size_t kFaBudget = cf_hbm_budget(ctx, ctx->pspill_bytes, 0.1, (size_t)4 << 30);
+    // (k > kSmallCap: a fifth, so that the two-per-CU kernel gets ~2 regions per CU at k = 5000)
+    size_t kFaBudget = cf_hbm_budget(ctx, ctx->pspill_bytes, kmax > (uint64_t)kSmallCap ? 0.2 : 0.1, (size_t)4 << 30);
     // chunks over the bucket's users (plan order: largest k first), each within the budget
     struct Chunk {
         uint32_t u0, nu;
@@ -1260,7 +1261,7 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
     std::vector<uint64_t> meta;
     int blocks = 0;
     size_t fa_bytes = 0, meta_bytes = 0, ws_bytes = 0, rows_bytes = 0;
-    a.rows_d = kmax > CF_SPILL_MAX_K ? ((size_t)kmax + 63) / 64 * 64 : 0;
+    a.rows_d = kmax > (uint64_t)kSmallCap ? ((size_t)kmax + 63) / 64 * 64 : 0;
     // at least 32 regions (8 when one region is over 1 GB: k > ~16k)
     const size_t min_blocks = a.fa_d * sizeof(double) > ((size_t)1 << 30) ? 8 : 32;
     for (;;) {
@@ -1352,30 +1353,18 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
             const uint32_t u = plan->h_order[b.first + c.u0 + i];
             return plan->h_item_off[u + 1] - plan->h_item_off[u];
         };
-        uint32_t nh = 0, nb = 0;
-        while (nh < c.nu && k_of(nh) > (uint64_t)CF_SPILL_MAX_K) ++nh;
-        nb = nh;
+        uint32_t nb = 0;
         while (nb < c.nu && k_of(nb) > (uint64_t)kSmallCap) ++nb;
         CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, 256, stream));
         hipLaunchKernelGGL(spill_basis_kernel<T>, dim3(a.nu), dim3(kT), 0, stream, a);
         CF_HIP_CHECK(ctx, hipGetLastError());
-        const uint64_t hsplit = roff_h[nh];
-        if (hsplit > 0) {   // k > CF_SPILL_MAX_K: per-row arrays in HBM, one workgroup per CU
-            SpArgs<T> ah = a;
-            ah.counter = a.counter + 16;   // its own zeroed counter
-            ah.w0 = 0;
-            ah.w1 = (uint32_t)hsplit;
-            hipLaunchKernelGGL((spill_predict_kernel<T, 0, 1>), dim3((unsigned)std::min<uint64_t>(blocks, hsplit)),
-                               dim3(kT), 0, stream, ah);
-            CF_HIP_CHECK(ctx, hipGetLastError());
-        }
         const uint64_t split = roff_h[nb];
-        if (split > hsplit) {   // heaviest first, one workgroup per CU
+        if (split > 0) {   // k > kSmallCap: per-row arrays in HBM, two workgroups per CU, heaviest first
             SpArgs<T> ab = a;
-            ab.w0 = (uint32_t)hsplit;
+            ab.w0 = 0;
             ab.w1 = (uint32_t)split;
-            hipLaunchKernelGGL((spill_predict_kernel<T, CF_SPILL_MAX_K, 1>),
-                               dim3((unsigned)std::min<uint64_t>(blocks, split - hsplit)), dim3(kT), 0, stream, ab);
+            hipLaunchKernelGGL((spill_predict_kernel<T, 0, 2>), dim3((unsigned)std::min<uint64_t>(blocks, split)),
+                               dim3(kT), 0, stream, ab);
             CF_HIP_CHECK(ctx, hipGetLastError());
         }
         if (items > split) {

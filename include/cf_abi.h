@@ -60,6 +60,13 @@ int cf_version(void);
 int cf_device_count(void);
 int cf_create(int device, cf_ctx** out);
 void cf_destroy(cf_ctx* ctx);
+/* Waits for the context's device, then frees its cached HBM workspaces (eigen and predictor
+ * spill paths, the tridiagonal path, the predictor scratch, the knn2 planes); each is
+ * allocated again, at the size its next call plans, when that call runs.  The spill paths
+ * size their workspaces from the device's free HBM, so a workspace the predictor left behind
+ * shrinks the next eigen call's and costs it waves: call this between stages of a long-lived
+ * context (bench.py's config-5 legs).  No reference counterpart (one call per process there). */
+int cf_release_workspaces(cf_ctx* ctx);
 const char* cf_last_error(const cf_ctx* ctx);
 /* Eigensolver of the k <= CF_MAX_K users: CF_EIGEN_JACOBI (default; one-sided Jacobi in
  * LDS, cf_eigen.hip) or CF_EIGEN_TRIDIAG (Householder + batched QL, cf_eigen_tri.hip). */

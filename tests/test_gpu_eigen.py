@@ -130,6 +130,22 @@ def test_eigen_spill_path_mixed(gpu_ctx):
     _check_batch(gpu_ctx, W, off, items, "spill")
 
 
+def test_release_workspaces_then_rerun_bit_identical(gpu_ctx):
+    """cf_release_workspaces frees the cached spill workspace between two eigen calls; the
+    second call allocates it again and its blocks equal the first call's bit for bit."""
+    W = cases.item_graph(900, 0.5, seed=45)
+    off, items = cases.user_items(900, [700, 150, 400], seed=46)
+    gpu_ctx.upload_graph_dense(W)
+    a = gpu_ctx.eigen_batch(off, items)
+    gpu_ctx.release_workspaces()
+    gpu_ctx.release_workspaces()   # idempotent
+    b = gpu_ctx.eigen_batch(off, items)
+    assert np.array_equal(a.m, b.m)
+    for u in range(3):
+        for x, y in zip(a.block(u), b.block(u)):
+            assert np.array_equal(x, y), u
+
+
 def test_eigen_spill_path_sparse(gpu_ctx):
     """Spill users on a sparse graph: lambda = 0 per component, lambda = 1 per isolated item."""
     W = cases.item_graph(900, 0.01, seed=43, isolated_frac=0.2)
