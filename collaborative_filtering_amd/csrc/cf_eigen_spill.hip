@@ -1836,14 +1836,16 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
         const uint64_t extra = r.kind == kHuge ? lo.extra_huge : r.kind == kBig ? (mc_on ? lo.extra_big : 3ull * lo.vs) : 0ull;
         return base_stride(r.kmax) + extra;
     };
-    // workspace cap: half of this context's share of the free HBM (>= 24 GB, but at most half
-    // the share: cf_hbm_budget); the side ranges get 60 % of it.  Staged users hold a slot sized
-    // for their own k for the whole launch, as many per wave as the side region holds: one wave
-    // lets every QL generator run at once (r04: 9 waves of 56 400-MB slots for C5's 10k users).
-    // A failed allocation halves the cap (more waves / fewer slots) down to one slot per range.
+    // workspace cap: three quarters of this context's share of the free HBM (>= 24 GB, but at
+    // most half the share: cf_hbm_budget); the side ranges get 60 % of it.  Staged users hold a
+    // slot sized for their own k for the whole launch, as many per wave as the side region
+    // holds: one wave lets every QL generator run at once (r04: 9 waves of 56 400-MB slots for
+    // C5's 10k users; r05 per-user slots: 2 waves at a half (72 GB), 1 at three quarters (96 GB),
+    // 27.7 -> 24.7 s, profiles/r05/budget_*_u1.log).  A failed allocation halves the cap (more
+    // waves / fewer slots) down to one slot per range.
     static const double budget_frac = [] {   // (A/B: CF_SPILL_BUDGET)
         const char* e = getenv("CF_SPILL_BUDGET");
-        return e ? atof(e) : 0.5;
+        return e ? atof(e) : 0.75;
     }();
     uint64_t budget = cf_hbm_budget(ctx, ctx->spill_bytes, budget_frac, 24ull << 30);
     const bool has_side = !rs.empty() && rs.front().kind != kRest;

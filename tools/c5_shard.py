@@ -55,18 +55,20 @@ for r in [int(x) for x in sys.argv[1:]] or [0]:
     d_mse = torch.zeros(n, dtype=torch.float32, device=dev)
     d_kk = torch.zeros(n, dtype=torch.int32, device=dev)
     plan = ctx.plan(off)
-    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     t = time.perf_counter()
     e[0].record(stream)
     plan.eigen_run(d_o, d_i, d_e, d_m, d_s, d_v, d_x, stream=stream.cuda_stream)
     e[1].record(stream)
     e[1].synchronize()
     print(f"shard {r}: eigen {e[0].elapsed_time(e[1]) / 1e3:.1f} s", flush=True)
+    ctx.release_workspaces()   # the eigen workspace would shrink the predictor's (both sized from free HBM)
+    e[3].record(stream)
     plan.predict_run(d_o, d_i, T(rat), d_m, d_v, d_e, d_x, d_s, CF_SIGS_OWN, d_mse, d_kk, stream=stream.cuda_stream)
     e[2].record(stream)
     e[2].synchronize()
     wall = time.perf_counter() - t
-    eig, pred = e[0].elapsed_time(e[1]) / 1e3, e[1].elapsed_time(e[2]) / 1e3
+    eig, pred = e[0].elapsed_time(e[1]) / 1e3, e[3].elapsed_time(e[2]) / 1e3
     mse = d_mse.cpu().numpy()
     kk = d_kk.cpu().numpy()
     print(json.dumps({"shard": r, "of": WORLD, "users": int(len(k)), "ratings": n,
