@@ -74,7 +74,7 @@ struct SpArgs {
     double* pred;
     double* ws;              // per slot: Q0, Q1 (Q and P = Q Q^T), Gbar, Gt (k^2 each), g, h, PG, PH
     const uint64_t* soff;    // per slot s of the chunk (nu + 1): doubles offset of its slot in ws
-    int* wsi;                // per slot: lim[k], cpos[k], hdr[4] = {Lu, basis, qsel, -}
+    int* wsi;                // per slot: lim[k], cpos[k], hdr[8] = {Lu, basis, qsel, G-mode, spill_basis_mc state}
     const uint64_t* sioff;   // per slot (nu + 1): ints offset of its slot in wsi
     const uint64_t* roff;    // per slot (nu + 1): first work item (= row) of the slot; roff[nu] items
     double* fa;              // per workgroup factorisation region
@@ -86,6 +86,8 @@ struct SpArgs {
     // arrays (ratings, C, Cbar, kept columns) in HBM, 4 x rows_d words each
     uint32_t* rows;
     size_t rows_d;
+    uint32_t s0;   // spill_basis_kernel: its first slot (the slots before it take spill_basis_mc)
+    int G;         // spill_basis_mc: workgroups per user
 };
 
 __device__ __forceinline__ double wsum(double v) {
@@ -95,7 +97,7 @@ __device__ __forceinline__ double wsum(double v) {
 }
 
 // out(i, j, C(i, j)) over the 64 x 64 output tiles (i0, j0) of an M x N product with
-// want(i0, j0), depth kend(j0) (triangular operands end early).  Operands are staged in
+// want(i0, j0), depth kend(j0) (triangular operands end early); tiles t0, t0 + ts, ... only.  Operands are staged in
 // LDS 16 deep (row stride kSt == 16 mod 32: the four 16-lane groups of a fragment read
 // hit disjoint banks) with the next chunk's loads in flight while the current one is
 // consumed; unconditional loads from clamped indices (a guarded load would become a
@@ -115,12 +117,13 @@ constexpr int kSt = 80;
 // their MFMAs (the callers keep j <= i only); tiles past M / N always do.
 template <bool A_LFAST, bool B_LFAST, int NBUF = 1, bool LOWER = false, class FA, class FB, class FK, class FW,
           class FO>
-__device__ void tile_gemm(int M, int N, FA ldA, FB ldB, FK kend, FW want, FO out, double* sA, double* sB) {
+__device__ void tile_gemm(int M, int N, FA ldA, FB ldB, FK kend, FW want, FO out, double* sA, double* sB, int t0 = 0,
+                          int ts = 1) {
     static_assert(NBUF == 1 || NBUF == 2, "one or two staging buffers");
     const int tid = threadIdx.x, lane = tid & 63;
     const int wr = (tid >> 6) >> 1, wc = (tid >> 6) & 1;
     const int ti = (M + 63) >> 6, tj = (N + 63) >> 6;
-    for (int t = 0; t < ti * tj; ++t) {
+    for (int t = t0; t < ti * tj; t += ts) {   // tiles t0, t0 + ts, ... (spill_basis_mc: one workgroup's share)
         const int i0 = (t / tj) << 6, j0 = (t % tj) << 6;
         if (!want(i0, j0)) continue;
         const int K = kend(j0);
@@ -403,6 +406,22 @@ __device__ void ldlt_bordered_wide(double* A, int L, int nrows, double* sA, doub
 }
 
 // ---- per-user tables ---------------------------------------------------------------------
+// the complement basis's +-1 test matrix Omega(i, j): a hash of the user's content (k and three
+// item ids), i and j
+__device__ __forceinline__ uint32_t omega_mix(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    h ^= h >> 15;
+    h *= 0x846CA68Bu;
+    return h ^ (h >> 16);
+}
+__device__ __forceinline__ uint32_t omega_seed(const uint32_t* it, int k) {
+    return omega_mix(omega_mix(omega_mix((uint32_t)k * 0x9E3779B1u + 0x7F4A7C15u) ^ it[0]) ^ it[k >> 1]) ^ it[k - 1];
+}
+__device__ __forceinline__ double omega_pm1(uint32_t seed, int i, int j) {
+    return (omega_mix(seed ^ ((uint32_t)i * 0x85EBCA6Bu) ^ ((uint32_t)j * 0xC2B2AE35u)) & 1u) ? 1.0 : -1.0;
+}
+
 template <typename T>
 __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
     __shared__ double sA[2 * 16 * kSt], sB[2 * 16 * kSt];   // tile_gemm<.., 2>: two staging buffers
@@ -410,7 +429,7 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
     __shared__ int s_hdr[4];
     __shared__ float s_dev[kW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t s = blockIdx.x;
+    const uint32_t s = a.s0 + blockIdx.x;
     const uint32_t u = a.order[a.first + s];
     const uint64_t base = a.item_off[u];
     const int k = (int)(a.item_off[u + 1] - base);
@@ -552,24 +571,8 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
         double* YY = QO + (size_t)Lu * du;
         __shared__ int s_fail;
         // Omega(i, j) = +-1 from a hash of the user's content (k and three item ids), i and j
-        const auto mix = [](uint32_t h) {
-            h ^= h >> 16;
-            h *= 0x7FEB352Du;
-            h ^= h >> 15;
-            h *= 0x846CA68Bu;
-            return h ^ (h >> 16);
-        };
-        const uint32_t seed = mix(mix(mix((uint32_t)k * 0x9E3779B1u + 0x7F4A7C15u) ^ a.items[base]) ^
-                                  a.items[base + (k >> 1)]) ^ a.items[base + k - 1];
-        const auto omega = [seed](int i, int j) -> double {
-            uint32_t h = seed ^ ((uint32_t)i * 0x85EBCA6Bu) ^ ((uint32_t)j * 0xC2B2AE35u);
-            h ^= h >> 16;
-            h *= 0x7FEB352Du;
-            h ^= h >> 15;
-            h *= 0x846CA68Bu;
-            h ^= h >> 16;
-            return (h & 1u) ? 1.0 : -1.0;
-        };
+        const uint32_t seed = omega_seed(a.items + base, k);
+        const auto omega = [seed](int i, int j) -> double { return omega_pm1(seed, i, j); };
         tile_gemm<false, false, 2>(
             Lu, du, [=](int i, int l) { return Q[(size_t)l * Lu + i]; }, [=](int l, int j) { return omega(l, j); },
             [=](int) { return k; }, [](int, int) { return true; },
@@ -645,6 +648,244 @@ __global__ __launch_bounds__(kT) void spill_basis_kernel(SpArgs<T> a) {
         hdr[1] = basis;
         hdr[2] = cur;
         hdr[3] = gm;   // complement basis W ready: G-mode for c < lim
+    }
+}
+
+// Multi-workgroup form of spill_basis_kernel for the largest users (k > kSmallCap): one
+// workgroup per user left most of the chip idle on the C5 sample's 19 users with k > 2816
+// (the basis kernel was 8.0 of the 10.1 s of their prediction, profiles/r05/
+// pbig_kernel_stats_x2.csv).  One launch per phase, a.G workgroups per user: the output tiles of
+// every tile product go to workgroup t % G, the rows / columns of the vector phases likewise.
+// Every value comes from the same code as in the one-workgroup kernel (the same tile, the same
+// sequential dot product, the same one-workgroup LDL^T), so the tables are bit-identical.
+// Cross-workgroup state, in the slot header: hdr[0] Lu (atomicMax), [1] basis, [2] current Q,
+// [3] G-mode ready, [4] the step's max |Gram - I| (float bits, atomicMax), [5] stepping done,
+// [6] a Cholesky-QR pivot failure (atomicOr).
+enum : int { kBmInit, kBmLim, kBmCopy, kBmGram, kBmApply, kBmStep, kBmGh, kBmP, kBmQO, kBmW, kBmYY, kBmLdl, kBmFs, kBmGw };
+template <typename T>
+__global__ __launch_bounds__(kT) void spill_basis_mc(SpArgs<T> a, int phase, int step) {
+    __shared__ double sA[2 * 16 * kSt], sB[2 * 16 * kSt];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int G = a.G;
+    const uint32_t s = blockIdx.x / G;
+    const int g = (int)(blockIdx.x % G);
+    const uint32_t u = a.order[a.first + s];
+    const uint64_t base = a.item_off[u];
+    const int k = (int)(a.item_off[u + 1] - base);
+    const int m = a.m[u];
+    const T* U = a.evecs + a.evec_off[u];
+    const size_t kk2 = (size_t)k * k;
+    double* slot = a.ws + a.soff[s];
+    double* Qb[2] = {slot, slot + kk2};
+    double* Gb = slot + 2 * kk2;
+    double* Gt = slot + 3 * kk2;
+    double* gh = slot + 4 * kk2;
+    int* lim = a.wsi + a.sioff[s];
+    int* cpos = lim + k;
+    int* hdr = cpos + k;
+    const int gt = g * kT + tid, gs = G * kT;   // rows / columns gt, gt + gs, ... are this thread's
+    if (phase == kBmInit) {
+        if (g == 0 && tid < 8) hdr[tid] = tid == 0 ? 2 : (tid == 1 ? 1 : 0);
+        return;
+    }
+    if (phase == kBmLim) {   // lim = first eigenvalue index above w_lim, clamped to [2, m] (:271-282)
+        for (int i = gt; i < k; i += gs) {
+            const double w_lim = (double)a.sigtab[a.sig_mode == CF_SIGS_COMPAT ? (uint64_t)i : base + i];
+            int l = m;
+            for (int j = 0; j < m; ++j)
+                if ((double)a.evals[base + j] > w_lim) {
+                    l = j;
+                    break;
+                }
+            l = min(max(l, 2), m);
+            lim[i] = l;
+            atomicMax(&hdr[0], l);
+        }
+        return;
+    }
+    const int Lu = hdr[0];
+    if (phase == kBmCopy) {   // rows with U(i, j) >= 1e-4 per column j < Lu; Q0 = U(:, 0:Lu) in fp64
+        for (int j = gt; j < Lu; j += gs) {
+            int cnt = 0;
+            for (int i = 0; i < k; ++i) {
+                const double v = (double)U[(size_t)i * m + j];
+                cnt += v >= 0.0001;
+                Qb[0][(size_t)i * Lu + j] = v;
+            }
+            cpos[j] = cnt;
+        }
+        return;
+    }
+    if (phase == kBmStep) {   // the step's outcome (grid: one workgroup per user)
+        if (tid != 0 || hdr[5] || !hdr[1]) return;
+        const float dev = __int_as_float(hdr[4]);
+        if (step == 0 && !(dev <= kOrthoMax)) {   // U far from orthonormal: dense path only
+            hdr[1] = 0;
+            hdr[5] = 1;
+            return;
+        }
+        hdr[2] ^= 1;
+        if (dev <= kOrthoDone) hdr[5] = 1;
+        hdr[4] = 0;
+        return;
+    }
+    if (phase == kBmGram || phase == kBmApply) {
+        if (hdr[5] || !hdr[1]) return;
+        const double* Q = Qb[hdr[2]];
+        double* Gm = step == 0 ? Gb : Gt;
+        if (phase == kBmGram) {
+            float dev = 0.0f;
+            tile_gemm<false, false, 2>(
+                Lu, Lu, [=](int i, int l) { return Q[(size_t)l * Lu + i]; },
+                [=](int l, int j) { return Q[(size_t)l * Lu + j]; }, [=](int) { return k; },
+                [](int, int) { return true; },
+                [&](int i, int j, double v) {
+                    Gm[(size_t)i * Lu + j] = v;
+                    dev = fmaxf(dev, (float)fabs(v - (i == j ? 1.0 : 0.0)));
+                },
+                sA, sB, g, G);
+            for (int off = 32; off >= 1; off >>= 1) dev = fmaxf(dev, __shfl_xor(dev, off));
+            if (lane == 0) atomicMax(&hdr[4], __float_as_int(dev));   // dev >= 0: int order = float order
+            return;
+        }
+        if (step == 0 && !(__int_as_float(hdr[4]) <= kOrthoMax)) return;
+        const double* Gr = Gm;
+        double* Qn = Qb[hdr[2] ^ 1];
+        tile_gemm<true, false, 2>(
+            k, Lu, [=](int i, int l) { return Q[(size_t)i * Lu + l]; },
+            [=](int l, int j) {
+                const double gv = Gr[(size_t)l * Lu + j];
+                return l < j ? -gv : (l == j ? 1.5 - 0.5 * gv : 0.0);
+            },
+            [=](int j0) { return min(Lu, j0 + 64); }, [](int, int) { return true; },
+            [=](int i, int j, double v) { Qn[(size_t)i * Lu + j] = v; }, sA, sB, g, G);
+        return;
+    }
+    if (!hdr[1]) return;   // no basis: no tables, no complement
+    const int cur = hdr[2];
+    const double* Q = Qb[cur];
+    if (phase == kBmGh) {   // g = Q^T r, h = Q^T 1
+        for (int j = gt; j < Lu; j += gs) {
+            double gg = 0.0, h = 0.0;
+            for (int i = 0; i < k; ++i) {
+                const double q = Q[(size_t)i * Lu + j];
+                gg = fma(q, (double)a.ratings[base + i], gg);
+                h += q;
+            }
+            gh[j] = gg;
+            gh[Lu + j] = h;
+        }
+        return;
+    }
+    if (phase == kBmP) {   // P = Q Q^T over [0, Lu) (k x k) into the spare Q buffer; PG = Q g, PH = Q h
+        double* P = Qb[cur ^ 1];
+        tile_gemm<true, true, 2, true>(
+            k, k, [=](int i, int l) { return Q[(size_t)i * Lu + l]; },
+            [=](int l, int j) { return Q[(size_t)j * Lu + l]; }, [=](int) { return Lu; },
+            [](int i0, int j0) { return j0 <= i0; },
+            [=](int i, int j, double v) {
+                if (j <= i) {
+                    P[(size_t)i * k + j] = v;
+                    P[(size_t)j * k + i] = v;
+                }
+            },
+            sA, sB, g, G);
+        double* pg = gh + 2 * Lu;
+        for (int i = g * kW + wave; i < k; i += G * kW) {
+            const double* qi = Q + (size_t)i * Lu;
+            double x = 0.0, y = 0.0;
+            for (int j = lane; j < Lu; j += 64) {
+                x = fma(qi[j], gh[j], x);
+                y = fma(qi[j], gh[Lu + j], y);
+            }
+            x = wsum(x);
+            y = wsum(y);
+            if (lane == 0) {
+                pg[i] = x;
+                pg[k + i] = y;
+            }
+        }
+        return;
+    }
+    // complement basis W (spill_basis_kernel's regions and arithmetic)
+    const int du = k - Lu;
+    if (du <= 0) return;
+    double* Wm = Gt;
+    double* QO = Gb + (size_t)Lu * Lu;
+    double* YY = QO + (size_t)Lu * du;
+    const uint32_t seed = omega_seed(a.items + base, k);
+    const auto omega = [seed](int i, int j) -> double { return omega_pm1(seed, i, j); };
+    if (phase == kBmQO) {
+        tile_gemm<false, false, 2>(
+            Lu, du, [=](int i, int l) { return Q[(size_t)l * Lu + i]; }, [=](int l, int j) { return omega(l, j); },
+            [=](int) { return k; }, [](int, int) { return true; },
+            [=](int i, int j, double v) { QO[(size_t)i * du + j] = v; }, sA, sB, g, G);
+    } else if (phase == kBmW) {
+        tile_gemm<true, false, 2>(
+            k, du, [=](int i, int l) { return Q[(size_t)i * Lu + l]; }, [=](int l, int j) { return QO[(size_t)l * du + j]; },
+            [=](int) { return Lu; }, [](int, int) { return true; },
+            [=](int i, int j, double v) { Wm[(size_t)i * du + j] = omega(i, j) - v; }, sA, sB, g, G);
+    } else if (phase == kBmYY) {
+        tile_gemm<false, false, 2, true>(
+            du, du, [=](int i, int l) { return Wm[(size_t)l * du + i]; }, [=](int l, int j) { return Wm[(size_t)l * du + j]; },
+            [=](int) { return k; }, [](int i0, int j0) { return j0 <= i0; },
+            [=](int i, int j, double v) {
+                if (j <= i) YY[tri(i, j)] = v;
+            },
+            sA, sB, g, G);
+    } else if (phase == kBmLdl) {
+        if (g == 0) ldlt_bordered_wide(YY, du, du, sA, sB);
+    } else if (phase == kBmFs) {   // forward substitution in 16-column register panels, then the scaling
+        double dmax = 0.0;
+        for (int j = 0; j < du; ++j) dmax = fmax(dmax, YY[tri(j, j)]);
+        bool fail = false;
+        for (int i = gt; i < k; i += gs) {
+            double* xi = Wm + (size_t)i * du;
+            for (int p0 = 0; p0 < du; p0 += 16) {
+                const int bw = min(16, du - p0);
+                double acc[16];
+                int rb[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    acc[q] = q < bw ? xi[p0 + q] : 0.0;
+                    rb[q] = tri(p0 + min(q, bw - 1), 0);
+                }
+                for (int t = 0; t < p0; ++t) {
+                    const double xt = xi[t];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) acc[q] = fma(-YY[rb[q] + t], xt, acc[q]);
+                }
+#pragma unroll
+                for (int q = 1; q < 16; ++q)
+#pragma unroll
+                    for (int t = 0; t < q; ++t) acc[q] = fma(-YY[rb[q] + p0 + t], acc[t], acc[q]);
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    if (q < bw) xi[p0 + q] = acc[q];
+            }
+            for (int j = 0; j < du; ++j) {
+                const double dj = YY[tri(j, j)];
+                fail |= !(dj > 1e-12 * dmax);
+                xi[j] = dj > 0.0 ? xi[j] / sqrt(dj) : 0.0;
+            }
+        }
+        if (fail) atomicOr(&hdr[6], 1);
+    } else if (phase == kBmGw) {   // W^T r, W^T 1 when the Cholesky-QR had no failed pivot
+        const int gm = hdr[6] == 0;
+        if (gm) {
+            double* gw = gh + 2 * (size_t)Lu + 2 * (size_t)k;
+            for (int j = gt; j < du; j += gs) {
+                double gg = 0.0, h = 0.0;
+                for (int i = 0; i < k; ++i) {
+                    const double w = Wm[(size_t)i * du + j];
+                    gg = fma(w, (double)a.ratings[base + i], gg);
+                    h += w;
+                }
+                gw[j] = gg;
+                gw[du + j] = h;
+            }
+        }
+        if (g == 0 && tid == 0) hdr[3] = gm;
     }
 }
 
@@ -1250,6 +1491,13 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
     // still fails (another process or context took the memory meanwhile) both budgets halve
     // and the chunks are planned again.
     size_t kSlotBudget = cf_hbm_budget(ctx, ctx->pspill_bytes, 1.0 / 3.0, (size_t)8 << 30);
+    // CF_PSPILL_BASIS_MC=0: every user's basis on the one-workgroup kernel (A/B)
+    static const bool basis_mc = [] {
+        const char* e = getenv("CF_PSPILL_BASIS_MC");
+        return !(e && e[0] == '0');
+    }();
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
     // (k > kSmallCap: a fifth, so that the two-per-CU kernel gets ~2 regions per CU at k = 5000)
     size_t kFaBudget = cf_hbm_budget(ctx, ctx->pspill_bytes, kmax > (uint64_t)kSmallCap ? 0.2 : 0.1, (size_t)4 << 30);
     // chunks over the bucket's users (plan order: largest k first), each within the budget
@@ -1281,7 +1529,7 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
                 const uint64_t d = 4 * k * k + 4 * k;
                 if (c.nu > 0 && (sd + d) * sizeof(double) > kSlotBudget) break;
                 sd += d;
-                si += 2 * k + 4;
+                si += 2 * k + 8;
                 rows += k;
                 t_sd.push_back(sd);
                 t_si.push_back(si);
@@ -1356,8 +1604,34 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
         uint32_t nb = 0;
         while (nb < c.nu && k_of(nb) > (uint64_t)kSmallCap) ++nb;
         CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, 256, stream));
-        hipLaunchKernelGGL(spill_basis_kernel<T>, dim3(a.nu), dim3(kT), 0, stream, a);
-        CF_HIP_CHECK(ctx, hipGetLastError());
+        // the basis: [0, nb) on spill_basis_mc (about two workgroups per CU over them, one launch
+        // per phase), the rest one workgroup each
+        const uint32_t nbm = basis_mc ? nb : 0;
+        if (nbm > 0) {
+            SpArgs<T> am = a;
+            am.G = (int)std::max<uint32_t>(1, std::min<uint32_t>(64, (2 * (uint32_t)n_cu + nbm - 1) / nbm));
+            SpArgs<T> a1 = a;
+            a1.G = 1;
+            const dim3 gm(nbm * (uint32_t)am.G), g1(nbm);
+            hipLaunchKernelGGL(spill_basis_mc<T>, g1, dim3(kT), 0, stream, a1, (int)kBmInit, 0);
+            hipLaunchKernelGGL(spill_basis_mc<T>, gm, dim3(kT), 0, stream, am, (int)kBmLim, 0);
+            hipLaunchKernelGGL(spill_basis_mc<T>, gm, dim3(kT), 0, stream, am, (int)kBmCopy, 0);
+            for (int step = 0; step < kMaxSteps; ++step) {
+                hipLaunchKernelGGL(spill_basis_mc<T>, gm, dim3(kT), 0, stream, am, (int)kBmGram, step);
+                hipLaunchKernelGGL(spill_basis_mc<T>, gm, dim3(kT), 0, stream, am, (int)kBmApply, step);
+                hipLaunchKernelGGL(spill_basis_mc<T>, g1, dim3(kT), 0, stream, a1, (int)kBmStep, step);
+            }
+            for (int ph : {(int)kBmGh, (int)kBmP, (int)kBmQO, (int)kBmW, (int)kBmYY, (int)kBmLdl, (int)kBmFs, (int)kBmGw})
+                if (ph == kBmLdl) hipLaunchKernelGGL(spill_basis_mc<T>, g1, dim3(kT), 0, stream, a1, ph, 0);
+                else hipLaunchKernelGGL(spill_basis_mc<T>, gm, dim3(kT), 0, stream, am, ph, 0);
+            CF_HIP_CHECK(ctx, hipGetLastError());
+        }
+        if (c.nu > nbm) {
+            SpArgs<T> ab = a;
+            ab.s0 = nbm;
+            hipLaunchKernelGGL(spill_basis_kernel<T>, dim3(c.nu - nbm), dim3(kT), 0, stream, ab);
+            CF_HIP_CHECK(ctx, hipGetLastError());
+        }
         const uint64_t split = roff_h[nb];
         if (split > 0) {   // k > kSmallCap: per-row arrays in HBM, two workgroups per CU, heaviest first
             SpArgs<T> ab = a;
