@@ -897,6 +897,9 @@ __global__ __launch_bounds__(kT) void spill_basis_mc(SpArgs<T> a, int phase, int
 // The r04 <5000, 1> instantiation (every array in LDS, 116 KB, one per CU) measured 3% slower
 // on the C5 sample's k > 2816 users than <0, 2>, bit-identical (profiles/r05/big2_r1.log).
 constexpr int kSmallCap = 2816;
+#ifndef CF_PSPILL_ROWS_LDS
+#define CF_PSPILL_ROWS_LDS 1   // (A/B: 0 = the G-mode rows read from the HBM row arrays)
+#endif
 template <typename T, int CAP, int OCC>
 __global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
     constexpr int kNbuf = (CAP == 0 || CAP > kSmallCap) ? 2 : 1;
@@ -906,6 +909,10 @@ __global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
     __shared__ int s_conn_l[CAP ? CAP : 1];
     __shared__ int s_ncon_l[CAP ? CAP : 1];
     __shared__ int s_keep_l[CAP ? CAP : 1];
+    // CAP = 0: the G-mode Gram's row list staged in LDS when it fits (its gathers then start
+    // from an LDS read instead of a dependent global one)
+    constexpr int kRowsLds = 4096;
+    __shared__ int s_rows_l[CAP ? 1 : kRowsLds];
     uint32_t* const rows_g = CAP ? nullptr : a.rows + (size_t)blockIdx.x * 4 * a.rows_d;
     float* const s_rat = CAP ? s_rat_l : reinterpret_cast<float*>(rows_g);
     int* const s_conn = CAP ? s_conn_l : reinterpret_cast<int*>(rows_g + a.rows_d);
@@ -1033,6 +1040,11 @@ __global__ __launch_bounds__(kT, OCC) void spill_predict_kernel(SpArgs<T> a) {
             const bool via_c = c < nc;
             const int nrow = via_c ? c : nc;
             const int* rows = via_c ? s_conn : s_ncon;
+            if (CAP == 0 && CF_PSPILL_ROWS_LDS && nrow <= kRowsLds) {
+                for (int i = tid; i < nrow; i += kT) s_rows_l[i] = rows[i];
+                __syncthreads();
+                rows = s_rows_l;
+            }
             const auto By = [&](int l, int i) -> double {
                 return i < d ? X(rows[l], lim + i) : (double)s_rat[rows[l]] - mu;
             };
