@@ -1288,6 +1288,9 @@ __global__ __launch_bounds__(SP_T) void spill_mc_col(McArgs a, int j, int p) {
 // the slot; a column block always belongs to the same wave of g, so its z entries are updated
 // by one lane in ascending R: deterministic.  spill_mc_fin forms y = y_R + sum_g z_g in order.
 constexpr int MC_SYMV_T = 256;
+#ifndef CF_SYMV_ZPRE
+#define CF_SYMV_ZPRE 1   // (A/B: 0 = z loaded at the += itself)
+#endif
 constexpr int MC_TQ = 16 * 65;   // a wave's slab transposition scratch: 16 columns x 64 rows (+1 pad)
 // HUGE (k > CF_SPILL_MAX_K): v is read from the slot (L2-resident) instead of an LDS copy.
 template <bool HUGE>
@@ -1340,6 +1343,10 @@ __global__ __launch_bounds__(MC_SYMV_T) void spill_mc_symv(McArgs a, int j) {
                 const int c0 = cb0 + s16;
                 double x[16];
                 const double* mp = M + (size_t)c0 * n + r;
+                // z's old value is loaded with the slab, so the += below waits on that batch of
+                // loads instead of starting a round trip of its own per slab
+                const bool zl = CF_SYMV_ZPRE && C < R && qq == 0 && s16 + ci < cw;
+                const double zold = zl ? z[c0 + ci] : 0.0;
 #pragma unroll
                 for (int t = 0; t < 16; ++t) x[t] = (ract && s16 + t < cw) ? mp[(size_t)t * n] : 0.0;
 #pragma unroll
@@ -1355,7 +1362,10 @@ __global__ __launch_bounds__(MC_SYMV_T) void spill_mc_symv(McArgs a, int j) {
                     for (int rr = 0; rr < 16; ++rr) sacc += q[ci * 65 + qq * 16 + rr];
                     sacc += __shfl_xor(sacc, 16);
                     sacc += __shfl_xor(sacc, 32);
-                    if (qq == 0 && s16 + ci < cw) z[c0 + ci] += sacc;
+                    if (qq == 0 && s16 + ci < cw) {
+                        if (CF_SYMV_ZPRE) z[c0 + ci] = zold + sacc;
+                        else z[c0 + ci] += sacc;
+                    }
                 }
             }
         }
