@@ -74,7 +74,9 @@ struct SpillArgs {
     // slot is the user's, not the workgroup's, and a claim is (user, part), mc_parts parts
     // per user.
     int mc_stage;
-    int mc_parts;
+    int mc_parts;        // parts of each of the first mc_n2 users of the launch
+    int mc_parts_rest;   // parts of each of the others
+    int mc_n2;
     uint64_t vs;   // BIG / HUGE: stride of the slot's k-long vectors (McLayout), >= the launch's kmax
     const uint64_t* slot_off;   // staged stages: per unit of the wave, its slot's offset in `work`
     int de_lds;    // HUGE: QL's d / e in the dynamic LDS tail (else in the slot's per-part pair)
@@ -229,9 +231,21 @@ __global__ __launch_bounds__(SP_T) void eigen_spill_kernel(SpillArgs a) {
         const int idx = s_flag[0];
         __syncthreads();
         const int st = a.mc_stage;
-        const int P = st ? a.mc_parts : 1;
-        if (idx >= (int)a.count * P) break;   // uniform: every wave leaves together
-        const int ui = idx / P, part = idx - ui * P;
+        // claims: the first n2 users in P0 parts each, the rest in P1 (stage 2 gives the largest
+        // users of a batch smaller than the CU count one part more)
+        const int P0 = st ? a.mc_parts : 1, P1 = st ? a.mc_parts_rest : 1, n2 = st ? a.mc_n2 : 0;
+        if (idx >= n2 * P0 + ((int)a.count - n2) * P1) break;   // uniform: every wave leaves together
+        int ui, part, P;
+        if (idx < n2 * P0) {
+            ui = idx / P0;
+            part = idx - ui * P0;
+            P = P0;
+        } else {
+            const int j = idx - n2 * P0;
+            ui = n2 + j / P1;
+            part = j - (j / P1) * P1;
+            P = P1;
+        }
         const int mode = a.loc.mode;
         const uint32_t unit = a.order[a.first + ui];
         const uint32_t u = mode == 2 ? a.loc.pair_movie[unit] : unit;   // the unit whose items index the graph
@@ -1755,12 +1769,23 @@ static int spill_mc_launch(cf_ctx* ctx, const cf_plan* plan, SpillArgs a, uint32
         const uint32_t fill = std::max<uint32_t>(1, n_cu / cnt);   // every part in the first round
         // (the back-transform's parts split columns, nothing is repeated: as many as its
         // columns give, claimed dynamically over the CUs)
-        const int parts[3] = {(int)std::min<uint32_t>(fill, (kmax + MC_QL_ROWS - 1) / MC_QL_ROWS), 1,
-                              (int)((kmax + MC_BT_COLS - 1) / MC_BT_COLS)};
+        const uint32_t qcap = (kmax + MC_QL_ROWS - 1) / MC_QL_ROWS;
+        const int parts[3] = {(int)std::min<uint32_t>(fill, qcap), 1, (int)((kmax + MC_BT_COLS - 1) / MC_BT_COLS)};
+        // the CUs the uniform QL split leaves idle give the batch's largest users (its critical
+        // path) one more part each -- still one round
+        static const bool ql_extra = [] {
+            const char* e = getenv("CF_SPILL_QL_EXTRA");
+            return !(e && e[0] == '0');
+        }();
+        const uint32_t used = cnt * (uint32_t)parts[0];
+        const uint32_t n2 = (ql_extra && (uint32_t)parts[0] < qcap && used < n_cu) ? std::min(cnt, n_cu - used) : 0;
         for (int s = 0; s < 3; ++s) {
             a.mc_stage = 2 + s;
-            a.mc_parts = parts[s];
-            const uint32_t g = std::min<uint32_t>(cnt * (uint32_t)parts[s], n_cu);
+            a.mc_parts = s == 0 ? parts[0] + 1 : parts[s];
+            a.mc_parts_rest = parts[s];
+            a.mc_n2 = s == 0 ? (int)n2 : 0;
+            const uint32_t items = (uint32_t)a.mc_n2 * (uint32_t)a.mc_parts + (cnt - (uint32_t)a.mc_n2) * (uint32_t)parts[s];
+            const uint32_t g = std::min<uint32_t>(items, n_cu);
             CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, sizeof(unsigned int), st));
             hipLaunchKernelGGL(kern, dim3(g), dim3(SP_T), lds, st, a);
             CF_HIP_CHECK(ctx, hipGetLastError());
@@ -1973,6 +1998,8 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     a.evecs = d_evecs;
     if (loc) a.loc = *loc;
     a.mc_parts = 1;
+    a.mc_parts_rest = 1;
+    a.mc_n2 = 0;
     a.phase = ctx->spill_debug ? reinterpret_cast<unsigned long long*>(ws + 64) : nullptr;
     bool side_started = false;
     for (size_t i = 0; i < rs.size(); ++i) {
