@@ -230,3 +230,30 @@ def test_predict_spill_users_match_oracle(gpu_ctx, density, mode, wlim, min_good
     assert n_good >= min_good, (n_good, n_ill)
     print(f"spill density={density} mode={mode} wlim={wlim} well-conditioned={n_good} ill-conditioned={n_ill}")
 
+
+
+def test_spill_basis_mc_bit_identical(gpu_ctx, tmp_path):
+    """spill_basis_mc (the basis of users with k > 2816 on several workgroups per user, one
+    launch per phase) produces the tables of the one-workgroup spill_basis_kernel bit for bit:
+    a child process with CF_PSPILL_BASIS_MC=0 runs the same case (k = 3300 and 2950 beside 900
+    and 300 in one chunk), and every prediction, mse and kk must equal this process's."""
+    import os
+    import subprocess
+    import sys
+
+    from basis_mc_child import run_case
+
+    ref = run_case(gpu_ctx)
+    assert int(np.sum(ref["kk"] > 0)) > 1000
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "basis_mc_child.py")
+    out = tmp_path / "basis_one_wg.npz"
+    env = dict(os.environ, CF_PSPILL_BASIS_MC="0")
+    r = subprocess.run([sys.executable, child, str(out)], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    got = np.load(out)
+    for k, v in ref.items():
+        g = got[k]
+        same = np.array_equal(g, v, equal_nan=True) if g.dtype.kind == "f" else np.array_equal(g, v)
+        assert same, (k, int(np.sum(g != v)))
+    print(f"spill_basis_mc == spill_basis_kernel on {len(ref['mse'])} ratings "
+          f"({int(np.sum(np.isnan(ref['mse'])))} NaN)")
