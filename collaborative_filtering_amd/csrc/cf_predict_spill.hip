@@ -1508,6 +1508,10 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
         const char* e = getenv("CF_PSPILL_BASIS_MC");
         return !(e && e[0] == '0');
     }();
+    static const int basis_mc_min = [] {   // users above this k take spill_basis_mc (A/B: CF_PSPILL_BASIS_MC_MIN)
+        const char* e = getenv("CF_PSPILL_BASIS_MC_MIN");
+        return e ? atoi(e) : 768;
+    }();
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
     // (k > kSmallCap: a fifth, so that the two-per-CU kernel gets ~2 regions per CU at k = 5000)
@@ -1618,7 +1622,14 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
         CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, 256, stream));
         // the basis: [0, nb) on spill_basis_mc (about two workgroups per CU over them, one launch
         // per phase), the rest one workgroup each
-        const uint32_t nbm = basis_mc ? nb : 0;
+        // (every k > kSmallCap user, and the largest users above basis_mc_min up to one per CU:
+        // C5 sample's 192 < k <= 3072 group 1610 -> 496 ms at 768, profiles/r05/bmin_*_af1.log)
+        uint32_t nbm = 0;
+        if (basis_mc) {
+            uint32_t n_min = 0;
+            while (n_min < c.nu && k_of(n_min) > (uint64_t)basis_mc_min) ++n_min;
+            nbm = std::max(nb, std::min(n_min, (uint32_t)n_cu));
+        }
         if (nbm > 0) {
             SpArgs<T> am = a;
             am.G = (int)std::max<uint32_t>(1, std::min<uint32_t>(64, (2 * (uint32_t)n_cu + nbm - 1) / nbm));
