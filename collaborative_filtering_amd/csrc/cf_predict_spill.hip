@@ -1512,6 +1512,10 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
         const char* e = getenv("CF_PSPILL_BASIS_MC_MIN");
         return e ? atoi(e) : 768;
     }();
+    static const uint32_t basis_mc_w = [] {   // its workgroups per CU over those users (A/B: CF_PSPILL_BASIS_MC_W)
+        const char* e = getenv("CF_PSPILL_BASIS_MC_W");
+        return e ? (uint32_t)std::max(1, atoi(e)) : 4u;
+    }();
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
     // (k > kSmallCap: a fifth, so that the two-per-CU kernel gets ~2 regions per CU at k = 5000)
@@ -1620,8 +1624,10 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
         uint32_t nb = 0;
         while (nb < c.nu && k_of(nb) > (uint64_t)kSmallCap) ++nb;
         CF_HIP_CHECK(ctx, hipMemsetAsync(a.counter, 0, 256, stream));
-        // the basis: [0, nb) on spill_basis_mc (about two workgroups per CU over them, one launch
-        // per phase), the rest one workgroup each
+        // the basis: the largest users on spill_basis_mc (about four workgroups per CU over them,
+        // one launch per phase; 1 / 2 / 4 / 8 per CU: 2742 / 2670 / 2632 / 2643 ms on the C5
+        // sample's k > 2816 users, 665 / 495 / 414 / 395 ms on its 192 < k <= 3072 ones,
+        // profiles/r05/bw_*_ah{1,2}.log), the rest one workgroup each
         // (every k > kSmallCap user, and the largest users above basis_mc_min up to one per CU:
         // C5 sample's 192 < k <= 3072 group 1610 -> 496 ms at 768, profiles/r05/bmin_*_af1.log)
         uint32_t nbm = 0;
@@ -1632,7 +1638,7 @@ int cf_launch_predict_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b
         }
         if (nbm > 0) {
             SpArgs<T> am = a;
-            am.G = (int)std::max<uint32_t>(1, std::min<uint32_t>(64, (2 * (uint32_t)n_cu + nbm - 1) / nbm));
+            am.G = (int)std::max<uint32_t>(1, std::min<uint32_t>(64, (basis_mc_w * (uint32_t)n_cu + nbm - 1) / nbm));
             SpArgs<T> a1 = a;
             a1.G = 1;
             const dim3 gm(nbm * (uint32_t)am.G), g1(nbm);
