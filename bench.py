@@ -584,7 +584,7 @@ def main():
         phase("CPU baseline sample")
         result["cpu_baseline"] = cpu_baseline(args, wl, W_host,
                                               dev={"m": m_h, "kk": kk_h, "evals": evals_h, "sigs": sigs_h,
-                                                   "mse": mse_h} if world == 1 else None)
+                                                   "mse": mse_h} if world == 1 else None, ctx=ctx)
     del W_host
 
     # ---- secondary legs (rank 0, N=1; not part of `value`) -----------------------------
@@ -1509,7 +1509,110 @@ def predictor_flops(off, k, m, kk, evals, sigtab):
             "rank_deficient_frac": rdef / max(n, 1), "c0_rows": int(np.sum(c == 0))}
 
 
-def cpu_baseline(args, wl, W, dev=None):
+def end_to_end_agreement(ctx, wl, W, users, so, si, sr, m_o, sigs_o, evals_o, evecs_o, eoff_o, threads,
+                         max_users=300):
+    """how far the drop-in's predictions are from the reference's, end to end.
+
+    For the first users of the CPU sample: device eigens (the timed run's fp32 records) -> device
+    predictor (cf_predict_precomp_sel_f32) against oracle eigens (fp64 restatement of
+    compute_eigens) -> oracle neigh_program::apply (explicit inverse), both with each user's OWN
+    sigs as w_lim (the compat table differs between the full run and the sample by construction).
+    Every row is put in exactly one class, in this order:
+      c0             no connected item (kk = 0): NaN on both sides;
+      lim_differs    the two sides' lim differ (an eigenvalue within fp32 noise of w_lim);
+      filter_differs the signed zero-column filter keeps different columns (:284-304);
+      rank_deficient |S| > c: U_CS^T U_CS singular (reference: rounding noise, device: min-norm);
+      cluster_cut    lim cuts a cluster (oracle gap at the cut < 1e-3): span(U_S) undetermined;
+      ill_conditioned cond(U_CS^T U_CS) > 1e8;
+      comparable     everything else: |d pred| is reported and checked against tolerances."""
+    from collaborative_filtering_amd.api import CF_SIGS_OWN
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ref as orc
+
+    torch = wl.torch
+    nu = int(min(len(users), max_users))
+    su = users[:nu]
+    so, si, sr = so[:nu + 1], si[:int(so[nu])], sr[:int(so[nu])]
+    ks = np.diff(so).astype(np.int64)
+    # device records of these users (own evals/sigs/blocks), copied out of the resident run
+    m_d = wl.d_m.cpu().numpy()[su]
+    rows = np.concatenate([np.arange(int(wl.off[u]), int(wl.off[u + 1])) for u in su])
+    sig_d = wl.d_sigs[torch.from_numpy(rows).to(wl.d_sigs.device)].cpu().numpy()
+    ev_d = wl.d_evals[torch.from_numpy(rows).to(wl.d_sigs.device)].cpu().numpy()
+    blocks = [wl.d_evecs[int(wl.evec_off[u]):int(wl.evec_off[u]) + int(wl.k[u]) * int(m_d[i])]
+              for i, u in enumerate(su)]
+    peoff = np.zeros(nu, dtype=np.uint64)
+    peoff[1:] = np.cumsum([b.numel() for b in blocks])[:-1]
+    evec_d = torch.cat(blocks).cpu().numpy() if blocks else np.zeros(1, np.float32)
+    sel = np.ones(len(rows), dtype=np.uint8)
+    mse_d, kk_d, pred_d = ctx.predict_precomp(so.astype(np.uint64), si.astype(np.uint32), sr.astype(np.float32), m_d,
+                                              ev_d.astype(np.float64), peoff, evec_d, sig_d.astype(np.float64),
+                                              sig_mode=CF_SIGS_OWN, want_pred=True)
+    mse_o, kk_o, pred_o = orc.predict_batch(so, si, sr, m_o[:nu], evals_o, eoff_o[:nu], evecs_o, sigs_o, W,
+                                            compat=False, n_threads=threads, want_pred=True)
+    del sel
+    counts = {c: 0 for c in ("c0", "lim_differs", "filter_differs", "rank_deficient", "cluster_cut",
+                             "ill_conditioned", "comparable")}
+    kk_equal = int(np.sum(kk_d == kk_o))
+    dpred = []
+    for i in range(nu):
+        b, e = int(so[i]), int(so[i + 1])
+        k = e - b
+        it = si[b:e].astype(np.int64)
+        Cm = np.asarray(W[np.ix_(it, it)], dtype=np.float64) > 0.1
+        mo, md = int(m_o[i]), int(m_d[i])
+        Uo = evecs_o[int(eoff_o[i]):int(eoff_o[i]) + k * mo].reshape(k, mo)
+        Ud = evec_d[int(peoff[i]):int(peoff[i]) + k * md].reshape(k, md).astype(np.float64)
+        evo = np.zeros(mo)
+        evo[:min(mo, k)] = evals_o[b:b + min(mo, k)]
+        evd = np.zeros(md)
+        evd[:min(md, k)] = ev_d[b:b + min(md, k)]
+        Ko = Cm.astype(np.int32) @ (Uo >= 1e-4).astype(np.int32) > 0
+        Kd = Cm.astype(np.int32) @ (Ud >= 1e-4).astype(np.int32) > 0
+        for r in range(k):
+            c = int(Cm[r].sum())
+            if c == 0:
+                counts["c0"] += 1
+                continue
+            lo = int(np.clip(np.sum(evo <= sigs_o[b + r]), 2, mo))
+            ld = int(np.clip(np.sum(evd <= sig_d[b + r]), 2, md))
+            if lo != ld:
+                counts["lim_differs"] += 1
+                continue
+            S = np.nonzero(Ko[r, :lo])[0]
+            if not np.array_equal(S, np.nonzero(Kd[r, :lo])[0]):
+                counts["filter_differs"] += 1
+                continue
+            if len(S) > c or len(S) == 0:
+                counts["rank_deficient"] += 1
+                continue
+            if lo < mo and lo < len(evo) and abs(evo[lo] - evo[lo - 1]) < 1e-3:
+                counts["cluster_cut"] += 1
+                continue
+            G = Uo[np.nonzero(Cm[r])[0]][:, S]
+            sv = np.linalg.svd(G, compute_uv=False)
+            if sv[-1] <= 0 or (sv[0] / sv[-1]) ** 2 > 1e8:
+                counts["ill_conditioned"] += 1
+                continue
+            counts["comparable"] += 1
+            dpred.append(abs(float(pred_d[b + r]) - float(pred_o[b + r])))
+    dp = np.asarray(dpred) if dpred else np.zeros(1)
+    n_rows = int(so[-1])
+    comp = counts["comparable"]
+    return {
+        "users": nu, "rows": n_rows, "kk_equal_frac": kk_equal / max(n_rows, 1),
+        "classes": counts, "comparable_frac": comp / max(n_rows, 1),
+        "comparable_agree_frac": {f"{t:g}": float(np.mean(dp <= t)) if comp else None for t in (1e-6, 1e-4, 1e-3, 1e-2)},
+        "comparable_dpred_median": float(np.median(dp)) if comp else None,
+        "comparable_dpred_max": float(dp.max()) if comp else None,
+        "note": "device fp32 eigens -> device predictor vs oracle fp64 eigens -> oracle explicit-inverse predictor "
+                "on the same users, own sigs as w_lim on both sides; rows classed in the order listed in "
+                "bench.end_to_end_agreement (c0, lim_differs, filter_differs, rank_deficient, cluster_cut, "
+                "ill_conditioned, comparable); agree_frac = share of comparable rows with |d pred| <= tolerance"}
+
+
+def cpu_baseline(args, wl, W, dev=None, ctx=None):
     """The oracle in precompute_local_threads / local_calc_precomp form (fp64, the reference's
     dense LU inverse + 2 GEMMs + Householder/QL eigensolver; neigh_program::apply per rating
     with the explicit-inverse Gram) on a std::thread pool of all the host threads this
@@ -1562,7 +1665,16 @@ def cpu_baseline(args, wl, W, dev=None):
     rows_d = np.concatenate([np.arange(int(off[u]), int(off[u + 1])) for u in su])
     bound_d = at_bound_stats(so[:npu + 1], ks, dev["m"][su], dev["kk"][rows_d], dev["evals"][rows_d],
                              dev["sigs"], ratings[rows_d], dev["mse"][rows_d]) if dev else None
+    e2e = None
+    if dev is not None and ctx is not None:
+        try:
+            t = time.perf_counter()
+            e2e = end_to_end_agreement(ctx, wl, W, users, so, si, sr, m, sigs, evals, evecs, eoff, threads)
+            e2e["seconds"] = time.perf_counter() - t
+        except Exception as exc:   # noqa: BLE001 -- a diagnostic, never the bench line's failure
+            e2e = f"failed: {exc!r}"
     return {
+        "end_to_end": e2e,
         "value": n / eig_s,
         "unit": "user-subgraph eigendecomps/s",
         "cores": threads,

@@ -109,7 +109,25 @@ SIGNATURES = {
                                   c_void_p]),
     "cf_eigen_batch_multi": (c_int, [c_void_p, c_int, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_uint64, c_void_p]),
+    "cf_eigen_batch_stream": (c_int, [c_void_p, c_int, c_uint32, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
+                                      c_void_p]),
 }
+
+
+class EigenChunk(ctypes.Structure):
+    """cf_eigen_chunk (cf_abi.h): one chunk of cf_eigen_batch_stream's records."""
+    _fields_ = [("first", c_uint32), ("count", c_uint32), ("item_off", POINTER(c_uint64)),
+                ("m", POINTER(c_int32)), ("sigs", POINTER(c_float)), ("evals", POINTER(c_float)),
+                ("packed_off", POINTER(c_uint64)), ("evecs", POINTER(c_float))]
+
+
+class EigenStreamStats(ctypes.Structure):
+    """cf_eigen_stream_stats (cf_abi.h)."""
+    _fields_ = [("chunks", c_uint32), ("chunk_slot_bytes", c_uint64), ("max_chunk_slot_bytes", c_uint64),
+                ("own_peak_bytes", c_uint64), ("device_peak_bytes", c_uint64)]
+
+
+EIGEN_SINK = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(EigenChunk))
 
 _lib = None
 

@@ -463,6 +463,79 @@ def eigen_batch_multi(ctxs, item_off, items):
     return EigenResult(item_off, poff[:-1].copy(), m, sigs, evals, evecs[: int(poff[-1])]), split.astype(np.int64)
 
 
+def eigen_batch_stream(ctxs, item_off, items, on_chunk, chunk_bytes=0):
+    """cf_eigen_batch_stream: compute_eigens over users 0..n-1 in memory-bounded chunks
+    (precompute_local_threads.cpp:89-98, 306-314: one task per user, each record appended as it
+    completes).  on_chunk(first, m, sigs, evals, packed_off, evecs) receives numpy COPIES of each
+    chunk's arrays in user order (item_off chunk-local); a returned nonzero int stops the call.
+    Returns the stream stats as a dict."""
+    lib = _native.load()
+    if isinstance(ctxs, Context):
+        ctxs = [ctxs]
+    item_off = np.ascontiguousarray(item_off, dtype=np.uint64)
+    items = np.ascontiguousarray(items, dtype=np.uint32)
+    n_users = len(item_off) - 1
+    err = []
+
+    def sink(_user, cp):
+        c = cp.contents
+        try:
+            n = int(c.count)
+            off = np.ctypeslib.as_array(c.item_off, shape=(n + 1,)).copy()
+            po = np.ctypeslib.as_array(c.packed_off, shape=(n + 1,)).copy()
+            ne, npk = int(off[-1]), int(po[-1])
+            m = np.ctypeslib.as_array(c.m, shape=(n,)).copy() if n else np.zeros(0, np.int32)
+            sg = np.ctypeslib.as_array(c.sigs, shape=(ne,)).copy() if ne else np.zeros(0, np.float32)
+            ev = np.ctypeslib.as_array(c.evals, shape=(ne,)).copy() if ne else np.zeros(0, np.float32)
+            vv = np.ctypeslib.as_array(c.evecs, shape=(npk,)).copy() if npk else np.zeros(0, np.float32)
+            r = on_chunk(int(c.first), off, m, sg, ev, po, vv)
+            return int(r or 0)
+        except Exception as e:   # noqa: BLE001 -- reported after the call
+            err.append(e)
+            return 1
+
+    cb = _native.EIGEN_SINK(sink)
+    st = _native.EigenStreamStats()
+    arr = (c_void_p * len(ctxs))(*[c.h for c in ctxs])
+    rc = lib.cf_eigen_batch_stream(arr, len(ctxs), n_users, ptr(item_off), ptr(items), int(chunk_bytes), cb, None,
+                                   byref(st))
+    if err:
+        raise err[0]
+    _check(lib, ctxs[0].h, rc, "cf_eigen_batch_stream")
+    return {"chunks": st.chunks, "chunk_slot_bytes": st.chunk_slot_bytes,
+            "max_chunk_slot_bytes": st.max_chunk_slot_bytes, "own_peak_bytes": st.own_peak_bytes,
+            "device_peak_bytes": st.device_peak_bytes}
+
+
+def eigen_stream_result(ctxs, item_off, items, chunk_bytes=0):
+    """eigen_batch_stream gathered into one EigenResult with packed evecs (evec_off = packed
+    offsets, as eigen_batch_multi returns), plus the stats."""
+    item_off = np.ascontiguousarray(item_off, dtype=np.uint64)
+    n_users = len(item_off) - 1
+    n = int(item_off[-1])
+    m = np.zeros(n_users, dtype=np.int32)
+    sigs = np.zeros(n, dtype=np.float32)
+    evals = np.zeros(n, dtype=np.float32)
+    poff = np.zeros(n_users + 1, dtype=np.uint64)
+    parts = []
+    run = [0]
+
+    def on_chunk(first, off, mm, sg, ev, po, vv):
+        cnt = len(mm)
+        e0 = int(item_off[first])
+        m[first:first + cnt] = mm
+        sigs[e0:e0 + len(sg)] = sg
+        evals[e0:e0 + len(ev)] = ev
+        poff[first:first + cnt + 1] = po + run[0]
+        run[0] += int(po[-1])
+        parts.append(vv)
+        return 0
+
+    st = eigen_batch_stream(ctxs, item_off, items, on_chunk, chunk_bytes)
+    evecs = np.concatenate(parts) if parts else np.zeros(0, np.float32)
+    return EigenResult(item_off, poff[:-1].copy(), m, sigs, evals, evecs), st
+
+
 def predict_precomp_multi(ctxs, item_off, items, ratings, m, evals, evec_off, evecs, sigtab,
                           sig_mode=CF_SIGS_COMPAT, row_sel=None, want_pred=False):
     """cf_predict_precomp_multi: neigh_program::apply over one user set on contexts `ctxs`

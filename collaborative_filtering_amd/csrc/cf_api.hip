@@ -45,6 +45,38 @@ __global__ void dense_scatter_kernel(uint32_t n_items, const uint64_t* row_ptr, 
 
 }  // namespace
 
+size_t cf_evict_workspaces(cf_ctx* ctx) {
+    if (!ctx->d_spill && !ctx->d_tri) return 0;
+    if (hipDeviceSynchronize() != hipSuccess) return 0;   // every stream of the context is done with them
+    const size_t bytes = ctx->spill_bytes + ctx->tri_bytes;
+    if (ctx->d_spill) (void)hipFree(ctx->d_spill);
+    if (ctx->d_tri) (void)hipFree(ctx->d_tri);
+    ctx->d_spill = ctx->d_tri = nullptr;
+    ctx->spill_bytes = ctx->tri_bytes = 0;
+    return bytes;
+}
+
+int cf_malloc_evict(cf_ctx* ctx, void** p, size_t bytes, const char* what) {
+    *p = nullptr;
+    if (hipMalloc(p, bytes) == hipSuccess) return CF_OK;
+    (void)hipGetLastError();
+    *p = nullptr;
+    if (cf_evict_workspaces(ctx) > 0 && hipMalloc(p, bytes) == hipSuccess) return CF_OK;
+    (void)hipGetLastError();
+    *p = nullptr;
+    return cf_set_error(ctx, CF_ENOMEM, std::string(what) + " (" + std::to_string(bytes) + " bytes)");
+}
+
+int cf_debug_counters(cf_ctx* ctx) {
+    if (ctx->d_dbg) return CF_OK;
+    void* p = nullptr;
+    if (hipMalloc(&p, 16 * sizeof(unsigned long long)) != hipSuccess)
+        return cf_set_error(ctx, CF_ENOMEM, "debug counters");
+    ctx->d_dbg = static_cast<unsigned long long*>(p);
+    CF_HIP_CHECK(ctx, hipMemset(ctx->d_dbg, 0, 16 * sizeof(unsigned long long)));
+    return CF_OK;
+}
+
 int cf_launch_dense_scatter(cf_ctx* ctx, uint32_t n_items, const uint64_t* d_row_ptr,
                             const uint32_t* d_col, const float* d_w, float* d_dense,
                             hipStream_t stream) {
@@ -116,6 +148,7 @@ void cf_destroy(cf_ctx* ctx) {
     if (ctx->d_gcol) (void)hipFree(ctx->d_gcol);
     if (ctx->d_gw) (void)hipFree(ctx->d_gw);
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
+    if (ctx->d_dbg) (void)hipFree(ctx->d_dbg);
     if (ctx->d_phase) (void)hipFree(ctx->d_phase);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_pred_next) (void)hipFree(ctx->d_pred_next);
@@ -347,52 +380,40 @@ int cf_eigen_run(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, c
                            (hipStream_t)stream);
 }
 
+}  // extern "C"
+
+namespace {
+struct BatchSink {   // cf_eigen_batch: every chunk's records into the caller's flat arrays
+    const uint64_t* item_off;
+    const uint64_t* evec_off;
+    int32_t* m;
+    float *sigs, *evals, *evecs;
+};
+int batch_sink(void* user, const cf_eigen_chunk* c) {
+    const BatchSink& B = *static_cast<const BatchSink*>(user);
+    const uint64_t e0 = B.item_off[c->first];
+    std::memcpy(B.m + c->first, c->m, sizeof(int32_t) * c->count);
+    std::memcpy(B.sigs + e0, c->sigs, sizeof(float) * c->item_off[c->count]);
+    std::memcpy(B.evals + e0, c->evals, sizeof(float) * c->item_off[c->count]);
+    for (uint32_t u = 0; u < c->count; ++u)
+        std::memcpy(B.evecs + B.evec_off[c->first + u], c->evecs + c->packed_off[u],
+                    sizeof(float) * (c->packed_off[u + 1] - c->packed_off[u]));
+    return 0;
+}
+}  // namespace
+
+extern "C" {
+
 int cf_eigen_batch(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off, const uint32_t* items,
                    const uint64_t* evec_off, int32_t* m_out, float* sigs, float* evals, float* evecs) {
     if (!ctx || !item_off || !evec_off || !m_out || !sigs || !evals || !evecs)
         return cf_set_error(ctx, CF_EINVAL, "cf_eigen_batch: null argument");
     if (!has_graph(ctx)) return cf_set_error(ctx, CF_ESTATE, "cf_eigen_batch: no item graph uploaded");
     CF_TRY(set_device(ctx));
-    const uint64_t n_entries = item_off[n_users];
-    for (uint64_t e = 0; e < n_entries; ++e)
-        if (items[e] >= ctx->n_items) return cf_set_error(ctx, CF_EINVAL, "item index outside the graph");
-    const uint64_t n_evec = n_users ? evec_off[n_users - 1] +
-                                          cf_evec_slots((uint32_t)(item_off[n_users] - item_off[n_users - 1]))
-                                    : 0;
-    cf_plan* plan = nullptr;
-    CF_TRY(cf_plan_create(ctx, n_users, item_off, &plan));
-    DevBuf doff, ditems, deoff, dm, dsig, deval, devec;
-    int rc = dev_alloc(ctx, doff, sizeof(uint64_t) * (n_users + 1));
-    if (rc == CF_OK) rc = dev_alloc(ctx, ditems, sizeof(uint32_t) * n_entries);
-    if (rc == CF_OK) rc = dev_alloc(ctx, deoff, sizeof(uint64_t) * std::max<uint32_t>(n_users, 1));
-    if (rc == CF_OK) rc = dev_alloc(ctx, dm, sizeof(int32_t) * std::max<uint32_t>(n_users, 1));
-    if (rc == CF_OK) rc = dev_alloc(ctx, dsig, sizeof(float) * n_entries);
-    if (rc == CF_OK) rc = dev_alloc(ctx, deval, sizeof(float) * n_entries);
-    if (rc == CF_OK) rc = dev_alloc(ctx, devec, sizeof(float) * n_evec);
-    hipError_t e = hipSuccess;
-    if (rc == CF_OK) {
-        e = hipMemcpy(doff.p, item_off, sizeof(uint64_t) * (n_users + 1), hipMemcpyHostToDevice);
-        if (e == hipSuccess && n_entries)
-            e = hipMemcpy(ditems.p, items, sizeof(uint32_t) * n_entries, hipMemcpyHostToDevice);
-        if (e == hipSuccess && n_users)
-            e = hipMemcpy(deoff.p, evec_off, sizeof(uint64_t) * n_users, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemset(deval.p, 0, sizeof(float) * std::max<uint64_t>(n_entries, 1));
-        if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("eigen H2D: ") + hipGetErrorString(e));
-    }
-    if (rc == CF_OK)
-        rc = cf_launch_eigen(ctx, plan, (const uint64_t*)doff.p, (const uint32_t*)ditems.p,
-                             (const uint64_t*)deoff.p, (int32_t*)dm.p, (float*)dsig.p, (float*)deval.p,
-                             (float*)devec.p, nullptr);
-    if (rc == CF_OK) {
-        e = hipDeviceSynchronize();
-        if (e == hipSuccess && n_users) e = hipMemcpy(m_out, dm.p, sizeof(int32_t) * n_users, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && n_entries) e = hipMemcpy(sigs, dsig.p, sizeof(float) * n_entries, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && n_entries) e = hipMemcpy(evals, deval.p, sizeof(float) * n_entries, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && n_evec) e = hipMemcpy(evecs, devec.p, sizeof(float) * n_evec, hipMemcpyDeviceToHost);
-        if (e != hipSuccess) rc = cf_set_error(ctx, CF_EHIP, std::string("eigen run: ") + hipGetErrorString(e));
-    }
-    cf_plan_destroy(plan);
-    return rc;
+    // device memory bounded by the stream's chunks; the caller's arrays receive every chunk
+    BatchSink B{item_off, evec_off, m_out, sigs, evals, evecs};
+    cf_ctx* const ctxs[1] = {ctx};
+    return cf_eigen_batch_stream(ctxs, 1, n_users, item_off, items, 0, batch_sink, &B, nullptr);
 }
 
 int cf_predict_run_f64(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,

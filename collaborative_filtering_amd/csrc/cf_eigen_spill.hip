@@ -2000,7 +2000,7 @@ int cf_launch_eigen_spill(cf_ctx* ctx, const cf_plan* plan, const cf_bucket& b, 
     a.mc_parts = 1;
     a.mc_parts_rest = 1;
     a.mc_n2 = 0;
-    a.phase = ctx->spill_debug ? reinterpret_cast<unsigned long long*>(ws + 64) : nullptr;
+    a.phase = ctx->spill_debug ? ctx->d_dbg : nullptr;   // counters of their own (cf_debug_spill)
     bool side_started = false;
     for (size_t i = 0; i < rs.size(); ++i) {
         const Range& r = rs[i];
@@ -2067,14 +2067,14 @@ int cf_spill_join(cf_ctx* ctx, hipStream_t stream) {
 int cf_debug_spill(cf_ctx* ctx, int enable, uint64_t* out8) {
     if (!ctx) return CF_EINVAL;
     CF_TRY(set_device(ctx));
+    if (enable) CF_TRY(cf_debug_counters(ctx));
     ctx->spill_debug = enable != 0;
     if (out8) {
         for (int i = 0; i < 8; ++i) out8[i] = 0;
-        if (ctx->d_spill) {
+        if (ctx->d_dbg) {
             CF_HIP_CHECK(ctx, hipDeviceSynchronize());
-            CF_HIP_CHECK(ctx, hipMemcpy(out8, static_cast<char*>(ctx->d_spill) + 64, 8 * sizeof(uint64_t),
-                                        hipMemcpyDeviceToHost));
-            CF_HIP_CHECK(ctx, hipMemset(static_cast<char*>(ctx->d_spill) + 64, 0, 8 * sizeof(uint64_t)));
+            CF_HIP_CHECK(ctx, hipMemcpy(out8, ctx->d_dbg, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+            CF_HIP_CHECK(ctx, hipMemset(ctx->d_dbg, 0, 8 * sizeof(uint64_t)));
         }
     }
     return CF_OK;

@@ -790,13 +790,11 @@ static int tri_scratch(cf_ctx* ctx, const cf_plan* plan, TriArgs& a) {
         if (ctx->d_tri) (void)hipFree(ctx->d_tri);
         ctx->d_tri = nullptr;
         ctx->tri_bytes = 0;
-        if (hipMalloc(&ctx->d_tri, need) != hipSuccess)
-            return cf_set_error(ctx, CF_ENOMEM, "tridiagonal eigen scratch (" + std::to_string(need) + " bytes)");
+        CF_TRY(cf_malloc_evict(ctx, &ctx->d_tri, need, "tridiagonal eigen scratch"));
         ctx->tri_bytes = need;
-        CF_HIP_CHECK(ctx, hipMemset(ctx->d_tri, 0, 8 * sizeof(unsigned long long)));
     }
     char* p = static_cast<char*>(ctx->d_tri);
-    a.stats = ctx->tri_debug ? reinterpret_cast<unsigned long long*>(p) : nullptr;
+    a.stats = ctx->tri_debug ? ctx->d_dbg + 8 : nullptr;   // counters of their own (cf_debug_tri)
     p += 8 * sizeof(unsigned long long);
     a.dd = reinterpret_cast<double*>(p);
     p += ne * sizeof(double);
@@ -878,13 +876,14 @@ int cf_launch_eigen_tri(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item
 int cf_debug_tri(cf_ctx* ctx, int enable, uint64_t* out4) {   // out4: 8 slots
     if (!ctx) return CF_EINVAL;
     CF_TRY(set_device(ctx));
+    if (enable) CF_TRY(cf_debug_counters(ctx));
     ctx->tri_debug = enable != 0;
     if (out4) {
         for (int i = 0; i < 8; ++i) out4[i] = 0;
-        if (ctx->d_tri) {
+        if (ctx->d_dbg) {
             CF_HIP_CHECK(ctx, hipDeviceSynchronize());
-            CF_HIP_CHECK(ctx, hipMemcpy(out4, ctx->d_tri, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-            CF_HIP_CHECK(ctx, hipMemset(ctx->d_tri, 0, 8 * sizeof(uint64_t)));
+            CF_HIP_CHECK(ctx, hipMemcpy(out4, ctx->d_dbg + 8, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+            CF_HIP_CHECK(ctx, hipMemset(ctx->d_dbg + 8, 0, 8 * sizeof(uint64_t)));
         }
     }
     return CF_OK;

@@ -78,9 +78,9 @@ struct cf_ctx {
     // block-wide rating queue per predictor stream and the dense workgroups' factorisation
     // regions (pred_dense_kernel, cf_predict.hip), grown on demand
     uint32_t* d_dense_q = nullptr;
-    size_t dense_q_words = 0;   // per stream
+    size_t dense_q_words = 0;   // per stream (kAuxStreams copies are allocated)
     double* d_dense_ws = nullptr;
-    size_t dense_ws_doubles = 0;   // per stream
+    size_t dense_ws_doubles = 0;   // per stream (kAuxStreams copies are allocated)
     // the complement masks the eigen kernel hands to the predictor (24 B per rating), valid for
     // the plan / item arrays / graph generation of the eigen run that wrote them (cf_cmask_*)
     void* d_cmask = nullptr;            // 3 words per rating at 3 * item_off[u]
@@ -99,7 +99,10 @@ struct cf_ctx {
     // eigen spill-path workspace (counter + per-workgroup fp64 k x k), grown on demand.
     void* d_spill = nullptr;
     size_t spill_bytes = 0;
-    bool spill_debug = false;   // cf_debug_spill: phase counters in the workspace header
+    bool spill_debug = false;   // cf_debug_spill: phase counters (d_dbg[0..7])
+    // debug counters of cf_debug_spill ([0..7]) and cf_debug_tri ([8..15]): a buffer of their own,
+    // so releasing or evicting a workspace neither loses nor re-seeds them
+    unsigned long long* d_dbg = nullptr;
     // the spill bucket's k > 3072 range runs on its own stream beside the smaller ranges:
     // fork / done events; spill_side_pending = its done event still has to be joined
     hipStream_t spill_side = nullptr;
@@ -259,12 +262,20 @@ struct DevBuf {
     }
 };
 
+// Drop the context's cached eigen-side workspaces (the spill solver's and the tridiagonal
+// path's; every launch that needs them sizes them again) after the device is idle.  Returns the
+// bytes released.  The spill workspace may hold most of the context's HBM share (its budget is
+// 0.75 of it), so every allocation below falls back on this before it reports CF_ENOMEM.
+size_t cf_evict_workspaces(cf_ctx* ctx);
+// hipMalloc that evicts the cached workspaces and retries once on failure; CF_ENOMEM (with
+// `what` in the message) if the retry fails too.
+int cf_malloc_evict(cf_ctx* ctx, void** p, size_t bytes, const char* what);
+// the 16 debug counter words (ctx->d_dbg), allocated zeroed on first use
+int cf_debug_counters(cf_ctx* ctx);
+
 inline int dev_alloc(cf_ctx* ctx, DevBuf& b, size_t bytes) {
     if (bytes == 0) bytes = 16;
-    hipError_t e = hipMalloc(&b.p, bytes);
-    if (e != hipSuccess)
-        return cf_set_error(ctx, CF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
-    return CF_OK;
+    return cf_malloc_evict(ctx, &b.p, bytes, "device buffer");
 }
 
 inline int set_device(cf_ctx* ctx) {

@@ -277,10 +277,14 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
             I = rows[x];
             J = sl - rstart[x];
         };
-        // this thread's staged elements: column tid & 31 of the chunk, rows (tid >> 5) + 8 q
+        // this thread's staged elements: column tid % kWlimKc of the chunk, rows tid / kWlimKc +
+        // kRowStep q -- every row of the 16 nt row tiles, rows >= c staged as 0 (sR = -1), so no
+        // tile row reads stale LDS
         static_assert(kThreads % kWlimKc == 0, "one staged column per thread");
         const int scol = tid % kWlimKc, srow0 = tid / kWlimKc;
         constexpr int kRowStep = kThreads / kWlimKc;
+        static_assert(kRowStep * kWlimLoads >= 16 * kWlimTiles && 16 * kWlimTiles <= kWlimLd,
+                      "the staged rows cover every row tile");
         int sR[kWlimLoads];   // the graph row of each staged row (-1: past c)
 #pragma unroll
         for (int q = 0; q < kWlimLoads; ++q) {
@@ -322,11 +326,11 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
 #pragma unroll
                 for (int q = 0; q < kWlimLoads; ++q) {
                     const int r = srow0 + kRowStep * q;
-                    if (r < kWlimCmax) Ws[scol * kWlimLd + r] = (double)nxt[q];
+                    if (r < 16 * kWlimTiles) Ws[scol * kWlimLd + r] = (double)nxt[q];
                 }
                 for (int jj = tid; jj < kWlimKc; jj += kThreads)
                     Ds[jj] = j0 + jj < n ? 1.0 / ((double)th[j0 + jj] - mu) : 0.0;
-                // rows c .. 16 nt - 1 of the tiles stay zero (staged as 0.0 above: srow < 0)
+                // rows c .. 16 nt - 1 of the tiles are zero (staged as 0.0 above: sR < 0)
                 __syncthreads();
                 if (j0 + kWlimKc < n) fetch(j0 + kWlimKc);
 #pragma unroll

@@ -1783,20 +1783,26 @@ int cf_launch_predict(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_o
     CF_HIP_CHECK(ctx, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device));
     const uint32_t dense_grid = 2u * (uint32_t)std::max(1, n_cu);
     if (!fused) {
+        // always kAuxStreams copies (the most any call uses): a buffer sized for one copy by a
+        // call with the phase diagnostics on would otherwise be indexed past its end by the
+        // second stream of a later overlapped call
         const size_t qw = 4 + 2 * (size_t)kChunk * (size_t)std::max<uint32_t>(plan->kmax, 2);
         const size_t ww = (size_t)dense_grid * ((size_t)(CF_MAX_K + 2) * (CF_MAX_K + 3) / 2);
+        constexpr size_t kCopies = cf_ctx::kAuxStreams;
         if (qw > ctx->dense_q_words) {
             if (ctx->d_dense_q) (void)hipFree(ctx->d_dense_q);
             ctx->d_dense_q = nullptr;
             ctx->dense_q_words = 0;
-            CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_dense_q, sizeof(uint32_t) * qw * copies));
+            CF_TRY(cf_malloc_evict(ctx, reinterpret_cast<void**>(&ctx->d_dense_q), sizeof(uint32_t) * qw * kCopies,
+                                   "dense rating queue"));
             ctx->dense_q_words = qw;
         }
         if (ww > ctx->dense_ws_doubles) {
             if (ctx->d_dense_ws) (void)hipFree(ctx->d_dense_ws);
             ctx->d_dense_ws = nullptr;
             ctx->dense_ws_doubles = 0;
-            CF_HIP_CHECK(ctx, hipMalloc(&ctx->d_dense_ws, sizeof(double) * ww * copies));
+            CF_TRY(cf_malloc_evict(ctx, reinterpret_cast<void**>(&ctx->d_dense_ws), sizeof(double) * ww * kCopies,
+                                   "dense factorisation regions"));
             ctx->dense_ws_doubles = ww;
         }
     }

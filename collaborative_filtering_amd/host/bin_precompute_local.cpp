@@ -2,8 +2,10 @@
 // run_test_precompute.sh stage `./precompute_local 8`).
 //   :230-250 load movielens/*.validate -> users[uimax - uid][movie]
 //   :253-293 load out_fin_* -> item weights (directed, as parsed; last duplicate wins)
-//   :100-213 compute_eigens per user  -> cf_eigen_batch (HIP, one workgroup per user)
-//   :196-211 append "uid k m / evals / evecs" records to out_eigen_ (truncated first)
+//   :100-213 compute_eigens per user  -> cf_eigen_batch_stream (HIP, one workgroup per user,
+//            users in memory-bounded chunks)
+//   :196-211 append "uid k m / evals / evecs" records to out_eigen_ (truncated first), chunk
+//            by chunk as they complete (:89-98)
 // Differences (documented in DESIGN.md): the item graph is dense over the compact id
 // space of all ids seen (the reference's 2000x2000 matrix is only defined for ids
 // < 2000); users are written in ascending uid order with their movies ascending (the
@@ -15,6 +17,7 @@
 #include <cstdlib>
 #include <fstream>
 #include <map>
+#include <stdexcept>
 
 #include "cf_cli.hpp"
 
@@ -64,47 +67,56 @@ int main(int argc, char** argv) {
         }
         off[++u] = its.size();   // no k cap: k > CF_SPILL_MAX_K runs the spill path's HUGE layout
     }
-    // --devices N (or CF_DEVICES): ONE global user set range-split across N contexts by k^3
-    // cost, each on GPU (i % visible); the records are gathered to the first GPU over xGMI
-    // and written as one out_eigen_ identical to the one-device run
+    // --devices N (or CF_DEVICES): contexts on GPUs (i % visible) taking the chunks in turn
     const char* env_dev = std::getenv("CF_DEVICES");
     const int n_dev = std::max(1, std::atoi(cfcli::opt(argc, argv, "devices", env_dev ? env_dev : "1").c_str()));
-    std::vector<uint64_t> eoff(n_users + 1);
-    const uint64_t n_evec = cf_evec_offsets(n_users, off.data(), eoff.data());
-    std::vector<int32_t> m(n_users);
-    std::vector<float> sigs(off.back()), evals(off.back()), evecs(std::max<uint64_t>(n_evec, 1));
-    if (n_dev == 1) {
-        cf_ctx* ctx = cfcli::open_device();
-        cfcli::upload_edges(ctx, items, edges);
-        cfcli::check(ctx, cf_eigen_batch(ctx, n_users, off.data(), its.data(), eoff.data(), m.data(), sigs.data(),
-                                         evals.data(), evecs.data()),
-                     "cf_eigen_batch");
-        cf_destroy(ctx);
-    } else {
-        const int visible = cf_device_count();
-        if (visible <= 0) cfcli::die("no usable MI355X device");
-        const char* dev0 = std::getenv("CF_DEVICE");
-        const int base = dev0 ? std::atoi(dev0) : 0;
-        std::vector<cf_ctx*> ctxs(n_dev, nullptr);
-        for (int d = 0; d < n_dev; ++d) {
-            if (cf_create((base + d) % visible, &ctxs[d]) != CF_OK) cfcli::die("cf_create failed");
-            cfcli::upload_edges(ctxs[d], items, edges);
-        }
-        std::vector<uint32_t> split(n_dev + 1);
-        cfcli::check(ctxs[0], cf_eigen_batch_multi(ctxs.data(), n_dev, n_users, off.data(), its.data(), m.data(),
-                                                   sigs.data(), evals.data(), eoff.data(), evecs.data(),
-                                                   evecs.size(), split.data()),
-                     "cf_eigen_batch_multi");
-        for (int d = 0; d < n_dev; ++d)
-            std::printf("device part %d: users %u..%u on GPU %d\n", d, split[d], split[d + 1], (base + d) % visible);
-        for (auto* c : ctxs) cf_destroy(c);
+    const int visible = cf_device_count();
+    if (visible <= 0) cfcli::die("no usable MI355X device");
+    const char* dev0 = std::getenv("CF_DEVICE");
+    const int base = dev0 ? std::atoi(dev0) : 0;
+    std::vector<cf_ctx*> ctxs(n_dev, nullptr);
+    for (int d = 0; d < n_dev; ++d) {
+        if (cf_create((base + d) % visible, &ctxs[d]) != CF_OK) cfcli::die("cf_create failed");
+        cfcli::upload_edges(ctxs[d], items, edges);
     }
-    // out_eigen_: text records formatted on the reference's n_threads (its first argument,
-    // :217-222), or the binary form with --format binary
+    // out_eigen_: records appended chunk by chunk as they complete, in user order, like the
+    // reference's save_output appends each task's record (:89-98): memory is bounded by the
+    // chunk size, not by the user count.  Text records are formatted on the reference's
+    // n_threads (its first argument, :217-222), or the binary form with --format binary
+    // (SURVEY 8f item 1).  --chunk-bytes caps a chunk's eigenvector slots (0 = by free HBM and
+    // host RAM); the file is the same for every chunk size and device count.
     const int n_threads = std::max(1, std::atoi(argv[1]));
     const bool binary = cfcli::opt(argc, argv, "format", "text") == "binary";
-    cfio::write_eigen_file(out_path, false, n_threads, binary, n_users, uid.data(), off.data(), m.data(),
-                           movies.data(), sigs.data(), evals.data(), eoff.data(), evecs.data());
+    const uint64_t chunk_bytes = std::strtoull(cfcli::opt(argc, argv, "chunk-bytes", "0").c_str(), nullptr, 10);
+    cfio::start_eigen_file(out_path, binary, n_users);
+    struct Sink {
+        const std::string* path;
+        int n_threads;
+        bool binary;
+        const uint32_t* uid;
+        const uint64_t* off;
+        const uint32_t* movies;
+    } sk{&out_path, n_threads, binary, uid.data(), off.data(), movies.data()};
+    auto sink = [](void* user, const cf_eigen_chunk* c) -> int {
+        const Sink& S = *static_cast<const Sink*>(user);
+        try {
+            cfio::write_eigen_file(*S.path, true, S.n_threads, S.binary, c->count, S.uid + c->first, c->item_off, c->m,
+                                   S.movies + S.off[c->first], c->sigs, c->evals, c->packed_off, c->evecs);
+        } catch (const std::exception& e) {
+            std::fprintf(stderr, "error: %s\n", e.what());
+            return -1;
+        }
+        return 0;
+    };
+    cf_eigen_stream_stats st{};
+    cfcli::check(ctxs[0], cf_eigen_batch_stream(ctxs.data(), n_dev, n_users, off.data(), its.data(), chunk_bytes, sink,
+                                                &sk, &st),
+                 "cf_eigen_batch_stream");
+    std::printf("eigen stream: %u chunks of <= %.3f GB of slots (largest %.3f GB) on %d device(s); peak device "
+                "memory %.3f GB own, %.3f GB in use on the device\n",
+                st.chunks, st.chunk_slot_bytes / 1e9, st.max_chunk_slot_bytes / 1e9, n_dev, st.own_peak_bytes / 1e9,
+                st.device_peak_bytes / 1e9);
+    for (auto* c : ctxs) cf_destroy(c);
     std::printf("Wrote %u eigen records to %s\n", n_users, out_path.c_str());
     return 0;
 }

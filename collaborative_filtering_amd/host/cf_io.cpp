@@ -2,20 +2,7 @@
 #include "cf_io.hpp"
 
 #include <algorithm>
-#include <cstring>
-#include <fstream>
-#include <stdexcept>
-#include <thread>
-
 #include <atomic>
-
-#include <dirent.h>
-#include <fcntl.h>
-#include <sys/mman.h>
-#include <sys/stat.h>
-#include <unistd.h>
-
-#include <algorithm>
 #include <charconv>
 #include <cmath>
 #include <cstdio>
@@ -23,6 +10,13 @@
 #include <fstream>
 #include <sstream>
 #include <stdexcept>
+#include <thread>
+
+#include <dirent.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 namespace cfio {
 
@@ -598,9 +592,13 @@ void write_eigen_file(const std::string& path, bool append, int n_threads, bool 
             const uint64_t k = off[u + 1] - off[u], mm = (uint64_t)std::max(m[u], 0);
             at[u + 1] = at[u] + 4 * (3 + 2 * k + mm + k * mm);
         }
+        // appended records follow the file's current end (its header, with the total count,
+        // was written by start_eigen_file); otherwise the file is this call's records alone
         const uint64_t n = n_users;
-        f.write(kEigenMagic, sizeof(kEigenMagic));
-        f.write(reinterpret_cast<const char*>(&n), sizeof(n));
+        if (!append) {
+            f.write(kEigenMagic, sizeof(kEigenMagic));
+            f.write(reinterpret_cast<const char*>(&n), sizeof(n));
+        }
         f.close();
         const int wfd = ::open(path.c_str(), O_WRONLY);
         if (wfd < 0) throw std::runtime_error("cannot open " + path);
@@ -717,10 +715,29 @@ void write_eigen_file(const std::string& path, bool append, int n_threads, bool 
     if (failed) throw std::runtime_error("write failed: " + path);
 }
 
+void start_eigen_file(const std::string& path, bool binary, uint64_t n_total) {
+    std::ofstream f(path, std::ofstream::binary | std::ofstream::trunc);
+    if (!f) throw std::runtime_error("cannot open " + path);
+    if (binary) {
+        f.write(kEigenMagic, sizeof(kEigenMagic));
+        f.write(reinterpret_cast<const char*>(&n_total), sizeof(n_total));
+    }
+    if (!f) throw std::runtime_error("write failed: " + path);
+}
+
 }  // namespace cfio
 
 // C entry points used by the Python side (tests compare the formatting with printf, and the
 // parallel / binary out_eigen_ writers and readers with the serial text form).
+extern "C" int cfh_start_eigen(const char* path, int binary, uint64_t n_total) {
+    try {
+        cfio::start_eigen_file(path, binary != 0, n_total);
+    } catch (const std::exception&) {
+        return -1;
+    }
+    return 0;
+}
+
 extern "C" int cfh_write_eigen(const char* path, int append, int n_threads, int binary, uint32_t n_users,
                                const uint32_t* uid, const uint64_t* off, const int32_t* m, const uint32_t* movies,
                                const float* sigs, const float* evals, const uint64_t* eoff, const float* evecs) {

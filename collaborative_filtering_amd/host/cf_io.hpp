@@ -123,9 +123,16 @@ struct EigenFlat {
 EigenFlat load_eigen_flat(const std::string& path, int n_threads = 0);
 // out_eigen_ writer (precompute_local_threads.cpp:196-211): text records formatted on
 // n_threads threads (contiguous user ranges, written in user order), or the binary form
-// (the reference's own TODO, README.md:29).
+// (the reference's own TODO, README.md:29).  eoff[u] locates user u's k x m
+// block in evecs (slot offsets or packed offsets alike).  append: the records follow the
+// file's end (binary: no header of their own, see start_eigen_file).
 void write_eigen_file(const std::string& path, bool append, int n_threads, bool binary, uint32_t n_users,
                       const uint32_t* uid, const uint64_t* off, const int32_t* m, const uint32_t* movies,
                       const float* sigs, const float* evals, const uint64_t* eoff, const float* evecs);
+// A file written in pieces (bin/precompute_local's chunks, in user order): start_eigen_file
+// truncates it and, for the binary form, writes the header with the total record count; every
+// piece is then write_eigen_file(append = true).  The bytes equal one write_eigen_file over all
+// records.
+void start_eigen_file(const std::string& path, bool binary, uint64_t n_total);
 
 }  // namespace cfio

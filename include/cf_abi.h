@@ -175,13 +175,57 @@ uint64_t cf_evec_offsets(uint32_t n_users, const uint64_t* item_off, uint64_t* e
  *   evals[item_off[u] + j]   j < m  : eigenvalues of L2, ascending          (:164-166,193)
  *   evecs[evec_off[u] + i*m + j]    : eigenvector j, row i (k x m row-major) (:194,205-209)
  *   m_out[u]                        : lim, the stored eigenpair count       (:185-191)
- * k == 1 gives m == 2 with zero padding (reference: uninitialised, :193-194). */
+ * k == 1 gives m == 2 with zero padding (reference: uninitialised, :193-194).
+ * Device memory is bounded: the users run as the chunks of cf_eigen_batch_stream (below), each
+ * chunk's blocks copied into the caller's arrays; only the host arrays scale with n_users. */
 int cf_eigen_batch(cf_ctx* ctx, uint32_t n_users, const uint64_t* item_off,
                    const uint32_t* items, const uint64_t* evec_off, int32_t* m_out,
                    float* sigs, float* evals, float* evecs);
 int cf_eigen_run(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,
                  const uint32_t* d_items, const uint64_t* d_evec_off, int32_t* d_m,
                  float* d_sigs, float* d_evals, float* d_evecs, void* stream);
+
+/* ---- compute_eigens over any number of users at bounded memory ------------------
+ * The reference runs one compute_eigens task per user and appends each record to out_eigen_
+ * as it completes (precompute_local_threads.cpp:89-98, 306-314), so its memory does not grow
+ * with the user count.  cf_eigen_batch_stream cuts users 0..n_users-1 (input order) into
+ * contiguous chunks whose eigenvector slots (cf_evec_slots) fit chunk_bytes (0: a fifth of
+ * the first context's HBM share, at most a quarter of host RAM (<= 64 GB) over the staging
+ * sets), solves each chunk on the next free context (one per GPU, each with the graph
+ * uploaded), packs its k x m blocks on the device and calls sink(sink_user, chunk) once per
+ * chunk, in user order, from the calling thread, while the devices solve the next chunks.
+ * The chunk's arrays live until the sink returns:
+ *   item_off[count + 1]    chunk-local (item_off[0] = 0): user first+u has k = item_off[u+1] -
+ *                          item_off[u] items, its sigs / evals at item_off[u] (as cf_eigen_batch)
+ *   m[count], sigs, evals  as cf_eigen_batch
+ *   packed_off[count + 1]  user first+u's k x m row-major block at evecs + packed_off[u]
+ * A nonzero sink return stops the call (returned if negative, else CF_EINVAL).  The records
+ * equal one cf_eigen_batch over all users bit for bit, for every chunk size and device count.
+ * The contexts' eigen workspaces are released at the end (one-shot call).  stats (optional):
+ * chunk count, the budget used, the largest chunk's slot bytes, and the peaks of the call's
+ * own device bytes (its buffers + the contexts' workspaces) and of the device-wide bytes in
+ * use (hipMemGetInfo, after each chunk's solve). */
+typedef struct cf_eigen_chunk {
+    uint32_t first;
+    uint32_t count;
+    const uint64_t* item_off;
+    const int32_t* m;
+    const float* sigs;
+    const float* evals;
+    const uint64_t* packed_off;
+    const float* evecs;
+} cf_eigen_chunk;
+typedef int (*cf_eigen_sink)(void* sink_user, const cf_eigen_chunk* chunk);
+typedef struct cf_eigen_stream_stats {
+    uint32_t chunks;
+    uint64_t chunk_slot_bytes;
+    uint64_t max_chunk_slot_bytes;
+    uint64_t own_peak_bytes;
+    uint64_t device_peak_bytes;
+} cf_eigen_stream_stats;
+int cf_eigen_batch_stream(cf_ctx* const* ctxs, int n_dev, uint32_t n_users, const uint64_t* item_off,
+                          const uint32_t* items, uint64_t chunk_bytes, cf_eigen_sink sink, void* sink_user,
+                          cf_eigen_stream_stats* stats);
 
 /* ---- multi-GPU eigen stage and the out_eigen_ gather ----------
  * Replaces the thread pool of precompute_local_threads.cpp:300-314 and the single shared

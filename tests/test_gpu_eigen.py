@@ -146,6 +146,25 @@ def test_release_workspaces_then_rerun_bit_identical(gpu_ctx):
             assert np.array_equal(x, y), u
 
 
+def test_debug_spill_counters_survive_release():
+    """the spill phase counters live in a buffer of their own, so releasing
+    the workspace between the run and the read keeps them (they used to sit in the freed
+    workspace's header and read back as zeros)."""
+    from collaborative_filtering_amd.api import Context
+
+    W = cases.item_graph(900, 0.5, seed=45)
+    off, items = cases.user_items(900, [700, 150, 400], seed=46)
+    with Context(0) as ctx:
+        ctx.upload_graph_dense(W)
+        ctx.debug_spill(True)
+        ctx.eigen_batch(off, items)
+        ctx.release_workspaces()
+        r = ctx.debug_spill(True, read=True)
+        assert r["users"] == 2, r   # the two k > 192 users
+        assert r["tridiag_cyc_per_user"] > 0, r
+        assert ctx.debug_spill(False, read=True)["users"] == 0   # read clears them
+
+
 def test_eigen_spill_path_sparse(gpu_ctx):
     """Spill users on a sparse graph: lambda = 0 per component, lambda = 1 per isolated item."""
     W = cases.item_graph(900, 0.01, seed=43, isolated_frac=0.2)

@@ -1,7 +1,8 @@
 """Multi-GPU product path on the GPU box: cf_eigen_batch_multi over several
 contexts (on a one-GPU box they share device 0, the peer copies degenerate to local copies,
-the code path is the same), cf_pack_eigen_run, and bin/precompute_local --devices N, whose
-out_eigen_ must be byte-identical to the one-device file (precompute_local_threads.cpp:300-314
+the code path is the same), cf_pack_eigen_run, and bin/precompute_local --devices N (the
+chunks of cf_eigen_batch_stream dealt to the devices), whose out_eigen_ must be byte-identical
+to the one-device, one-chunk file (precompute_local_threads.cpp:300-314
 thread pool -> one range per GPU; :196-211 one out_eigen_)."""
 import os
 import subprocess
@@ -88,14 +89,18 @@ def test_precompute_local_devices_byte_identical(tmp_path, fmt):
     _run(wd, "knn")
     _run(wd, "knn2")
     outs = {}
-    for n_dev in (1, 2, 4):
-        out = f"out_eigen_d{n_dev}"
-        log = _run(wd, "precompute_local", "8", "--devices", str(n_dev), "--output", out, "--format", fmt)
-        if n_dev > 1:
-            assert log.count("device part") == n_dev
-        outs[n_dev] = open(os.path.join(wd, out), "rb").read()
-    assert len(outs[1]) > 1000
-    assert outs[2] == outs[1] and outs[4] == outs[1]
+    for n_dev, chunk in ((1, 0), (2, 0), (4, 0), (1, 60000), (3, 60000)):
+        out = f"out_eigen_d{n_dev}_c{chunk}"
+        log = _run(wd, "precompute_local", "8", "--devices", str(n_dev), "--output", out, "--format", fmt,
+                   "--chunk-bytes", str(chunk))
+        assert f"on {n_dev} device(s)" in log, log
+        n_chunks = int(log.split("eigen stream: ")[1].split()[0])
+        assert (n_chunks == 1) if chunk == 0 else (n_chunks >= 3), log
+        outs[(n_dev, chunk)] = open(os.path.join(wd, out), "rb").read()
+    ref = outs[(1, 0)]
+    assert len(ref) > 1000
+    for key, v in outs.items():
+        assert v == ref, key
 
 
 def _c2_subsample(n_users, seed):

@@ -257,3 +257,25 @@ def test_spill_basis_mc_bit_identical(gpu_ctx, tmp_path):
         assert same, (k, int(np.sum(g != v)))
     print(f"spill_basis_mc == spill_basis_kernel on {len(ref['mse'])} ratings "
           f"({int(np.sum(np.isnan(ref['mse'])))} NaN)")
+
+
+def test_dense_buffers_after_debug_phases_toggle():
+    """the block-wide rating queue and factorisation regions were sized for
+    one stream while the phase diagnostics were on, then indexed by the second stream of an
+    overlapped call.  On a fresh context: diagnostics on, predict, diagnostics off, predict
+    again -- the block-wide (nc > 62) ratings of both calls give the same kk and mse bits."""
+    from collaborative_filtering_amd.api import Context
+
+    ks = [150, 140, 130, 150, 140, 130]
+    W, off, items, rat, m, sigs, evals, evec_off, evecs, blocks = build_case(0.5, ks, seed=70)
+    sigtab = np.full_like(sigs, 0.3)
+    with Context(0) as ctx:
+        ctx.upload_graph_dense(W)
+        ctx.debug_phases(True)
+        mse1, kk1 = ctx.predict_precomp(off, items, rat, m, evals, evec_off, evecs, sigtab, sig_mode=CF_SIGS_OWN)
+        ctx.debug_phases(False)
+        mse2, kk2 = ctx.predict_precomp(off, items, rat, m, evals, evec_off, evecs, sigtab, sig_mode=CF_SIGS_OWN)
+    assert np.array_equal(kk1, kk2)
+    assert np.array_equal(mse1.view(np.uint32), mse2.view(np.uint32))
+    nc = np.concatenate([np.full(int(off[u + 1] - off[u]), int(off[u + 1] - off[u])) for u in range(len(ks))]) - kk1
+    assert int(np.sum(nc > 62)) > 20
