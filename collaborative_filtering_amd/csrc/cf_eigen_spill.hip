@@ -113,9 +113,9 @@ struct McLayout {
 __host__ __device__ constexpr uint64_t spill_base_stride(uint64_t k) {
     return 2ull * k * k + (uint64_t)SP_NB * k + 4ull * SP_QB * (k + 2 * SP_QB + 4) + 64;
 }
-// the symv's transposed partials z_g (G <= ceil(vs / 64) rows of vs) share the QL buffers'
-// space (gbuf): the tridiagonalisation is over before QL starts.  ceil(v/64) v <= ceil(v/896)
-// 64 (v + 36) for every v >= 1, so they fit.
+// the symv's transposed partials z_k (one per row-block pair: <= ceil(vs / 64) rows of vs) share
+// the QL buffers' space (gbuf): the tridiagonalisation is over before QL starts.  ceil(v/64) v <=
+// ceil(v/896) 64 (v + 36) for every v >= 1, so they fit.
 
 // LDS of one workgroup.  NL = the largest k of the launch's layout.  Up to SP_NL (3072) the
 // per-row vectors rc / rs / tau live in LDS too; a BIG launch (SP_NL < k <= CF_SPILL_MAX_K)
@@ -1297,10 +1297,11 @@ __global__ __launch_bounds__(SP_T) void spill_mc_col(McArgs a, int j, int p) {
 // pairs {k, nrb - 1 - k}, k = g, g + G, ... (nrb + 1 tiles a pair: balanced); wave w of it the
 // column blocks C = w, w + 4, ... <= R.  A tile (R, C) adds
 // A_RC v_C to the rows' partial y_R (lane = row, column-major loads coalesce) and, below the
-// diagonal, A_RC^T v_R to the workgroup's partial z_g over C's columns (the 64 x 16 products of
-// a slab transposed through the wave's LDS scratch, four 16-row sums per column).  z_g lives in
-// the slot; a column block always belongs to the same wave of g, so its z entries are updated
-// by one lane in ascending R: deterministic.  spill_mc_fin forms y = y_R + sum_g z_g in order.
+// diagonal, A_RC^T v_R to the pair's partial z_k over C's columns (the 64 x 16 products of a
+// slab transposed through the wave's LDS scratch, four 16-row sums per column).  z_k lives in
+// the slot; a column block always belongs to the same wave, so its z entries are updated by one
+// lane, R = k then nrb - 1 - k: deterministic, and independent of G.  spill_mc_fin forms y =
+// y_R + sum_k z_k in pair order.
 constexpr int MC_SYMV_T = 256;
 #ifndef CF_SYMV_ZPRE
 #define CF_SYMV_ZPRE 1   // (A/B: 0 = z loaded at the += itself)
@@ -1329,16 +1330,21 @@ __global__ __launch_bounds__(MC_SYMV_T) void spill_mc_symv(McArgs a, int j) {
     const int r0 = j + 1;
     const int nrb = (n - r0 + 63) >> 6;
     const int npair = (nrb + 1) >> 1;
-    if (g >= npair) return;   // uniform; spill_mc_fin sums z over g < min(G, npair)
-    double* z = M + bo + Lo.gbuf + (size_t)g * Lo.vs;
+    if (g >= npair) return;   // uniform; spill_mc_fin sums z over every pair
     if (!HUGE)
         for (int c = r0 + tid; c < n; c += MC_SYMV_T) vs_lds[c] = rc[c];
-    // z_g = 0 on this wave's column blocks, by the lanes that update them below
-    for (int C = wave; C < nrb; C += NWV)
-        for (int s16 = 0; s16 < 64; s16 += 16) {
-            const int c = r0 + C * 64 + s16 + lane;
-            if (lane < 16 && c < n) z[c] = 0.0;
-        }
+    // z_k = 0 for every pair k of this workgroup, on this wave's column blocks, by the lanes that
+    // update them below.  One partial per row-block PAIR (not per workgroup): the sums are then
+    // the same whatever G the launch uses (G depends on how many users share the wave, so a
+    // per-workgroup partial made a user's records depend on the other users of its batch)
+    for (int k = g; k < npair; k += a.G) {
+        double* zk = M + bo + Lo.gbuf + (size_t)k * Lo.vs;
+        for (int C = wave; C < nrb; C += NWV)
+            for (int s16 = 0; s16 < 64; s16 += 16) {
+                const int c = r0 + C * 64 + s16 + lane;
+                if (lane < 16 && c < n) zk[c] = 0.0;
+            }
+    }
     __syncthreads();
     double* q = tq[wave];
     const int ci = lane & 15, qq = lane >> 4;
@@ -1346,6 +1352,7 @@ __global__ __launch_bounds__(MC_SYMV_T) void spill_mc_symv(McArgs a, int j) {
         const int k = g + (it >> 1) * a.G;
         const int R = (it & 1) ? nrb - 1 - k : k;
         if ((it & 1) && R == k) continue;   // the middle block of an odd count (uniform)
+        double* z = M + bo + Lo.gbuf + (size_t)k * Lo.vs;
         const int r = r0 + R * 64 + lane;
         const bool ract = r < n;
         const double vr = ract ? vs[r] : 0.0;
@@ -1420,8 +1427,9 @@ __global__ __launch_bounds__(SP_T) void spill_mc_fin(McArgs a, int j, int p) {
         xw[tid] = mc[Lo.xw + tid];
     }
     __syncthreads();
-    // y = the row-block partials + the transposed partials z_g of spill_mc_symv, in order
-    const int gz = min(a.G, (((n - r0 + 63) >> 6) + 1) >> 1);
+    // y = the row-block partials + the transposed partials z_k of spill_mc_symv (one per
+    // row-block pair), in pair order
+    const int gz = (((n - r0 + 63) >> 6) + 1) >> 1;
     const double* z = mc + Lo.gbuf;
     double yv = 0.0;
     for (int r = r0 + tid; r < n; r += SP_T) {

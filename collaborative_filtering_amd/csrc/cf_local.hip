@@ -182,17 +182,41 @@ __global__ __launch_bounds__(kThreads) void local_predict_kernel(LocalPredArgs a
 // 1 / (theta_j - mu) applied to the A operand in registers; the next chunk's loads are in
 // flight while the current one is multiplied.  The accumulators then move to the packed
 // lower triangle (which aliases the staging area) for the LDL^T.
-constexpr int kWlimCmax = 184;   // F packed fp64 in LDS (133 KB): every pair of a k <= 180 user
-constexpr int kWlimTiles = (kWlimCmax + 15) / 16;   // 12 row tiles
-constexpr int kWlimKc = 16;      // columns of W_R staged per chunk
-constexpr int kWlimLd = 16 * kWlimTiles + 4;        // staged row stride (doubles)
-constexpr int kWlimSlots = 21;   // lower tiles of the busiest wave at 12 row tiles
-constexpr int kWlimLoads = (kWlimCmax * kWlimKc + kThreads - 1) / kThreads;   // 12 floats per thread
+// Three size classes of the kernel, by c: F's packed triangle is sized for the class's
+// largest c, so the common small systems (c <= 64: 17 KB of LDS, 4 accumulator tiles per
+// wave) run eight workgroups per CU instead of the one that a 184-row triangle (136 KB)
+// leaves room for -- the iterations are latency chains (staged W_R chunks, one barrier per
+// LDL^T pivot), and more resident pairs hide them (r05: one 29 s launch at one wave per SIMD).
+constexpr int kWlimCmax = 184;   // largest class: every pair of a k <= 180 user
 constexpr int kWlimIters = 64;
 constexpr double kWlimTol = 1e-10;   // relative bracket width at exit (w_lim is fp32)
-constexpr int kWlimFElems = kWlimCmax * (kWlimCmax + 1) / 2;
-constexpr int kWlimStageElems = kWlimKc * kWlimLd + kWlimKc;
-static_assert(kWlimStageElems <= kWlimFElems, "the staging area fits inside F's packed triangle");
+// accumulator tiles of the busiest wave under the snake row-tile map {w, 7 - w, 8 + w}
+constexpr int wlim_slots(int T) {
+    int best = 0;
+    for (int w = 0; w < 4; ++w) {
+        const int pr[3] = {w, 7 - w, 8 + w};
+        int sl = 0;
+        for (int x = 0; x < 3; ++x)
+            if (pr[x] < T) sl += T - pr[x];
+        best = sl > best ? sl : best;
+    }
+    return best;
+}
+template <int CMAX>
+struct WlimGeom {
+    static constexpr int kTiles = (CMAX + 15) / 16;                  // row tiles of F
+    static constexpr int kLd = 16 * kTiles + 4;                      // staged row stride (doubles)
+    static constexpr int kSlots = wlim_slots(kTiles);
+    // columns of W_R staged per chunk (a barrier pair and a load round trip each): 64 / 32 for
+    // the classes with room, 16 where F fills the LDS
+    static constexpr int kKc = kTiles <= 4 ? 64 : (kTiles <= 8 ? 32 : 16);
+    static constexpr int kLoads = (16 * kTiles * kKc + kThreads - 1) / kThreads;   // floats per thread
+    static constexpr int kFElems = CMAX * (CMAX + 1) / 2;
+    static constexpr int kStageElems = kKc * kLd + kKc;
+    static constexpr int kSmem = kFElems > kStageElems ? kFElems : kStageElems;   // F aliases the staging
+    static_assert(kTiles <= 12, "the snake row-tile map covers 12 row tiles");
+};
+static_assert(WlimGeom<184>::kSlots == 21 && WlimGeom<64>::kSlots == 4 && WlimGeom<128>::kSlots == 9, "slots");
 struct WlimArgs {
     uint32_t n_pairs;
     const uint32_t* pair_movie;
@@ -201,12 +225,15 @@ struct WlimArgs {
     const uint32_t* items;
     const float* theta;     // per movie unit at item_off: eigenvalues of B, ascending
     const uint64_t* w_off;  // per movie unit: its n x n eigenvector block, row-major
-    const float* W;
+    const float* W;         // B's eigenvectors (spill eigen mode 3)
+    const float* W_sym;     // units with sym[v] != 0: L2's own eigenvectors (mode 1), B = L2^2
+    const uint8_t* sym;
     const uint64_t* test_off;
     const uint32_t* test_user;
     const float* test_rating;
     float* wlim;
     uint8_t* solved;
+    int32_t* pair_c;        // rated rows per pair (-1: not counted yet), shared by the classes
 };
 
 // #{theta_j < x} (or <= x) over the ascending eigenvalues
@@ -221,10 +248,21 @@ __device__ __forceinline__ int count_below(const float* th, int n, double x, boo
     return l;
 }
 
-__global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
+// Pairs with CLO < c <= CMAX (c = rated rows of the unit); the others are left to their class.
+// Waves per SIMD the class is held to (its registers): 2 for c <= 128 (two workgroups per CU; at
+// 3 or 4 the c <= 64 class spills 0.6 KB per lane), 1 for the largest class (LDS for one).
+constexpr int wlim_wpe(int cmax) { return cmax <= 64 ? 2 : (cmax <= 128 ? 2 : 1); }
+template <int CMAX, int CLO>
+__global__ __launch_bounds__(kThreads, wlim_wpe(CMAX)) void local_wlim_kernel(WlimArgs a) {
     using f64x4 = __attribute__((ext_vector_type(4))) double;
-    __shared__ double s_F[kWlimFElems];   // packed lower F; the staging tiles alias its start
-    __shared__ int s_R[kWlimCmax];
+    using Geo = WlimGeom<CMAX>;
+    constexpr int kWlimTiles = Geo::kTiles;
+    constexpr int kWlimLd = Geo::kLd;
+    constexpr int kWlimSlots = Geo::kSlots;
+    constexpr int kWlimLoads = Geo::kLoads;
+    constexpr int kWlimKc = Geo::kKc;
+    __shared__ double s_F[Geo::kSmem];   // packed lower F; the staging tiles alias its start
+    __shared__ int s_R[CMAX];
     __shared__ int s_c[kThreads / 64];
     __shared__ double s_x[4];
     double* const Ws = s_F;                        // [kWlimKc][kWlimLd]
@@ -238,6 +276,11 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
         const uint32_t v = a.pair_movie[p], user = a.pair_user[p];
         const uint64_t base = a.item_off[v];
         const int n = (int)(a.item_off[v + 1] - base);
+        {   // another class's pair: skip before any work (its count is known after the first class)
+            const int c0 = a.pair_c[p];
+            if (c0 >= 0 && (c0 <= CLO || c0 > CMAX)) continue;   // uniform
+        }
+        if (n > 65535) continue;   // 32-bit offsets into the n x n block below: mode 2 (solved = 0)
         // rated rows, ascending (row 0, the movie itself, counts as unrated: :405-413)
         int c = 0;
         for (int b0 = 0; b0 < n; b0 += kThreads) {
@@ -252,16 +295,14 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
                 all += s_c[w];
             }
             const int pos = off + __popcll(bal & ((1ull << lane) - 1ull));
-            if (rated && pos < kWlimCmax) s_R[pos] = i;
+            if (rated && pos < CMAX) s_R[pos] = i;
             c += all;
             __syncthreads();
         }
-        if (c > kWlimCmax) {   // uniform
-            if (tid == 0) a.solved[p] = 0;
-            continue;
-        }
+        if (tid == 0) a.pair_c[p] = c;
+        if (c <= CLO || c > CMAX) continue;   // uniform: another class's (c > kWlimCmax: mode 2)
         const float* th = a.theta + base;
-        const float* Wv = a.W + a.w_off[v];
+        const float* Wv = (a.sym && a.sym[v] ? a.W_sym : a.W) + a.w_off[v];
         // this wave's row tiles (snake order over the rows, largest first) and tile slots
         const int nt = (c + 15) >> 4;
         const int pr[3] = {wave, 7 - wave, 8 + wave};
@@ -285,14 +326,17 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
         constexpr int kRowStep = kThreads / kWlimKc;
         static_assert(kRowStep * kWlimLoads >= 16 * kWlimTiles && 16 * kWlimTiles <= kWlimLd,
                       "the staged rows cover every row tile");
-        int sR[kWlimLoads];   // the graph row of each staged row (-1: past c)
+        // 32-bit element offsets of this thread's staged rows in the unit's n x n block (n <=
+        // 65535 keeps them in range; ~0u: past c) -- 64-bit addresses per load were hoisted and
+        // spilled
+        uint32_t roff[kWlimLoads];
 #pragma unroll
         for (int q = 0; q < kWlimLoads; ++q) {
             const int r = srow0 + kRowStep * q;
-            sR[q] = r < c ? s_R[r] : -1;
+            roff[q] = r < c ? (uint32_t)s_R[r] * (uint32_t)n + (uint32_t)scol : ~0u;
         }
         double lo = (double)th[0], hi = (double)th[min(c, n - 1)];
-        double Llo = 0.0, Lhi = 0.0;      // log |det F| at the ends (valid when s*** != 0)
+        double Llo = 0.0, Lhi = 0.0;      // log2 |det F| at the ends (valid when s*** != 0)
         int slo = 0, shi = 0;             // sign of det F at the ends (0: unknown)
         int kept = 0;                     // +1 / -1: which end the last two steps kept
         int last_secant = 0;
@@ -304,7 +348,9 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
             const bool secant = slo != 0 && shi != 0 && slo != shi && poles <= 0 &&
                                 !(last_secant && (hi - lo) > 0.5 * w_prev);
             if (secant) {
-                const double t = 1.0 / (1.0 + exp(fmin(fmax(Lhi - Llo, -700.0), 700.0)));   // |f_lo| / (|f_lo| + |f_hi|)
+                // |f_lo| / (|f_lo| + |f_hi|), from log2 |det F| in fp32 hardware exp2 (the weight only
+                // places mu inside the bracket; the inertia count decides which end moves)
+                const float t = __frcp_rn(1.0f + exp2f(fminf(fmaxf((float)(Lhi - Llo), -120.0f), 120.0f)));
                 const double m2 = lo + t * (hi - lo);
                 if (m2 > lo && m2 < hi) mu = m2;
             }
@@ -317,8 +363,11 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
             float nxt[kWlimLoads];
             auto fetch = [&](int j0) {
 #pragma unroll
-                for (int q = 0; q < kWlimLoads; ++q)
-                    nxt[q] = (sR[q] >= 0 && j0 + scol < n) ? Wv[(size_t)sR[q] * n + j0 + scol] : 0.0f;
+                for (int q = 0; q < kWlimLoads; ++q) {   // branch-free: an in-range load, then a select
+                    const bool ok = roff[q] != ~0u && j0 + scol < n;
+                    const float x = Wv[ok ? roff[q] + (uint32_t)j0 : 0u];
+                    nxt[q] = ok ? x : 0.0f;
+                }
             };
             fetch(0);
             for (int j0 = 0; j0 < n; j0 += kWlimKc) {
@@ -330,14 +379,19 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
                 }
                 for (int jj = tid; jj < kWlimKc; jj += kThreads)
                     Ds[jj] = j0 + jj < n ? 1.0 / ((double)th[j0 + jj] - mu) : 0.0;
-                // rows c .. 16 nt - 1 of the tiles are zero (staged as 0.0 above: sR < 0)
+                // rows c .. 16 nt - 1 of the tiles are zero (staged as 0.0 above: roff = ~0u)
                 __syncthreads();
                 if (j0 + kWlimKc < n) fetch(j0 + kWlimKc);
-#pragma unroll
+                // an offset the compiler cannot see through: the operand addresses below are
+                // recomputed per chunk instead of hoisted out of the chunk loop (they were, for
+                // every (ks, slot), and spilled)
+                int opq = 0;
+                asm volatile("" : "+v"(opq));
+#pragma unroll 2
                 for (int ks = 0; ks < kWlimKc / 4; ++ks) {
                     const int kk = 4 * ks + (lane >> 4);
                     const double dk = Ds[kk];
-                    const double* wrow = Ws + kk * kWlimLd + (lane & 15);
+                    const double* wrow = Ws + opq + kk * kWlimLd + (lane & 15);
                     int pI = -1;
                     double av = 0.0;
 #pragma unroll
@@ -377,7 +431,9 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
                 neg += dk < 0.0;
                 sgn = dk < 0.0 ? -sgn : (dk == 0.0 ? 0 : sgn);
                 if (dk != 0.0) {
-                    ldet += log(fabs(dk));
+                    int ex;   // log2 |dk| = exponent + log2(mantissa): no fp64 log in the loop (its
+                    const double mt = frexp(fabs(dk), &ex);   // constants were hoisted and spilled)
+                    ldet += (double)ex + (double)__log2f((float)mt);
                     const double rdk = 1.0 / dk;
                     const int m = c - 1 - k;   // trailing rows k+1 .. c-1
                     for (int e = tid; e < m * (m + 1) / 2; e += kThreads) {
@@ -397,13 +453,13 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
                     hi = mu;
                     shi = sgn;
                     Lhi = ldet;
-                    if (kept == -1 && slo != 0) Llo -= 0.6931471805599453;
+                    if (kept == -1 && slo != 0) Llo -= 1.0;   // halve |f| (log2)
                     kept = -1;
                 } else {
                     lo = mu;
                     slo = sgn;
                     Llo = ldet;
-                    if (kept == 1 && shi != 0) Lhi -= 0.6931471805599453;
+                    if (kept == 1 && shi != 0) Lhi -= 1.0;
                     kept = 1;
                 }
                 s_x[0] = lo;
@@ -428,6 +484,76 @@ __global__ __launch_bounds__(kThreads) void local_wlim_kernel(WlimArgs a) {
             a.wlim[p] = (float)sqrt(fmax(0.5 * (lo + hi), 0.0));   // as mode 2 (:435-436)
             a.solved[p] = 1;
         }
+    }
+}
+
+// A unit whose local W is symmetric (every w(nb_i -> nb_j) > 0.1 equal to w(nb_j -> nb_i), the
+// thresholded values bit for bit; row and column 0 are the movie's own row by construction,
+// :326-334) has L2 = D^-1/2 (D - W) D^-1/2 symmetric up to the rounding of its two scalings,
+// so B = L2 L2^T = L2^2 to that rounding: B's eigenpairs are (lambda_j^2, v_j) of the mode-1
+// eigendecomposition the predictor already has, and mode 3 is not needed for it.  (On the
+// knn2 graphs of integer ratings w(a, b) == w(b, a) bitwise; a numpy model of the C2-style
+// spill units put the w_lim difference at 2e-8 relative.)  sym[v] starts at 1 for the spill
+// units; one workgroup per (unit, row block) clears it on the first asymmetric pair.
+__global__ __launch_bounds__(kThreads) void local_sym_kernel(const uint32_t* units, uint32_t n_units,
+                                                             const uint64_t* item_off, const uint32_t* items,
+                                                             GraphDev graph, uint8_t* sym) {
+    constexpr int kRows = 8;
+    for (uint32_t w = blockIdx.x; ; w += gridDim.x) {
+        // work item w -> (unit, row block): units in order, ceil(n / kRows) blocks each
+        uint32_t v = 0, rb = w;
+        bool found = false;
+        for (uint32_t x = 0; x < n_units; ++x) {
+            const uint32_t u = units[x];
+            const uint32_t nb = (uint32_t)((item_off[u + 1] - item_off[u] + kRows - 1) / kRows);
+            if (rb < nb) {
+                v = u;
+                found = true;
+                break;
+            }
+            rb -= nb;
+        }
+        if (!found) return;
+        if (!sym[v]) continue;
+        const uint64_t base = item_off[v];
+        const int n = (int)(item_off[v + 1] - base);
+        bool asym = false;
+        for (int i = 1 + (int)rb * kRows; i < n && i < 1 + ((int)rb + 1) * kRows; ++i) {
+            const uint32_t ai = items[base + i];
+            const GraphRow ri = graph.row(ai);
+            for (int j = i + 1 + (int)threadIdx.x; j < n; j += kThreads) {
+                const uint32_t aj = items[base + j];
+                float x = ri[aj], y = graph.row(aj)[ai];
+                if (!((double)x > 0.1)) x = 0.0f;
+                if (!((double)y > 0.1)) y = 0.0f;
+                asym |= __float_as_uint(x) != __float_as_uint(y);
+            }
+        }
+        if (__syncthreads_or(asym) && threadIdx.x == 0) sym[v] = 0;
+    }
+}
+
+// theta_j = lambda_j^2 of a symmetric unit (its B = L2^2), from the mode-1 eigenvalues (fp32,
+// ascending); a unit whose squares are not ascending (a negative lambda_0 of magnitude above
+// lambda_1 -- not seen: lambda_0 = 0 to rounding for a connected unit) is handed back to mode 3.
+__global__ __launch_bounds__(kThreads) void local_theta_kernel(const uint32_t* units, uint32_t n_units,
+                                                               const uint64_t* item_off, const float* evals,
+                                                               float* theta, uint8_t* sym) {
+    for (uint32_t x = blockIdx.x; x < n_units; x += gridDim.x) {
+        const uint32_t v = units[x];
+        if (!sym[v]) continue;
+        const uint64_t base = item_off[v];
+        const int n = (int)(item_off[v + 1] - base);
+        bool bad = false;
+        for (int i = threadIdx.x; i < n; i += kThreads) {
+            const double l = (double)evals[base + i];
+            theta[base + i] = (float)(l * l);
+            if (i > 0) {
+                const double l0 = (double)evals[base + i - 1];
+                bad |= (float)(l * l) < (float)(l0 * l0);
+            }
+        }
+        if (__syncthreads_or(bad) && threadIdx.x == 0) sym[v] = 0;
     }
 }
 
@@ -521,13 +647,16 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
         cf_plan_destroy(mplan);
         return rc;
     }
+    cf_plan* p3plan = nullptr;   // mode 3's plan: the asymmetric spill units
     auto cleanup = [&]() {
         cf_plan_destroy(mplan);
         cf_plan_destroy(pplan);
+        cf_plan_destroy(p3plan);
     };
     const uint64_t n_entries = movie_off[n_movies];
     DevBuf d_moff, d_mitems, d_sqoff, d_evals, d_evecs, d_l2, d_nout, d_toff, d_tuser, d_trat, d_pm, d_pu,
-        d_po, d_wlim, d_mse, d_kk, d_pred, d_lim, d_theta, d_bvec, d_solved;
+        d_po, d_wlim, d_mse, d_kk, d_pred, d_lim, d_theta, d_bvec, d_solved, d_sym, d_units, d_pairc;
+    uint32_t n_sym_units = 0;
     // spill pairs' w_lim by bisection on the movie's B = L2 L2^T (local_wlim_kernel), unless
     // cf_set_local_wlim(ctx, 0) keeps the per-pair tridiagonalisation for every one
     const bool use_bisect = ctx->local_wlim_bisect && n_pairs > n_small;
@@ -565,24 +694,69 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
                                         static_cast<int32_t*>(d_nout.p), 0)))
             break;
         if (use_bisect) {
-            // the eigenpairs of every large movie's B = L2 L2^T (spill eigen mode 3), then one
-            // bisection per spill pair; the pairs it leaves (c > kWlimCmax) go to mode 2 below
+            // the eigenpairs of every large movie's B = L2 L2^T, then one bisection per spill
+            // pair; the pairs it leaves (c > kWlimCmax) go to mode 2 below.  Units with a
+            // symmetric W take B's eigenpairs from mode 1 (local_sym_kernel); the others run
+            // spill eigen mode 3 (CF_LOCAL_SYM=0: every unit on mode 3, for A/B)
+            static const bool sym_on = [] {
+                const char* e = getenv("CF_LOCAL_SYM");
+                return !(e && e[0] == '0');
+            }();
             if ((rc = alloc_copy(d_theta, nullptr, sizeof(float) * n_entries))) break;
-            if ((rc = alloc_copy(d_bvec, nullptr, sizeof(float) * sq_off[n_movies]))) break;
             if ((rc = alloc_copy(d_solved, nullptr, n_pairs))) break;
             CF_HIP_CHECK(ctx, hipMemset(d_solved.p, 0, n_pairs));
-            for (const cf_bucket& b : mplan->buckets) {
-                if (b.emax != kSpillBucket || !b.count) continue;
-                cf_spill_local loc{};
-                loc.mode = 3;
-                loc.l2 = static_cast<float*>(d_l2.p);
-                loc.l2_off = sqo;
-                if ((rc = cf_launch_eigen_spill(ctx, mplan, b, moff, mit, sqo, static_cast<int32_t*>(d_nout.p), nullptr,
-                                                static_cast<float*>(d_theta.p), static_cast<float*>(d_bvec.p), 0,
-                                                &loc)))
+            std::vector<uint32_t> spill_units;
+            for (uint32_t v = 0; v < n_movies; ++v)
+                if (plan_off[v + 1] - plan_off[v] > (uint64_t)CF_MAX_K) spill_units.push_back(v);
+            std::vector<uint8_t> sym(n_movies, 0);
+            if ((rc = alloc_copy(d_sym, nullptr, n_movies))) break;
+            CF_HIP_CHECK(ctx, hipMemset(d_sym.p, 0, n_movies));
+            if (sym_on && !spill_units.empty()) {
+                for (uint32_t v : spill_units) sym[v] = 1;
+                if ((rc = alloc_copy(d_units, spill_units.data(), sizeof(uint32_t) * spill_units.size()))) break;
+                CF_HIP_CHECK(ctx, hipMemcpy(d_sym.p, sym.data(), n_movies, hipMemcpyHostToDevice));
+                const uint32_t nu = (uint32_t)spill_units.size();
+                const auto* du = static_cast<const uint32_t*>(d_units.p);
+                auto* ds = static_cast<uint8_t*>(d_sym.p);
+                hipLaunchKernelGGL(local_sym_kernel, dim3(4096), dim3(kThreads), 0, 0, du, nu, moff, mit, graph_dev(ctx), ds);
+                hipLaunchKernelGGL(local_theta_kernel, dim3(std::min<uint32_t>(nu, 1024u)), dim3(kThreads), 0, 0, du, nu,
+                                   moff, static_cast<const float*>(d_evals.p), static_cast<float*>(d_theta.p), ds);
+                if (hipGetLastError() != hipSuccess) {
+                    rc = cf_set_error(ctx, CF_EHIP, "local symmetry kernels");
                     break;
+                }
+                CF_HIP_CHECK(ctx, hipMemcpy(sym.data(), d_sym.p, n_movies, hipMemcpyDeviceToHost));
             }
-            if (rc != CF_OK) break;
+            // mode 3 over the asymmetric spill units only (symmetric ones get k = 0 in its plan)
+            bool any_mode3 = false;
+            std::vector<uint64_t> p3_off(n_movies + 1, 0);
+            for (uint32_t v = 0; v < n_movies; ++v) {
+                const uint64_t n = plan_off[v + 1] - plan_off[v];
+                const bool m3 = n > (uint64_t)CF_MAX_K && !sym[v];
+                any_mode3 |= m3;
+                p3_off[v + 1] = p3_off[v] + (m3 ? n : 0);
+            }
+            n_sym_units = 0;
+            for (uint32_t v : spill_units) n_sym_units += sym[v];
+            if (getenv("CF_LOCAL_VERBOSE"))
+                fprintf(stderr, "[local] %u of %zu spill units symmetric (mode 3 skipped)\n", n_sym_units,
+                        spill_units.size());
+            if (any_mode3) {
+                if ((rc = alloc_copy(d_bvec, nullptr, sizeof(float) * sq_off[n_movies]))) break;
+                if ((rc = cf_plan_create_cap(ctx, n_movies, p3_off.data(), ~0ull, &p3plan))) break;
+                for (const cf_bucket& b : p3plan->buckets) {
+                    if (b.emax != kSpillBucket || !b.count) continue;
+                    cf_spill_local loc{};
+                    loc.mode = 3;
+                    loc.l2 = static_cast<float*>(d_l2.p);
+                    loc.l2_off = sqo;
+                    if ((rc = cf_launch_eigen_spill(ctx, p3plan, b, moff, mit, sqo, static_cast<int32_t*>(d_nout.p),
+                                                    nullptr, static_cast<float*>(d_theta.p),
+                                                    static_cast<float*>(d_bvec.p), 0, &loc)))
+                        break;
+                }
+                if (rc != CF_OK) break;
+            }
             WlimArgs wa{};
             wa.n_pairs = n_pairs - n_small;
             wa.pair_movie = static_cast<const uint32_t*>(d_pm.p) + n_small;
@@ -592,15 +766,27 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
             wa.theta = static_cast<const float*>(d_theta.p);
             wa.w_off = sqo;
             wa.W = static_cast<const float*>(d_bvec.p);
+            wa.W_sym = static_cast<const float*>(d_evecs.p);
+            wa.sym = static_cast<const uint8_t*>(d_sym.p);
             wa.test_off = static_cast<const uint64_t*>(d_toff.p);
             wa.test_user = static_cast<const uint32_t*>(d_tuser.p);
             wa.test_rating = static_cast<const float*>(d_trat.p);
             wa.wlim = static_cast<float*>(d_wlim.p) + n_small;
             wa.solved = static_cast<uint8_t*>(d_solved.p) + n_small;
+            if ((rc = alloc_copy(d_pairc, nullptr, sizeof(int32_t) * std::max<uint32_t>(wa.n_pairs, 1)))) break;
+            CF_HIP_CHECK(ctx, hipMemset(d_pairc.p, 0xFF, sizeof(int32_t) * std::max<uint32_t>(wa.n_pairs, 1)));   // -1
+            wa.pair_c = static_cast<int32_t*>(d_pairc.p);
             int cus = 0;
             CF_HIP_CHECK(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-            const uint32_t blocks = std::min<uint32_t>(wa.n_pairs, (uint32_t)std::max(1, cus) * 8u);
-            hipLaunchKernelGGL(local_wlim_kernel, dim3(blocks), dim3(kThreads), 0, 0, wa);
+            // the small class first (it counts every pair's c), then the larger ones, which skip
+            // the other classes' pairs at once; a grid of a few workgroups per resident slot
+            const uint32_t cu = (uint32_t)std::max(1, cus);
+            hipLaunchKernelGGL((local_wlim_kernel<64, -1>), dim3(std::min<uint32_t>(wa.n_pairs, cu * 32u)), dim3(kThreads),
+                               0, 0, wa);
+            hipLaunchKernelGGL((local_wlim_kernel<128, 64>), dim3(std::min<uint32_t>(wa.n_pairs, cu * 8u)),
+                               dim3(kThreads), 0, 0, wa);
+            hipLaunchKernelGGL((local_wlim_kernel<kWlimCmax, 128>), dim3(std::min<uint32_t>(wa.n_pairs, cu * 4u)),
+                               dim3(kThreads), 0, 0, wa);
             if (hipGetLastError() != hipSuccess) {
                 rc = cf_set_error(ctx, CF_EHIP, "local_wlim_kernel launch");
                 break;
