@@ -301,7 +301,9 @@ def main():
         return
     if args.prep == "only":
         with Context(dev_index) as pctx:
-            print(json.dumps(prep_leg(args, pctx, dev, torch)), flush=True)
+            res = prep_leg(args, pctx, dev, torch)
+            if not args.pmc_child:
+                print(json.dumps(res), flush=True)
         return
 
     if args.fused == "on" and world > 1:
@@ -1161,6 +1163,7 @@ def prep_leg(args, ctx, dev, torch):
     user = np.repeat(np.arange(n_users, dtype=np.uint32), k.astype(np.int64))
     validate = (np.random.default_rng(seed).random(n) < 0.2).astype(np.uint8)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    reps = 1 if args.pmc_child else 3   # the PMC collector's child: one regroup, nothing else
     d_user, d_movie, d_rat, d_val = T(user.view(np.int32)), T(items.view(np.int32)), T(rats), T(validate)
     U32 = lambda m: torch.empty(max(m, 1), dtype=torch.int32, device=dev)
     OFF = lambda: torch.empty(n_items + 1, dtype=torch.int64, device=dev)
@@ -1175,12 +1178,15 @@ def prep_leg(args, ctx, dev, torch):
     reg_ms, fold_ms = [], []
     rank = np.random.default_rng(5).permutation(n_users).astype(np.uint32)
     d_rank, d_order = T(rank.view(np.int32)), U32(n)
-    for rep in range(3):
+    for rep in range(reps):
         rc = L.cf_knn_regroup_run(ctx.h, n, n_users, n_items, ptr(d_user), ptr(d_movie), ptr(d_rat), ptr(d_val),
                                   ptr(tro), ptr(tru), ptr(trr), ptr(teo), ptr(teu), ptr(ter), ptr(eo), ptr(edg),
                                   cap, ctypes_void(sp))
         ctx._chk(rc, "cf_knn_regroup_run")
         reg_ms.append(ctx.prep_timing())
+        if args.pmc_child:
+            torch.cuda.synchronize(dev)
+            return None
         rc = L.cf_fold_order_run(ctx.h, n, n_users, ptr(d_user), ptr(d_rank), ptr(d_order), ctypes_void(sp))
         ctx._chk(rc, "cf_fold_order_run")
         fold_ms.append(ctx.prep_timing())
@@ -1204,6 +1210,15 @@ def prep_leg(args, ctx, dev, torch):
                      "note": "24 B per rating (SURVEY 8d: 12 read + 12 written) + 4 B per co-rated entry; the "
                              "two sorts and the bitmap are several passes over that"},
     }
+    if args.pmc == "auto" and not args.pmc_child:
+        tr = pmc_traffic(args, prep=True)
+        if tr is not None:
+            fetch, write = tr["prep"]
+            out["roofline"].update({
+                "traffic": 2.0 * fetch + write, "traffic_fetch_bytes_raw": fetch, "traffic_write_bytes": write,
+                "traffic_note": "HBM bytes of every kernel of ONE cf_knn_regroup_run in a child call (the "
+                                "regroup kernels and rocprim's radix sorts and scans), rocprofv3 --pmc FETCH_SIZE "
+                                "and WRITE_SIZE in separate passes; traffic = 2 x FETCH_SIZE + WRITE_SIZE"})
     if not args.no_cpu_baseline:
         # the oracle's C++ restatement with the reference's containers (a std::map per movie and
         # role, sorted unique co-rated lists) on every host thread, over the WHOLE rating set, so
@@ -1378,7 +1393,7 @@ def knn2_leg(args, ctx, dev, torch):
     return out
 
 
-def pmc_traffic(args, knn2=False):
+def pmc_traffic(args, knn2=False, prep=False):
     """FETCH_SIZE and WRITE_SIZE (bytes) summed over the predict_kernel and eigen_kernel
     launches of one child step, each counter in its own rocprofv3 run (MI355X_MICROARCH.md:
     FETCH_SIZE costs 3 TCC slots, WRITE_SIZE 2, so they cannot share a pass).  knn2: the
@@ -1392,12 +1407,14 @@ def pmc_traffic(args, knn2=False):
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None
-    out = {"predict": [0.0, 0.0], "eigen": [0.0, 0.0], "eigen12": [0.0, 0.0], "knn2": [0.0, 0.0]}
+    out = {"predict": [0.0, 0.0], "eigen": [0.0, 0.0], "eigen12": [0.0, 0.0], "knn2": [0.0, 0.0], "prep": [0.0, 0.0]}
     child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", args.config,
              "--users", str(args.users)]
     if knn2:
         child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--knn2", "only", "--knn2-users",
                  str(args.knn2_users), "--knn2-items", str(args.knn2_items)]
+    if prep:
+        child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--prep", "only", "--no-cpu-baseline"]
     env = dict(os.environ, TMPDIR="/tmp")
     for slot, counter in enumerate(("FETCH_SIZE", "WRITE_SIZE")):
         d = tempfile.mkdtemp(prefix="cf_pmc_", dir="/tmp")
@@ -1408,6 +1425,10 @@ def pmc_traffic(args, knn2=False):
             path = os.path.join(d, "run_counter_collection.csv")
             for r in csv.DictReader(open(path)):
                 name = r["Kernel_Name"]
+                if prep:   # every kernel of the one regroup call but torch's own
+                    if not re.search(r"at::native", name) and r["Counter_Name"] == counter:
+                        out["prep"][slot] += float(r["Counter_Value"]) * 1024.0
+                    continue
                 if knn2:
                     if re.search(r"knn2_(code|i8|f32)_kernel", name) and r["Counter_Name"] == counter:
                         out["knn2"][slot] += float(r["Counter_Value"]) * 1024.0

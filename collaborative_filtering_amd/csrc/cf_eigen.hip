@@ -122,6 +122,7 @@ struct EigenArgs {
     uint32_t cmask_users;
     const uint8_t* solved;      // kSigma, spill pairs: w_lim already written (local_wlim_kernel)
     int skip_spill;             // kSigma: every spill pair is solved, no spill launch
+    int skip_emax_min;          // > 0: LDS buckets with emax >= it are left out (the hybrid method)
 };
 
 // Test rating of `user` for compact item `movie` (0 if absent): binary search of the
@@ -846,6 +847,7 @@ int launch_buckets_on(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStrea
         }
         int rc;
         if (b.emax == kSpillBucket && args.skip_spill) continue;
+        if (args.skip_emax_min > 0 && b.emax >= args.skip_emax_min) continue;
         if (b.emax == kSpillBucket) {
             // n > 192: the fp64 HBM-workspace solver; a8 units in its local-graph / w_lim modes
             cf_spill_local loc{};
@@ -1083,8 +1085,25 @@ int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off
     args.cmask_words = args.cmask_out ? ctx->cmask_bytes / sizeof(uint64_t) : 0;
     args.cmask_fp = args.cmask_out ? ctx->d_cmask_fp : nullptr;
     args.cmask_users = args.cmask_out ? ctx->cmask_users : 0;
+    // CF_EIGEN_HYBRID=1 (A/B): bucket 12 (k 177-192) on the Householder + QL path, the other
+    // buckets on Jacobi.  Its users get no complement masks (the predictor gathers their rows;
+    // their fingerprints stay unwritten, so no stale mask can match)
+    static const bool hybrid = [] {
+        const char* e = getenv("CF_EIGEN_HYBRID");
+        return e && e[0] == '1';
+    }();
+    bool tri12 = false;
+    if (hybrid)
+        for (const cf_bucket& b : plan->buckets) tri12 |= b.emax == 12 && b.count > 0;
+    if (tri12) {
+        args.skip_emax_min = 12;
+        if (args.cmask_out && ctx->d_cmask_fp)   // bucket 12 writes none: no fingerprint may survive
+            CF_HIP_CHECK(ctx, hipMemsetAsync(ctx->d_cmask_fp, 0, sizeof(uint64_t) * ctx->cmask_users, stream));
+    }
     cf_cmask_mark(ctx, plan, d_item_off, d_items, false);
-    const int rc = launch_all_buckets(ctx, plan, args, stream);
+    int rc = launch_all_buckets(ctx, plan, args, stream);
+    if (rc == CF_OK && tri12)
+        rc = cf_launch_eigen_tri(ctx, plan, d_item_off, d_items, d_evec_off, d_m, d_sigs, d_evals, d_evecs, stream, 12);
     cf_cmask_mark(ctx, plan, d_item_off, d_items, rc == CF_OK && args.cmask_out);
     return rc;
 }

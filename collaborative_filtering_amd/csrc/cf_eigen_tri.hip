@@ -742,6 +742,7 @@ int cf_tri_prepare(cf_ctx* ctx, cf_plan* plan, const uint64_t* item_off) {
     for (const cf_bucket& b : plan->buckets) {
         if (b.emax == kSpillBucket || b.count == 0) continue;
         uint32_t start = b.first;
+        open = false;   // a group never spans buckets (cf_launch_eigen_tri's emax_min runs whole groups)
         for (uint32_t j = b.first; j < b.first + b.count; ++j) {
             const uint32_t u = plan->h_order[j];
             const uint64_t k = item_off[u + 1] - item_off[u];
@@ -814,7 +815,7 @@ static int tri_scratch(cf_ctx* ctx, const cf_plan* plan, TriArgs& a) {
 
 int cf_launch_eigen_tri(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,
                         const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals, float* d_evecs,
-                        hipStream_t stream) {
+                        hipStream_t stream, int emax_min) {
     if (plan->tri_groups.empty()) return CF_OK;
     TriArgs a{};
     CF_TRY(tri_scratch(ctx, plan, a));
@@ -842,6 +843,10 @@ int cf_launch_eigen_tri(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item
     }
     for (uint32_t gi = 0; gi < plan->tri_groups.size(); ++gi) {
         const cf_tri_group& g = plan->tri_groups[gi];
+        bool wanted = false;   // groups lie inside one bucket: its chunks share one emax
+        for (const cf_tri_chunk& c : plan->tri_chunks)
+            if (c.group == gi) wanted = c.emax >= emax_min;
+        if (!wanted) continue;
         a.group_first = g.first;
         for (const cf_tri_chunk& c : plan->tri_chunks) {
             if (c.group != gi) continue;

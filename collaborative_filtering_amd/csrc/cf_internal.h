@@ -347,9 +347,10 @@ int cf_launch_local_predict_spill(cf_ctx* ctx, uint32_t n_pairs, int nmax, const
                                   const uint32_t* d_test_user, const float* d_test_rating, float* d_mse,
                                   int32_t* d_kk, double* d_pred, int32_t* d_lim, hipStream_t stream);
 int cf_tri_prepare(cf_ctx* ctx, cf_plan* plan, const uint64_t* item_off);
+// emax_min: only the LDS buckets with emax >= emax_min (1: all; the hybrid method: 12)
 int cf_launch_eigen_tri(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off, const uint32_t* d_items,
                         const uint64_t* d_evec_off, int32_t* d_m, float* d_sigs, float* d_evals, float* d_evecs,
-                        hipStream_t stream);
+                        hipStream_t stream, int emax_min = 1);
 // Jacobi kernel over plan order [first, first + count) of LDS bucket emax, only for users
 // with flag[j - first] != 0 (fallback of the tridiagonal path); d_cmask (optional) receives
 // the predictor's complement masks, 3 words per rating at 3 * item_off[u] (the fused step).

@@ -189,7 +189,7 @@ __global__ __launch_bounds__(kThreads) void local_predict_kernel(LocalPredArgs a
 // LDL^T pivot), and more resident pairs hide them (r05: one 29 s launch at one wave per SIMD).
 constexpr int kWlimCmax = 184;   // largest class: every pair of a k <= 180 user
 constexpr int kWlimIters = 64;
-constexpr double kWlimTol = 1e-10;   // relative bracket width at exit (w_lim is fp32)
+constexpr double kWlimTol = 1e-9;    // relative bracket width at exit (w_lim = sqrt, fp32: 5e-10 << 6e-8)
 // accumulator tiles of the busiest wave under the snake row-tile map {w, 7 - w, 8 + w}
 constexpr int wlim_slots(int T) {
     int best = 0;
@@ -207,9 +207,9 @@ struct WlimGeom {
     static constexpr int kTiles = (CMAX + 15) / 16;                  // row tiles of F
     static constexpr int kLd = 16 * kTiles + 4;                      // staged row stride (doubles)
     static constexpr int kSlots = wlim_slots(kTiles);
-    // columns of W_R staged per chunk (a barrier pair and a load round trip each): 64 / 32 for
-    // the classes with room, 16 where F fills the LDS
-    static constexpr int kKc = kTiles <= 4 ? 64 : (kTiles <= 8 ? 32 : 16);
+    // columns of W_R staged per chunk (a barrier pair and a load round trip each): 32 for the
+    // classes with room, 16 where F's registers fill the file (64 spilled)
+    static constexpr int kKc = (kTiles > 4 && kTiles <= 8) ? 32 : 16;
     static constexpr int kLoads = (16 * kTiles * kKc + kThreads - 1) / kThreads;   // floats per thread
     static constexpr int kFElems = CMAX * (CMAX + 1) / 2;
     static constexpr int kStageElems = kKc * kLd + kKc;
@@ -234,6 +234,7 @@ struct WlimArgs {
     float* wlim;
     uint8_t* solved;
     int32_t* pair_c;        // rated rows per pair (-1: not counted yet), shared by the classes
+    unsigned long long* stats;   // optional (CF_LOCAL_VERBOSE): per class {pairs, iterations, secant steps, c}
 };
 
 // #{theta_j < x} (or <= x) over the ascending eigenvalues
@@ -265,6 +266,7 @@ __global__ __launch_bounds__(kThreads, wlim_wpe(CMAX)) void local_wlim_kernel(Wl
     __shared__ int s_R[CMAX];
     __shared__ int s_c[kThreads / 64];
     __shared__ double s_x[4];
+    __shared__ double s_red[2 * (kThreads / 64)];
     double* const Ws = s_F;                        // [kWlimKc][kWlimLd]
     double* const Ds = s_F + kWlimKc * kWlimLd;    // [kWlimKc]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -336,14 +338,59 @@ __global__ __launch_bounds__(kThreads, wlim_wpe(CMAX)) void local_wlim_kernel(Wl
             roff[q] = r < c ? (uint32_t)s_R[r] * (uint32_t)n + (uint32_t)scol : ~0u;
         }
         double lo = (double)th[0], hi = (double)th[min(c, n - 1)];
+        bool guess = false;   // hi is the Rayleigh bound: the first trial point sits just below it
+        if (c > 0) {
+            // A tighter upper end: lambda_min(B_hh) <= the Rayleigh quotient of x = w_0 with its
+            // rated rows zeroed (B's lowest eigenvector, whose eigenvalue the deletion lifts the
+            // least).  In B's eigenbasis z = W^T x = e_0 - s, s_j = sum_{r in R} W_rj W_r0, so
+            // x^T B x / x^T x = sum_j theta_j z_j^2 / sum_j z_j^2: c n multiply-adds, about one
+            // F-build's loads and no MFMA, against the ~5 bisections from theta_c it saves (r06:
+            // 29-31 iterations per pair on the C2 leg).  The 1e-6 margin covers fp32 W's
+            // departure from orthonormality.
+            double* w0 = s_F;   // c <= CMAX doubles; F / the staging are not in use yet
+            for (int r = tid; r < c; r += kThreads) w0[r] = (double)Wv[(uint32_t)s_R[r] * (uint32_t)n];
+            __syncthreads();
+            double num = 0.0, den = 0.0;
+            for (int j = tid; j < n; j += kThreads) {
+                double sj = 0.0;
+                for (int r = 0; r < c; ++r) sj = fma((double)Wv[(uint32_t)s_R[r] * (uint32_t)n + (uint32_t)j], w0[r], sj);
+                const double z = (j == 0 ? 1.0 : 0.0) - sj;
+                num = fma((double)th[j] * z, z, num);
+                den = fma(z, z, den);
+            }
+            num = wave_sum(num);
+            den = wave_sum(den);
+            if (lane == 0) {
+                s_red[2 * wave] = num;
+                s_red[2 * wave + 1] = den;
+            }
+            __syncthreads();
+            num = den = 0.0;
+            for (int w = 0; w < kThreads / 64; ++w) {
+                num += s_red[2 * w];
+                den += s_red[2 * w + 1];
+            }
+            if (den > 0.0) {
+                const double rq = num / den * (1.0 + 1e-6);
+                if (rq > lo && rq < hi) {
+                    hi = rq;
+                    guess = true;
+                }
+            }
+            __syncthreads();   // w0 (s_F) is reused as the staging area below
+        }
         double Llo = 0.0, Lhi = 0.0;      // log2 |det F| at the ends (valid when s*** != 0)
         int slo = 0, shi = 0;             // sign of det F at the ends (0: unknown)
         int kept = 0;                     // +1 / -1: which end the last two steps kept
         int last_secant = 0;
         double w_prev = hi - lo;
+        int n_it = 0, n_sec = 0;
         for (int it = 0; it < kWlimIters && c > 0 && hi - lo > kWlimTol * fabs(hi); ++it) {
+            ++n_it;
             // ---- next mu: Illinois regula falsi inside a pole-free bracket, else bisection
-            double mu = 0.5 * (lo + hi);
+            // (the Rayleigh bound lies within ~0.4% above lambda_min on the test units: the first
+            // trial 1% of the bracket below it usually lands under the root, a 1% bracket)
+            double mu = it == 0 && guess ? lo + 0.99 * (hi - lo) : 0.5 * (lo + hi);
             const int poles = count_below(th, n, hi) - count_below(th, n, lo, true);   // theta_j in (lo, hi)
             const bool secant = slo != 0 && shi != 0 && slo != shi && poles <= 0 &&
                                 !(last_secant && (hi - lo) > 0.5 * w_prev);
@@ -355,6 +402,7 @@ __global__ __launch_bounds__(kThreads, wlim_wpe(CMAX)) void local_wlim_kernel(Wl
                 if (m2 > lo && m2 < hi) mu = m2;
             }
             last_secant = secant;
+            n_sec += secant;
             w_prev = hi - lo;
             // ---- F(mu) = W_R diag(1 / (theta - mu)) W_R^T on the matrix cores
             f64x4 acc[kWlimSlots];
@@ -387,7 +435,7 @@ __global__ __launch_bounds__(kThreads, wlim_wpe(CMAX)) void local_wlim_kernel(Wl
                 // every (ks, slot), and spilled)
                 int opq = 0;
                 asm volatile("" : "+v"(opq));
-#pragma unroll 2
+#pragma unroll
                 for (int ks = 0; ks < kWlimKc / 4; ++ks) {
                     const int kk = 4 * ks + (lane >> 4);
                     const double dk = Ds[kk];
@@ -483,6 +531,13 @@ __global__ __launch_bounds__(kThreads, wlim_wpe(CMAX)) void local_wlim_kernel(Wl
         if (tid == 0) {
             a.wlim[p] = (float)sqrt(fmax(0.5 * (lo + hi), 0.0));   // as mode 2 (:435-436)
             a.solved[p] = 1;
+            if (a.stats) {
+                const int cls = CMAX <= 64 ? 0 : (CMAX <= 128 ? 1 : 2);
+                atomicAdd(&a.stats[4 * cls + 0], 1ull);
+                atomicAdd(&a.stats[4 * cls + 1], (unsigned long long)n_it);
+                atomicAdd(&a.stats[4 * cls + 2], (unsigned long long)n_sec);
+                atomicAdd(&a.stats[4 * cls + 3], (unsigned long long)c);
+            }
         }
     }
 }
@@ -655,7 +710,7 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
     };
     const uint64_t n_entries = movie_off[n_movies];
     DevBuf d_moff, d_mitems, d_sqoff, d_evals, d_evecs, d_l2, d_nout, d_toff, d_tuser, d_trat, d_pm, d_pu,
-        d_po, d_wlim, d_mse, d_kk, d_pred, d_lim, d_theta, d_bvec, d_solved, d_sym, d_units, d_pairc;
+        d_po, d_wlim, d_mse, d_kk, d_pred, d_lim, d_theta, d_bvec, d_solved, d_sym, d_units, d_pairc, d_wstats;
     uint32_t n_sym_units = 0;
     // spill pairs' w_lim by bisection on the movie's B = L2 L2^T (local_wlim_kernel), unless
     // cf_set_local_wlim(ctx, 0) keeps the per-pair tridiagonalisation for every one
@@ -776,6 +831,12 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
             if ((rc = alloc_copy(d_pairc, nullptr, sizeof(int32_t) * std::max<uint32_t>(wa.n_pairs, 1)))) break;
             CF_HIP_CHECK(ctx, hipMemset(d_pairc.p, 0xFF, sizeof(int32_t) * std::max<uint32_t>(wa.n_pairs, 1)));   // -1
             wa.pair_c = static_cast<int32_t*>(d_pairc.p);
+            const bool verbose = getenv("CF_LOCAL_VERBOSE") != nullptr;
+            if (verbose) {
+                if ((rc = alloc_copy(d_wstats, nullptr, 12 * sizeof(unsigned long long)))) break;
+                CF_HIP_CHECK(ctx, hipMemset(d_wstats.p, 0, 12 * sizeof(unsigned long long)));
+                wa.stats = static_cast<unsigned long long*>(d_wstats.p);
+            }
             int cus = 0;
             CF_HIP_CHECK(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
             // the small class first (it counts every pair's c), then the larger ones, which skip
@@ -790,6 +851,16 @@ extern "C" int cf_local_calc(cf_ctx* ctx, uint32_t n_movies, const uint64_t* mov
             if (hipGetLastError() != hipSuccess) {
                 rc = cf_set_error(ctx, CF_EHIP, "local_wlim_kernel launch");
                 break;
+            }
+            if (verbose) {
+                unsigned long long st[12];
+                CF_HIP_CHECK(ctx, hipMemcpy(st, d_wstats.p, sizeof(st), hipMemcpyDeviceToHost));
+                for (int cl = 0; cl < 3; ++cl)
+                    fprintf(stderr, "[local] w_lim class c <= %d: %llu pairs, %.2f iterations (%.2f secant), mean c %.1f\n",
+                            cl == 0 ? 64 : (cl == 1 ? 128 : kWlimCmax), st[4 * cl],
+                            st[4 * cl] ? (double)st[4 * cl + 1] / st[4 * cl] : 0.0,
+                            st[4 * cl] ? (double)st[4 * cl + 2] / st[4 * cl] : 0.0,
+                            st[4 * cl] ? (double)st[4 * cl + 3] / st[4 * cl] : 0.0);
             }
             // the per-pair solver's workspace is sized by the largest unit (2 n^2 fp64 per slot:
             // 1.6 GB at n = 10,000): skip its launch when the bisection solved every spill pair

@@ -1,0 +1,9 @@
+# Round 6 batch C: local_calc tests + the C2 local_calc leg (w_lim classes, Rayleigh bracket).
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+tag=${1:-c1}
+timeout -k 10 700 python -u -m pytest tests/test_gpu_local.py -x -v -s --timeout 400 --timeout-method thread > gpurun_out/r6_local_tests_$tag.log 2>&1
+rc=$?; echo tests_rc=$rc; grep -E "passed|failed|FAILED|Error|unit n =|bisection:" gpurun_out/r6_local_tests_$tag.log | tail -12 | cut -c1-300
+[ $rc -eq 0 ] || exit $rc
+CF_LOCAL_VERBOSE=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6_localprof_$tag -o run -- python3 -u tools/local_leg.py c2 1 > gpurun_out/r6_local_leg_$tag.log 2>&1
+echo leg_rc=$?; grep -E "^\[local\]|predictions_per_s" gpurun_out/r6_local_leg_$tag.log | cut -c1-400
+f=$(find gpurun_out/r6_localprof_$tag -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cp "$f" gpurun_out/r6_local_kernel_stats_$tag.csv && cut -d, -f1-4 "$f" | head -10 | cut -c1-150
