@@ -36,6 +36,8 @@ SIGNATURES = {
     "cf_last_error": (c_char_p, [c_void_p]),
     "cf_set_jacobi": (c_int, [c_void_p, c_float, c_int]),
     "cf_set_eigen_refine": (c_int, [c_void_p, c_int, c_float, c_float]),
+    "cf_set_eigen_split": (c_int, [c_void_p, c_int]),
+    "cf_debug_split_schedule": (c_int, [c_int, c_int, POINTER(c_int), POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
     "cf_set_step_masks": (c_int, [c_void_p, c_int]),
     "cf_set_local_wlim": (c_int, [c_void_p, c_int]),
     "cf_debug_predict_nmax": (c_int, [c_int]),

@@ -101,6 +101,10 @@ class Context:
         """Jacobi sweeps to stop_rel, then the first-order Gram refinement (cf_set_eigen_refine)."""
         self._chk(self.lib.cf_set_eigen_refine(self.h, int(enable), stop_rel, delta), "cf_set_eigen_refine")
 
+    def set_eigen_split(self, enable: bool = True):
+        """Buckets with k > 128: Jacobi sweeps in the split layout, two users per CU (cf_set_eigen_split)."""
+        self._chk(self.lib.cf_set_eigen_split(self.h, int(enable)), "cf_set_eigen_split")
+
     def set_local_wlim(self, bisect: bool = True):
         """local_calc spill pairs: w_lim by bisection on the movie's B = L2 L2^T (cf_set_local_wlim)."""
         self._chk(self.lib.cf_set_local_wlim(self.h, int(bisect)), "cf_set_local_wlim")

@@ -180,6 +180,8 @@ void cf_destroy(cf_ctx* ctx) {
     }
     if (ctx->h_pspill_meta) (void)hipHostFree(ctx->h_pspill_meta);
     if (ctx->d_tri) (void)hipFree(ctx->d_tri);
+    for (uint32_t* p : ctx->d_split_sched)
+        if (p) (void)hipFree(p);
     for (hipEvent_t& e : ctx->knn_ev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t& e : ctx->aux_event)

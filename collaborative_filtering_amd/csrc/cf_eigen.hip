@@ -26,118 +26,10 @@
 //
 // No MFMA: the matrices are tiny and the work is rotation-shaped, not GEMM-shaped.
 
-#include "cf_internal.h"
+#include "cf_eigen_common.h"
 
 namespace {
-
-constexpr int kGroup = 8;   // lanes per column pair (half a DPP row)
-// Stopping rule: iterate while a sweep made a rotation with |gamma| > kSigRot * tol * sqrt(al be)
-// (rotations above tol are always applied).  A numpy model of this kernel on C2 users kept the
-// same eigenvalue error and final off-diagonal level with 1-2 fewer sweeps (of ~10) at
-// kSigRot = 4..16; on the GPU (C2 mix) 4 / 8 / 16 gave 8.47 / 8.22 / 7.95 sweeps with the same
-// parity (profiles/r02/eigen_ab_v4_kappa.txt).  kSigRot2 = kSigRot^2 = 256.
-#ifndef CF_EIGEN_SIGROT2
-#define CF_EIGEN_SIGROT2 256.0f
-#endif
-constexpr float kSigRot2 = CF_EIGEN_SIGROT2;
-
-using f2 = __attribute__((ext_vector_type(2))) float;
-using f4 = __attribute__((ext_vector_type(4))) float;
-// A column read as volatile 8-byte loads: plain loads 64 B apart get fused into
-// ds_read2_b64, which the LDS serves at half the rate of two ds_read_b64 (128 vs 256 B/clk;
-// MI355X_MICROARCH.md, LDS table).  Volatile accesses are never fused.
-__device__ __forceinline__ f2 lds_ld(const f2* p) {
-    return *(const volatile __attribute__((address_space(3))) f2*)(p);
-}
-// Column stores likewise: un-fused ds_write_b64 instead of ds_write2_b64 (CF_EIGEN_FUSED_ST=1
-// keeps the compiler's pairing, for A/B).
-__device__ __forceinline__ void lds_st(f2* p, f2 v) {
-#if defined(CF_EIGEN_FUSED_ST) && CF_EIGEN_FUSED_ST
-    *p = v;
-#else
-    *(volatile __attribute__((address_space(3))) f2*)(p) = v;
-#endif
-}
-
-
-template <int CTRL>
-__device__ __forceinline__ float dpp_mov(float x) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
-}
-
-// All-reduce (sum) over the 8 lanes of a column pair; every lane receives the total.
-__device__ __forceinline__ float pair_sum(float x) {
-    x += dpp_mov<0xB1>(x);   // quad_perm [1,0,3,2]
-    x += dpp_mov<0x4E>(x);   // quad_perm [2,3,0,1]
-    x += dpp_mov<0x141>(x);  // row_half_mirror (lanes i <-> 7-i within 8)
-    return x;
-}
-
-// Launch modes (uniform per launch):
-//   kUser  : a2-a4, one user's item subgraph (compute_eigens, precompute_local_threads.cpp)
-//   kLocal : a8, one movie's local graph (local_calc.cpp:268-378): star-shaped W, w > 0.1,
-//            no 0 -> 1 degree rule, all n eigenpairs, full L2 written out
-//   kSigma : a8 w_lim (local_calc.cpp:402-436) of one (movie, test user) pair: the singular
-//            values of the unrated rows of the movie's L2, by the same one-sided Jacobi
-enum EigenMode : int { kUser = 0, kLocal = 1, kSigma = 2 };
-
-struct EigenArgs {
-    int mode;
-    const uint32_t* order;
-    uint32_t first;
-    const uint64_t* item_off;
-    const uint32_t* items;
-    GraphDev graph;
-    uint64_t n_items;
-    const uint64_t* evec_off;
-    int32_t* m_out;
-    float* sigs;
-    float* evals;
-    float* evecs;
-    float tol_scale;
-    int max_sweeps;
-    // kUser: stop after a sweep with no rotation above stop_rel * sqrt(al be), then one
-    // first-order Gram refinement (section 4b) when refine != 0; else the kSigRot * tol rule
-    int refine;
-    float stop_rel;
-    float refine_delta;
-    float close_sigrot;   // close pairs converge to close_sigrot * tol
-    int sort_sweeps;      // reorder the columns by norm before every sweep: 2 ascending, 1 descending, 0 off
-    unsigned long long* stats;
-    // kLocal / kSigma
-    float* l2;                  // per movie n x n row-major L2 (kLocal writes, kSigma reads)
-    const uint64_t* l2_off;
-    const uint32_t* pair_movie; // kSigma: unit -> (movie unit, test user)
-    const uint32_t* pair_user;
-    const uint64_t* test_off;   // test ratings CSR over compact item ids, users ascending
-    const uint32_t* test_user;
-    const float* test_rating;
-    float* wlim;                // kSigma output per pair
-    const int* only_flag;       // non-null: run only units j with only_flag[blockIdx.x] != 0
-    // kUser, optional: the predictor's complement masks from the gathered W, 3 words per row at
-    // 3 * item_off[u] (bit i of word 3r + (i >> 6) = !(w(item_r -> item_i) > 0.1), cf_predict.hip)
-    uint64_t* cmask_out;
-    uint64_t cmask_words;       // its extent (users beyond it write none)
-    uint64_t* cmask_fp;         // per user: cf_items_fp of the items the masks were built from
-    uint32_t cmask_users;
-    const uint8_t* solved;      // kSigma, spill pairs: w_lim already written (local_wlim_kernel)
-    int skip_spill;             // kSigma: every spill pair is solved, no spill launch
-    int skip_emax_min;          // > 0: LDS buckets with emax >= it are left out (the hybrid method)
-};
-
-// Test rating of `user` for compact item `movie` (0 if absent): binary search of the
-// ascending user list (the reference's map lookup with a default of 0, local_calc.cpp:318).
-__device__ __forceinline__ float test_rating(const EigenArgs& a, uint32_t movie, uint32_t user) {
-    uint64_t lo = a.test_off[movie];
-    const uint64_t end = a.test_off[movie + 1];
-    uint64_t hi = end;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (a.test_user[mid] < user) lo = mid + 1;
-        else hi = mid;
-    }
-    return (lo < end && a.test_user[lo] == user) ? a.test_rating[lo] : 0.0f;
-}
+using namespace cf_eig;
 
 // Bucket geometry: k <= NR = 16 * EMAX rows.  A column is read/written as float2
 // (ds_read_b64 / ds_write_b64): lane l of a pair owns rows 16t + 2l, 16t + 2l + 1.
@@ -172,7 +64,10 @@ struct EigenGeom {
 static_assert(EigenGeom<12, true>::LD % 64 == 16, "narrow bucket-12 layout must be conflict-free");
 static_assert(EigenGeom<12, true>::bytes() <= 163840, "narrow bucket-12 layout exceeds 160 KiB LDS");
 
-template <int EMAX, bool NARROW = false>
+// RESUME (kUser, buckets >= kSplitEmaxMin): the split-storage kernel (cf_eigen_split.hip) has run
+// stages 1-4 and left B column-major in the user's eigenvector slot, the drifts in evals and the
+// sigs written; this instantiation loads them and runs stages 4b and 5.
+template <int EMAX, bool NARROW = false, bool RESUME = false>
 __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NARROW>::WPE)) void eigen_kernel(EigenArgs a) {
     using G = EigenGeom<EMAX, NARROW>;
     constexpr int NR = G::NR;
@@ -218,6 +113,13 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
     for (int i = tid; i < nrows; i += NT) s_item[i] = a.items[base + i];
     for (int idx = tid; idx < G::NC * LD; idx += NT) B[idx] = 0.0f;
     __syncthreads();
+    if constexpr (RESUME) {
+        const float* hb = a.evecs + a.evec_off[u];
+        for (int j = wave; j < k; j += NW)
+            for (int i = lane; i < k; i += 64) B[bidx(i, j)] = hb[(size_t)j * k + i];
+        for (int j = tid; j < k; j += NT) s_dev[j] = a.evals[base + j];
+        __syncthreads();
+    } else
     if (mode == kSigma) {
         // ---- 1s. B's columns = the unrated rows of the movie's L2 (row 0 counts as
         // unrated, :405-413), in row order (ordered ballot compaction into s_perm)
@@ -352,6 +254,7 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
     float* s_nrm = s_l2d;
     constexpr int NG = NT / kGroup;
     int sweep = 0;
+    if constexpr (!RESUME) {
     for (; sweep < a.max_sweeps && k > 1; ++sweep) {
         for (int c = g; c < k; c += NG) {
             const f2* bc = reinterpret_cast<const f2*>(B + c * LD);
@@ -549,8 +452,9 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
         if (tid == 0) s_flag[0] = 0;
         __syncthreads();
     }
+    }   // !RESUME
     if (a.stats && tid == 0) t_phase2 = __builtin_amdgcn_s_memtime();
-    if (a.stats && tid == 0) {
+    if (!RESUME && a.stats && tid == 0) {
         atomicAdd(&a.stats[0], (unsigned long long)(sweep + 1));
         atomicAdd(&a.stats[1], 1ull);
         atomicMax(&a.stats[2], (unsigned long long)(sweep + 1));
@@ -736,9 +640,14 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
         // monotone in mu and the order is ascending in mu, so it equals the count of
         // eigenpairs with !(lambda > smm): one block-wide count instead of a serial walk.
         float smm = 0.0f;
-        for (int i = 0; i < k; ++i)
-            if (smm < s_sig[i]) smm = s_sig[i];
-        smm = (float)((double)smm + 0.01);              // (:182)
+        if constexpr (RESUME) {
+            // sigs hold (float)(sig + 0.01), monotone in sig: their max is the max's image
+            for (int i = 0; i < k; ++i) smm = fmaxf(smm, a.sigs[base + i]);
+        } else {
+            for (int i = 0; i < k; ++i)
+                if (smm < s_sig[i]) smm = s_sig[i];
+            smm = (float)((double)smm + 0.01);          // (:182)
+        }
         const bool below = tid < k && !((double)(s_mu[tid] - 1.0f) > (double)smm);
         int lim = __syncthreads_count(below);
         if (lim < 2) lim = 2;                            // (:190-191)
@@ -752,7 +661,7 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
     }
     __syncthreads();
     const int m = s_flag[1];
-    if (mode == kUser)
+    if (mode == kUser && !RESUME)
         for (int i = tid; i < k; i += NT) a.sigs[base + i] = (float)((double)s_sig[i] + 0.01);
     for (int r = tid; r < m && r < k; r += NT) a.evals[base + r] = s_mu[s_perm[r]] - 1.0f;
     float* out = a.evecs + a.evec_off[u];
@@ -768,40 +677,80 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
     }
     if (a.stats && tid == 0) {
         const unsigned long long t3 = __builtin_amdgcn_s_memtime();
-        atomicAdd(&a.stats[4], t_phase1 - t_phase0);
-        atomicAdd(&a.stats[5], t_phase2 - t_phase1);
         atomicAdd(&a.stats[6], t3 - t_phase2);
-        int steps = 0;   // steps per sweep of the recursive-halving ordering
-        for (int L = 0; ((n + (1 << L) - 1) >> L) >= 2; ++L) steps += (((n + (1 << L) - 1) >> L) + 1) >> 1;
-        atomicAdd(&a.stats[7], (unsigned long long)((sweep + 1) * steps));
+        if constexpr (!RESUME) {   // the split kernel counts its own phases and steps
+            atomicAdd(&a.stats[4], t_phase1 - t_phase0);
+            atomicAdd(&a.stats[5], t_phase2 - t_phase1);
+            int steps = 0;   // steps per sweep of the recursive-halving ordering
+            for (int L = 0; ((n + (1 << L) - 1) >> L) >= 2; ++L) steps += (((n + (1 << L) - 1) >> L) + 1) >> 1;
+            atomicAdd(&a.stats[7], (unsigned long long)((sweep + 1) * steps));
+        }
     }
 }
 
-template <int EMAX, bool NARROW = false>
-int launch_bucket(cf_ctx* ctx, const EigenArgs& args, uint32_t count, hipStream_t stream) {
+template <int EMAX, bool NARROW = false, bool RESUME = false>
+int launch_bucket_k(cf_ctx* ctx, const EigenArgs& args, uint32_t count, hipStream_t stream) {
     using G = EigenGeom<EMAX, NARROW>;
     const size_t lds = G::bytes();
     static_assert(G::bytes() <= 163840, "eigen bucket exceeds 160 KiB LDS");
     static bool configured = false;
     if (!configured) {
-        CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_kernel<EMAX, NARROW>,
+        CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)eigen_kernel<EMAX, NARROW, RESUME>,
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         configured = true;
     }
-    hipLaunchKernelGGL((eigen_kernel<EMAX, NARROW>), dim3(count), dim3(G::NT), lds, stream, args);
+    hipLaunchKernelGGL((eigen_kernel<EMAX, NARROW, RESUME>), dim3(count), dim3(G::NT), lds, stream, args);
     CF_HIP_CHECK(ctx, hipGetLastError());
     return CF_OK;
 }
 
+// kUser launches of buckets >= kSplitEmaxMin go to the split-storage sweeps (two users per CU)
+// followed by the RESUME instantiation (refinement + epilogue) when the split path takes them.
+template <int EMAX, bool NARROW = false>
+int launch_bucket(cf_ctx* ctx, const EigenArgs& args, uint32_t count, hipStream_t stream, uint32_t kmax = 0) {
+    if constexpr (EMAX >= kSplitEmaxMin) {
+        bool handled = false;
+        CF_TRY(launch_split_sweeps(ctx, args, EMAX, count, kmax, stream, &handled));
+        if (handled) return launch_bucket_k<EMAX, NARROW, true>(ctx, args, count, stream);
+    }
+    return launch_bucket_k<EMAX, NARROW, false>(ctx, args, count, stream);
+}
+
 // Bucket 12 in the conflict-free narrow layout when every unit fits it (kmax = the bucket's
 // largest k; units are sorted largest first).  CF_EIGEN_NARROW=0 keeps the 192-column layout.
-int launch_bucket12(cf_ctx* ctx, const EigenArgs& args, uint32_t count, uint32_t kmax, hipStream_t stream) {
+int launch_bucket12_layout(cf_ctx* ctx, const EigenArgs& args, uint32_t count, uint32_t kmax, hipStream_t stream) {
     static const bool narrow_on = [] {
         const char* e = getenv("CF_EIGEN_NARROW");
         return !(e && e[0] == '0');
     }();
-    if (narrow_on && kmax <= (uint32_t)EigenGeom<12, true>::NC) return launch_bucket<12, true>(ctx, args, count, stream);
-    return launch_bucket<12>(ctx, args, count, stream);
+    if (narrow_on && kmax <= (uint32_t)EigenGeom<12, true>::NC) return launch_bucket<12, true>(ctx, args, count, stream, kmax);
+    return launch_bucket<12>(ctx, args, count, stream, kmax);
+}
+
+// kUser: the users above the split layout's largest k (kSplitKmax12; sorted first) take the
+// full-LDS kernel in a launch of their own, the rest the split sweeps.
+int launch_bucket12(cf_ctx* ctx, const cf_plan* plan, const EigenArgs& args, uint32_t count, uint32_t kmax,
+                    hipStream_t stream) {
+    if (plan && args.mode == kUser && kmax > (uint32_t)kSplitKmax12 && count > 1) {
+        auto k_at = [&](uint32_t j) {
+            const uint32_t u = plan->h_order[args.first + j];
+            return (uint32_t)(plan->h_item_off[u + 1] - plan->h_item_off[u]);
+        };
+        uint32_t lo = 0, hi = count;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (k_at(mid) > (uint32_t)kSplitKmax12) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo > 0 && lo < count) {
+            CF_TRY(launch_bucket12_layout(ctx, args, lo, kmax, stream));
+            EigenArgs rest = args;
+            rest.first += lo;
+            if (rest.only_flag) rest.only_flag += lo;
+            return launch_bucket12_layout(ctx, rest, count - lo, k_at(lo), stream);
+        }
+    }
+    return launch_bucket12_layout(ctx, args, count, kmax, stream);
 }
 
 }  // namespace
@@ -884,10 +833,10 @@ int launch_buckets_on(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStrea
             case 6: rc = launch_bucket<6>(ctx, args, b.count, stream); break;
             case 7: rc = launch_bucket<7>(ctx, args, b.count, stream); break;
             case 8: rc = launch_bucket<8>(ctx, args, b.count, stream); break;
-            case 9: rc = launch_bucket<9>(ctx, args, b.count, stream); break;
-            case 10: rc = launch_bucket<10>(ctx, args, b.count, stream); break;
-            case 11: rc = launch_bucket<11>(ctx, args, b.count, stream); break;
-            case 12: rc = launch_bucket12(ctx, args, b.count, b.kmax, stream); break;
+            case 9: rc = launch_bucket<9>(ctx, args, b.count, stream, b.kmax); break;
+            case 10: rc = launch_bucket<10>(ctx, args, b.count, stream, b.kmax); break;
+            case 11: rc = launch_bucket<11>(ctx, args, b.count, stream, b.kmax); break;
+            case 12: rc = launch_bucket12(ctx, plan, args, b.count, b.kmax, stream); break;
             default: return cf_set_error(ctx, CF_ERANGE, "eigen bucket out of range (k > 192)");
         }
         if (rc != CF_OK) return rc;
@@ -994,8 +943,8 @@ int cf_launch_local_sigma(cf_ctx* ctx, const cf_plan* pair_plan, const uint64_t*
     return launch_all_buckets(ctx, pair_plan, args, stream);
 }
 
-static int launch_emax(cf_ctx* ctx, int emax, const EigenArgs& args, uint32_t count, uint32_t kmax,
-                       hipStream_t stream) {
+static int launch_emax(cf_ctx* ctx, const cf_plan* plan, int emax, const EigenArgs& args, uint32_t count,
+                       uint32_t kmax, hipStream_t stream) {
     switch (emax) {
         case 1: return launch_bucket<1>(ctx, args, count, stream);
         case 2: return launch_bucket<2>(ctx, args, count, stream);
@@ -1005,10 +954,10 @@ static int launch_emax(cf_ctx* ctx, int emax, const EigenArgs& args, uint32_t co
         case 6: return launch_bucket<6>(ctx, args, count, stream);
         case 7: return launch_bucket<7>(ctx, args, count, stream);
         case 8: return launch_bucket<8>(ctx, args, count, stream);
-        case 9: return launch_bucket<9>(ctx, args, count, stream);
-        case 10: return launch_bucket<10>(ctx, args, count, stream);
-        case 11: return launch_bucket<11>(ctx, args, count, stream);
-        case 12: return launch_bucket12(ctx, args, count, kmax, stream);   // the layout cf_launch_eigen picks
+        case 9: return launch_bucket<9>(ctx, args, count, stream, kmax);
+        case 10: return launch_bucket<10>(ctx, args, count, stream, kmax);
+        case 11: return launch_bucket<11>(ctx, args, count, stream, kmax);
+        case 12: return launch_bucket12(ctx, plan, args, count, kmax, stream);   // the layout cf_launch_eigen picks
         default: return cf_set_error(ctx, CF_ERANGE, "eigen bucket out of range (k > 192)");
     }
 }
@@ -1046,7 +995,7 @@ int cf_launch_eigen_flagged(cf_ctx* ctx, const cf_plan* plan, int emax, uint32_t
     // units are sorted largest k first within a bucket, so the range's first unit has its kmax
     const uint32_t u0 = plan->h_order[first];
     const uint32_t kmax = (uint32_t)(plan->h_item_off[u0 + 1] - plan->h_item_off[u0]);
-    return launch_emax(ctx, emax, args, count, kmax, stream);
+    return launch_emax(ctx, plan, emax, args, count, kmax, stream);
 }
 
 int cf_launch_eigen(cf_ctx* ctx, const cf_plan* plan, const uint64_t* d_item_off,

@@ -158,6 +158,10 @@ struct cf_ctx {
     hipEvent_t step_bucket_ev[16] = {};
     hipEvent_t step_sync_ev[4] = {};
     hipEvent_t step_time_ev[3] = {};
+    // split-storage Jacobi (cf_eigen_split.hip): per LDS bucket emax, the device copy of the
+    // sweep schedule tables of every k the bucket's split kernel takes (built on first use)
+    uint32_t* d_split_sched[13] = {};
+    int eigen_split = -1;   // -1: not read yet (CF_EIGEN_SPLIT, default on); cf_set_eigen_split
     // graph filter (cf_graph_filter): device time of the last call's supersteps, its edges
     float filter_ms = 0.0f;
     uint64_t filter_nnz = 0;

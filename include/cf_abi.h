@@ -81,6 +81,18 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
  * are more than delta apart.  Defaults: enable 1, stop_rel 1e-3, delta 1e-2; pairs closer than delta sweep to 8 tol.
  * enable 0 restores the sweeps-only rule (stop after a sweep with no rotation above 16 tol). */
 int cf_set_eigen_refine(cf_ctx* ctx, int enable, float stop_rel, float delta);
+/* LDS Jacobi buckets with k > 128: enable != 0 (default; env CF_EIGEN_SPLIT=0 turns
+ * it off) runs their sweeps in the split layout -- the fixed column of every pair in registers,
+ * only the traveling half in LDS, two users per CU -- and the refinement and epilogue in the
+ * full-LDS kernel; 0 keeps the whole solve in the full-LDS kernel.  Same algorithm, same outputs
+ * up to the rotation order inside odd segments.  Same call site as cf_eigen_run. */
+int cf_set_eigen_split(cf_ctx* ctx, int enable);
+/* Host only (no device): builds and verifies the split layout's sweep schedule for k columns in
+ * LDS bucket emax (every pair of columns meets once per sweep, no two lane groups touch one LDS
+ * slot in a level change, register groups and slots within capacity).  Returns CF_OK and the
+ * steps per sweep, levels, and the largest register-group and slot counts of any level, or
+ * CF_ERANGE when the split layout does not take k (those users keep the full-LDS kernel). */
+int cf_debug_split_schedule(int emax, int k, int* steps, int* levels, int* max_groups, int* max_slots);
 /* Complement-mask handoff (default on): an eigen run over a plan (cf_eigen_run, cf_step_run)
  * also writes, per rating, the 3 x 64-bit mask of the user's items that are NOT out-neighbours
  * (w <= 0.1) of that item, from the graph entries it gathers anyway (24 B per rating of HBM,
