@@ -416,7 +416,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    bucket_ms = ctx.eigen_bucket_timing(False, read=True)
+    bucket_ms, bucket_sw_ms = ctx.eigen_bucket_timing(False, read=True, sweeps=True)
     if world > 1:
         coll_dev = dev if backend == "nccl" else torch.device("cpu")
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
@@ -460,7 +460,7 @@ def main():
     ctx.eigen_bucket_timing(True)
     wl.eigen(sp)
     torch.cuda.synchronize(dev)
-    bucket_alone_ms = ctx.eigen_bucket_timing(False, read=True)
+    bucket_alone_ms, bucket_sw_alone_ms = ctx.eigen_bucket_timing(False, read=True, sweeps=True)
     jstats = ctx.debug_stats(False, read=True)
 
     # ---- accounting -------------------------------------------------------------------
@@ -479,7 +479,7 @@ def main():
     else:
         n_pred_total = n_pred_local
     value = wl.U / step_s
-    roof_eigen = eigen_roofline(wl.k, m_h, eig_s, jstats, bucket_ms, bucket_alone_ms)
+    roof_eigen = eigen_roofline(wl.k, m_h, eig_s, jstats, bucket_ms, bucket_alone_ms, bucket_sw_ms, bucket_sw_alone_ms)
     pred_acc = predictor_flops(wl.off, wl.k, m_h, kk_h, evals_h, sigs_h)
     roof_pred = predict_roofline(pred_acc, pred_s)
     dominant_is_pred = pred_s >= eig_s
@@ -574,10 +574,10 @@ def main():
         tr = pmc_traffic(args)
         if tr is not None:
             dom = roof_eigen.get("dominant")
-            if dom and dom.get("kernel") == "eigen_kernel<12, true>":
+            if dom and dom.get("emax", 12) == 12 and "12" in (dom.get("kernel") or ""):
                 f12, w12 = tr["eigen12"]
                 dom["traffic"] = 2.0 * f12 + w12
-                dom["traffic_note"] = "2 x FETCH_SIZE + WRITE_SIZE of the one eigen_kernel<12, true> launch of a child step"
+                dom["traffic_note"] = f"2 x FETCH_SIZE + WRITE_SIZE of the one {dom['kernel']} launch of a child step"
                 if "stage" in roof_eigen:   # the top level is the dominant kernel's: its own traffic
                     roof_eigen["traffic"] = dom["traffic"]
                     roof_eigen["traffic_note"] = dom["traffic_note"] + " (MI355X_MICROARCH.md's gfx950 correction)"
@@ -644,7 +644,7 @@ def main():
         dist.destroy_process_group()
 
 
-def eigen_roofline(k, m_h, eig_s, jstats, bucket_ms=None, bucket_alone_ms=None):
+def eigen_roofline(k, m_h, eig_s, jstats, bucket_ms=None, bucket_alone_ms=None, sw_ms=None, sw_alone_ms=None):
     kf = k.astype(np.float64)
     flops = float(np.sum(9.0 * kf ** 3 + 4.0 * kf ** 2))
     # algorithmic bytes: item ids in, W_u entries (index+weight), sigs/evals/evecs out
@@ -670,16 +670,19 @@ def eigen_roofline(k, m_h, eig_s, jstats, bucket_ms=None, bucket_alone_ms=None):
         "executed_flops_per_stage": exe,
         "executed_TFLOPs": exe / eig_s / 1e12,
         "executed_frac": exe / eig_s / 1e12 / FP32_PEAK_TFLOPS,
-        **({"dominant": eigen_dominant(k, bucket_ms, bucket_alone_ms)} if bucket_ms is not None else {}),
+        **({"dominant": eigen_dominant(k, bucket_ms, bucket_alone_ms, sw_ms, sw_alone_ms)} if bucket_ms is not None else {}),
     }
 
 
-def eigen_dominant(k, bucket_ms, bucket_alone_ms=None):
-    """The dominant kernel of the eigen stage, eigen_kernel<12, true> (bucket 12: 176 < k <= 192,
-    one launch per step), and every other LDS bucket: algorithmic flops per launch (9k^3 + 4k^2
-    per user) over the launch's duration from cf_eigen_bucket_timing (HIP events on
-    the aux stream it runs on, mean over the timed steps; it co-runs with the other buckets on
-    the second stream, as in a rocprofv3 kernel trace of the step)."""
+def eigen_dominant(k, bucket_ms, bucket_alone_ms=None, sw_ms=None, sw_alone_ms=None):
+    """The dominant launch of the eigen stage (bucket 12: 176 < k <= 192, one per step) and every
+    other LDS bucket: algorithmic flops per launch (9k^3 + 4k^2 per user) over the
+    launch's duration from cf_eigen_bucket_timing_split (HIP events on the aux stream it runs on, mean
+    over the timed steps; it co-runs with the other buckets on the second stream, as in a rocprofv3
+    kernel trace of the step).  A bucket in the split layout is two kernels back to
+    back, split_sweep_kernel<e> (gather, assembly, sweeps) and eigen_kernel<e, .., RESUME>
+    (refinement, epilogue): the launch is the pair, its flops the whole eigensolve, and the sweep
+    kernel's own share is reported beside it (sweeps_ms)."""
     kf = k.astype(np.float64)
     emax = np.ceil(kf / 16.0).astype(np.int64)
     rows = []
@@ -689,11 +692,19 @@ def eigen_dominant(k, bucket_ms, bucket_alone_ms=None):
         if not sel.any() or ms <= 0:
             continue
         fl = float(np.sum(9.0 * kf[sel] ** 3 + 4.0 * kf[sel] ** 2))
-        rows.append({"emax": e, "users": int(sel.sum()), "flops_per_launch": fl, "ms_per_launch": ms,
-                     "achieved_TFLOPs": fl / ms / 1e9, "frac": fl / ms / 1e9 / FP32_PEAK_TFLOPS})
+        row = {"emax": e, "users": int(sel.sum()), "flops_per_launch": fl, "ms_per_launch": ms,
+               "achieved_TFLOPs": fl / ms / 1e9, "frac": fl / ms / 1e9 / FP32_PEAK_TFLOPS}
+        if sw_ms is not None and float(sw_ms[e]) > 0:
+            row["sweeps_ms"] = float(sw_ms[e])
+        rows.append(row)
     dom = max(rows, key=lambda r: r["ms_per_launch"]) if rows else None
-    out = {"kernel": "eigen_kernel<12, true>" if dom and dom["emax"] == 12 else
-                     (f"eigen_kernel<{dom['emax']}>" if dom else None),
+
+    def name(r):
+        base = "eigen_kernel<12, true>" if r["emax"] == 12 else f"eigen_kernel<{r['emax']}>"
+        if "sweeps_ms" in r:
+            return f"split_sweep_kernel<{r['emax']}> + " + base[:-1] + ", RESUME>"
+        return base
+    out = {"kernel": name(dom) if dom else None,
            "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS, "buckets": rows,
            "note": "per-launch algorithmic flops / the launch's HIP-event duration in the timed steps "
                    "(mean); the stage-level achieved/frac above divides the whole stage's flops by the "
@@ -702,12 +713,16 @@ def eigen_dominant(k, bucket_ms, bucket_alone_ms=None):
         out.update({"users": dom["users"], "flops_per_launch": dom["flops_per_launch"],
                     "ms_per_launch": dom["ms_per_launch"], "achieved": dom["achieved_TFLOPs"],
                     "frac": dom["frac"]})
+        if "sweeps_ms" in dom:
+            out["sweeps_ms"] = dom["sweeps_ms"]
         if bucket_alone_ms is not None and float(bucket_alone_ms[dom["emax"]]) > 0:
             ms_a = float(bucket_alone_ms[dom["emax"]])
             out.update({"alone_ms": ms_a, "alone_frac": dom["flops_per_launch"] / ms_a / 1e9 / FP32_PEAK_TFLOPS,
                         "alone_note": "the same launch alone on the GPU (one stream, the untimed sweep-count "
                                       "pass); a rocprofv3 average over a run's launches mixes this one with the "
                                       "co-running in-step ones"})
+            if sw_alone_ms is not None and float(sw_alone_ms[dom["emax"]]) > 0:
+                out["alone_sweeps_ms"] = float(sw_alone_ms[dom["emax"]])
     return out
 
 
@@ -1452,14 +1467,15 @@ def pmc_traffic(args, knn2=False, prep=False):
                         out["knn2"][slot] += float(r["Counter_Value"]) * 1024.0
                     continue
                 key = "predict" if re.search(r"pred_(basis|rating|dense)_kernel<|spill_(basis|predict)_kernel<", name) \
-                    else "eigen" if re.search(r"eigen_kernel<", name) else None
+                    else "eigen" if re.search(r"eigen_kernel<|split_sweep_kernel<", name) else None
                 if key and r["Counter_Name"] == counter:
                     out[key][slot] += float(r["Counter_Value"]) * 1024.0   # the counter is in KiB
                     kn = re.search(r"(pred_basis|pred_rating|pred_dense|spill_basis|spill_predict)_kernel", name)
                     if kn:   # the predictor's split per kernel
                         out.setdefault("predict_by_kernel", {}).setdefault(kn.group(1), [0.0, 0.0])[slot] += \
                             float(r["Counter_Value"]) * 1024.0
-                    if re.search(r"eigen_kernel<12, ?true>", name):   # the dominant kernel alone
+                    # the dominant launch alone: bucket 12's kernel (narrow layout), or its split pair
+                    if re.search(r"eigen_kernel<12, ?true|split_sweep_kernel<12>", name):
                         out["eigen12"][slot] += float(r["Counter_Value"]) * 1024.0
         except (subprocess.SubprocessError, OSError, KeyError, ValueError):
             return None

@@ -45,6 +45,7 @@ SIGNATURES = {
     "cf_set_eigen_method": (c_int, [c_void_p, c_int]),
     "cf_debug_stats": (c_int, [c_void_p, c_int, c_void_p]),
     "cf_eigen_bucket_timing": (c_int, [c_void_p, c_int, c_void_p]),
+    "cf_eigen_bucket_timing_split": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
     "cf_debug_phases": (c_int, [c_void_p, c_int, c_void_p]),
     "cf_debug_spill": (c_int, [c_void_p, c_int, c_void_p]),
     "cf_debug_tri": (c_int, [c_void_p, c_int, c_void_p]),

@@ -101,8 +101,9 @@ class Context:
         """Jacobi sweeps to stop_rel, then the first-order Gram refinement (cf_set_eigen_refine)."""
         self._chk(self.lib.cf_set_eigen_refine(self.h, int(enable), stop_rel, delta), "cf_set_eigen_refine")
 
-    def set_eigen_split(self, enable: bool = True):
-        """Buckets with k > 128: Jacobi sweeps in the split layout, two users per CU (cf_set_eigen_split)."""
+    def set_eigen_split(self, enable=True):
+        """Jacobi sweeps in the split layout, several users per CU (cf_set_eigen_split): False off,
+        True the default buckets, or an int 5..12 = the smallest bucket that takes it."""
         self._chk(self.lib.cf_set_eigen_split(self.h, int(enable)), "cf_set_eigen_split")
 
     def set_local_wlim(self, bisect: bool = True):
@@ -125,11 +126,14 @@ class Context:
                     "jacobi_cyc_per_step": int(out[5]) / max(int(out[7]), 1)}
         return None
 
-    def eigen_bucket_timing(self, enable: bool = True, read: bool = False):
-        """cf_eigen_bucket_timing: per k-bucket device ms of the last eigen run (index = emax)."""
+    def eigen_bucket_timing(self, enable: bool = True, read: bool = False, sweeps: bool = False):
+        """cf_eigen_bucket_timing_split: per k-bucket device ms of the last eigen runs (index = emax);
+        with sweeps=True also the split-layout buckets' sweep-kernel share (-1 elsewhere)."""
         out = np.zeros(13, dtype=np.float32) if read else None
-        self._chk(self.lib.cf_eigen_bucket_timing(self.h, int(enable), ptr(out)), "cf_eigen_bucket_timing")
-        return out
+        sw = np.zeros(13, dtype=np.float32) if read else None
+        self._chk(self.lib.cf_eigen_bucket_timing_split(self.h, int(enable), ptr(out), ptr(sw)),
+                  "cf_eigen_bucket_timing_split")
+        return (out, sw) if sweeps else out
 
     def debug_spill(self, enable: bool = True, read: bool = False):
         """Spill-path phase cycles (thread 0 s_memtime sums) when read."""

@@ -115,6 +115,7 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
     __syncthreads();
     if constexpr (RESUME) {
         const float* hb = a.evecs + a.evec_off[u];
+#pragma unroll 1
         for (int j = wave; j < k; j += NW)
             for (int i = lane; i < k; i += 64) B[bidx(i, j)] = hb[(size_t)j * k + i];
         for (int j = tid; j < k; j += NT) s_dev[j] = a.evals[base + j];
@@ -642,7 +643,10 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
         float smm = 0.0f;
         if constexpr (RESUME) {
             // sigs hold (float)(sig + 0.01), monotone in sig: their max is the max's image
-            for (int i = 0; i < k; ++i) smm = fmaxf(smm, a.sigs[base + i]);
+            // (staged through s_sig, which this instantiation does not otherwise use)
+            for (int i = tid; i < k; i += NT) s_sig[i] = a.sigs[base + i];
+            __syncthreads();
+            for (int i = 0; i < k; ++i) smm = fmaxf(smm, s_sig[i]);
         } else {
             for (int i = 0; i < k; ++i)
                 if (smm < s_sig[i]) smm = s_sig[i];
@@ -708,10 +712,16 @@ int launch_bucket_k(cf_ctx* ctx, const EigenArgs& args, uint32_t count, hipStrea
 // followed by the RESUME instantiation (refinement + epilogue) when the split path takes them.
 template <int EMAX, bool NARROW = false>
 int launch_bucket(cf_ctx* ctx, const EigenArgs& args, uint32_t count, hipStream_t stream, uint32_t kmax = 0) {
-    if constexpr (EMAX >= kSplitEmaxMin) {
+    if constexpr (EMAX >= kSplitEmaxLow) {
         bool handled = false;
         CF_TRY(launch_split_sweeps(ctx, args, EMAX, count, kmax, stream, &handled));
-        if (handled) return launch_bucket_k<EMAX, NARROW, true>(ctx, args, count, stream);
+        if (handled) {
+            if (ctx->split_mid_ev) {   // cf_eigen_bucket_timing: the sweeps' share of the bucket
+                CF_HIP_CHECK(ctx, hipEventRecord(ctx->split_mid_ev, stream));
+                ctx->split_mid_recorded = true;
+            }
+            return launch_bucket_k<EMAX, NARROW, true>(ctx, args, count, stream);
+        }
     }
     return launch_bucket_k<EMAX, NARROW, false>(ctx, args, count, stream);
 }
@@ -823,16 +833,20 @@ int launch_buckets_on(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStrea
         }
         const bool timed = ctx->bucket_timing && args.mode == kUser && b.emax >= 1 && b.emax <= 12;
         const int slot = ctx->bucket_run % cf_ctx::kBucketRuns;
-        if (timed) CF_HIP_CHECK(ctx, hipEventRecord(ctx->bucket_ev[slot][b.emax][0], stream));
+        if (timed) {
+            CF_HIP_CHECK(ctx, hipEventRecord(ctx->bucket_ev[slot][b.emax][0], stream));
+            ctx->split_mid_ev = ctx->bucket_ev[slot][b.emax][2];
+            ctx->split_mid_recorded = false;
+        }
         switch (b.emax) {
             case 1: rc = launch_bucket<1>(ctx, args, b.count, stream); break;
             case 2: rc = launch_bucket<2>(ctx, args, b.count, stream); break;
             case 3: rc = launch_bucket<3>(ctx, args, b.count, stream); break;
             case 4: rc = launch_bucket<4>(ctx, args, b.count, stream); break;
-            case 5: rc = launch_bucket<5>(ctx, args, b.count, stream); break;
-            case 6: rc = launch_bucket<6>(ctx, args, b.count, stream); break;
-            case 7: rc = launch_bucket<7>(ctx, args, b.count, stream); break;
-            case 8: rc = launch_bucket<8>(ctx, args, b.count, stream); break;
+            case 5: rc = launch_bucket<5>(ctx, args, b.count, stream, b.kmax); break;
+            case 6: rc = launch_bucket<6>(ctx, args, b.count, stream, b.kmax); break;
+            case 7: rc = launch_bucket<7>(ctx, args, b.count, stream, b.kmax); break;
+            case 8: rc = launch_bucket<8>(ctx, args, b.count, stream, b.kmax); break;
             case 9: rc = launch_bucket<9>(ctx, args, b.count, stream, b.kmax); break;
             case 10: rc = launch_bucket<10>(ctx, args, b.count, stream, b.kmax); break;
             case 11: rc = launch_bucket<11>(ctx, args, b.count, stream, b.kmax); break;
@@ -843,6 +857,8 @@ int launch_buckets_on(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStrea
         if (timed) {
             CF_HIP_CHECK(ctx, hipEventRecord(ctx->bucket_ev[slot][b.emax][1], stream));
             ctx->bucket_recorded[slot][b.emax] = true;
+            ctx->bucket_mid[slot][b.emax] = ctx->split_mid_recorded;
+            ctx->split_mid_ev = nullptr;
         }
     }
     if (ctx->bucket_timing && args.mode == kUser) ++ctx->bucket_run;
@@ -865,17 +881,18 @@ int launch_all_buckets(cf_ctx* ctx, const cf_plan* plan, EigenArgs args, hipStre
 }
 }  // namespace
 
-extern "C" int cf_eigen_bucket_timing(cf_ctx* ctx, int enable, float* ms13) {
+extern "C" int cf_eigen_bucket_timing_split(cf_ctx* ctx, int enable, float* ms13, float* sweeps_ms13) {
     if (!ctx) return CF_EINVAL;
     CF_TRY(set_device(ctx));
+    ctx->split_mid_ev = nullptr;
     if (enable && !ctx->bucket_ev[0][1][0])
         for (auto& run : ctx->bucket_ev)
             for (auto& pr : run)
                 for (hipEvent_t& e : pr) CF_HIP_CHECK(ctx, hipEventCreate(&e));
     if (ms13) {   // mean over the recorded runs (the last kBucketRuns of them)
         for (int e = 0; e < 13; ++e) {
-            double sum = 0.0;
-            int cnt = 0;
+            double sum = 0.0, sum_a = 0.0;
+            int cnt = 0, cnt_a = 0;
             for (int r = 0; r < cf_ctx::kBucketRuns; ++r) {
                 if (!ctx->bucket_recorded[r][e]) continue;
                 float ms = 0.0f;
@@ -883,14 +900,25 @@ extern "C" int cf_eigen_bucket_timing(cf_ctx* ctx, int enable, float* ms13) {
                 CF_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->bucket_ev[r][e][0], ctx->bucket_ev[r][e][1]));
                 sum += ms;
                 ++cnt;
+                if (ctx->bucket_mid[r][e]) {
+                    CF_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->bucket_ev[r][e][0], ctx->bucket_ev[r][e][2]));
+                    sum_a += ms;
+                    ++cnt_a;
+                }
                 ctx->bucket_recorded[r][e] = false;
+                ctx->bucket_mid[r][e] = false;
             }
             ms13[e] = cnt ? (float)(sum / cnt) : -1.0f;
+            if (sweeps_ms13) sweeps_ms13[e] = cnt_a ? (float)(sum_a / cnt_a) : -1.0f;
         }
         ctx->bucket_run = 0;
     }
     ctx->bucket_timing = enable != 0;
     return CF_OK;
+}
+
+extern "C" int cf_eigen_bucket_timing(cf_ctx* ctx, int enable, float* ms13) {
+    return cf_eigen_bucket_timing_split(ctx, enable, ms13, nullptr);
 }
 
 int cf_launch_local_eigen(cf_ctx* ctx, const cf_plan* movie_plan, const uint64_t* d_item_off,
@@ -950,10 +978,10 @@ static int launch_emax(cf_ctx* ctx, const cf_plan* plan, int emax, const EigenAr
         case 2: return launch_bucket<2>(ctx, args, count, stream);
         case 3: return launch_bucket<3>(ctx, args, count, stream);
         case 4: return launch_bucket<4>(ctx, args, count, stream);
-        case 5: return launch_bucket<5>(ctx, args, count, stream);
-        case 6: return launch_bucket<6>(ctx, args, count, stream);
-        case 7: return launch_bucket<7>(ctx, args, count, stream);
-        case 8: return launch_bucket<8>(ctx, args, count, stream);
+        case 5: return launch_bucket<5>(ctx, args, count, stream, kmax);
+        case 6: return launch_bucket<6>(ctx, args, count, stream, kmax);
+        case 7: return launch_bucket<7>(ctx, args, count, stream, kmax);
+        case 8: return launch_bucket<8>(ctx, args, count, stream, kmax);
         case 9: return launch_bucket<9>(ctx, args, count, stream, kmax);
         case 10: return launch_bucket<10>(ctx, args, count, stream, kmax);
         case 11: return launch_bucket<11>(ctx, args, count, stream, kmax);

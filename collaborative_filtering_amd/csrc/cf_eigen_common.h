@@ -122,7 +122,8 @@ __device__ __forceinline__ float test_rating(const EigenArgs& a, uint32_t movie,
 // user's eigenvector slot and each column's drift d_j in evals[item_off[u] + j]; eigen_kernel's
 // RESUME instantiation (cf_eigen.hip) then runs the refinement and the epilogue from there.
 // *handled = false (and nothing launched) when the split path does not take this launch.
-constexpr int kSplitEmaxMin = 9;
+constexpr int kSplitEmaxMin = 9;    // default smallest bucket of the split layout (cf_set_eigen_split)
+constexpr int kSplitEmaxLow = 5;    // smallest bucket it is built for
 constexpr int kSplitKmax12 = 180;   // bucket 12: largest k of the split layout (90 LDS slots)
 int launch_split_sweeps(cf_ctx* ctx, const EigenArgs& a, int emax, uint32_t count, uint32_t kmax, hipStream_t stream,
                         bool* handled);

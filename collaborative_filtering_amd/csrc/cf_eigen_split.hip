@@ -47,6 +47,10 @@ constexpr int split_ld(int nr) {   // smallest LD >= nr with LD == 16 or 48 (mod
     return ld;
 }
 
+// users per CU by bucket: LDS (<= 160 KB / UPC) and the sweeps' registers (512 / ceil(UPC * EMAX / 4)
+// per lane, 4 * EMAX for the two columns of a pair plus ~30) both have to fit
+constexpr int split_upc(int emax) { return emax >= 9 ? 2 : 3; }
+
 template <int EMAX>
 struct SplitGeom {
     static constexpr int NR = 16 * EMAX;                  // rows (zero past k)
@@ -57,8 +61,12 @@ struct SplitGeom {
     static constexpr int KLO = 16 * (EMAX - 1) + 1;
     static constexpr int KHI = EMAX == 12 ? kSplitKmax12 : NR;   // largest k the layout takes
     static constexpr int LD = split_ld(NR);
-    static constexpr int WPE = (2 * EMAX + 3) / 4;        // waves per SIMD at two users per CU
-    static constexpr int CB = 64;                         // assembly: columns per LDS tile
+    static constexpr int UPC = split_upc(EMAX);           // users per CU
+    // waves per SIMD the registers are sized for: a workgroup's EMAX waves land on the SIMDs
+    // round-robin from a varying start, so UPC of them may stack ceil(EMAX / 4) each on one SIMD
+    static constexpr int WPE = UPC * ((EMAX + 3) / 4);
+    // assembly: columns per LDS tile (the tile lives in the slot area)
+    static constexpr int CB = (NS * LD) / (KHI + 1) < 64 ? (NS * LD) / (KHI + 1) : 64;
     // table words per k: nlev, f0, FL[kMaxLev], role[kMaxLev][NG], trans[kMaxLev][NG], end_g[NG], end_s[NS]
     static constexpr int OFF_FL = 2;
     static constexpr int OFF_ROLE = OFF_FL + kMaxLev;
@@ -74,12 +82,10 @@ struct SplitGeom {
                + sizeof(int) * NR                 // rank -> column
                + sizeof(int) * 4;                 // flags
     }
+    static_assert(bytes() * UPC <= 163840, "UPC users must share a CU's LDS");
+    static_assert(WPE <= 8, "at most 8 waves per SIMD");
+    static_assert(CB >= 16, "assembly tile");
 };
-static_assert(SplitGeom<12>::bytes() <= 81920, "two bucket-12 users must share a CU");
-static_assert(SplitGeom<11>::bytes() <= 81920 && SplitGeom<10>::bytes() <= 81920 && SplitGeom<9>::bytes() <= 81920,
-              "two users must share a CU");
-static_assert(SplitGeom<12>::CB * (SplitGeom<12>::KHI + 1) <= SplitGeom<12>::NS * SplitGeom<12>::LD, "assembly tile");
-static_assert(SplitGeom<9>::CB * (SplitGeom<9>::KHI + 1) <= SplitGeom<9>::NS * SplitGeom<9>::LD, "assembly tile");
 
 // ------------------------------------------------------------------------------------------------
 // Host: the schedule.  Level L splits every segment of >= 2 columns into a fixed part F (in lane
@@ -564,53 +570,72 @@ __global__ __launch_bounds__(SplitGeom<EMAX>::NT, SplitGeom<EMAX>::WPE) void spl
         const uint64_t fp = cf_items_fp(s_item, k, base, lane);
         if (lane == 0) a.cmask_fp[u] = fp;
     }
-    for (int i = wave; i < k; i += NW) {
-        const GraphRow row = a.graph.row(s_item[i]);
-        float* wr = hb + (size_t)i * k;
+    // W rows go to the slot and, RB at a time, through LDS (the slot area, LDT = k | 1: a thread
+    // per row reads its row conflict-free) for the degree and sig_min passes
+    const int LDT = k | 1;
+    const int RB = (NS * LD) / LDT;
+    float* tile = Bs;
+    for (int r0 = 0; r0 < k; r0 += RB) {
+        const int rb = min(RB, k - r0);
+        for (int i = r0 + wave; i < r0 + rb; i += NW) {
+            const GraphRow row = a.graph.row(s_item[i]);
+            float* wr = hb + (size_t)i * k;
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            const int j = 64 * t + lane;
-            const float w = j < k ? row[s_item[j]] : 0.0f;
-            if (j < k) wr[j] = w;
-            if (masks) {
-                // the predictor's mask words of row i (cf_eigen.hip stage 1)
-                const unsigned long long bal = __ballot(j < k && !((double)w > 0.1));
-                if (lane == 0) a.cmask_out[3 * (base + i) + t] = bal;
+            for (int t = 0; t < 3; ++t) {
+                const int j = 64 * t + lane;
+                const float w = j < k ? row[s_item[j]] : 0.0f;
+                if (j < k) {
+                    wr[j] = w;
+                    tile[(i - r0) * LDT + j] = w;
+                }
+                if (masks) {
+                    // the predictor's mask words of row i (cf_eigen.hip stage 1)
+                    const unsigned long long bal = __ballot(j < k && !((double)w > 0.1));
+                    if (lane == 0) a.cmask_out[3 * (base + i) + t] = bal;
+                }
             }
         }
-    }
-    __syncthreads();
-
-    // ---- 2. degrees (fp64, j in order), s, L2 diagonal, sig_min: cf_eigen.hip stage 2 --------
-    for (int i = tid; i < k; i += NT) {
-        const float* wr = hb + (size_t)i * k;
-        double d = 0.0;
-        for (int j = 0; j < k; ++j) d += (double)wr[j];
-        if (d == 0.0) d = 1.0;                       // (:137-140)
-        const double s = sqrt(1.0 / d);              // (:149-153)
-        s_s[i] = (float)s;
-        s_l2d[i] = (float)((s * (d - (double)wr[i])) * s);
-    }
-    __syncthreads();
-    for (int i = tid; i < k; i += NT) {
-        const float* wr = hb + (size_t)i * k;
-        const float si = s_s[i];
-        float acc = 0.0f;
-        for (int j = 0; j < k; ++j) {
-            const float l2 = (j == i) ? s_l2d[i] : -(si * wr[j]) * s_s[j];
-            acc = fmaf(l2, l2, acc);
+        __syncthreads();
+        // ---- 2a. degrees (fp64, j in order), s, L2 diagonal: cf_eigen.hip stage 2
+        for (int i = r0 + tid; i < r0 + rb; i += NT) {
+            const float* wr = tile + (i - r0) * LDT;
+            double d = 0.0;
+            for (int j = 0; j < k; ++j) d += (double)wr[j];
+            if (d == 0.0) d = 1.0;                       // (:137-140)
+            const double s = sqrt(1.0 / d);              // (:149-153)
+            s_s[i] = (float)s;
+            s_l2d[i] = (float)((s * (d - (double)wr[i])) * s);
         }
-        if (a.sigs) a.sigs[base + i] = (float)((double)sqrtf(acc) + 0.01);   // (:172-176, :182)
+        __syncthreads();
     }
-    __syncthreads();
+    // ---- 2b. sig_min from the full rows (every s_j known): the rows again, from the slot
+    for (int r0 = 0; r0 < k; r0 += RB) {
+        const int rb = min(RB, k - r0);
+        if (r0 > 0 || rb < k) {   // a single block is still in LDS
+            for (int idx = tid; idx < rb * k; idx += NT) {
+                const int i = idx / k, j = idx - i * k;
+                tile[i * LDT + j] = hb[(size_t)(r0 + i) * k + j];
+            }
+            __syncthreads();
+        }
+        for (int i = r0 + tid; i < r0 + rb; i += NT) {
+            const float* wr = tile + (i - r0) * LDT;
+            const float si = s_s[i];
+            float acc = 0.0f;
+            for (int j = 0; j < k; ++j) {
+                const float l2 = (j == i) ? s_l2d[i] : -(si * wr[j]) * s_s[j];
+                acc = fmaf(l2, l2, acc);
+            }
+            if (a.sigs) a.sigs[base + i] = (float)((double)sqrtf(acc) + 0.01);   // (:172-176, :182)
+        }
+        __syncthreads();
+    }
 
     // ---- 3. B = sym_lower(L2) + I, 64 columns at a time: B(r, c) = -(s_max W(max, min)) s_min --
     // (cf_eigen.hip stage 3).  Tile column cc of the block holds B(:, c0 + cc); it is written over
     // rows c0.. of the row-major W, which no later block reads (they need W(r, c) with r >= their
     // c0, or their own rows).
     {
-        float* tile = Bs;
-        const int LDT = k | 1;
         for (int c0 = 0; c0 < k; c0 += G::CB) {
             const int cb = min(G::CB, k - c0);
             // r > c: W(r, c), lanes over the block's columns (a row segment per pass)
@@ -899,13 +924,18 @@ int launch_emax_split(cf_ctx* ctx, const EigenArgs& a, uint32_t count, uint32_t 
 int launch_split_sweeps(cf_ctx* ctx, const EigenArgs& a, int emax, uint32_t count, uint32_t kmax, hipStream_t stream,
                         bool* handled) {
     *handled = false;
-    if (a.mode != kUser || emax < kSplitEmaxMin || emax > 12 || count == 0) return CF_OK;
-    if (ctx->eigen_split < 0) {
+    if (a.mode != kUser || emax < kSplitEmaxLow || emax > 12 || count == 0) return CF_OK;
+    if (ctx->eigen_split < 0) {   // CF_EIGEN_SPLIT: 0 off, else the smallest bucket (default kSplitEmaxMin)
         const char* e = getenv("CF_EIGEN_SPLIT");
-        ctx->eigen_split = (e && e[0] == '0') ? 0 : 1;
+        ctx->eigen_split = e ? atoi(e) : 1;
     }
-    if (!ctx->eigen_split) return CF_OK;
+    const int emin = ctx->eigen_split == 1 ? kSplitEmaxMin : ctx->eigen_split;
+    if (!ctx->eigen_split || emax < emin) return CF_OK;
     switch (emax) {
+        case 5: return launch_emax_split<5>(ctx, a, count, kmax, stream, handled);
+        case 6: return launch_emax_split<6>(ctx, a, count, kmax, stream, handled);
+        case 7: return launch_emax_split<7>(ctx, a, count, kmax, stream, handled);
+        case 8: return launch_emax_split<8>(ctx, a, count, kmax, stream, handled);
         case 9: return launch_emax_split<9>(ctx, a, count, kmax, stream, handled);
         case 10: return launch_emax_split<10>(ctx, a, count, kmax, stream, handled);
         case 11: return launch_emax_split<11>(ctx, a, count, kmax, stream, handled);
@@ -920,17 +950,32 @@ using namespace cf_eig;
 
 extern "C" int cf_set_eigen_split(cf_ctx* ctx, int enable) {
     if (!ctx) return CF_EINVAL;
-    ctx->eigen_split = enable ? 1 : 0;
+    if (enable < 0 || (enable > 1 && (enable < kSplitEmaxLow || enable > 12))) return CF_EINVAL;
+    ctx->eigen_split = enable;
     return CF_OK;
 }
+
+namespace {
+template <int EMAX>
+void geom_of(int* ng, int* ns, int* klo, int* khi) {
+    *ng = SplitGeom<EMAX>::NG;
+    *ns = SplitGeom<EMAX>::NS;
+    *klo = SplitGeom<EMAX>::KLO;
+    *khi = SplitGeom<EMAX>::KHI;
+}
+}  // namespace
 
 extern "C" int cf_debug_split_schedule(int emax, int k, int* steps, int* levels, int* max_groups, int* max_slots) {
     int NG, NS, klo, khi;
     switch (emax) {
-        case 9: NG = SplitGeom<9>::NG; NS = SplitGeom<9>::NS; klo = SplitGeom<9>::KLO; khi = SplitGeom<9>::KHI; break;
-        case 10: NG = SplitGeom<10>::NG; NS = SplitGeom<10>::NS; klo = SplitGeom<10>::KLO; khi = SplitGeom<10>::KHI; break;
-        case 11: NG = SplitGeom<11>::NG; NS = SplitGeom<11>::NS; klo = SplitGeom<11>::KLO; khi = SplitGeom<11>::KHI; break;
-        case 12: NG = SplitGeom<12>::NG; NS = SplitGeom<12>::NS; klo = SplitGeom<12>::KLO; khi = SplitGeom<12>::KHI; break;
+        case 5: geom_of<5>(&NG, &NS, &klo, &khi); break;
+        case 6: geom_of<6>(&NG, &NS, &klo, &khi); break;
+        case 7: geom_of<7>(&NG, &NS, &klo, &khi); break;
+        case 8: geom_of<8>(&NG, &NS, &klo, &khi); break;
+        case 9: geom_of<9>(&NG, &NS, &klo, &khi); break;
+        case 10: geom_of<10>(&NG, &NS, &klo, &khi); break;
+        case 11: geom_of<11>(&NG, &NS, &klo, &khi); break;
+        case 12: geom_of<12>(&NG, &NS, &klo, &khi); break;
         default: return CF_ERANGE;
     }
     if (k < klo || k > khi) return CF_ERANGE;

@@ -151,8 +151,11 @@ struct cf_ctx {
     // k-bucket and eigen run, for the last kBucketRuns runs (a ring), read and cleared together
     static constexpr int kBucketRuns = 16;
     bool bucket_timing = false;
-    hipEvent_t bucket_ev[kBucketRuns][13][2] = {};
+    hipEvent_t bucket_ev[kBucketRuns][13][3] = {};   // start, end, and (split layout) after the sweeps
     bool bucket_recorded[kBucketRuns][13] = {};
+    bool bucket_mid[kBucketRuns][13] = {};
+    hipEvent_t split_mid_ev = nullptr;   // set around one timed bucket launch: recorded after kernel A
+    bool split_mid_recorded = false;
     int bucket_run = 0;   // runs recorded since the last read
     hipStream_t step_stream[2] = {};
     hipEvent_t step_bucket_ev[16] = {};

@@ -81,11 +81,12 @@ int cf_set_jacobi(cf_ctx* ctx, float tol_scale, int max_sweeps);
  * are more than delta apart.  Defaults: enable 1, stop_rel 1e-3, delta 1e-2; pairs closer than delta sweep to 8 tol.
  * enable 0 restores the sweeps-only rule (stop after a sweep with no rotation above 16 tol). */
 int cf_set_eigen_refine(cf_ctx* ctx, int enable, float stop_rel, float delta);
-/* LDS Jacobi buckets with k > 128: enable != 0 (default; env CF_EIGEN_SPLIT=0 turns
- * it off) runs their sweeps in the split layout -- the fixed column of every pair in registers,
- * only the traveling half in LDS, two users per CU -- and the refinement and epilogue in the
- * full-LDS kernel; 0 keeps the whole solve in the full-LDS kernel.  Same algorithm, same outputs
- * up to the rotation order inside odd segments.  Same call site as cf_eigen_run. */
+/* LDS Jacobi, split layout: the sweeps of the users in buckets emax >= the minimum run
+ * with the fixed column of every pair in registers and only the traveling half in LDS, several users
+ * per CU, and the refinement and epilogue in the full-LDS kernel.  enable: 0 off (everything in the
+ * full-LDS kernel), 1 the default minimum bucket (9: k > 128), 5..12 an explicit minimum; env
+ * CF_EIGEN_SPLIT sets the same.  Same algorithm, same outputs up to the rotation order inside odd
+ * segments.  Same call site as cf_eigen_run. */
 int cf_set_eigen_split(cf_ctx* ctx, int enable);
 /* Host only (no device): builds and verifies the split layout's sweep schedule for k columns in
  * LDS bucket emax (every pair of columns meets once per sweep, no two lane groups touch one LDS
@@ -145,6 +146,10 @@ int cf_debug_predict_nmax(int lmax);
  * other buckets may co-run on the second stream, so these are the kernels' in-step
  * durations, as a profiler's per-dispatch trace shows them. */
 int cf_eigen_bucket_timing(cf_ctx* ctx, int enable, float* ms13);
+/* As cf_eigen_bucket_timing; sweeps_ms13[e] (optional) also receives, for buckets that ran in the
+ * split layout, the mean ms from the bucket's start to the end of its sweep kernel
+ * (split_sweep_kernel<e>; the rest of the bucket is eigen_kernel<e, .., RESUME>), else -1. */
+int cf_eigen_bucket_timing_split(cf_ctx* ctx, int enable, float* ms13, float* sweeps_ms13);
 
 /* ---- item graph (out_fin_) ---------------------------------------------------
  * Directed weighted graph exactly as parsed: w(a,b) and w(b,a) are independent.

@@ -102,3 +102,25 @@ def test_split_many_users(gpu_ctx):
         sub_off.append(sub_off[-1] + len(sub_items[-1]))
     gpu_ctx.set_eigen_split(True)
     _check_batch(gpu_ctx, W, np.array(sub_off, dtype=np.uint64), np.concatenate(sub_items), "split_many")
+
+
+KS_LOW = [65, 66, 79, 80, 81, 95, 96, 97, 111, 112, 113, 120, 127, 128]
+
+
+def test_split_low_buckets(gpu_ctx):
+    """Buckets 5-8 (k 65-128) in the split layout (cf_set_eigen_split(5): three to five users per
+    CU): oracle parity and the full-LDS kernel's eigenvalues."""
+    W = cases.item_graph(320, 0.9, seed=71)
+    off, items = cases.user_items(320, KS_LOW, seed=72)
+    gpu_ctx.set_eigen_split(5)
+    try:
+        _check_batch(gpu_ctx, W, off, items, "split_low")
+        a = _run(gpu_ctx, W, off, items, 5)
+        b = _run(gpu_ctx, W, off, items, False)
+        for u in range(len(KS_LOW)):
+            sa, ea, _ = a.block(u)
+            sb, eb, _ = b.block(u)
+            assert np.array_equal(sa, sb) and int(a.m[u]) == int(b.m[u]), u
+            assert np.max(np.abs(ea - eb)) <= 1e-5, u
+    finally:
+        gpu_ctx.set_eigen_split(True)

@@ -13,7 +13,8 @@ import pytest
 from collaborative_filtering_amd import _native
 
 # bucket emax -> (lane groups, LDS slots, smallest k, largest k)
-GEOM = {9: (72, 72, 129, 144), 10: (80, 80, 145, 160), 11: (88, 88, 161, 176), 12: (96, 90, 177, 180)}
+GEOM = {5: (40, 40, 65, 80), 6: (48, 48, 81, 96), 7: (56, 56, 97, 112), 8: (64, 64, 113, 128),
+        9: (72, 72, 129, 144), 10: (80, 80, 145, 160), 11: (88, 88, 161, 176), 12: (96, 90, 177, 180)}
 
 
 def _full_steps(k):
@@ -43,4 +44,4 @@ def test_split_schedule_out_of_range():
     lib = _native.load()
     z = ctypes.c_int()
     assert lib.cf_debug_split_schedule(12, 181, ctypes.byref(z), ctypes.byref(z), ctypes.byref(z), ctypes.byref(z)) != 0
-    assert lib.cf_debug_split_schedule(8, 120, ctypes.byref(z), ctypes.byref(z), ctypes.byref(z), ctypes.byref(z)) != 0
+    assert lib.cf_debug_split_schedule(4, 60, ctypes.byref(z), ctypes.byref(z), ctypes.byref(z), ctypes.byref(z)) != 0

@@ -28,7 +28,7 @@ for kk in ks:
          torch.zeros(users, dtype=torch.int32, device=dev), torch.zeros(n, device=dev), torch.zeros(n, device=dev),
          torch.zeros(ne, device=dev)]
     for sp in splits:
-        ctx.set_eigen_split(bool(sp))
+        ctx.set_eigen_split(sp)
         plan.eigen_run(*d)
         torch.cuda.synchronize()
         t = time.perf_counter()
