@@ -668,6 +668,8 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
     if (mode == kUser && !RESUME)
         for (int i = tid; i < k; i += NT) a.sigs[base + i] = (float)((double)s_sig[i] + 0.01);
     for (int r = tid; r < m && r < k; r += NT) a.evals[base + r] = s_mu[s_perm[r]] - 1.0f;
+    if constexpr (RESUME)   // the split kernel's drift scratch past m (the full-LDS kernel leaves it untouched)
+        for (int r = m + tid; r < k; r += NT) a.evals[base + r] = 0.0f;
     float* out = a.evecs + a.evec_off[u];
     for (int idx = tid; idx < k * m; idx += NT) {
         const int i = idx / m;
