@@ -715,8 +715,9 @@ int launch_bucket_k(cf_ctx* ctx, const EigenArgs& args, uint32_t count, hipStrea
 template <int EMAX, bool NARROW = false>
 int launch_bucket(cf_ctx* ctx, const EigenArgs& args, uint32_t count, hipStream_t stream, uint32_t kmax = 0) {
     if constexpr (EMAX >= kSplitEmaxLow) {
-        bool handled = false;
-        CF_TRY(launch_split_sweeps(ctx, args, EMAX, count, kmax, stream, &handled));
+        bool handled = false, finished = false;
+        CF_TRY(launch_split_sweeps(ctx, args, EMAX, count, kmax, stream, &handled, &finished));
+        if (handled && finished) return CF_OK;
         if (handled) {
             if (ctx->split_mid_ev) {   // cf_eigen_bucket_timing: the sweeps' share of the bucket
                 CF_HIP_CHECK(ctx, hipEventRecord(ctx->split_mid_ev, stream));

@@ -125,7 +125,9 @@ __device__ __forceinline__ float test_rating(const EigenArgs& a, uint32_t movie,
 constexpr int kSplitEmaxMin = 9;    // default smallest bucket of the split layout (cf_set_eigen_split)
 constexpr int kSplitEmaxLow = 5;    // smallest bucket it is built for
 constexpr int kSplitKmax12 = 180;   // bucket 12: largest k of the split layout (90 LDS slots)
+// *finished: the split kernel also ran the refinement and the epilogue (CF_EIGEN_SPLIT_FINISH=1): no
+// RESUME launch follows.
 int launch_split_sweeps(cf_ctx* ctx, const EigenArgs& a, int emax, uint32_t count, uint32_t kmax, hipStream_t stream,
-                        bool* handled);
+                        bool* handled, bool* finished);
 
 }  // namespace cf_eig

@@ -80,7 +80,8 @@ struct SplitGeom {
                                 + 4 * NR)         // fresh norm, drift per column; s; L2 diagonal
                + sizeof(uint32_t) * NR            // items
                + sizeof(int) * NR                 // rank -> column
-               + sizeof(int) * 4;                 // flags
+               + sizeof(int) * 4                  // flags
+               + sizeof(unsigned long long) * 3;  // phase stamps (cf_debug_stats)
     }
     static_assert(bytes() * UPC <= 163840, "UPC users must share a CU's LDS");
     static_assert(WPE <= 8, "at most 8 waves per SIMD");
@@ -527,7 +528,9 @@ const std::vector<uint32_t>& host_table(int* kmax_ok) {
 
 // ------------------------------------------------------------------------------------------------
 // Device
-template <int EMAX>
+// FINISH: the refinement (cf_eigen.hip 4b) and the epilogue (5) run here too, from the slot through
+// LDS row blocks, instead of in eigen_kernel's RESUME instantiation (one user per CU).
+template <int EMAX, bool FINISH>
 __global__ __launch_bounds__(SplitGeom<EMAX>::NT, SplitGeom<EMAX>::WPE) void split_sweep_kernel(EigenArgs a,
                                                                                              const uint32_t* sched) {
     using G = SplitGeom<EMAX>;
@@ -544,13 +547,15 @@ __global__ __launch_bounds__(SplitGeom<EMAX>::NT, SplitGeom<EMAX>::WPE) void spl
     uint32_t* s_item = reinterpret_cast<uint32_t*>(s_l2d + NR);
     int* s_map = reinterpret_cast<int*>(s_item + NR);
     int* s_flag = s_map + NR;
+    // phase stamps of thread 0 (cf_debug_stats) in LDS, off the VGPR budget
+    unsigned long long* s_stamp = reinterpret_cast<unsigned long long*>(s_flag + 4);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int g = tid / kGroup;
     const int lig = tid % kGroup;
-    unsigned long long t_phase0 = (a.stats && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
+    if (a.stats && tid == 0) s_stamp[0] = __builtin_amdgcn_s_memtime();
     if (a.only_flag && !a.only_flag[blockIdx.x]) return;
     const uint32_t u = a.order[a.first + blockIdx.x];
     const uint64_t base = a.item_off[u];
@@ -563,7 +568,10 @@ __global__ __launch_bounds__(SplitGeom<EMAX>::NT, SplitGeom<EMAX>::WPE) void spl
 
     // ---- 1. gather W (row i = w(item_i -> item_j)) into the slot, complement masks ----------
     for (int i = tid; i < k; i += NT) s_item[i] = a.items[base + i];
-    if (tid == 0) s_flag[0] = 0;
+    if (tid == 0) {
+        s_flag[0] = 0;
+        s_flag[1] = 0;   // the largest sig written (float bits, all positive)
+    }
     __syncthreads();
     const bool masks = a.cmask_out && 3 * (base + (uint64_t)k) <= a.cmask_words && u < a.cmask_users;
     if (masks && wave == 0) {
@@ -626,7 +634,9 @@ __global__ __launch_bounds__(SplitGeom<EMAX>::NT, SplitGeom<EMAX>::WPE) void spl
                 const float l2 = (j == i) ? s_l2d[i] : -(si * wr[j]) * s_s[j];
                 acc = fmaf(l2, l2, acc);
             }
-            if (a.sigs) a.sigs[base + i] = (float)((double)sqrtf(acc) + 0.01);   // (:172-176, :182)
+            const float sg = (float)((double)sqrtf(acc) + 0.01);   // (:172-176, :182)
+            if (a.sigs) a.sigs[base + i] = sg;
+            if (FINISH) atomicMax(&s_flag[1], __float_as_int(sg));
         }
         __syncthreads();
     }
@@ -673,7 +683,7 @@ __global__ __launch_bounds__(SplitGeom<EMAX>::NT, SplitGeom<EMAX>::WPE) void spl
             __syncthreads();
         }
     }
-    unsigned long long t_phase1 = (a.stats && tid == 0) ? __builtin_amdgcn_s_memtime() : 0ull;
+    if (a.stats && tid == 0) s_stamp[1] = __builtin_amdgcn_s_memtime();
 
     // ---- 4. sweeps ----------------------------------------------------------------------------
     // uniform: kept in scalar registers (readfirstlane), off the VGPR budget of the sweeps
@@ -879,24 +889,222 @@ __global__ __launch_bounds__(SplitGeom<EMAX>::NT, SplitGeom<EMAX>::WPE) void spl
         if (tid == 0) s_flag[0] = 0;
         __syncthreads();
     }
-    // ---- 5. drifts for the refinement / epilogue kernel ----------------------------------------
-    for (int j = tid; j < k; j += NT) a.evals[base + j] = s_cd[j];
+    if (a.stats && tid == 0) s_stamp[2] = __builtin_amdgcn_s_memtime();
+    if constexpr (!FINISH) {
+        // ---- 5. drifts for the refinement / epilogue kernel (eigen_kernel<.., RESUME>)
+        for (int j = tid; j < k; j += NT) a.evals[base + j] = s_cd[j];
+    } else {
+        // ---- 5'. first-order Gram refinement (cf_eigen.hip 4b) from the column-major slot ------
+        float* s_mu = s_l2d;   // free after the assembly
+        float* tile = Bs;      // the slot area, free after the last sweep
+        const int nb = (k + 15) >> 4;
+        const int m16 = lane & 15, kq = lane >> 4;
+        const int jc = wave * 16 + m16;   // this lane's column (wave < nb; NW >= nb)
+        const bool jv = wave < nb && jc < k;
+        f4 kv[EMAX];
+#pragma unroll
+        for (int I = 0; I < EMAX; ++I) kv[I] = f4{0.f, 0.f, 0.f, 0.f};
+        if (refine) {
+            for (int c = tid; c < k; c += NT) s_mu[c] = s_cn[c] / (1.0f + s_cd[c]);   // fresh mu^2
+            // F = B^T B over row blocks of RB1 rows: column segments staged in LDS, the same 16-row
+            // chunks in the same order as cf_eigen.hip's F loop
+            constexpr int RB1 = (((NS * LD) / G::KHI - 4) / 16) * 16;
+            constexpr int LDR1 = RB1 + 4;   // f4-aligned column segments
+            static_assert(RB1 >= 16, "refinement row block");
+            for (int R0 = 0; R0 < k; R0 += RB1) {
+                __syncthreads();
+                for (int idx = tid; idx < k * RB1; idx += NT) {
+                    const int c = idx / RB1, r = idx - c * RB1;
+                    tile[c * LDR1 + r] = (R0 + r < k) ? hb[(size_t)c * k + R0 + r] : 0.0f;
+                }
+                __syncthreads();
+                if (wave < nb) {
+                    const int nc16 = (min(RB1, k - R0) + 15) >> 4;
+                    const f4* pj = reinterpret_cast<const f4*>(tile + (jv ? jc : 0) * LDR1 + 4 * kq);
+                    for (int c = 0; c < nc16; ++c) {
+                        const f4 y = jv ? pj[4 * c] : f4{0.f, 0.f, 0.f, 0.f};
+                        // two row tiles per operand step (cf_eigen.hip takes four: the accumulators of
+                        // all EMAX tiles already hold 4 * EMAX of this kernel's 80 registers)
+#pragma unroll
+                        for (int I0 = 0; I0 < EMAX; I0 += 2) {
+                            f4 x[2];
+#pragma unroll
+                            for (int g2 = 0; g2 < 2; ++g2) {
+                                const int ci = (I0 + g2) * 16 + m16;
+                                x[g2] = (I0 + g2 < nb && ci < k) ? reinterpret_cast<const f4*>(tile + ci * LDR1 + 4 * kq)[4 * c]
+                                                                 : f4{0.f, 0.f, 0.f, 0.f};
+                            }
+#pragma unroll
+                            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                                for (int g2 = 0; g2 < 2; ++g2)
+                                    if (I0 + g2 < EMAX && I0 + g2 < nb)
+                                        kv[I0 + g2] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[g2][t], y[t], kv[I0 + g2], 0, 0, 0);
+                        }
+                    }
+                }
+            }
+            // K(i, j) = F(i, j) / (mu_i^2 - mu_j^2), |mu_i - mu_j| > delta, i != j (cf_eigen.hip 4b)
+            if (wave < nb) {
+                const float muj2 = jv ? s_mu[jc] : 1.0f;
+                const float muj = sqrtf(muj2);
+                const float dlt = a.refine_delta;
+                float ksq = 0.0f;
+#pragma unroll
+                for (int I = 0; I < EMAX; ++I)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = I * 16 + 4 * kq + r;
+                        float kvv = 0.0f;
+                        if (I < nb && jv && i < k && i != jc) {
+                            const float mui2 = s_mu[i];
+                            if (fabsf(sqrtf(mui2) - muj) > dlt) kvv = kv[I][r] / (mui2 - muj2);
+                        }
+                        kv[I][r] = -kvv;
+                        ksq = fmaf(kvv, kvv, ksq);
+                    }
+                ksq += __shfl_xor(ksq, 16);
+                ksq += __shfl_xor(ksq, 32);
+                if (kq == 0 && jv) s_cd[jc] += ksq;
+            }
+        }
+        __syncthreads();
+        // the slot column-major -> row-major in place (pair swaps): the update and the output read
+        // and write whole rows, which a row block owns
+        for (int i = wave; i < k; i += NW)
+            for (int jj = i + 1 + lane; jj < k; jj += 64) {
+                const float x = hb[(size_t)i * k + jj], y = hb[(size_t)jj * k + i];
+                hb[(size_t)i * k + jj] = y;
+                hb[(size_t)jj * k + i] = x;
+            }
+        __syncthreads();
+        if (refine) {
+            // B(R, J) - B(R, :) K(:, J) for row blocks R of 48 rows, written back over rows R
+            constexpr int RB3x = (((NS * LD) / G::KHI - 1) / 16) * 16;   // rows whose k columns fit the area
+            constexpr int RB3 = RB3x < 48 ? RB3x : 48, LDR3 = RB3 + 1;
+            static_assert(RB3 >= 16 && G::KHI * LDR3 <= NS * LD, "update row block");
+            for (int R0 = 0; R0 < k; R0 += RB3) {
+                for (int idx = tid; idx < RB3 * k; idx += NT) {
+                    const int r = idx / k, c = idx - r * k;
+                    tile[c * LDR3 + r] = (R0 + r < k) ? hb[(size_t)(R0 + r) * k + c] : 0.0f;
+                }
+                __syncthreads();
+                if (wave < nb) {
+                    f4 out[RB3 / 16];
+#pragma unroll
+                    for (int q = 0; q < RB3 / 16; ++q)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) out[q][r] = jv ? tile[jc * LDR3 + 16 * q + 4 * kq + r] : 0.0f;
+#pragma unroll
+                    for (int I = 0; I < EMAX; ++I) {
+                        if (I < nb) {
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) {
+                                const int c = I * 16 + 4 * kq + t;
+#pragma unroll
+                                for (int q = 0; q < RB3 / 16; ++q) {
+                                    const float av = c < k ? tile[c * LDR3 + 16 * q + m16] : 0.0f;
+                                    out[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, kv[I][t], out[q], 0, 0, 0);
+                                }
+                            }
+                        }
+                    }
+                    if (jv)
+#pragma unroll
+                        for (int q = 0; q < RB3 / 16; ++q)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const int row = R0 + 16 * q + 4 * kq + r;
+                                if (row < k) hb[(size_t)row * k + jc] = out[q][r];
+                            }
+                }
+                __syncthreads();
+            }
+        }
+        // ---- 6'. epilogue (cf_eigen.hip 5): fp64 norms and sign sums, rank, lim, the k x m block --
+        for (int jj = tid; jj < k; jj += NT) {
+            double acc = 0.0, sum = 0.0;
+            for (int r = 0; r < k; ++r) {
+                const double v = (double)hb[(size_t)r * k + jj];
+                acc = fma(v, v, acc);
+                sum += v;
+            }
+            const double nrm = sqrt(acc);
+            s_mu[jj] = (float)(nrm / sqrt(1.0 + (double)s_cd[jj]));   // lambda_j + 1
+            s_s[jj] = (float)((sum < 0.0 ? -1.0 : 1.0) / nrm);        // unit-normalises v_j, sum >= 0
+        }
+        __syncthreads();
+        for (int jj = tid; jj < k; jj += NT) {
+            const float mj = s_mu[jj];
+            int rank = 0;
+            for (int i = 0; i < k; ++i) {
+                const float mi = s_mu[i];
+                rank += (mi < mj) || (mi == mj && i < jj);
+            }
+            s_map[rank] = jj;
+        }
+        // lim = #{!(lambda > smm)} (cf_eigen.hip 5); smm = the largest sig written (sig + 0.01 rounded)
+        const float smm = __int_as_float(s_flag[1]);
+        const bool below = tid < k && !((double)(s_mu[tid] - 1.0f) > (double)smm);
+        int lim = __syncthreads_count(below);
+        if (lim < 2) lim = 2;
+        if (tid == 0) a.m_out[u] = lim;
+        const int m = min(lim, k);
+        for (int r = tid; r < k; r += NT) a.evals[base + r] = r < m ? s_mu[s_map[r]] - 1.0f : 0.0f;
+        // the k x m row-major block over the row-major Bref, rows in increasing order through LDS: a
+        // block's output rows land on rows it or an earlier block held (m <= k)
+        const int LDO = k + 1;
+        const int RBo = (NS * LD) / LDO;
+        for (int i0 = 0; i0 < k; i0 += RBo) {
+            const int rb = min(RBo, k - i0);
+            for (int idx = tid; idx < rb * k; idx += NT) {
+                const int r = idx / k, c = idx - r * k;
+                tile[r * LDO + c] = hb[(size_t)(i0 + r) * k + c];
+            }
+            __syncthreads();
+            for (int idx = tid; idx < rb * lim; idx += NT) {
+                const int r = idx / lim, cc = idx - r * lim;
+                float v = 0.0f;
+                if (cc < k) {
+                    const int jj = s_map[cc];
+                    v = tile[r * LDO + jj] * s_s[jj];
+                }
+                hb[(size_t)(i0 + r) * lim + cc] = v;
+            }
+            __syncthreads();
+        }
+    }
     if (a.stats && tid == 0) {
-        const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+        const unsigned long long t3 = __builtin_amdgcn_s_memtime();
         atomicAdd(&a.stats[0], (unsigned long long)(sweep + 1));
         atomicAdd(&a.stats[1], 1ull);
         atomicMax(&a.stats[2], (unsigned long long)(sweep + 1));
         if (sweep >= a.max_sweeps) atomicAdd(&a.stats[3], 1ull);
-        atomicAdd(&a.stats[4], t_phase1 - t_phase0);
-        atomicAdd(&a.stats[5], t2 - t_phase1);
+        atomicAdd(&a.stats[4], s_stamp[1] - s_stamp[0]);
+        atomicAdd(&a.stats[5], s_stamp[2] - s_stamp[1]);
+        if (FINISH) atomicAdd(&a.stats[6], t3 - s_stamp[2]);
         atomicAdd(&a.stats[7], (unsigned long long)((sweep + 1) * steps_sweep));
     }
 }
 
+template <int EMAX, bool FINISH>
+int launch_split_kernel(cf_ctx* ctx, const EigenArgs& a, uint32_t count, hipStream_t stream) {
+    using G = SplitGeom<EMAX>;
+    static bool configured = false;
+    if (!configured) {
+        CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)split_sweep_kernel<EMAX, FINISH>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::bytes()));
+        configured = true;
+    }
+    hipLaunchKernelGGL((split_sweep_kernel<EMAX, FINISH>), dim3(count), dim3(G::NT), G::bytes(), stream, a,
+                       (const uint32_t*)ctx->d_split_sched[EMAX]);
+    CF_HIP_CHECK(ctx, hipGetLastError());
+    return CF_OK;
+}
+
 template <int EMAX>
 int launch_emax_split(cf_ctx* ctx, const EigenArgs& a, uint32_t count, uint32_t kmax, hipStream_t stream,
-                      bool* handled) {
-    using G = SplitGeom<EMAX>;
+                      bool* handled, bool* finished) {
     int ok_hi = 0;
     const std::vector<uint32_t>& tab = host_table<EMAX>(&ok_hi);
     if ((int)kmax > ok_hi) return CF_OK;   // not every k of the launch has a schedule
@@ -906,15 +1114,16 @@ int launch_emax_split(cf_ctx* ctx, const EigenArgs& a, uint32_t count, uint32_t 
         ctx->d_split_sched[EMAX] = static_cast<uint32_t*>(p);
         CF_HIP_CHECK(ctx, hipMemcpy(p, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
-    static bool configured = false;
-    if (!configured) {
-        CF_HIP_CHECK(ctx, hipFuncSetAttribute((const void*)split_sweep_kernel<EMAX>,
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::bytes()));
-        configured = true;
+    if (ctx->split_finish < 0) {   // CF_EIGEN_SPLIT_FINISH=1: refinement + epilogue in the split kernel
+        const char* e = getenv("CF_EIGEN_SPLIT_FINISH");
+        ctx->split_finish = (e && e[0] == '1') ? 1 : 0;
     }
-    hipLaunchKernelGGL(split_sweep_kernel<EMAX>, dim3(count), dim3(G::NT), G::bytes(), stream, a,
-                       (const uint32_t*)ctx->d_split_sched[EMAX]);
-    CF_HIP_CHECK(ctx, hipGetLastError());
+    if (ctx->split_finish) {
+        CF_TRY((launch_split_kernel<EMAX, true>(ctx, a, count, stream)));
+        *finished = true;
+    } else {
+        CF_TRY((launch_split_kernel<EMAX, false>(ctx, a, count, stream)));
+    }
     *handled = true;
     return CF_OK;
 }
@@ -922,8 +1131,9 @@ int launch_emax_split(cf_ctx* ctx, const EigenArgs& a, uint32_t count, uint32_t 
 }  // namespace
 
 int launch_split_sweeps(cf_ctx* ctx, const EigenArgs& a, int emax, uint32_t count, uint32_t kmax, hipStream_t stream,
-                        bool* handled) {
+                        bool* handled, bool* finished) {
     *handled = false;
+    *finished = false;
     if (a.mode != kUser || emax < kSplitEmaxLow || emax > 12 || count == 0) return CF_OK;
     if (ctx->eigen_split < 0) {   // CF_EIGEN_SPLIT: 0 off, else the smallest bucket (default kSplitEmaxMin)
         const char* e = getenv("CF_EIGEN_SPLIT");
@@ -932,14 +1142,14 @@ int launch_split_sweeps(cf_ctx* ctx, const EigenArgs& a, int emax, uint32_t coun
     const int emin = ctx->eigen_split == 1 ? kSplitEmaxMin : ctx->eigen_split;
     if (!ctx->eigen_split || emax < emin) return CF_OK;
     switch (emax) {
-        case 5: return launch_emax_split<5>(ctx, a, count, kmax, stream, handled);
-        case 6: return launch_emax_split<6>(ctx, a, count, kmax, stream, handled);
-        case 7: return launch_emax_split<7>(ctx, a, count, kmax, stream, handled);
-        case 8: return launch_emax_split<8>(ctx, a, count, kmax, stream, handled);
-        case 9: return launch_emax_split<9>(ctx, a, count, kmax, stream, handled);
-        case 10: return launch_emax_split<10>(ctx, a, count, kmax, stream, handled);
-        case 11: return launch_emax_split<11>(ctx, a, count, kmax, stream, handled);
-        case 12: return launch_emax_split<12>(ctx, a, count, kmax, stream, handled);
+        case 5: return launch_emax_split<5>(ctx, a, count, kmax, stream, handled, finished);
+        case 6: return launch_emax_split<6>(ctx, a, count, kmax, stream, handled, finished);
+        case 7: return launch_emax_split<7>(ctx, a, count, kmax, stream, handled, finished);
+        case 8: return launch_emax_split<8>(ctx, a, count, kmax, stream, handled, finished);
+        case 9: return launch_emax_split<9>(ctx, a, count, kmax, stream, handled, finished);
+        case 10: return launch_emax_split<10>(ctx, a, count, kmax, stream, handled, finished);
+        case 11: return launch_emax_split<11>(ctx, a, count, kmax, stream, handled, finished);
+        case 12: return launch_emax_split<12>(ctx, a, count, kmax, stream, handled, finished);
         default: return CF_OK;
     }
 }
