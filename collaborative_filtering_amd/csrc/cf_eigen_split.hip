@@ -1114,11 +1114,13 @@ int launch_emax_split(cf_ctx* ctx, const EigenArgs& a, uint32_t count, uint32_t 
         ctx->d_split_sched[EMAX] = static_cast<uint32_t*>(p);
         CF_HIP_CHECK(ctx, hipMemcpy(p, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
-    if (ctx->split_finish < 0) {   // CF_EIGEN_SPLIT_FINISH=1: refinement + epilogue in the split kernel
+    if (ctx->split_finish < 0) {   // CF_EIGEN_SPLIT_FINISH: 1 every bucket, 0 none, unset buckets <= 8
         const char* e = getenv("CF_EIGEN_SPLIT_FINISH");
-        ctx->split_finish = (e && e[0] == '1') ? 1 : 0;
+        ctx->split_finish = !e ? 2 : (e[0] == '1') ? 1 : 0;
     }
-    if (ctx->split_finish) {
+    // buckets <= 8: their RESUME twin spills (eigen_kernel<8, .., true>: 320 VGPRs), and K's 4 * EMAX
+    // accumulators fit beside the sweeps' registers; above, kernel B is faster
+    if (ctx->split_finish == 1 || (ctx->split_finish == 2 && EMAX <= 8)) {
         CF_TRY((launch_split_kernel<EMAX, true>(ctx, a, count, stream)));
         *finished = true;
     } else {

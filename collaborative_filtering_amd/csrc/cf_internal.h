@@ -165,7 +165,7 @@ struct cf_ctx {
     // sweep schedule tables of every k the bucket's split kernel takes (built on first use)
     uint32_t* d_split_sched[13] = {};
     int eigen_split = -1;   // -1: not read yet (CF_EIGEN_SPLIT, default on); cf_set_eigen_split
-    int split_finish = -1;  // -1: not read yet (CF_EIGEN_SPLIT_FINISH); refinement + epilogue in the split kernel
+    int split_finish = -1;  // -1: not read yet (CF_EIGEN_SPLIT_FINISH); 1 / 0 / 2 = refinement + epilogue in the split kernel always / never / buckets <= 8
     // graph filter (cf_graph_filter): device time of the last call's supersteps, its edges
     float filter_ms = 0.0f;
     uint64_t filter_nnz = 0;
