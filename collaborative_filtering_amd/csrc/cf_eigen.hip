@@ -115,9 +115,14 @@ __global__ __launch_bounds__((EigenGeom<EMAX, NARROW>::NT), (EigenGeom<EMAX, NAR
     __syncthreads();
     if constexpr (RESUME) {
         const float* hb = a.evecs + a.evec_off[u];
-#pragma unroll 1
-        for (int j = wave; j < k; j += NW)
-            for (int i = lane; i < k; i += 64) B[bidx(i, j)] = hb[(size_t)j * k + i];
+        // flat over the k x k block, eight loads in flight per thread (a loop per column waited out
+        // one HBM round trip per column)
+        const int kk = k * k;
+#pragma unroll 8
+        for (int idx = tid; idx < kk; idx += NT) {
+            const int j = idx / k;
+            B[bidx(idx - j * k, j)] = hb[idx];
+        }
         for (int j = tid; j < k; j += NT) s_dev[j] = a.evals[base + j];
         __syncthreads();
     } else

@@ -585,21 +585,37 @@ __global__ __launch_bounds__(SplitGeom<EMAX>::NT, SplitGeom<EMAX>::WPE) void spl
     float* tile = Bs;
     for (int r0 = 0; r0 < k; r0 += RB) {
         const int rb = min(RB, k - r0);
-        for (int i = r0 + wave; i < r0 + rb; i += NW) {
-            const GraphRow row = a.graph.row(s_item[i]);
-            float* wr = hb + (size_t)i * k;
+        // four rows per wave at a time: all twelve graph loads in flight before the stores (the
+        // compiler may not move a row's loads above the previous row's stores to the slot)
+        for (int i0 = r0 + 4 * wave; i0 < r0 + rb; i0 += 4 * NW) {
+            float w[4][3];
 #pragma unroll
-            for (int t = 0; t < 3; ++t) {
-                const int j = 64 * t + lane;
-                const float w = j < k ? row[s_item[j]] : 0.0f;
-                if (j < k) {
-                    wr[j] = w;
-                    tile[(i - r0) * LDT + j] = w;
+            for (int q = 0; q < 4; ++q) {
+                const int i = i0 + q;
+                const GraphRow row = a.graph.row(s_item[i < r0 + rb ? i : r0]);
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    const int j = 64 * t + lane;
+                    w[q][t] = (i < r0 + rb && j < k) ? row[s_item[j]] : 0.0f;
                 }
-                if (masks) {
-                    // the predictor's mask words of row i (cf_eigen.hip stage 1)
-                    const unsigned long long bal = __ballot(j < k && !((double)w > 0.1));
-                    if (lane == 0) a.cmask_out[3 * (base + i) + t] = bal;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int i = i0 + q;
+                if (i >= r0 + rb) break;
+                float* wr = hb + (size_t)i * k;
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    const int j = 64 * t + lane;
+                    if (j < k) {
+                        wr[j] = w[q][t];
+                        tile[(i - r0) * LDT + j] = w[q][t];
+                    }
+                    if (masks) {
+                        // the predictor's mask words of row i (cf_eigen.hip stage 1)
+                        const unsigned long long bal = __ballot(j < k && !((double)w[q][t] > 0.1));
+                        if (lane == 0) a.cmask_out[3 * (base + i) + t] = bal;
+                    }
                 }
             }
         }
