@@ -1,6 +1,6 @@
 # Round 6: bucket-12-on-Householder+QL hybrid vs all-Jacobi eigen (CF_EIGEN_HYBRID), C4 step
 # (profile-steps-only, same box, back to back) and the eigen parity tests under the hybrid.
-# usage: tools/gpu_r6_hybrid.sh TAG
+# usage: tools/ab/gpu_r6_hybrid.sh TAG
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 tag=${1:-a}
 for h in 0 1; do

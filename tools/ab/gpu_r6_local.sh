@@ -1,5 +1,5 @@
 # Round 6: local_calc (w_lim classes + symmetric units) and eigen stream tests, then the C2
-# local_calc leg under rocprofv3 kernel stats.  usage: tools/gpu_r6_local.sh TAG
+# local_calc leg under rocprofv3 kernel stats.  usage: tools/ab/gpu_r6_local.sh TAG
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 tag=${1:-a}
 timeout -k 10 900 python -u -m pytest tests/test_gpu_stream.py tests/test_gpu_local.py -x -v -s --timeout 400 --timeout-method thread > gpurun_out/r6_local_tests_$tag.log 2>&1
