@@ -1475,7 +1475,7 @@ def pmc_traffic(args, knn2=False, prep=False):
                         out.setdefault("predict_by_kernel", {}).setdefault(kn.group(1), [0.0, 0.0])[slot] += \
                             float(r["Counter_Value"]) * 1024.0
                     # the dominant launch alone: bucket 12's kernel (narrow layout), or its split pair
-                    if re.search(r"eigen_kernel<12, ?true|split_sweep_kernel<12>", name):
+                    if re.search(r"eigen_kernel<12, ?true|split_sweep_kernel<12[,>]", name):
                         out["eigen12"][slot] += float(r["Counter_Value"]) * 1024.0
         except (subprocess.SubprocessError, OSError, KeyError, ValueError):
             return None
